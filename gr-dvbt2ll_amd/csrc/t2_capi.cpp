@@ -1,0 +1,683 @@
+// t2_capi.cpp -- C ABI (include/dvbt2ll_hip.h): handles, device tables, launches.
+//
+// Each handle mirrors one reference gr::block: the constructor work happens in
+// *_create (host planning in t2_plan.cpp + one upload of the device tables), and
+// *_general_work runs the block's kernels synchronously on the handle's HIP stream
+// with the caller's host buffers (GNU Radio's circular buffers).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include "../../include/dvbt2ll_hip.h"
+#include "t2_kernels.h"
+#include "t2_plan.h"
+
+using namespace t2;
+
+namespace {
+
+#define HIP_TRY(expr)                                   \
+  do {                                                  \
+    hipError_t e_ = (expr);                             \
+    if (e_ != hipSuccess) {                             \
+      last_hip_error() = e_;                            \
+      return e_ == hipErrorOutOfMemory ? DVBT2LL_ENOMEM : DVBT2LL_EDEVICE; \
+    }                                                   \
+  } while (0)
+
+hipError_t &last_hip_error() {
+  static thread_local hipError_t e = hipSuccess;
+  return e;
+}
+
+// device buffer with grow-on-demand
+struct DevBuf {
+  void *p = nullptr;
+  size_t n = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  int ensure(size_t bytes) {
+    if (bytes <= n) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (hipMalloc(&p, bytes) != hipSuccess) return DVBT2LL_ENOMEM;
+    n = bytes;
+    return 0;
+  }
+  template <class T> T *as() const { return (T *)p; }
+};
+
+template <class T>
+int upload(DevBuf &b, const std::vector<T> &v) {
+  if (v.empty()) return 0;
+  if (b.ensure(v.size() * sizeof(T))) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+int upload_raw(DevBuf &b, const void *src, size_t bytes) {
+  if (b.ensure(bytes)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+  return 0;
+}
+
+struct DeviceCtx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int init(int dev) {
+    device = dev;
+    HIP_TRY(hipSetDevice(dev));
+    HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    return 0;
+  }
+  ~DeviceCtx() {
+    if (stream) { (void)hipSetDevice(device); (void)hipStreamDestroy(stream); }
+  }
+};
+
+// ---------------------------------------------------------------- FEC tables on device
+struct FecTables {
+  FecPlan plan;
+  DevBuf tab, m1, m2, rowptr, ent, prbs, crc8, crcsh;
+  FecDev dev{};
+  int init(int framesize, int rate, int constellation, int mode, int inband, int fecblocks, int tsrate) {
+    if (build_fec(framesize, rate, constellation, plan)) return DVBT2LL_EINVAL;
+    int r;
+    if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) || (r = upload(m2, plan.bch_m2)) ||
+        (r = upload(rowptr, plan.ldpc_rowptr)) || (r = upload(ent, plan.ldpc_ent)) ||
+        (r = upload(prbs, plan.prbs_bytes)) || (r = upload(crc8, plan.crc8_tab)) || (r = upload(crcsh, plan.crc8_shift)))
+      return r;
+    dev.bch_tab = tab.as<uint64_t>();
+    dev.bch_m1 = m1.as<uint64_t>();
+    dev.bch_m2 = m2.as<uint64_t>();
+    dev.ldpc_rowptr = rowptr.as<uint16_t>();
+    dev.ldpc_ent = ent.as<uint32_t>();
+    dev.prbs = prbs.as<uint8_t>();
+    dev.crc8_tab = crc8.as<uint8_t>();
+    dev.crc8_shift = crcsh.as<uint8_t>();
+    dev.kbch = plan.kbch; dev.nbch = plan.nbch; dev.P = plan.nparity; dev.nldpc = plan.nldpc;
+    dev.q = plan.q; dev.nent = (int)plan.ldpc_ent.size(); dev.chunk = plan.bch_chunk;
+    dev.parity_il = plan.parity_interleave ? 1 : 0;
+    dev.hem = mode ? 1 : 0;
+    dev.inband = inband ? 1 : 0;
+    dev.fec_blocks = fecblocks > 0 ? fecblocks : 1;
+    dev.ts_rate = tsrate;
+    return 0;
+  }
+};
+
+struct MapTables {
+  MapPlan plan;
+  DevBuf lut, perm, shift;
+  MapDev dev{};
+  int init(int framesize, int rate, int constellation, int rotation, const FecPlan &fec) {
+    if (build_map(framesize, rate, constellation, rotation, plan)) return DVBT2LL_EINVAL;
+    int r = upload_raw(lut, plan.lut, sizeof(plan.lut));
+    if (r) return r;
+    dev.lut = lut.as<float2>();
+    dev.mode = plan.mode; dev.mod = plan.mod; dev.W = plan.W; dev.R = plan.R; dev.cs = plan.cs;
+    dev.nldpc = plan.nldpc; dev.nbch = fec.nbch; dev.q = fec.q; dev.rotation = plan.rotation;
+    dev.parity_il = fec.parity_interleave ? 1 : 0;
+    dev.F = 1;
+    memcpy(dev.twist, plan.twist, 16);
+    memcpy(dev.mux, plan.mux, 16);
+    return 0;
+  }
+};
+
+int hip_status(hipError_t e) {
+  if (e == hipSuccess) return DVBT2LL_OK;
+  last_hip_error() = e;
+  return e == hipErrorOutOfMemory ? DVBT2LL_ENOMEM : DVBT2LL_EDEVICE;
+}
+
+}  // namespace
+
+// ============================================================================ common
+extern "C" const char *dvbt2ll_strerror(int status) {
+  switch (status) {
+    case DVBT2LL_OK: return "ok";
+    case DVBT2LL_EINVAL: return "invalid parameter combination";
+    case DVBT2LL_ENOMEM: return "out of memory";
+    case DVBT2LL_EDEVICE: return hipGetErrorString(last_hip_error());
+    case DVBT2LL_ESHORT: return "not enough input items";
+    default: return "unknown status";
+  }
+}
+extern "C" const char *dvbt2ll_version(void) { return "dvbt2ll-mi355x 0.1 (gfx950)"; }
+extern "C" int dvbt2ll_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ============================================================================ bbheaderbch
+struct dvbt2ll_bbheaderbch {
+  DeviceCtx ctx;
+  FecTables fec;
+  dvbt2ll_bbheaderbch_params p{};
+  int64_t blocks_done = 0;       // fec_block state = blocks_done % fecblocks
+  int64_t consumed_total = 0;    // absolute TS offset of the next input byte
+  std::vector<uint8_t> history;  // last <= 376 consumed TS bytes (previous packet for CRC-8)
+  DevBuf din, dout;
+  std::vector<uint8_t> hbuf;
+};
+
+extern "C" int dvbt2ll_bbheaderbch_create(const dvbt2ll_bbheaderbch_params *p, int device, dvbt2ll_bbheaderbch **out) {
+  if (!p || !out) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  std::unique_ptr<dvbt2ll_bbheaderbch> h(new (std::nothrow) dvbt2ll_bbheaderbch());
+  if (!h) return DVBT2LL_ENOMEM;
+  h->p = *p;
+  if (p->inband && p->fecblocks < 1) return DVBT2LL_EINVAL;
+  int r = h->ctx.init(device);
+  if (r) return r;
+  if ((r = h->fec.init(p->framesize, p->rate, 3, p->mode, p->inband, p->fecblocks, p->tsrate))) return r;
+  *out = h.release();
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_bbheaderbch_output_multiple(const dvbt2ll_bbheaderbch *h) { return h ? h->fec.plan.nbch : 0; }
+extern "C" int dvbt2ll_bbheaderbch_forecast(const dvbt2ll_bbheaderbch *h, int nout, int *nin) {
+  if (!h || !nin) return DVBT2LL_EINVAL;
+  const FecPlan &f = h->fec.plan;
+  int n = (nout - 80 - (f.nbch - f.kbch)) / 8;       // bbheader:207-216
+  if (h->p.mode) n += (((f.kbch - 80) / 8) / 187) + 1;
+  *nin = n;
+  return DVBT2LL_OK;
+}
+
+// input bytes consumed by nblocks FEC blocks starting at absolute block b0 / stream offset
+static int64_t bb_consumed(const FecDev &d, int64_t b0, int64_t nblocks) {
+  auto J = [&](int64_t B) {
+    int64_t pay = (d.kbch - 80) / 8;
+    int64_t npad = d.inband ? (B + d.fec_blocks - 1) / d.fec_blocks : 0;
+    return B * pay - 13 * npad;
+  };
+  auto pos_after = [&](int64_t B) -> int64_t {   // stream offset after block B-1
+    int64_t j = J(B);
+    if (!d.hem || j == 0) return j;
+    int64_t last = j - 1;
+    return 188 * (last / 187) + 1 + (last % 187) + 1;
+  };
+  return pos_after(b0 + nblocks) - pos_after(b0);
+}
+
+extern "C" int dvbt2ll_bbheaderbch_general_work(dvbt2ll_bbheaderbch *h, int nout, int nin, const void *in, void *out,
+                                                int *consumed) {
+  if (!h || nout < 0 || (nout && (!in || !out))) return DVBT2LL_EINVAL;
+  const FecDev &d = h->fec.dev;
+  int nb = nout / d.nbch;
+  if (consumed) *consumed = 0;
+  if (nb == 0) return 0;
+  int64_t need = bb_consumed(d, h->blocks_done, nb);
+  if (need > nin) return DVBT2LL_ESHORT;
+  // device buffer: [history | new input]; ts_base = absolute offset of history start
+  int64_t hist = (int64_t)h->history.size();
+  h->hbuf.resize(hist + need);
+  if (hist) memcpy(h->hbuf.data(), h->history.data(), hist);
+  memcpy(h->hbuf.data() + hist, in, need);
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  if (h->din.ensure(h->hbuf.size() + 16) || h->dout.ensure((size_t)nb * d.nbch)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(h->din.p, h->hbuf.data(), h->hbuf.size(), hipMemcpyHostToDevice, h->ctx.stream));
+  FecIO io{};
+  io.in = h->din.as<uint8_t>();
+  io.ts_base = h->consumed_total - hist;
+  io.ts_len = (int64_t)h->hbuf.size();
+  io.first_block = h->blocks_done;
+  io.out = h->dout.as<uint8_t>();
+  io.nblocks = nb;
+  HIP_TRY(launch_fec(FEC_TS_TO_BITS, d, io, h->ctx.stream));
+  HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)nb * d.nbch, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  h->blocks_done += nb;
+  h->consumed_total += need;
+  size_t keep = std::min<size_t>(376, h->hbuf.size());
+  h->history.assign(h->hbuf.end() - keep, h->hbuf.end());
+  if (consumed) *consumed = (int)need;
+  return nb * d.nbch;
+}
+extern "C" void dvbt2ll_bbheaderbch_destroy(dvbt2ll_bbheaderbch *h) { delete h; }
+
+// ============================================================================ ldpc
+struct dvbt2ll_ldpc {
+  DeviceCtx ctx;
+  FecTables fec;
+  DevBuf din, dout;
+};
+extern "C" int dvbt2ll_ldpc_create(const dvbt2ll_ldpc_params *p, int device, dvbt2ll_ldpc **out) {
+  if (!p || !out) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  std::unique_ptr<dvbt2ll_ldpc> h(new (std::nothrow) dvbt2ll_ldpc());
+  if (!h) return DVBT2LL_ENOMEM;
+  int r = h->ctx.init(device);
+  if (r) return r;
+  if ((r = h->fec.init(p->framesize, p->rate, 3, 0, 0, 1, 0))) return r;
+  *out = h.release();
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_ldpc_output_multiple(const dvbt2ll_ldpc *h) { return h ? h->fec.plan.nldpc : 0; }
+extern "C" int dvbt2ll_ldpc_forecast(const dvbt2ll_ldpc *h, int nout, int *nin) {
+  if (!h || !nin) return DVBT2LL_EINVAL;
+  *nin = (nout / h->fec.plan.nldpc) * h->fec.plan.nbch;
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_ldpc_general_work(dvbt2ll_ldpc *h, int nout, int nin, const void *in, void *out, int *consumed) {
+  if (!h || nout < 0 || (nout && (!in || !out))) return DVBT2LL_EINVAL;
+  const FecDev &d = h->fec.dev;
+  int nb = nout / d.nldpc;
+  if (consumed) *consumed = 0;
+  if (nb == 0) return 0;
+  if ((int64_t)nb * d.nbch > nin) return DVBT2LL_ESHORT;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  if (h->din.ensure((size_t)nb * d.nbch) || h->dout.ensure((size_t)nb * d.nldpc)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(h->din.p, in, (size_t)nb * d.nbch, hipMemcpyHostToDevice, h->ctx.stream));
+  FecIO io{};
+  io.in = h->din.as<uint8_t>();
+  io.out = h->dout.as<uint8_t>();
+  io.nblocks = nb;
+  HIP_TRY(launch_fec(FEC_BITS_TO_BITS, d, io, h->ctx.stream));
+  HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)nb * d.nldpc, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  if (consumed) *consumed = nb * d.nbch;
+  return nb * d.nldpc;
+}
+extern "C" void dvbt2ll_ldpc_destroy(dvbt2ll_ldpc *h) { delete h; }
+
+// ============================================================================ interleavermod
+struct dvbt2ll_interleavermod {
+  DeviceCtx ctx;
+  FecPlan fec;
+  MapTables map;
+  DevBuf din, dout;
+};
+extern "C" int dvbt2ll_interleavermod_create(const dvbt2ll_interleavermod_params *p, int device,
+                                             dvbt2ll_interleavermod **out) {
+  if (!p || !out) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  std::unique_ptr<dvbt2ll_interleavermod> h(new (std::nothrow) dvbt2ll_interleavermod());
+  if (!h) return DVBT2LL_ENOMEM;
+  if (build_fec(p->framesize, p->rate, p->constellation, h->fec)) return DVBT2LL_EINVAL;
+  int r = h->ctx.init(device);
+  if (r) return r;
+  if ((r = h->map.init(p->framesize, p->rate, p->constellation, p->rotation, h->fec))) return r;
+  *out = h.release();
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_interleavermod_output_multiple(const dvbt2ll_interleavermod *h) { return h ? h->map.plan.cs : 0; }
+extern "C" int dvbt2ll_interleavermod_forecast(const dvbt2ll_interleavermod *h, int nout, int *nin) {
+  if (!h || !nin) return DVBT2LL_EINVAL;
+  *nin = (nout / h->map.plan.cs) * h->map.plan.nldpc;   // interleavermod:264-268
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_interleavermod_general_work(dvbt2ll_interleavermod *h, int nout, int nin, const void *in,
+                                                   void *out, int *consumed) {
+  if (!h || nout < 0 || (nout && (!in || !out))) return DVBT2LL_EINVAL;
+  const MapDev &d = h->map.dev;
+  int nb = nout / d.cs;
+  if (consumed) *consumed = 0;
+  if (nb == 0) return 0;
+  if ((int64_t)nb * d.nldpc > nin) return DVBT2LL_ESHORT;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  if (h->din.ensure((size_t)nb * d.nldpc) || h->dout.ensure((size_t)nb * d.cs * 8)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(h->din.p, in, (size_t)nb * d.nldpc, hipMemcpyHostToDevice, h->ctx.stream));
+  MapIO io{};
+  io.in = h->din.as<uint8_t>();
+  io.out = h->dout.as<float2>();
+  io.nblocks = nb;
+  io.packed_in = 0;
+  io.apply_ci = 0;
+  HIP_TRY(launch_map(d, io, h->ctx.stream));
+  HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)nb * d.cs * 8, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  if (consumed) *consumed = nb * d.nldpc;
+  return nb * d.cs;
+}
+extern "C" void dvbt2ll_interleavermod_destroy(dvbt2ll_interleavermod *h) { delete h; }
+
+// ============================================================================ framemapperfint
+static FmParams to_fm(const dvbt2ll_framemapperfint_params &p) {
+  return FmParams{p.framesize, p.rate, p.constellation, p.rotation, p.fecblocks, p.tiblocks, p.carriermode,
+                  p.fftsize, p.guardinterval, p.l1constellation, p.pilotpattern, p.t2frames, p.numdatasyms,
+                  p.paprmode, p.version, p.preamble, p.inputmode, p.reservedbiasbits, p.l1scrambled, p.inband};
+}
+
+struct dvbt2ll_framemapperfint {
+  DeviceCtx ctx;
+  FramePlan plan;
+  DevBuf map, aux, din, dout;
+  int t2_frame_num = 0;
+};
+extern "C" int dvbt2ll_framemapperfint_create(const dvbt2ll_framemapperfint_params *p, int device,
+                                              dvbt2ll_framemapperfint **out) {
+  if (!p || !out) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  std::unique_ptr<dvbt2ll_framemapperfint> h(new (std::nothrow) dvbt2ll_framemapperfint());
+  if (!h) return DVBT2LL_ENOMEM;
+  if (build_frame(to_fm(*p), h->plan)) return DVBT2LL_EINVAL;
+  int r = h->ctx.init(device);
+  if (r) return r;
+  if ((r = upload(h->map, h->plan.gather_in)) || (r = upload(h->aux, h->plan.aux))) return r;
+  *out = h.release();
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_framemapperfint_output_multiple(const dvbt2ll_framemapperfint *h) { return h ? h->plan.M : 0; }
+extern "C" int dvbt2ll_framemapperfint_stream_items(const dvbt2ll_framemapperfint *h) { return h ? h->plan.S : 0; }
+extern "C" int dvbt2ll_framemapperfint_forecast(const dvbt2ll_framemapperfint *h, int nout, int *nin) {
+  if (!h || !nin) return DVBT2LL_EINVAL;
+  *nin = h->plan.S * (nout / h->plan.M);   // framemapper:1942-1946
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_framemapperfint_general_work(dvbt2ll_framemapperfint *h, int nout, int nin, const void *in,
+                                                    void *out, int *consumed) {
+  if (!h || nout < 0 || (nout && (!in || !out))) return DVBT2LL_EINVAL;
+  const FramePlan &f = h->plan;
+  if (consumed) *consumed = 0;
+  if (nout < f.M) return 0;
+  if (nin < f.S) return DVBT2LL_ESHORT;
+  // one T2 frame per call (the reference consumes exactly one frame, framemapper:2147)
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  if (h->din.ensure((size_t)f.S * 8) || h->dout.ensure((size_t)f.M * 8)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(h->din.p, in, (size_t)f.S * 8, hipMemcpyHostToDevice, h->ctx.stream));
+  GatherIO io{};
+  io.in = h->din.as<float2>();
+  io.out = h->dout.as<float2>();
+  io.map = h->map.as<int32_t>();
+  io.aux = h->aux.as<float2>() + (size_t)h->t2_frame_num * f.aux_len;
+  io.M = f.M;
+  HIP_TRY(launch_gather(io, h->ctx.stream));
+  HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)f.M * 8, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  h->t2_frame_num = (h->t2_frame_num + 1) % f.t2frames;
+  if (consumed) *consumed = f.S;
+  return f.M;
+}
+extern "C" void dvbt2ll_framemapperfint_destroy(dvbt2ll_framemapperfint *h) { delete h; }
+
+// ============================================================================ pilotgenp1insert
+static PgParams to_pg(const dvbt2ll_pilotgenp1insert_params &p) {
+  return PgParams{p.carriermode, p.fftsize, p.pilotpattern, p.guardinterval, p.numdatasyms, p.paprmode, p.version,
+                  p.preamble, p.misogroup, p.equalization, p.bandwidth, p.vlength};
+}
+
+struct OfdmTables {
+  DevBuf map, aux, tw, isinc, p1;
+  OfdmDev dev{};
+  int init(const PilotPlan &pp, const std::vector<int32_t> &bin_map, const std::vector<cf32> &aux_host,
+           int aux_len, int t2frames) {
+    int r;
+    if ((r = upload(map, bin_map)) || (r = upload(aux, aux_host)) || (r = upload(tw, pp.twiddle)) ||
+        (r = upload(p1, pp.p1)))
+      return r;
+    if (pp.eq && (r = upload(isinc, pp.isinc))) return r;
+    dev.bin_map = map.as<int32_t>();
+    dev.aux = aux.as<float2>();
+    dev.twiddle = tw.as<float2>();
+    dev.isinc = pp.eq ? isinc.as<float>() : nullptr;
+    dev.p1 = p1.as<float2>();
+    dev.N = pp.N; dev.G = pp.G; dev.Nsym = pp.Nsym; dev.aux_len = aux_len; dev.t2frames = t2frames;
+    dev.norm = pp.normalization;
+    return 0;
+  }
+};
+
+struct dvbt2ll_pilotgenp1insert {
+  DeviceCtx ctx;
+  PilotPlan plan;
+  OfdmTables ofdm;
+  DevBuf din, dout;
+  int out_items = 0;
+};
+extern "C" int dvbt2ll_pilotgenp1insert_create(const dvbt2ll_pilotgenp1insert_params *p, int device,
+                                               dvbt2ll_pilotgenp1insert **out) {
+  if (!p || !out) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  std::unique_ptr<dvbt2ll_pilotgenp1insert> h(new (std::nothrow) dvbt2ll_pilotgenp1insert());
+  if (!h) return DVBT2LL_ENOMEM;
+  if (build_pilot(to_pg(*p), h->plan)) return DVBT2LL_EINVAL;
+  int r = h->ctx.init(device);
+  if (r) return r;
+  std::vector<cf32> aux(AUX_L1PRE, cf32{0.f, 0.f});
+  for (int i = 0; i < 12; i++) aux[AUX_PILOT0 + i] = h->plan.pilot_values[i];
+  if ((r = h->ofdm.init(h->plan, h->plan.bin_map, aux, AUX_L1PRE, 1))) return r;
+  h->out_items = h->plan.Nsym * (h->plan.N + h->plan.G) + 2048;
+  *out = h.release();
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_pilotgenp1insert_output_multiple(const dvbt2ll_pilotgenp1insert *h) { return h ? h->out_items : 0; }
+extern "C" int dvbt2ll_pilotgenp1insert_active_items(const dvbt2ll_pilotgenp1insert *h) { return h ? h->plan.active : 0; }
+extern "C" int dvbt2ll_pilotgenp1insert_forecast(const dvbt2ll_pilotgenp1insert *h, int nout, int *nin) {
+  if (!h || !nin) return DVBT2LL_EINVAL;
+  *nin = h->plan.active * (nout / h->out_items);   // pilotgen:1240-1243
+  return DVBT2LL_OK;
+}
+static int pg_run(dvbt2ll_pilotgenp1insert *h, const void *in, void *out, int carriers_only) {
+  const PilotPlan &pp = h->plan;
+  size_t out_n = carriers_only ? (size_t)pp.Nsym * pp.N : (size_t)h->out_items;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  if (h->din.ensure((size_t)pp.active * 8) || h->dout.ensure(out_n * 8)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(h->din.p, in, (size_t)pp.active * 8, hipMemcpyHostToDevice, h->ctx.stream));
+  OfdmIO io{};
+  io.cells = h->din.as<float2>();
+  io.cell_stride = pp.active;
+  io.out = h->dout.as<float2>();
+  io.out_stride = (int64_t)out_n;
+  io.first_frame = 0;
+  io.nframes = 1;
+  io.carriers_only = carriers_only;
+  HIP_TRY(launch_ofdm(h->ofdm.dev, io, h->ctx.stream));
+  HIP_TRY(hipMemcpyAsync(out, h->dout.p, out_n * 8, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  return 0;
+}
+extern "C" int dvbt2ll_pilotgenp1insert_general_work(dvbt2ll_pilotgenp1insert *h, int nout, int nin, const void *in,
+                                                     void *out, int *consumed) {
+  if (!h || nout < 0 || (nout && (!in || !out))) return DVBT2LL_EINVAL;
+  if (consumed) *consumed = 0;
+  if (nout < h->out_items) return 0;
+  if (nin < h->plan.active) return DVBT2LL_ESHORT;
+  int r = pg_run(h, in, out, 0);   // one T2 frame per call (pilotgen:2903)
+  if (r) return r;
+  if (consumed) *consumed = h->plan.active;
+  return h->out_items;
+}
+extern "C" int dvbt2ll_pilotgenp1insert_debug_carriers(dvbt2ll_pilotgenp1insert *h, const void *in, void *carriers) {
+  if (!h || !in || !carriers) return DVBT2LL_EINVAL;
+  return pg_run(h, in, carriers, 1);
+}
+extern "C" void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h) { delete h; }
+
+// ============================================================================ chain
+struct dvbt2ll_chain {
+  DeviceCtx ctx;
+  dvbt2ll_chain_params p{};
+  FecTables fec;
+  MapTables map;
+  FramePlan frame;
+  PilotPlan pilot;
+  OfdmTables ofdm;
+  DevBuf cw, cells, perm, shift, ts_tmp, iq_tmp;
+  int max_frames = 0;
+  int64_t cw_stride = 0;
+  int64_t iq_per_frame = 0;
+  int64_t ts_per_frame = 0;
+  int pay = 0;
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double ms[3] = {0, 0, 0};
+  int64_t launches[3] = {0, 0, 0};
+  ~dvbt2ll_chain() {
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
+extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, dvbt2ll_chain **out) {
+  if (!p || !out || p->max_frames < 1) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  const dvbt2ll_framemapperfint_params &f = p->fm;
+  if (f.inband) return DVBT2LL_EINVAL;   // in-band type B signalling: block API only
+  std::unique_ptr<dvbt2ll_chain> h(new (std::nothrow) dvbt2ll_chain());
+  if (!h) return DVBT2LL_ENOMEM;
+  h->p = *p;
+  h->max_frames = p->max_frames;
+  FmParams fm = to_fm(f);
+  PgParams pg{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
+              f.preamble, p->misogroup, p->equalization, p->bandwidth, fft_points(f.fftsize)};
+  if (build_frame(fm, h->frame) || build_pilot(pg, h->pilot)) return DVBT2LL_EINVAL;
+  if (h->pilot.active != h->frame.M) return DVBT2LL_EINVAL;
+  int r = h->ctx.init(device);
+  if (r) return r;
+  if ((r = h->fec.init(f.framesize, f.rate, f.constellation, f.inputmode, 0, f.fecblocks, 0))) return r;
+  if ((r = h->map.init(f.framesize, f.rate, f.constellation, f.rotation, h->fec.plan))) return r;
+  if ((r = upload(h->perm, h->frame.ci_perm)) || (r = upload(h->shift, h->frame.ci_shift))) return r;
+  h->map.dev.ci_perm = h->perm.as<int16_t>();
+  h->map.dev.ci_shift = h->shift.as<int32_t>();
+  h->map.dev.F = h->frame.F;
+  // compose: IFFT bin -> mapped cell -> time-interleaver-input cell (or aux entry)
+  const PilotPlan &pp = h->pilot;
+  std::vector<int32_t> cmap(pp.bin_map.size());
+  for (size_t i = 0; i < cmap.size(); i++) {
+    int32_t c = pp.bin_map[i];
+    cmap[i] = c >= 0 ? h->frame.gather_t[c] : c;
+  }
+  std::vector<cf32> aux = h->frame.aux;
+  for (int v = 0; v < h->frame.t2frames; v++)
+    for (int i = 0; i < 12; i++) aux[(size_t)v * h->frame.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
+  if ((r = h->ofdm.init(pp, cmap, aux, h->frame.aux_len, h->frame.t2frames))) return r;
+  h->cw_stride = ((h->fec.plan.nldpc / 8) + 255) / 256 * 256;
+  h->iq_per_frame = (int64_t)pp.Nsym * (pp.N + pp.G) + 2048;
+  h->pay = (h->fec.plan.kbch - 80) / 8;
+  h->ts_per_frame = (int64_t)h->frame.F * h->pay;
+  int64_t nblk = (int64_t)h->frame.F * h->max_frames;
+  if (h->cw.ensure((size_t)nblk * h->cw_stride) || h->cells.ensure((size_t)h->frame.S * 8 * h->max_frames))
+    return DVBT2LL_ENOMEM;
+  for (auto &e : h->ev) HIP_TRY(hipEventCreate(&e));
+  *out = h.release();
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info) {
+  if (!h || !info) return DVBT2LL_EINVAL;
+  info->fec_blocks_per_frame = h->frame.F;
+  info->payload_bytes_per_block = h->pay;
+  info->ts_bytes_per_frame = h->p.fm.inputmode ? (h->ts_per_frame * 188 + 186) / 187 : h->ts_per_frame;
+  info->iq_samples_per_frame = h->iq_per_frame;
+  info->cell_size = h->frame.cs;
+  info->stream_items = h->frame.S;
+  info->mapped_items = h->frame.M;
+  info->num_symbols = h->pilot.Nsym;
+  info->fft_size = h->pilot.N;
+  info->guard_interval = h->pilot.G;
+  info->cw_stride_bytes = h->cw_stride;
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_base, int64_t ts_len,
+                                        int64_t first_frame, int nframes, void *iq_dev, void *stream) {
+  if (!h || !ts_dev || !iq_dev || nframes < 1 || nframes > h->max_frames || first_frame < 0 || ts_base < 0)
+    return DVBT2LL_EINVAL;
+  hipStream_t s = stream ? (hipStream_t)stream : h->ctx.stream;
+  const int F = h->frame.F;
+  // the TS slice must cover every byte the frames consume plus the packet before the
+  // first one touched (its CRC-8 replaces the next sync byte, bbheader:701-713)
+  int64_t start = first_frame * h->ts_per_frame, end = (first_frame + nframes) * h->ts_per_frame;
+  if (h->p.fm.inputmode) {
+    start = 188 * (start / 187) + (start % 187);
+    end = 188 * (end / 187) + (end % 187) + 1;
+  }
+  int64_t lo = start >= 188 ? (start / 188) * 188 - 188 : 0;
+  if (ts_base > lo || ts_base + ts_len < end) return DVBT2LL_EINVAL;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[0], s));
+  FecIO fio{};
+  fio.in = (const uint8_t *)ts_dev;
+  fio.ts_base = ts_base;
+  fio.ts_len = ts_len;
+  fio.first_block = first_frame * F;
+  fio.out = h->cw.as<uint8_t>();
+  fio.cw_stride = h->cw_stride;
+  fio.nblocks = F * nframes;
+  HIP_TRY(launch_fec(FEC_TS_TO_TEMPU, h->fec.dev, fio, s));
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], s));
+  MapIO mio{};
+  mio.in = h->cw.as<uint8_t>();
+  mio.cw_stride = h->cw_stride;
+  mio.out = h->cells.as<float2>();
+  mio.nblocks = F * nframes;
+  mio.packed_in = 1;
+  mio.apply_ci = 1;
+  HIP_TRY(launch_map(h->map.dev, mio, s));
+  if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
+  OfdmIO oio{};
+  oio.cells = h->cells.as<float2>();
+  oio.cell_stride = h->frame.S;
+  oio.out = (float2 *)iq_dev;
+  oio.out_stride = h->iq_per_frame;
+  oio.first_frame = first_frame;
+  oio.nframes = nframes;
+  HIP_TRY(launch_ofdm(h->ofdm.dev, oio, s));
+  if (h->timing) {
+    HIP_TRY(hipEventRecord(h->ev[3], s));
+    HIP_TRY(hipEventSynchronize(h->ev[3]));
+    for (int k = 0; k < 3; k++) {
+      float t = 0;
+      HIP_TRY(hipEventElapsedTime(&t, h->ev[k], h->ev[k + 1]));
+      h->ms[k] += t;
+      h->launches[k] += 1;
+    }
+  }
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
+                                      int64_t first_frame, int nframes, void *iq) {
+  if (!h || !ts || !iq || nframes < 1 || nframes > h->max_frames) return DVBT2LL_EINVAL;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  size_t iq_bytes = (size_t)nframes * h->iq_per_frame * 8;
+  if (h->ts_tmp.ensure((size_t)ts_len + 16) || h->iq_tmp.ensure(iq_bytes)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(h->ts_tmp.p, ts, (size_t)ts_len, hipMemcpyHostToDevice, h->ctx.stream));
+  int r = dvbt2ll_chain_run_device(h, h->ts_tmp.p, ts_base, ts_len, first_frame, nframes, h->iq_tmp.p, nullptr);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(iq, h->iq_tmp.p, iq_bytes, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable) {
+  if (!h) return DVBT2LL_EINVAL;
+  h->timing = enable != 0;
+  for (int k = 0; k < 3; k++) { h->ms[k] = 0; h->launches[k] = 0; }
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages) {
+  if (!h || !ms || nstages < 1) return DVBT2LL_EINVAL;
+  for (int k = 0; k < nstages && k < 3; k++) {
+    ms[k] = h->ms[k];
+    if (launches) launches[k] = h->launches[k];
+  }
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes) {
+  if (!h || !out || bytes < 0 || (size_t)bytes > h->cw.n) return DVBT2LL_EINVAL;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, h->cw.p, (size_t)bytes, hipMemcpyDeviceToHost));
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells) {
+  if (!h || !out || cells < 0 || (size_t)cells * 8 > h->cells.n) return DVBT2LL_EINVAL;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(out, h->cells.p, (size_t)cells * 8, hipMemcpyDeviceToHost));
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_chain_synchronize(dvbt2ll_chain *h) {
+  if (!h) return DVBT2LL_EINVAL;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  return DVBT2LL_OK;
+}
+extern "C" void dvbt2ll_chain_destroy(dvbt2ll_chain *h) { delete h; }

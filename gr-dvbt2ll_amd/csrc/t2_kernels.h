@@ -1,0 +1,89 @@
+// t2_kernels.h -- device-side argument blocks and host launchers for the DVB-T2 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace t2 {
+
+// ---------------------------------------------------------------- FEC (BB + BCH + LDPC)
+enum FecMode {
+  FEC_TS_TO_TEMPU = 0,   // chain: TS bytes -> packed interleaver-input codeword
+  FEC_TS_TO_BITS = 1,    // bbheaderbch block: TS bytes -> unpacked nbch bits
+  FEC_BITS_TO_BITS = 2,  // ldpc block: unpacked nbch bits -> unpacked nldpc bits (natural)
+};
+
+struct FecDev {
+  const uint64_t *bch_tab;      // 256 x 3
+  const uint64_t *bch_m1;       // 192 x 3
+  const uint64_t *bch_m2;       // 192 x 3
+  const uint16_t *ldpc_rowptr;  // q + 1
+  const uint32_t *ldpc_ent;     // nent
+  const uint8_t *prbs;          // kbch / 8
+  const uint8_t *crc8_tab;      // 256
+  const uint8_t *crc8_shift;    // 8 x 256
+  int kbch, nbch, P, nldpc, q, nent, chunk, parity_il;
+  int hem, inband, fec_blocks, ts_rate;
+};
+
+struct FecIO {
+  const uint8_t *in;       // TS bytes (ts modes) or unpacked bits
+  int64_t ts_base;         // absolute stream offset of in[0] (ts modes)
+  int64_t ts_len;
+  int64_t first_block;     // absolute FEC block index of launch block 0
+  uint8_t *out;            // packed codewords (stride cw_stride) or unpacked bits
+  int64_t cw_stride;
+  int nblocks;
+};
+
+// ---------------------------------------------------------------- bit interleave + QAM + CI
+struct MapDev {
+  const float2 *lut;       // 256
+  const int16_t *ci_perm;  // cs (chain only)
+  const int32_t *ci_shift; // F  (chain only)
+  int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
+  uint8_t twist[16], mux[16];
+};
+struct MapIO {
+  const uint8_t *in;   // packed tempu codewords (stride cw_stride) or unpacked natural bits
+  int64_t cw_stride;
+  float2 *out;         // cells
+  int nblocks;
+  int packed_in;       // 1: chain layout; 0: unpacked bits (interleavermod block)
+  int apply_ci;        // 1: write in time-interleaver input order
+};
+
+// ---------------------------------------------------------------- OFDM symbols
+struct OfdmDev {
+  const int32_t *bin_map;   // Nsym x N (IFFT input order)
+  const float2 *aux;        // t2frames x aux_len
+  const float2 *twiddle;    // N
+  const float *isinc;       // N or null
+  const float2 *p1;         // 2048
+  int N, G, Nsym, aux_len, t2frames;
+  float norm;
+};
+struct OfdmIO {
+  const float2 *cells;      // per frame: cell_stride entries
+  int64_t cell_stride;
+  float2 *out;              // per frame: out_stride samples
+  int64_t out_stride;
+  int64_t first_frame;
+  int nframes;
+  int carriers_only;        // test hook: write pre-IFFT bins (natural bin order) instead
+};
+
+// ---------------------------------------------------------------- frame-mapper gather
+struct GatherIO {
+  const float2 *in;
+  float2 *out;
+  const int32_t *map;       // M
+  const float2 *aux;        // aux_len (one variant)
+  int M;
+};
+
+hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s);
+hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s);
+hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s);
+hipError_t launch_gather(const GatherIO &io, hipStream_t s);
+
+}  // namespace t2

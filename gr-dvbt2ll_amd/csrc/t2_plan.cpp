@@ -1,0 +1,939 @@
+// t2_plan.cpp -- host-side configuration planning (see t2_plan.h).
+//
+// Compiled with -ffp-contract=off: the float constellation, pilot and L1 cell values
+// must round exactly as the reference's (which is built -O3 without -march, i.e. no FMA).
+#include "t2_plan.h"
+
+#include <cmath>
+#include <cstring>
+#include <algorithm>
+
+#include "gen/dvbt2_std_tables.h"
+
+namespace t2 {
+
+namespace {
+
+// enum values of include/dvbt2ll/dvbt2ll_config.h:60-202
+enum { R12 = 0, R35, R23, R34, R45, R56, R13, R25 };
+enum { QPSK = 0, QAM16, QAM64, QAM256 };
+enum { FFT2K = 0, FFT8K, FFT4K, FFT1K, FFT16K, FFT32K, FFT8KT2GI, FFT32KT2GI, FFT16KT2GI = 11 };
+enum { GI132 = 0, GI116, GI18, GI14, GI1128, GI19128, GI19256 };
+enum { PAPROFF = 0, PAPRACE, PAPRTR, PAPRBOTH };
+enum { PP1 = 0, PP2, PP3, PP4, PP5, PP6, PP7, PP8 };
+
+constexpr int kNormal = 64800, kShort = 16200;
+
+// ---------------------------------------------------------------- GF(2) polynomials < x^192
+struct Poly192 {
+  uint64_t w[3] = {0, 0, 0};
+  bool bit(int i) const { return (w[i >> 6] >> (i & 63)) & 1; }
+  void set(int i) { w[i >> 6] |= 1ull << (i & 63); }
+  void flip(int i) { w[i >> 6] ^= 1ull << (i & 63); }
+};
+
+// v * x mod g for deg g = P (g holds the low P coefficients)
+Poly192 times_x(Poly192 v, const Poly192 &g, int P) {
+  bool top = v.bit(P - 1);
+  v.w[2] = (v.w[2] << 1) | (v.w[1] >> 63);
+  v.w[1] = (v.w[1] << 1) | (v.w[0] >> 63);
+  v.w[0] <<= 1;
+  for (int k = 0; k < 3; k++) {
+    int lo = 64 * k;
+    if (P <= lo) v.w[k] = 0;
+    else if (P < lo + 64) v.w[k] &= (1ull << (P - lo)) - 1;
+  }
+  if (top)
+    for (int k = 0; k < 3; k++) v.w[k] ^= g.w[k];
+  return v;
+}
+
+// BCH generator: product of the first P/16 (normal) or all 12 (short) minimal polynomials
+// (reference bch_poly_build_tables, bbheader:424-502)
+Poly192 bch_generator(bool normal, int P) {
+  std::vector<uint8_t> acc{1};
+  int n = normal ? P / 16 : 12;
+  for (int k = 0; k < n; k++) {
+    const uint8_t *m = normal ? T2_BCH_MINPOLY_NORMAL[k] : T2_BCH_MINPOLY_SHORT[k];
+    int lm = normal ? 17 : 15;
+    std::vector<uint8_t> r(acc.size() + lm - 1, 0);
+    for (size_t i = 0; i < acc.size(); i++)
+      if (acc[i])
+        for (int j = 0; j < lm; j++) r[i + j] ^= m[j];
+    acc.swap(r);
+  }
+  Poly192 g;
+  for (int i = 0; i < P; i++)
+    if (acc[i]) g.set(i);
+  return g;
+}
+
+// rows of the GF(2) matrix of v -> v * x^K mod g, lane-friendly layout: row r = 3 words
+std::vector<uint64_t> shift_matrix(const Poly192 &g, int P, long K) {
+  Poly192 c;
+  c.set(0);
+  for (long i = 0; i < K; i++) c = times_x(c, g, P);
+  std::vector<Poly192> cols(P);
+  for (int i = 0; i < P; i++) {
+    cols[i] = c;
+    c = times_x(c, g, P);
+  }
+  std::vector<uint64_t> rows(192 * 3, 0);
+  for (int r = 0; r < P; r++)
+    for (int i = 0; i < P; i++)
+      if (cols[i].bit(r)) rows[r * 3 + (i >> 6)] |= 1ull << (i & 63);
+  return rows;
+}
+
+const t2_ldpc_code_t *find_code(int normal, int rate) {
+  for (int i = 0; i < T2_LDPC_NCODES; i++)
+    if (T2_LDPC_CODES[i].framesize_normal == normal && T2_LDPC_CODES[i].rate == rate) return &T2_LDPC_CODES[i];
+  return nullptr;
+}
+
+// PRBS 1 + x^14 + x^15, init 100101010000000 (BB scrambler, dummy cells, L1 scrambler)
+void prbs15(uint8_t *bits, int n) {
+  unsigned s = 0x4A80;
+  for (int i = 0; i < n; i++) {
+    unsigned b = (s ^ (s >> 1)) & 1;
+    bits[i] = (uint8_t)b;
+    s = (s >> 1) | (b << 14);
+  }
+}
+
+int cell_size_of(int normal, int constellation) {
+  static const int n[4] = {32400, 16200, 10800, 8100}, s[4] = {8100, 4050, 2700, 2025};
+  if (constellation < 0 || constellation > 3) return 0;
+  return normal ? n[constellation] : s[constellation];
+}
+
+}  // namespace
+
+int fft_points(int fftsize) {
+  switch (fftsize) {
+    case FFT1K: return 1024;
+    case FFT2K: return 2048;
+    case FFT4K: return 4096;
+    case FFT8K: case FFT8KT2GI: return 8192;
+    case FFT16K: case FFT16KT2GI: return 16384;
+    case FFT32K: case FFT32KT2GI: return 32768;
+    default: return 0;
+  }
+}
+
+// ============================================================================ FEC
+// FEC parameters: reference bbheaderbch ctor lib/bbheaderbch_bb_impl.cc:51-165
+static bool fec_numbers(int normal, int rate, int *kbch, int *nbch, int *q, int *P) {
+  struct E { int k, n, q, p; };
+  static const E N[6] = {{32208, 32400, 90, 192}, {38688, 38880, 72, 192}, {43040, 43200, 60, 160},
+                         {48408, 48600, 45, 192}, {51648, 51840, 36, 192}, {53840, 54000, 30, 160}};
+  static const E S[8] = {{7032, 7200, 25, 168}, {9552, 9720, 18, 168}, {10632, 10800, 15, 168},
+                         {11712, 11880, 12, 168}, {12432, 12600, 10, 168}, {13152, 13320, 8, 168},
+                         {5232, 5400, 30, 168}, {6312, 6480, 27, 168}};
+  const E *e = nullptr;
+  if (normal && rate >= 0 && rate <= R56) e = &N[rate];
+  if (!normal && rate >= 0 && rate <= R25) e = &S[rate];
+  if (!e) return false;
+  *kbch = e->k; *nbch = e->n; *q = e->q; *P = e->p;
+  return true;
+}
+
+int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
+  int normal = framesize == 1;
+  if (framesize != 0 && framesize != 1) return -1;
+  if (!fec_numbers(normal, rate, &fp.kbch, &fp.nbch, &fp.q, &fp.nparity)) return -1;
+  fp.normal = normal;
+  fp.rate = rate;
+  fp.nldpc = normal ? kNormal : kShort;
+  fp.pbits = fp.nldpc - fp.nbch;
+  // QPSK carries parity interleaving only for rates 1/3 and 2/5 (interleavermod:291-314)
+  fp.parity_interleave = !(constellation == QPSK && rate != R13 && rate != R25);
+  const int P = fp.nparity;
+  Poly192 g = bch_generator(normal, P);
+  // byte table: d(x) * x^P mod g
+  fp.bch_tab.assign(256 * 3, 0);
+  for (int d = 0; d < 256; d++) {
+    Poly192 v;
+    v.w[0] = (uint64_t)d;
+    for (int i = 0; i < P; i++) v = times_x(v, g, P);
+    for (int k = 0; k < 3; k++) fp.bch_tab[d * 3 + k] = v.w[k];
+  }
+  const int L = fp.kbch / 8;
+  fp.bch_chunk = (L + 255) / 256;
+  fp.bch_m1 = shift_matrix(g, P, 8L * fp.bch_chunk);
+  fp.bch_m2 = shift_matrix(g, P, 8L * fp.bch_chunk * 64);
+  // LDPC: info group gidx (360 bits) with address x lands in parity row a = x mod q with
+  // cyclic offset b = x div q (columns c = (b + n) mod 360, since pbits = 360 q)
+  const t2_ldpc_code_t *c = find_code(normal, rate);
+  if (!c || c->q != fp.q || c->nrows * 360 != fp.nbch) return -1;
+  std::vector<std::vector<uint32_t>> rows(fp.q);
+  int off = c->addr_off;
+  for (int gidx = 0; gidx < c->nrows; gidx++) {
+    int cnt = T2_LDPC_ROWLEN[c->row_off + gidx];
+    for (int e = 0; e < cnt; e++) {
+      int x = T2_LDPC_ADDR[off + e];
+      rows[x % fp.q].push_back(((uint32_t)gidx << 16) | (uint32_t)(x / fp.q));
+    }
+    off += cnt;
+  }
+  fp.ldpc_rowptr.assign(fp.q + 1, 0);
+  fp.ldpc_ent.clear();
+  for (int a = 0; a < fp.q; a++) {
+    fp.ldpc_rowptr[a] = (uint16_t)fp.ldpc_ent.size();
+    fp.ldpc_ent.insert(fp.ldpc_ent.end(), rows[a].begin(), rows[a].end());
+  }
+  fp.ldpc_rowptr[fp.q] = (uint16_t)fp.ldpc_ent.size();
+  // BB scrambler bytes (init_bb_randomiser, bbheader:357-369)
+  std::vector<uint8_t> bits(fp.kbch);
+  prbs15(bits.data(), fp.kbch);
+  fp.prbs_bytes.assign(L, 0);
+  for (int i = 0; i < fp.kbch; i++) fp.prbs_bytes[i >> 3] |= bits[i] << (7 - (i & 7));
+  // CRC-8 (x^8+x^7+x^6+x^4+x^2+1, MSB first) table and zero-byte extension tables
+  fp.crc8_tab.assign(256, 0);
+  for (int i = 0; i < 256; i++) {
+    unsigned r = (unsigned)i;
+    for (int k = 0; k < 8; k++) r = ((r & 0x80) ? (r << 1) ^ 0xD5u : r << 1) & 0xFFu;
+    fp.crc8_tab[i] = (uint8_t)r;
+  }
+  fp.crc8_shift.assign(8 * 256, 0);
+  for (int k = 0; k < 8; k++) {
+    int after = 187 - std::min(24 * k + 24, 187);
+    for (int s = 0; s < 256; s++) {
+      uint8_t v = (uint8_t)s;
+      for (int i = 0; i < after; i++) v = fp.crc8_tab[v];
+      fp.crc8_shift[k * 256 + s] = v;
+    }
+  }
+  return 0;
+}
+
+// ============================================================================ QAM / bit interleaver
+// complex<float> *= complex<float> as libstdc++ performs it (no contraction)
+static cf32 cmul(cf32 a, cf32 b) {
+  volatile float ac = a.re * b.re, bd = a.im * b.im, ad = a.re * b.im, bc = a.im * b.re;
+  return cf32{ac - bd, ad + bc};
+}
+
+// Gray-mapped QAM, optionally rotated: interleavermod ctor lib/interleavermod_bc_impl.cc:169-253
+void qam_table(int constellation, int rotation, cf32 *lut, int *mod) {
+  static const double a16[4] = {3, 1, -3, -1};
+  static const double a64[8] = {7, 5, 1, 3, -7, -5, -1, -3};
+  static const double a256[16] = {15, 13, 9, 11, 1, 3, 7, 5, -15, -13, -9, -11, -1, -3, -7, -5};
+  int bits = constellation == QAM16 ? 4 : constellation == QAM64 ? 6 : constellation == QAM256 ? 8 : 2;
+  int n = 1 << bits;
+  static const double norm2[4] = {2.0, 10.0, 42.0, 170.0};
+  static const double deg[4] = {29.0, 16.8, 8.6, 3.576334375};
+  int ci = bits == 2 ? 0 : bits == 4 ? 1 : bits == 6 ? 2 : 3;
+  double norm = std::sqrt(norm2[ci]);
+  const double *amp = ci == 1 ? a16 : ci == 2 ? a64 : a256;
+  for (int i = 0; i < n; i++) {
+    if (ci == 0) {
+      lut[i].re = (float)((i & 2 ? -1.0 : 1.0) / norm);
+      lut[i].im = (float)((i & 1 ? -1.0 : 1.0) / norm);
+      continue;
+    }
+    // even bit positions (from the MSB) select the real amplitude, odd ones the imaginary
+    int ri = 0, ii = 0;
+    for (int b = 0; b < bits / 2; b++) {
+      ri |= ((i >> (bits - 1 - 2 * b)) & 1) << (bits / 2 - 1 - b);
+      ii |= ((i >> (bits - 2 - 2 * b)) & 1) << (bits / 2 - 1 - b);
+    }
+    lut[i].re = (float)(amp[ri] / norm);
+    lut[i].im = (float)(amp[ii] / norm);
+  }
+  if (rotation) {
+    double phi = (2.0 * M_PI * deg[ci]) / 360.0;
+    cf32 r{(float)std::cos(phi), (float)std::sin(phi)};
+    for (int i = 0; i < n; i++) lut[i] = cmul(lut[i], r);
+  }
+  *mod = bits;
+}
+
+int build_map(int framesize, int rate, int constellation, int rotation, MapPlan &mp) {
+  int normal = framesize == 1;
+  mp.cs = cell_size_of(normal, constellation);
+  if (!mp.cs) return -1;
+  mp.nldpc = normal ? kNormal : kShort;
+  mp.rotation = rotation ? 1 : 0;
+  qam_table(constellation, rotation, mp.lut, &mp.mod);
+  const uint8_t *tw = nullptr, *mx = nullptr;
+  switch (constellation) {      // interleavermod:333-350, 422-439, 519-528, 617-625
+    case QPSK: mp.mode = MAP_PAIRS; mp.W = 2; break;
+    case QAM16:
+      mp.mode = MAP_TWIST2; mp.W = 8;
+      tw = normal ? T2_BI_TWIST16N : T2_BI_TWIST16S;
+      mx = (rate == R35 && normal) ? T2_BI_MUX16_35 : (rate == R13 && !normal) ? T2_BI_MUX16_13
+         : (rate == R25 && !normal) ? T2_BI_MUX16_25 : T2_BI_MUX16;
+      break;
+    case QAM64:
+      mp.mode = MAP_TWIST2; mp.W = 12;
+      tw = normal ? T2_BI_TWIST64N : T2_BI_TWIST64S;
+      mx = (rate == R35 && normal) ? T2_BI_MUX64_35 : (rate == R13 && !normal) ? T2_BI_MUX64_13
+         : (rate == R25 && !normal) ? T2_BI_MUX64_25 : T2_BI_MUX64;
+      break;
+    default:
+      if (normal) {
+        mp.mode = MAP_TWIST2; mp.W = 16; tw = T2_BI_TWIST256N;
+        mx = rate == R35 ? T2_BI_MUX256_35 : rate == R23 ? T2_BI_MUX256_23 : T2_BI_MUX256;
+      } else {
+        mp.mode = MAP_TWIST1; mp.W = 8; tw = T2_BI_TWIST256S;
+        mx = rate == R13 ? T2_BI_MUX256S_13 : rate == R25 ? T2_BI_MUX256S_25 : T2_BI_MUX256S;
+      }
+      break;
+  }
+  mp.R = mp.nldpc / mp.W;
+  for (int e = 0; e < mp.W && tw; e++) {
+    mp.twist[e] = tw[e];
+    mp.mux[e] = mx[e];
+  }
+  return 0;
+}
+
+// ============================================================================ frame mapper
+namespace {
+
+struct Counts { int n_p2, c_p2, c_data, n_fc, c_fc; };
+
+// N_P2/C_P2 (framemapper:290-356) and C_DATA/N_FC/C_FC (framemapper:425-915)
+bool active_counts(int fftsize, int carriermode, int pp, int papr, int gi, int preamble, Counts &c) {
+  int N = fft_points(fftsize);
+  if (!N || pp < PP1 || pp > PP8) return false;
+  bool siso = preamble == 0 || preamble == 3;
+  int lg = 0;
+  for (int t = N; t > 1024; t >>= 1) lg++;           // 0..5 for 1K..32K
+  static const int np2[6] = {16, 8, 4, 2, 1, 1};
+  static const int cp2s[6] = {558, 1118, 2236, 4472, 8944, 22432};
+  static const int cp2m[6] = {546, 1098, 2198, 4398, 8814, 17612};
+  c.n_p2 = np2[lg];
+  c.c_p2 = siso ? cp2s[lg] : cp2m[lg];
+  c.c_data = c.n_fc = c.c_fc = 0;
+  int ext = N >= 8192 ? carriermode : 0;
+  bool found = false;
+  for (int i = 0; i < T2_NCELL_COUNTS; i++) {
+    const t2_cell_counts_t &e = T2_CELL_COUNTS[i];
+    if (e.fft == N && e.ext == ext && e.pp == pp + 1) {
+      c.c_data = e.c_data; c.n_fc = e.n_fc; c.c_fc = e.c_fc; found = true;
+    }
+  }
+  if (!found) return false;
+  if (papr == PAPRTR || papr == PAPRBOTH) {
+    static const int tr[6] = {10, 18, 36, 72, 144, 288};
+    if (c.c_data) c.c_data -= tr[lg];
+    if (c.n_fc) c.n_fc -= tr[lg];
+    if (c.c_fc) c.c_fc -= tr[lg];
+  }
+  if (siso && ((gi == GI1128 && pp == PP7) || (gi == GI132 && pp == PP4) || (gi == GI116 && pp == PP2) ||
+               (gi == GI19256 && pp == PP2)))
+    c.n_fc = c.c_fc = 0;
+  return true;
+}
+
+// Frequency-interleaver address generator (EN 302 755 9.4.1; framemapper:357-424, 916-960):
+// yields the permuted addresses H(q) in generation order; callers keep those below a limit.
+void fi_addresses(int N, bool odd, std::vector<int> &out) {
+  int nr = 0;
+  for (int t = N; t > 1; t >>= 1) nr++;               // log2 N
+  int deg = nr - 1;
+  static const uint8_t *perm_even[6] = {T2_FI_BITPERM1KEVEN, T2_FI_BITPERM2KEVEN, T2_FI_BITPERM4KEVEN,
+                                        T2_FI_BITPERM8KEVEN, T2_FI_BITPERM16KEVEN, T2_FI_BITPERM32K};
+  static const uint8_t *perm_odd[6] = {T2_FI_BITPERM1KODD, T2_FI_BITPERM2KODD, T2_FI_BITPERM4KODD,
+                                       T2_FI_BITPERM8KODD, T2_FI_BITPERM16KODD, T2_FI_BITPERM32K};
+  static const uint32_t taps[6] = {(1u << 0) | (1u << 4), (1u << 0) | (1u << 3), (1u << 0) | (1u << 2),
+                                   (1u << 0) | (1u << 1) | (1u << 4) | (1u << 6),
+                                   (1u << 0) | (1u << 1) | (1u << 4) | (1u << 5) | (1u << 9) | (1u << 11),
+                                   (1u << 0) | (1u << 1) | (1u << 2) | (1u << 12)};
+  int lg = nr - 10;
+  const uint8_t *bp = odd ? perm_odd[lg] : perm_even[lg];
+  out.clear();
+  out.reserve(N);
+  uint32_t r = 0;
+  for (int i = 0; i < N; i++) {
+    if (i < 2) r = 0;
+    else if (i == 2) r = 1;
+    else {
+      uint32_t fb = __builtin_popcount(r & taps[lg]) & 1;
+      r = ((r & ((1u << deg) - 1)) >> 1) | (fb << (deg - 1));
+    }
+    int h = 0;
+    for (int n = 0; n < deg; n++) h |= ((r >> n) & 1) << bp[n];
+    out.push_back(h + (i & 1) * (N / 2));
+  }
+}
+
+// H tables for one cell count (P2 / data / FC); 32K uses Heven = Hodd^-1 (framemapper:961-977)
+void fi_tables(int N, int ncells, std::vector<int> &Heven, std::vector<int> &Hodd) {
+  std::vector<int> ae, ao;
+  fi_addresses(N, false, ae);
+  fi_addresses(N, true, ao);
+  Heven.clear();
+  Hodd.clear();
+  for (int v : ae) if (v < ncells) Heven.push_back(v);
+  for (int v : ao) if (v < ncells) Hodd.push_back(v);
+  if (N == 32768) {
+    Heven.assign(Hodd.size(), 0);
+    for (size_t j = 0; j < Hodd.size(); j++) Heven[Hodd[j]] = (int)j;
+  }
+}
+
+// Cell-interleaver permutation (framemapper:998-1107)
+void ci_permutation(int cs, std::vector<int16_t> &perm, int *degree) {
+  int deg;
+  uint32_t taps;
+  if (cs == 32400) { deg = 15; taps = (1u << 0) | (1u << 1) | (1u << 2) | (1u << 12); }
+  else if (cs == 16200 || cs == 10800) { deg = 14; taps = (1u << 0) | (1u << 1) | (1u << 4) | (1u << 5) | (1u << 9) | (1u << 11); }
+  else if (cs == 8100) { deg = 13; taps = (1u << 0) | (1u << 1) | (1u << 4) | (1u << 6); }
+  else if (cs == 4050 || cs == 2700) { deg = 12; taps = (1u << 0) | (1u << 2); }
+  else { deg = 11; taps = (1u << 0) | (1u << 3); }
+  *degree = deg;
+  perm.clear();
+  uint32_t r = 0;
+  for (int i = 0; i < (1 << deg); i++) {
+    if (i < 2) r = 0;
+    else if (i == 2) r = 1;
+    else {
+      uint32_t fb = __builtin_popcount(r & taps) & 1;
+      r = ((r & ((1u << (deg - 1)) - 1)) >> 1) | (fb << (deg - 2));
+    }
+    uint32_t v = r | ((uint32_t)(i & 1) << (deg - 1));
+    r = v;
+    if ((int)v < cs) perm.push_back((int16_t)v);
+  }
+}
+
+// ---- L1 signalling (framemapper:1366-1910)
+struct Bits {
+  std::vector<uint8_t> b;
+  void put(uint64_t v, int n) { for (int i = n - 1; i >= 0; i--) b.push_back((v >> i) & 1); }
+};
+
+uint32_t crc32_mpeg2(const std::vector<uint8_t> &bits) {
+  uint32_t crc = 0xffffffffu;
+  for (uint8_t x : bits) {
+    uint32_t fb = ((crc >> 31) ^ x) & 1;
+    crc <<= 1;
+    if (fb) crc ^= 0x04C11DB7u;
+  }
+  return crc;
+}
+
+// BCH(168) + LDPC of a k-bit (already shortened) block into cw (16200 bits)
+void l1_encode(std::vector<uint8_t> &cw, int k, int nbch, int rate_id) {
+  static const Poly192 g = bch_generator(false, 168);
+  // straightforward long division (clarity over speed: config time only)
+  std::vector<uint8_t> rem(168, 0);
+  for (int i = 0; i < k; i++) {
+    uint8_t fb = rem[167] ^ cw[i];
+    for (int j = 167; j > 0; j--) rem[j] = rem[j - 1] ^ (fb & g.bit(j));
+    rem[0] = fb & g.bit(0);
+  }
+  for (int n = 0; n < 168; n++) cw[k + n] = rem[167 - n];
+  const t2_ldpc_code_t *c = find_code(0, rate_id);
+  int pbits = kShort - nbch;
+  std::vector<uint8_t> p(pbits, 0);
+  int off = c->addr_off, im = 0;
+  for (int gi = 0; gi < c->nrows; gi++) {
+    int cnt = T2_LDPC_ROWLEN[c->row_off + gi];
+    for (int n = 0; n < 360; n++, im++)
+      if (cw[im])
+        for (int e = 0; e < cnt; e++) p[(T2_LDPC_ADDR[off + e] + n * c->q) % pbits] ^= 1;
+    off += cnt;
+  }
+  for (int j = 1; j < pbits; j++) p[j] ^= p[j - 1];
+  for (int j = 0; j < pbits; j++) cw[nbch + j] = p[j];
+}
+
+}  // namespace
+
+int build_frame(const FmParams &p, FramePlan &fp) {
+  int normal = p.framesize == 1;
+  fp.cs = cell_size_of(normal, p.constellation);
+  if (!fp.cs || p.fecblocks < 1 || p.t2frames < 1 || p.t2frames > 255 || p.numdatasyms < 1) return -1;
+  if (p.tiblocks < 0 || (p.tiblocks > p.fecblocks)) return -1;
+  int N = fft_points(p.fftsize);
+  Counts c;
+  if (!active_counts(p.fftsize, p.carriermode, p.pilotpattern, p.paprmode, p.guardinterval, p.preamble, c))
+    return -1;
+  if (!c.c_data || (c.n_fc && p.numdatasyms < 2)) return -1;
+  fp.N_P2 = c.n_p2; fp.C_P2 = c.c_p2; fp.C_DATA = c.c_data; fp.N_FC = c.n_fc; fp.C_FC = c.c_fc;
+  fp.F = p.fecblocks;
+  fp.t2frames = p.t2frames;
+  static const int eta_of[4] = {1, 2, 4, 6};
+  if (p.l1constellation < 0 || p.l1constellation > 3) return -1;
+  fp.eta = eta_of[p.l1constellation];
+  // L1-post size (framemapper:978-987)
+  const int KSIG_POST = 350, KBCH12 = 7032, NBCH12 = 7200, KBCH14 = 3072, NBCH14 = 3240;
+  int npunc_t = (6 * (KBCH12 - KSIG_POST)) / 5;
+  int npost_t = KSIG_POST + 168 + 9000 - npunc_t;
+  if (fp.N_P2 == 1) fp.N_post = (int)std::ceil((float)npost_t / (2 * (float)fp.eta)) * 2 * fp.eta;
+  else fp.N_post = (int)std::ceil((float)npost_t / ((float)fp.eta * (float)fp.N_P2)) * fp.eta * fp.N_P2;
+  fp.N_punc = npunc_t - (fp.N_post - npost_t);
+  fp.Lp = fp.N_post / fp.eta;
+  fp.S = fp.cs * fp.F;
+  fp.num_data_symbols = fp.N_FC ? p.numdatasyms - 1 : p.numdatasyms;
+  fp.M = fp.N_P2 * fp.C_P2 + fp.num_data_symbols * fp.C_DATA + fp.N_FC;
+  int fixed = fp.S + 1840 + fp.Lp + (fp.N_FC - fp.C_FC);
+  if (fp.M < fixed) return -1;   // reference: "too many FEC blocks in T2 frame"
+  fp.D = fp.M - fixed;
+
+  // ---- cell interleaver (framemapper:1973-1998): per-TI-block running n, skip shifts >= cs
+  int deg;
+  ci_permutation(fp.cs, fp.ci_perm, &deg);
+  int small_fec, big_fec, n_big, n_small;
+  if (p.tiblocks == 0) { small_fec = big_fec = 1; n_big = 0; n_small = p.fecblocks; }
+  else {
+    small_fec = (int)std::floor((float)p.fecblocks / (float)p.tiblocks);
+    big_fec = (int)std::ceil((float)p.fecblocks / (float)p.tiblocks);
+    n_big = p.fecblocks % p.tiblocks;
+    n_small = p.tiblocks - n_big;
+  }
+  fp.ci_shift.clear();
+  std::vector<int> ti_first, ti_count;           // FEC blocks per TI block
+  for (int s = 0, r0 = 0; s < n_small + n_big; s++) {
+    int nb = s < n_small ? small_fec : big_fec;
+    ti_first.push_back(r0);
+    ti_count.push_back(nb);
+    r0 += nb;
+    unsigned n = 0;
+    for (int r = 0; r < nb; r++) {
+      int shift;
+      do {
+        unsigned rev = 0;
+        for (int b = 0; b < deg; b++) rev |= ((n >> b) & 1u) << (deg - 1 - b);
+        shift = (int)(rev << 1);
+        n++;
+      } while (shift >= fp.cs);
+      fp.ci_shift.push_back(shift);
+    }
+  }
+  // ---- time interleaver (framemapper:1999-2028): stream position -> TI input position
+  std::vector<int> ti_src(fp.S);
+  if (p.tiblocks != 0) {
+    int s_out = 0;
+    for (size_t b = 0; b < ti_first.size(); b++) {
+      int cols = 5 * ti_count[b], rows = fp.cs / 5, base = ti_first[b] * fp.cs;
+      for (int k = 0; k < rows; k++)
+        for (int w = 0; w < cols; w++) ti_src[s_out++] = base + rows * w + k;
+    }
+  } else {
+    for (int s = 0; s < fp.S; s++) ti_src[s] = s;
+  }
+  // inverse cell interleave: TI input position t -> framemapper input index
+  std::vector<int> perm_inv(fp.cs);
+  for (int w = 0; w < fp.cs; w++) perm_inv[fp.ci_perm[w]] = w;
+
+  // ---- frame vector [L1pre | L1post | data | dummy | zeros] and the P2 zig-zag
+  //      (framemapper:2029-2103): frame_out index -> frame-vector index
+  const int Lp = fp.Lp, M = fp.M;
+  std::vector<int> zz(M);
+  if (fp.N_P2 == 1) {
+    for (int f = 0; f < M; f++) zz[f] = f;
+  } else {
+    int NP = fp.N_P2, CP = fp.C_P2, pre = 1840 / NP, post = Lp / NP, dpart = CP - pre - post;
+    int idx = 0;
+    for (int n = 0; n < NP; n++) {
+      for (int j = 0; j < pre; j++) zz[n * CP + j] = n + j * NP;
+      for (int j = 0; j < post; j++) zz[n * CP + pre + j] = 1840 + n + j * NP;
+      for (int j = 0; j < dpart; j++) zz[n * CP + pre + post + j] = 1840 + Lp + n * dpart + j;
+      idx = (n + 1) * CP;
+    }
+    for (int f = idx, v = 1840 + Lp + NP * dpart; f < M; f++, v++) zz[f] = v;
+  }
+  // ---- frequency interleaver (framemapper:2104-2142), symbol parity restarts per frame
+  std::vector<int> He, Ho, HeP, HoP, HeF, HoF;
+  fi_tables(N, fp.C_DATA, He, Ho);
+  fi_tables(N, fp.C_P2, HeP, HoP);
+  if (fp.N_FC) fi_tables(N, fp.N_FC, HeF, HoF);
+  if ((int)He.size() != fp.C_DATA || (int)HeP.size() != fp.C_P2) return -1;
+  fp.gather_t.assign(M, 0);
+  fp.gather_in.assign(M, 0);
+  const int aux_dummy = AUX_L1PRE + 1840 + Lp;
+  auto resolve = [&](int o, int f) {
+    int v = zz[f];
+    int code_t, code_in;
+    if (v < 1840) code_t = code_in = -(AUX_L1PRE + v) - 1;
+    else if (v < 1840 + Lp) code_t = code_in = -(AUX_L1PRE + v) - 1;
+    else if (v < 1840 + Lp + fp.S) {
+      int t = ti_src[v - 1840 - Lp];
+      int r = t / fp.cs, pos = t % fp.cs;
+      int w = perm_inv[((pos - fp.ci_shift[r]) % fp.cs + fp.cs) % fp.cs];
+      code_t = t;
+      code_in = r * fp.cs + w;
+    } else if (v < 1840 + Lp + fp.S + fp.D) code_t = code_in = -(aux_dummy + (v - 1840 - Lp - fp.S)) - 1;
+    else code_t = code_in = -AUX_ZERO - 1;
+    fp.gather_t[o] = code_t;
+    fp.gather_in[o] = code_in;
+  };
+  int o = 0, base = 0, symbol = 0;
+  for (int j = 0; j < fp.N_P2; j++, symbol++, base += fp.C_P2) {
+    const std::vector<int> &H = symbol % 2 ? HoP : HeP;
+    for (int k = 0; k < fp.C_P2; k++) resolve(o++, base + H[k]);
+  }
+  for (int j = 0; j < fp.num_data_symbols; j++, symbol++, base += fp.C_DATA) {
+    const std::vector<int> &H = symbol % 2 ? Ho : He;
+    for (int k = 0; k < fp.C_DATA; k++) resolve(o++, base + H[k]);
+  }
+  if (fp.N_FC) {
+    const std::vector<int> &H = symbol % 2 ? HoF : HeF;
+    for (int k = 0; k < fp.N_FC; k++) resolve(o++, base + H[k]);
+  }
+
+  // ---- L1 signalling cells
+  int qmod;
+  cf32 l1lut[64];
+  static const int l1c[4] = {0, QPSK, QAM16, QAM64};
+  if (p.l1constellation > 0) qam_table(l1c[p.l1constellation], 0, l1lut, &qmod);
+  bool v131 = p.version == 2, resv = p.reservedbiasbits && v131;
+  fp.aux_len = AUX_L1PRE + 1840 + Lp + fp.D;
+  fp.aux.assign((size_t)fp.t2frames * fp.aux_len, cf32{0.f, 0.f});
+  // L1-pre (framemapper:1366-1534): BPSK, shortened/punctured LDPC(16200) 1/4
+  std::vector<cf32> pre(1840);
+  {
+    Bits b;
+    b.put(0, 8); b.put(p.carriermode, 1); b.put(p.preamble, 3); b.put(p.fftsize & 7, 3); b.put(0, 1);
+    b.put(0, 1); b.put(p.guardinterval, 3); b.put(p.paprmode, 4); b.put(p.l1constellation, 4);
+    b.put(0, 2); b.put(0, 2); b.put(fp.N_post / fp.eta, 18); b.put(KSIG_POST - 32, 18);
+    b.put(p.pilotpattern, 4); b.put(0, 8); b.put(0, 16); b.put(0x3085, 16); b.put(0x8001, 16);
+    b.put(p.t2frames, 8); b.put(p.numdatasyms, 12); b.put(0, 3); b.put(0, 1); b.put(1, 3); b.put(0, 3);
+    b.put(p.version, 4); b.put(v131 ? p.l1scrambled : 0, 1); b.put(0, 1); b.put(resv ? 0xf : 0, 4);
+    b.put(crc32_mpeg2(b.b), 32);
+    std::vector<uint8_t> cw(kShort, 0);
+    std::copy(b.b.begin(), b.b.end(), cw.begin());
+    l1_encode(cw, KBCH14, NBCH14, 100);
+    std::vector<uint8_t> punct(kShort - NBCH14, 0);
+    for (int cgrp = 0; cgrp < 32; cgrp++) {
+      int cnt = cgrp < 31 ? 360 : 328;
+      for (int c2 = 0; c2 < cnt; c2++) punct[c2 * 36 + T2_L1_PRE_PUNCTURE[cgrp]] = 1;
+    }
+    int k = 0;
+    auto bpsk = [](uint8_t x) { return cf32{x ? -1.0f : 1.0f, 0.0f}; };
+    for (int w = 0; w < 200; w++) pre[k++] = bpsk(cw[w]);
+    for (int w = 0; w < 168; w++) pre[k++] = bpsk(cw[KBCH14 + w]);
+    for (int w = 0; w < kShort - NBCH14; w++)
+      if (!punct[w]) pre[k++] = bpsk(cw[NBCH14 + w]);
+    if (k != 1840) return -1;
+  }
+  // L1-post (framemapper:1536-1910) for every FRAME_IDX value
+  std::vector<uint8_t> l1rand(KBCH12);
+  prbs15(l1rand.data(), KBCH12);
+  const uint8_t *pad = p.l1constellation == 2 ? T2_L1_POST_PADDING_16QAM
+                     : p.l1constellation == 3 ? T2_L1_POST_PADDING_64QAM : T2_L1_POST_PADDING_BQPSK;
+  const uint8_t *pun = p.l1constellation == 2 ? T2_L1_POST_PUNCTURE_16QAM
+                     : p.l1constellation == 3 ? T2_L1_POST_PUNCTURE_64QAM : T2_L1_POST_PUNCTURE_BQPSK;
+  std::vector<uint8_t> dummybits(fp.D > 0 ? fp.D : 1);
+  prbs15(dummybits.data(), (int)dummybits.size());
+  for (int v = 0; v < fp.t2frames; v++) {
+    Bits b;
+    b.put(1, 15); b.put(1, 8); b.put(0, 4); b.put(0, 8); b.put(0, 3); b.put(729833333u, 32);
+    b.put(0, 8); b.put(1, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3); b.put(0, 8); b.put(1, 8);
+    b.put(p.rate, 3); b.put(p.constellation, 3); b.put(p.rotation, 1); b.put(p.framesize, 2);
+    b.put(p.fecblocks, 10); b.put(1, 8); b.put(p.tiblocks, 8); b.put(0, 1); b.put(0, 1);
+    b.put((p.inband && v131) ? 1 : 0, 1); b.put(resv ? 0x7ff : 0, 11);
+    b.put(p.version == 0 ? 0 : p.inputmode + 1, 2); b.put(0, 1); b.put(0, 1); b.put(0, 2);
+    b.put(resv ? 0x3fffffff : 0, 30); b.put(v, 8); b.put(0, 22); b.put(0, 22); b.put(0, 8);
+    b.put(0, 3); b.put(resv ? 0xff : 0, 8); b.put(0, 8); b.put(0, 22); b.put(p.fecblocks, 10);
+    b.put(resv ? 0xff : 0, 8); b.put(resv ? 0xff : 0, 8);
+    b.put(crc32_mpeg2(b.b), 32);
+    int nsig = (int)b.b.size();
+    if (v131 && p.l1scrambled)
+      for (int i = 0; i < nsig; i++) b.b[i] ^= l1rand[i];
+    // shortening: groups in padding order, partial group filled from its end
+    std::vector<uint8_t> shortened(KBCH12, 0);
+    int m, last;
+    if (nsig <= 360) { m = 19; last = 360 - nsig; }
+    else { m = (KBCH12 - nsig) / 360; last = KBCH12 - nsig - 360 * m; }
+    for (int n = 0; n < m; n++) {
+      int len = pad[n] == 19 ? 192 : 360;
+      for (int w = 0; w < len; w++) shortened[pad[n] * 360 + w] = 1;
+    }
+    int gl = pad[m] == 19 ? 192 : 360;
+    for (int w = 0; w < last; w++) shortened[pad[m] * 360 + gl - last + w] = 1;
+    std::vector<uint8_t> cw(kShort, 0);
+    for (int n = 0, i = 0; n < KBCH12; n++) cw[n] = shortened[n] ? 0 : b.b[i++];
+    l1_encode(cw, KBCH12, NBCH12, 101);
+    std::vector<uint8_t> punct(kShort - NBCH12, 0);
+    for (int cg = 0; cg <= fp.N_punc / 360; cg++) {
+      int cnt = cg < fp.N_punc / 360 ? 360 : fp.N_punc % 360;
+      for (int c2 = 0; c2 < cnt; c2++) punct[c2 * 25 + pun[cg]] = 1;
+    }
+    std::vector<uint8_t> post;
+    for (int w = 0; w < KBCH12; w++) if (!shortened[w]) post.push_back(cw[w]);
+    for (int w = 0; w < 168; w++) post.push_back(cw[KBCH12 + w]);
+    for (int w = 0; w < kShort - NBCH12; w++) if (!punct[w]) post.push_back(cw[NBCH12 + w]);
+    if ((int)post.size() != fp.N_post) return -1;
+    cf32 *dst = &fp.aux[(size_t)v * fp.aux_len + AUX_L1PRE + 1840];
+    int produced = 0;
+    if (p.l1constellation == 0) {
+      for (int d = 0; d < fp.N_post; d++) dst[produced++] = cf32{post[d] ? -1.0f : 1.0f, 0.0f};
+    } else if (p.l1constellation == 1) {
+      for (int d = 0; d < fp.N_post / 2; d++) dst[produced++] = l1lut[(post[2 * d] << 1) | post[2 * d + 1]];
+    } else {
+      // column-row bit interleaver then demux by source index (framemapper:1832-1908)
+      int ncols = p.l1constellation == 2 ? 8 : 12, rows = fp.N_post / ncols, half = ncols / 2;
+      const uint8_t *mux = p.l1constellation == 2 ? T2_L1_MUX16 : T2_L1_MUX64;
+      for (int k = 0; k < rows; k++) {
+        int pack = 0;
+        for (int e = 0; e < ncols; e++) pack = (pack << 1) | post[rows * mux[e] + k];
+        dst[produced++] = l1lut[pack >> half];
+        dst[produced++] = l1lut[pack & ((1 << half) - 1)];
+      }
+    }
+    if (produced != Lp) return -1;
+    cf32 *row = &fp.aux[(size_t)v * fp.aux_len];
+    std::copy(pre.begin(), pre.end(), row + AUX_L1PRE);
+    for (int i = 0; i < fp.D; i++) row[aux_dummy + i] = cf32{dummybits[i] ? -1.0f : 1.0f, 0.0f};
+  }
+  return 0;
+}
+
+// ============================================================================ pilots + OFDM
+namespace {
+enum CarrierKind : uint8_t { K_DATA = 0, K_ZERO, K_P2, K_P2INV, K_SP, K_SPINV, K_CP, K_CPINV };
+
+const uint16_t *reserved_tones(int N, bool tr, int *n) {
+  switch (N) {
+    case 1024: *n = 10; return tr ? T2_TR_PAPR_MAP_1K : T2_P2_PAPR_MAP_1K;
+    case 2048: *n = 18; return tr ? T2_TR_PAPR_MAP_2K : T2_P2_PAPR_MAP_2K;
+    case 4096: *n = 36; return tr ? T2_TR_PAPR_MAP_4K : T2_P2_PAPR_MAP_4K;
+    case 8192: *n = 72; return tr ? T2_TR_PAPR_MAP_8K : T2_P2_PAPR_MAP_8K;
+    case 16384: *n = 144; return tr ? T2_TR_PAPR_MAP_16K : T2_P2_PAPR_MAP_16K;
+    default: *n = 288; return tr ? T2_TR_PAPR_MAP_32K : T2_P2_PAPR_MAP_32K;
+  }
+}
+
+// complex IDFT in double (radix-2, unnormalised, e^{+j})
+void idft_double(std::vector<double> &re, std::vector<double> &im) {
+  size_t n = re.size();
+  for (size_t i = 1, j = 0; i < n; i++) {
+    size_t bit = n >> 1;
+    for (; j & bit; bit >>= 1) j ^= bit;
+    j ^= bit;
+    if (i < j) { std::swap(re[i], re[j]); std::swap(im[i], im[j]); }
+  }
+  for (size_t len = 2; len <= n; len <<= 1) {
+    for (size_t i = 0; i < n; i += len)
+      for (size_t k = 0; k < len / 2; k++) {
+        double a = 2.0 * M_PI * (double)k / (double)len, wr = std::cos(a), wi = std::sin(a);
+        double br = re[i + k + len / 2], bi = im[i + k + len / 2];
+        double tr = br * wr - bi * wi, ti = br * wi + bi * wr;
+        re[i + k + len / 2] = re[i + k] - tr; im[i + k + len / 2] = im[i + k] - ti;
+        re[i + k] += tr; im[i + k] += ti;
+      }
+  }
+}
+}  // namespace
+
+int build_pilot(const PgParams &p, PilotPlan &pp) {
+  pp.fft = fft_points(p.fftsize);
+  if (!pp.fft || p.vlength != pp.fft || p.numdatasyms < 1) return -1;
+  const int N = pp.N = p.vlength;
+  Counts c;
+  if (!active_counts(p.fftsize, p.carriermode, p.pilotpattern, p.paprmode, p.guardinterval, p.preamble, c))
+    return -1;
+  if (!c.c_data) return -1;
+  bool miso = !(p.preamble == 0 || p.preamble == 3);
+  bool tx2 = miso && p.misogroup == 1;
+  bool ext = p.carriermode == 1 && N >= 8192;
+  pp.N_P2 = c.n_p2;
+  // carriers (pilotgen:120-175)
+  switch (N) {
+    case 1024: pp.C_PS = 853; break;
+    case 2048: pp.C_PS = 1705; break;
+    case 4096: pp.C_PS = 3409; break;
+    case 8192: pp.C_PS = ext ? 6913 : 6817; break;
+    case 16384: pp.C_PS = ext ? 13921 : 13633; break;
+    default: pp.C_PS = ext ? 27841 : 27265; break;
+  }
+  int kx = N == 8192 ? 48 : N == 16384 ? 144 : N == 32768 ? 288 : 0;   // extended-carrier count
+  pp.K_EXT = ext ? kx : 0;
+  pp.K_OFFSET = ext ? 0 : kx;
+  const int C_PS = pp.C_PS, K_EXT = pp.K_EXT;
+  static const int dxs[8] = {3, 6, 6, 12, 12, 24, 24, 6}, dys[8] = {4, 2, 4, 2, 4, 2, 4, 16};
+  const int dx = dxs[p.pilotpattern], dy = dys[p.pilotpattern];
+  // pilot amplitudes (pilotgen:748-992, 1083-1094): values built in double, stored float
+  double a_p2 = (N == 32768 && !miso) ? std::sqrt(37.0) / 5.0 : std::sqrt(31.0) / 5.0;
+  double a_cp = N <= 2048 ? 4.0 / 3.0 : N == 4096 ? (4.0 * std::sqrt(2.0)) / 3.0 : 8.0 / 3.0;
+  static const double a_sp_t[8] = {4.0 / 3.0, 4.0 / 3.0, 7.0 / 4.0, 7.0 / 4.0, 7.0 / 3.0, 7.0 / 3.0, 7.0 / 3.0, 7.0 / 3.0};
+  double amps[3] = {a_p2, a_sp_t[p.pilotpattern], a_cp};
+  for (int t = 0; t < 3; t++) {
+    float pos = (float)amps[t], neg = (float)-amps[t];
+    pp.pilot_values[4 * t + 0] = cf32{pos, 0.f};   // normal, prbs^pn = 0
+    pp.pilot_values[4 * t + 1] = cf32{neg, 0.f};   // normal, 1
+    pp.pilot_values[4 * t + 2] = cf32{neg, 0.f};   // inverted, 0
+    pp.pilot_values[4 * t + 3] = cf32{pos, 0.f};   // inverted, 1
+  }
+  // reference PRBS w_k (pilotgen:1245-1258) and PN sequence
+  std::vector<uint8_t> prbs(27841);
+  {
+    unsigned s = 0x7ff;
+    for (int i = 0; i < 27841; i++) {
+      prbs[i] = s & 1;
+      unsigned b = (s ^ (s >> 2)) & 1;
+      s = (s >> 1) | (b << 10);
+    }
+  }
+  auto pn = [](int j) { return (T2_PN_SEQ_BYTES[j >> 3] >> (7 - (j & 7))) & 1; };
+
+  // --- carrier maps
+  std::vector<uint8_t> p2(C_PS, K_DATA), fc(C_PS, K_DATA);
+  auto p2kind = [&](int i) { return (tx2 && ((i / 3) % 2) && (i % 3 == 0)) ? K_P2INV : K_P2; };
+  int step = (N == 32768 && !miso) ? 6 : 3;
+  for (int i = 0; i < C_PS; i += step) p2[i] = tx2 ? p2kind(i) : K_P2;
+  if (ext)
+    for (int i = 0; i < K_EXT; i++) {
+      p2[i] = tx2 ? p2kind(i) : K_P2;
+      int k = i + C_PS - K_EXT;
+      p2[k] = tx2 ? p2kind(k) : K_P2;
+    }
+  if (miso) p2[K_EXT + 1] = p2[K_EXT + 2] = p2[C_PS - K_EXT - 2] = p2[C_PS - K_EXT - 3] = K_P2;
+  {
+    int nres;
+    const uint16_t *res = reserved_tones(N, false, &nres);
+    int koff = N >= 8192 ? K_EXT : 0;
+    for (int i = 0; i < nres; i++) p2[res[i] + koff] = K_ZERO;
+    if (miso)
+      for (int i = 0; i < nres; i++) {
+        int ki = res[i] + K_EXT;
+        bool up = (ki % 3) == 1 && (i == nres - 1 || ki + 1 != res[i + 1] + K_EXT);
+        bool dn = (ki % 3) == 2 && (i == 0 || ki - 1 != res[i - 1] + K_EXT);
+        if (up) p2[ki + 1] = K_P2;
+        if (dn) p2[ki - 1] = K_P2;
+      }
+  }
+  for (int i = 0; i < C_PS; i += dx) fc[i] = (tx2 && ((i / dx) % 2)) ? K_SPINV : K_SP;
+  if ((N == 1024 && (p.pilotpattern == PP4 || p.pilotpattern == PP5)) || (N == 2048 && p.pilotpattern == PP7))
+    fc[C_PS - 2] = K_SP;
+  fc[0] = fc[C_PS - 1] = (tx2 && ((p.numdatasyms + pp.N_P2 - 1) % 2)) ? K_SPINV : K_SP;
+  if (p.paprmode == PAPRTR || p.paprmode == PAPRBOTH) {
+    int nres;
+    const uint16_t *res = reserved_tones(N, false, &nres);
+    int koff = N >= 8192 ? K_EXT : 0;
+    for (int i = 0; i < nres; i++) fc[res[i] + koff] = K_ZERO;
+  }
+  // data-symbol maps, one per symbol phase (symbol mod dy) (init_pilots, pilotgen:1285-2782)
+  std::vector<std::vector<uint8_t>> dmap(dy, std::vector<uint8_t>(C_PS, K_DATA));
+  for (int ph = 0; ph < dy; ph++) {
+    std::vector<uint8_t> &m = dmap[ph];
+    for (int s = 0; s < T2_NCP_STEPS; s++) {
+      const t2_cp_step_t &st = T2_CP_STEPS[s];
+      if (st.fft != N || st.pp != p.pilotpattern + 1 || (st.ext_only && p.carriermode != 1)) continue;
+      const uint16_t *list = T2_CP_LIST + T2_CP_LIST_SPAN[st.list][0];
+      for (int i = 0; i < st.count; i++) {
+        int k = st.modulus ? list[i] % st.modulus : list[i];
+        m[k] = (st.miso_inv && tx2 && ((k / dx) % 2) && (k % dx) == 0) ? K_CPINV : K_CP;
+      }
+    }
+    for (int i = 0; i < C_PS; i++) {
+      int rem = ((i - K_EXT) % (dx * dy) + dx * dy) % (dx * dy);
+      if (rem == dx * (ph % dy)) m[i] = (tx2 && ((i / dx) % 2)) ? K_SPINV : K_SP;
+    }
+    m[0] = m[C_PS - 1] = (tx2 && (ph % 2)) ? K_SPINV : K_SP;
+    if (p.paprmode == PAPRTR || p.paprmode == PAPRBOTH) {
+      int shift = p.carriermode == 0 ? dx * (ph % dy) : dx * ((ph + K_EXT / dx) % dy);
+      int nres;
+      const uint16_t *res = reserved_tones(N, true, &nres);
+      for (int i = 0; i < nres; i++) m[res[i] + shift] = K_ZERO;
+    }
+  }
+  pp.Nsym = p.numdatasyms + pp.N_P2;
+  pp.active = c.n_fc ? pp.N_P2 * c.c_p2 + (p.numdatasyms - 1) * c.c_data + c.n_fc
+                     : pp.N_P2 * c.c_p2 + p.numdatasyms * c.c_data;
+  pp.left_nulls = (N - C_PS) / 2 + 1;
+  // --- per-symbol gather maps, indexed by IFFT input position k (bin n = (k + N/2) mod N)
+  pp.bin_map.assign((size_t)pp.Nsym * N, -AUX_ZERO - 1);
+  int consumed = 0;
+  for (int j = 0; j < pp.Nsym; j++) {
+    const uint8_t *m = j < pp.N_P2 ? p2.data()
+                     : (c.n_fc && j == pp.Nsym - 1) ? fc.data() : dmap[j % dy].data();
+    int32_t *row = &pp.bin_map[(size_t)j * N];
+    int pnj = pn(j);
+    for (int cc = 0; cc < C_PS; cc++) {
+      int n = pp.left_nulls + cc;
+      int k = (n + N / 2) % N;
+      int b = prbs[cc + pp.K_OFFSET] ^ pnj;
+      int code;
+      switch (m[cc]) {
+        case K_DATA: code = consumed++; break;
+        case K_ZERO: code = -AUX_ZERO - 1; break;
+        case K_P2: code = -(AUX_PILOT0 + 0 + b) - 1; break;
+        case K_P2INV: code = -(AUX_PILOT0 + 2 + b) - 1; break;
+        case K_SP: code = -(AUX_PILOT0 + 4 + b) - 1; break;
+        case K_SPINV: code = -(AUX_PILOT0 + 6 + b) - 1; break;
+        case K_CP: code = -(AUX_PILOT0 + 8 + b) - 1; break;
+        default: code = -(AUX_PILOT0 + 10 + b) - 1; break;
+      }
+      row[k] = code;
+    }
+  }
+  if (consumed != pp.active) return -1;   // carrier maps must agree with C_P2/C_DATA/N_FC
+  switch (p.guardinterval) {
+    case GI132: pp.G = N / 32; break;
+    case GI116: pp.G = N / 16; break;
+    case GI18: pp.G = N / 8; break;
+    case GI14: pp.G = N / 4; break;
+    case GI1128: pp.G = N / 128; break;
+    case GI19128: pp.G = (N * 19) / 128; break;
+    case GI19256: pp.G = (N * 19) / 256; break;
+    default: return -1;
+  }
+  pp.normalization = (float)(5.0 / std::sqrt(27.0 * C_PS));
+  // --- P1 (pilotgen:1119-1178): DBPSK over 384 carriers, MSS from S1/S2, scrambled
+  {
+    int s1 = p.preamble, s2 = (p.fftsize & 7) << 1;
+    std::vector<int> seq;
+    for (int i = 0; i < 8; i++) for (int j = 7; j >= 0; j--) seq.push_back((T2_P1_S1[s1][i] >> j) & 1);
+    for (int i = 0; i < 32; i++) for (int j = 7; j >= 0; j--) seq.push_back((T2_P1_S2[s2][i] >> j) & 1);
+    for (int i = 0; i < 8; i++) for (int j = 7; j >= 0; j--) seq.push_back((T2_P1_S1[s1][i] >> j) & 1);
+    std::vector<double> fr(1024, 0.0);
+    int prev = 1;
+    unsigned sr = 0x4e46;
+    for (int i = 0; i < 384; i++) {
+      int cur = seq[i] ? -prev : prev;
+      prev = cur;
+      unsigned b = (sr ^ (sr >> 1)) & 1;
+      sr = (sr >> 1) | (b << 14);
+      fr[T2_P1_CARRIERS[i] + 86] = cur * (b ? -1.0 : 1.0);
+    }
+    pp.p1.assign(2048, cf32{0.f, 0.f});
+    float inv = (float)std::sqrt(384.0);
+    std::vector<cf32> t0(1024), t1(1024);
+    for (int pass = 0; pass < 2; pass++) {
+      std::vector<double> re(1024), im(1024, 0.0);
+      for (int i = 0; i < 1024; i++) {
+        int src = (i + 512) % 1024;                    // fftshift
+        re[i] = pass == 0 ? fr[src] : fr[(src + 1023) % 1024];   // 1-bin shifted copy
+      }
+      idft_double(re, im);
+      std::vector<cf32> &t = pass == 0 ? t0 : t1;
+      for (int i = 0; i < 1024; i++) t[i] = cf32{(float)re[i] / inv, (float)im[i] / inv};
+    }
+    int k = 0;
+    for (int j = 0; j < 542; j++) pp.p1[k++] = t1[j];
+    for (int j = 0; j < 1024; j++) pp.p1[k++] = t0[j];
+    for (int j = 542; j < 1024; j++) pp.p1[k++] = t1[j];
+  }
+  // --- inverse-sinc equaliser (pilotgen:1179-1219)
+  pp.eq = p.equalization ? 1 : 0;
+  if (pp.eq) {
+    static const double fss[6] = {131.0 * 1000000.0 / 71.0, 5.0 * 8000000.0 / 7.0, 6.0 * 8000000.0 / 7.0,
+                                  7.0 * 8000000.0 / 7.0, 8.0 * 8000000.0 / 7.0, 10.0 * 8000000.0 / 7.0};
+    double fs = (p.bandwidth >= 0 && p.bandwidth < 6) ? fss[p.bandwidth] : 1.0;
+    double fstep = fs / N, f = 0.0, rms = 0.0;
+    pp.isinc.assign(N, 0.f);
+    for (int i = 0; i < N / 2; i++) {
+      double x = M_PI * f / fs, sinc = i == 0 ? 1.0 : std::sin(x) / x;
+      rms += sinc * sinc;
+      pp.isinc[i + N / 2] = pp.isinc[N / 2 - i - 1] = (float)(1.0 / sinc);
+      f = f + fstep;
+    }
+    float r = (float)std::sqrt(rms / (N / 2));
+    for (int i = 0; i < N; i++) pp.isinc[i] *= r;
+  }
+  pp.twiddle.resize(N);
+  for (int e = 0; e < N; e++) {
+    double a = 2.0 * M_PI * (double)e / (double)N;
+    pp.twiddle[e] = cf32{(float)std::cos(a), (float)std::sin(a)};
+  }
+  return 0;
+}
+
+}  // namespace t2

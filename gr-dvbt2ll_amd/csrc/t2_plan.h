@@ -1,0 +1,96 @@
+// t2_plan.h -- configuration-time planning for the MI355X DVB-T2 chain.
+//
+// Everything the reference blocks compute in their constructors (FEC parameters, BCH
+// generator, LDPC address tables, QAM tables, cell/frequency interleaver permutations,
+// L1 signalling cells, pilot carrier maps, P1) is computed once here on the host and
+// turned into the compact device-side tables the kernels consume:
+//   * FecPlan   -> bit-packed BCH (byte table + Horner matrices) and a quasi-cyclic LDPC
+//                  schedule (row a of the q x 360 parity array <- rotated info groups)
+//   * MapPlan   -> bit-interleaver geometry + constellation LUT
+//   * FramePlan -> cell interleaver shifts/permutation and a gather map from every mapped
+//                  (frequency-interleaved) cell to its source cell / L1 / dummy entry
+//   * PilotPlan -> per-symbol gather map from every IFFT input bin to a source cell,
+//                  pilot value or zero; P1 samples; twiddles
+// Reference constructors: lib/bbheaderbch_bb_impl.cc:42-196, lib/interleavermod_bc_impl.cc:42-255,
+// lib/framemapperfint_cc_impl.cc:41-1190, lib/pilotgenp1insert_cc_impl.cc:43-1229.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace t2 {
+
+struct cf32 {
+  float re, im;
+};
+
+// ----------------------------------------------------------------------------- FEC
+struct FecPlan {
+  int normal = 0, rate = 0;
+  int kbch = 0, nbch = 0, nparity = 0, nldpc = 0, q = 0, pbits = 0;
+  bool parity_interleave = true;      // tempu carries parity in [a][c] (interleaved) order
+  int bch_chunk = 0;                  // message bytes per lane chunk (256 lanes)
+  std::vector<uint64_t> bch_tab;      // 256 x 3 words: d(x) * x^P mod g(x)
+  std::vector<uint64_t> bch_m1;       // 192 rows x 3 words: v -> v * x^(8*chunk) mod g
+  std::vector<uint64_t> bch_m2;       // 192 rows x 3 words: v -> v * x^(8*chunk*64) mod g
+  std::vector<uint16_t> ldpc_rowptr;  // q + 1
+  std::vector<uint32_t> ldpc_ent;     // (group << 16) | rotation, grouped by parity row
+  std::vector<uint8_t> prbs_bytes;    // BB scrambler, kbch/8 bytes
+  std::vector<uint8_t> crc8_tab;      // CRC-8 (0xD5) table, 256
+  std::vector<uint8_t> crc8_shift;    // 8 x 256: crc after appending k zero bytes (packet CRC combine)
+};
+int build_fec(int framesize, int rate, int constellation, FecPlan &fp);
+
+// ----------------------------------------------------------------------------- bit interleave + map
+enum MapMode { MAP_PAIRS = 0, MAP_TWIST2 = 1, MAP_TWIST1 = 2 };
+struct MapPlan {
+  int mode = 0, mod = 0, W = 0, R = 0, cs = 0, nldpc = 0, rotation = 0;
+  uint8_t twist[16] = {0}, mux[16] = {0};
+  cf32 lut[256] = {};
+};
+int build_map(int framesize, int rate, int constellation, int rotation, MapPlan &mp);
+// reference QAM tables (used for data cells and L1-post cells)
+void qam_table(int constellation, int rotation, cf32 *lut, int *mod);
+
+// ----------------------------------------------------------------------------- frame mapper
+struct FmParams {
+  int framesize, rate, constellation, rotation, fecblocks, tiblocks, carriermode, fftsize,
+      guardinterval, l1constellation, pilotpattern, t2frames, numdatasyms, paprmode, version,
+      preamble, inputmode, reservedbiasbits, l1scrambled, inband;
+};
+// aux table (per t2_frame_num variant): [0] zero, [1..12] pilot values, then L1-pre,
+// L1-post, dummy cells.  Gather codes: >= 0 cell index, < 0 -> aux index (-code - 1).
+constexpr int AUX_ZERO = 0;
+constexpr int AUX_PILOT0 = 1;
+constexpr int AUX_L1PRE = 13;
+struct FramePlan {
+  int cs = 0, F = 0, S = 0, M = 0, N_P2 = 0, C_P2 = 0, C_DATA = 0, N_FC = 0, C_FC = 0;
+  int eta = 0, N_post = 0, N_punc = 0, Lp = 0, D = 0, num_data_symbols = 0, t2frames = 0;
+  int aux_len = 0;                       // entries per variant
+  std::vector<int16_t> ci_perm;          // cs
+  std::vector<int32_t> ci_shift;         // F (per FEC block of a frame)
+  std::vector<int32_t> gather_t;         // M: mapped cell -> time-interleaver-input index | aux
+  std::vector<int32_t> gather_in;        // M: mapped cell -> framemapper input index | aux
+  std::vector<cf32> aux;                 // t2frames x aux_len
+};
+int build_frame(const FmParams &p, FramePlan &fp);
+
+// ----------------------------------------------------------------------------- pilots + OFDM
+struct PgParams {
+  int carriermode, fftsize, pilotpattern, guardinterval, numdatasyms, paprmode, version, preamble,
+      misogroup, equalization, bandwidth, vlength;
+};
+struct PilotPlan {
+  int N = 0, fft = 0, C_PS = 0, K_EXT = 0, K_OFFSET = 0, G = 0, Nsym = 0, N_P2 = 0, active = 0;
+  int left_nulls = 0, eq = 0;
+  float normalization = 0.f;
+  cf32 pilot_values[12] = {};            // aux[1..12]
+  std::vector<int32_t> bin_map;          // Nsym x N, indexed by IFFT input position k (fftshifted)
+  std::vector<float> isinc;              // N (pre-shift bin order), only if eq
+  std::vector<cf32> p1;                  // 2048
+  std::vector<cf32> twiddle;             // N: exp(+2 pi i e / N)
+};
+int build_pilot(const PgParams &p, PilotPlan &pp);
+
+int fft_points(int fftsize);
+
+}  // namespace t2

@@ -1,0 +1,76 @@
+"""Fused TS -> IQ chain (dvbt2ll_chain_* in include/dvbt2ll_hip.h).
+
+Equivalent to bbheaderbch_bb -> ldpc_bb -> interleavermod_bc -> framemapperfint_cc ->
+pilotgenp1insert_cc for whole T2 frames, with device-resident buffers.  Frame k of the
+stream is encoded with the state the reference blocks would hold at that point, so frames
+(and therefore GPUs) can be processed independently.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import lib, check, _ChainParams, _ChainInfo, _FmParams
+from .configs import ts_for_frames
+
+
+class Chain:
+    def __init__(self, cfg, max_frames=1, device=0):
+        self.cfg = cfg
+        fm = _FmParams(*[int(v) for v in cfg.fm_args()])
+        p = _ChainParams(fm, int(cfg.misogroup), int(cfg.equalization), int(cfg.bandwidth), int(max_frames))
+        h = ctypes.c_void_p()
+        self._h = None
+        check(lib().dvbt2ll_chain_create(ctypes.byref(p), int(device), ctypes.byref(h)), "chain create")
+        self._h = h
+        self.max_frames = max_frames
+        info = _ChainInfo()
+        check(lib().dvbt2ll_chain_get_info(self._h, ctypes.byref(info)), "chain info")
+        self.info = {f: getattr(info, f) for f, _ in _ChainInfo._fields_}
+
+    @property
+    def iq_per_frame(self):
+        return self.info["iq_samples_per_frame"]
+
+    def run_device(self, ts_ptr, ts_base, ts_len, first_frame, nframes, iq_ptr, stream=0):
+        check(lib().dvbt2ll_chain_run_device(self._h, ctypes.c_void_p(ts_ptr), int(ts_base), int(ts_len),
+                                             int(first_frame), int(nframes), ctypes.c_void_p(iq_ptr),
+                                             ctypes.c_void_p(stream or None)), "chain run")
+
+    def run(self, first_frame, nframes, ts=None, ts_base=None, seed=1):
+        """host convenience: synthetic TS (or the given buffer) -> IQ numpy array"""
+        if ts is None:
+            ts, ts_base = ts_for_frames(self.cfg, first_frame, nframes, seed)
+        ts = np.ascontiguousarray(ts, np.uint8)
+        iq = np.zeros(nframes * self.iq_per_frame, np.complex64)
+        check(lib().dvbt2ll_chain_run_host(self._h, ts.ctypes.data_as(ctypes.c_void_p), int(ts_base), len(ts),
+                                           int(first_frame), int(nframes), iq.ctypes.data_as(ctypes.c_void_p)),
+              "chain run")
+        return iq
+
+    def set_timing(self, enable):
+        check(lib().dvbt2ll_chain_set_timing(self._h, int(bool(enable))), "timing")
+
+    def timing(self):
+        ms = (ctypes.c_double * 3)()
+        n = (ctypes.c_int64 * 3)()
+        check(lib().dvbt2ll_chain_get_timing(self._h, ms, n, 3), "timing")
+        return list(ms), list(n)
+
+    def debug_codewords(self, nblocks):
+        stride = self.info["cw_stride_bytes"]
+        out = np.zeros(nblocks * stride, np.uint8)
+        check(lib().dvbt2ll_chain_debug_codewords(self._h, out.ctypes.data_as(ctypes.c_void_p), len(out)), "cw")
+        return out.reshape(nblocks, stride)
+
+    def debug_cells(self, ncells):
+        out = np.zeros(ncells, np.complex64)
+        check(lib().dvbt2ll_chain_debug_cells(self._h, out.ctypes.data_as(ctypes.c_void_p), ncells), "cells")
+        return out
+
+    def synchronize(self):
+        check(lib().dvbt2ll_chain_synchronize(self._h), "sync")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().dvbt2ll_chain_destroy(self._h)
+            self._h = None

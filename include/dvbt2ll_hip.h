@@ -1,0 +1,185 @@
+/*
+ * dvbt2ll_hip.h -- C ABI of the MI355X-native DVB-T2 transmit chain.
+ *
+ * Drop-in boundary for the four gr-dvbt2ll blocks (plus the gr-dtv LDPC block the
+ * shipped flowgraph places between bbheaderbch and interleavermod).  Each block is an
+ * opaque handle that reproduces the reference gr::block contract:
+ *
+ *   make()            -> dvbt2ll_<blk>_create()      (reference include/dvbt2ll/<blk>.h:49)
+ *   set_output_multiple -> dvbt2ll_<blk>_output_multiple()
+ *   forecast()        -> dvbt2ll_<blk>_forecast()
+ *   general_work()    -> dvbt2ll_<blk>_general_work() (+ consume_each via *consumed)
+ *
+ * Buffers passed to general_work are HOST buffers owned by the caller (GNU Radio
+ * circular buffers); the call is synchronous and retains no pointer.  Handles own
+ * their device memory and one HIP stream.  Instances are independent; one instance
+ * must not be called from two threads at once (GNU Radio never does).
+ *
+ * The fused chain (dvbt2ll_chain_*) runs TS bytes -> IQ for whole T2 frames with
+ * device-resident buffers; it is what bench.py measures.
+ *
+ * Enum arguments use the reference's numeric values (include/dvbt2ll/dvbt2ll_config.h:60-202).
+ * Errors: the reference throws std::bad_alloc from constructors and silently accepts
+ * invalid parameter combinations; this ABI returns negative status codes instead.
+ */
+#ifndef DVBT2LL_HIP_H
+#define DVBT2LL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DVBT2LL_OK 0
+#define DVBT2LL_EINVAL (-1)   /* invalid parameter combination                       */
+#define DVBT2LL_ENOMEM (-2)   /* device/host allocation failed (reference: bad_alloc) */
+#define DVBT2LL_EDEVICE (-3)  /* HIP runtime / kernel launch error                     */
+#define DVBT2LL_ESHORT (-4)   /* fewer input items than forecast() requires            */
+
+const char *dvbt2ll_strerror(int status);
+const char *dvbt2ll_version(void);
+/* number of visible HIP devices (0 when no GPU) -- never initialises a context */
+int dvbt2ll_device_count(void);
+
+/* ---------------------------------------------------------------------------
+ * bbheaderbch_bb: TS bytes -> BBFRAME + BCH, one unpacked bit per output byte.
+ * Replaces gr::dvbt2ll::bbheaderbch_bb::make(framesize, rate, mode, inband, fecblocks,
+ * tsrate) (include/dvbt2ll/bbheaderbch_bb.h:49; lib/bbheaderbch_bb_impl.cc:32-37).
+ * ------------------------------------------------------------------------- */
+typedef struct dvbt2ll_bbheaderbch dvbt2ll_bbheaderbch;
+typedef struct {
+  int framesize, rate, mode, inband, fecblocks, tsrate;
+} dvbt2ll_bbheaderbch_params;
+int dvbt2ll_bbheaderbch_create(const dvbt2ll_bbheaderbch_params *p, int device, dvbt2ll_bbheaderbch **out);
+int dvbt2ll_bbheaderbch_output_multiple(const dvbt2ll_bbheaderbch *h);             /* nbch (impl.cc:195) */
+int dvbt2ll_bbheaderbch_forecast(const dvbt2ll_bbheaderbch *h, int noutput_items, int *ninput_items_required);
+int dvbt2ll_bbheaderbch_general_work(dvbt2ll_bbheaderbch *h, int noutput_items, int ninput_items,
+                                     const void *in, void *out, int *consumed);
+void dvbt2ll_bbheaderbch_destroy(dvbt2ll_bbheaderbch *h);
+
+/* ---------------------------------------------------------------------------
+ * ldpc_bb: nbch unpacked bits -> nldpc unpacked bits (natural parity order).
+ * Replaces gr-dtv dvb_ldpc_bb(standard=DVBT2, framesize, rate, MOD_OTHER) as wired in
+ * apps/vv009-4kshort.grc:386-460; arithmetic = lib/bbheaderbch_bb_impl.cc:533-646.
+ * ------------------------------------------------------------------------- */
+typedef struct dvbt2ll_ldpc dvbt2ll_ldpc;
+typedef struct {
+  int framesize, rate;
+} dvbt2ll_ldpc_params;
+int dvbt2ll_ldpc_create(const dvbt2ll_ldpc_params *p, int device, dvbt2ll_ldpc **out);
+int dvbt2ll_ldpc_output_multiple(const dvbt2ll_ldpc *h);                           /* nldpc */
+int dvbt2ll_ldpc_forecast(const dvbt2ll_ldpc *h, int noutput_items, int *ninput_items_required);
+int dvbt2ll_ldpc_general_work(dvbt2ll_ldpc *h, int noutput_items, int ninput_items, const void *in,
+                              void *out, int *consumed);
+void dvbt2ll_ldpc_destroy(dvbt2ll_ldpc *h);
+
+/* ---------------------------------------------------------------------------
+ * interleavermod_bc: nldpc unpacked bits -> cell_size complex64 cells per FEC block.
+ * Replaces gr::dvbt2ll::interleavermod_bc::make(framesize, rate, constellation, rotation)
+ * (include/dvbt2ll/interleavermod_bc.h:49; lib/interleavermod_bc_impl.cc:32-37).
+ * ------------------------------------------------------------------------- */
+typedef struct dvbt2ll_interleavermod dvbt2ll_interleavermod;
+typedef struct {
+  int framesize, rate, constellation, rotation;
+} dvbt2ll_interleavermod_params;
+int dvbt2ll_interleavermod_create(const dvbt2ll_interleavermod_params *p, int device,
+                                  dvbt2ll_interleavermod **out);
+int dvbt2ll_interleavermod_output_multiple(const dvbt2ll_interleavermod *h);       /* cell_size (:254) */
+int dvbt2ll_interleavermod_forecast(const dvbt2ll_interleavermod *h, int noutput_items, int *ninput_items_required);
+int dvbt2ll_interleavermod_general_work(dvbt2ll_interleavermod *h, int noutput_items, int ninput_items,
+                                        const void *in, void *out, int *consumed);
+void dvbt2ll_interleavermod_destroy(dvbt2ll_interleavermod *h);
+
+/* ---------------------------------------------------------------------------
+ * framemapperfint_cc: one T2 frame of stream cells -> mapped (frequency-interleaved)
+ * cells.  Replaces gr::dvbt2ll::framemapperfint_cc::make(...20 parameters...)
+ * (include/dvbt2ll/framemapperfint_cc.h:49; lib/framemapperfint_cc_impl.cc:31-36).
+ * ------------------------------------------------------------------------- */
+typedef struct dvbt2ll_framemapperfint dvbt2ll_framemapperfint;
+typedef struct {
+  int framesize, rate, constellation, rotation, fecblocks, tiblocks, carriermode, fftsize,
+      guardinterval, l1constellation, pilotpattern, t2frames, numdatasyms, paprmode, version,
+      preamble, inputmode, reservedbiasbits, l1scrambled, inband;
+} dvbt2ll_framemapperfint_params;
+int dvbt2ll_framemapperfint_create(const dvbt2ll_framemapperfint_params *p, int device,
+                                   dvbt2ll_framemapperfint **out);
+int dvbt2ll_framemapperfint_output_multiple(const dvbt2ll_framemapperfint *h);     /* mapped_items */
+int dvbt2ll_framemapperfint_stream_items(const dvbt2ll_framemapperfint *h);
+int dvbt2ll_framemapperfint_forecast(const dvbt2ll_framemapperfint *h, int noutput_items, int *ninput_items_required);
+int dvbt2ll_framemapperfint_general_work(dvbt2ll_framemapperfint *h, int noutput_items, int ninput_items,
+                                         const void *in, void *out, int *consumed);
+void dvbt2ll_framemapperfint_destroy(dvbt2ll_framemapperfint *h);
+
+/* ---------------------------------------------------------------------------
+ * pilotgenp1insert_cc: one T2 frame of mapped cells -> P1 + OFDM symbols with GI.
+ * Replaces gr::dvbt2ll::pilotgenp1insert_cc::make(carriermode, fftsize, pilotpattern,
+ * guardinterval, numdatasyms, paprmode, version, preamble, misogroup, equalization,
+ * bandwidth, vlength) (include/dvbt2ll/pilotgenp1insert_cc.h:49; impl.cc:33-38).
+ * ------------------------------------------------------------------------- */
+typedef struct dvbt2ll_pilotgenp1insert dvbt2ll_pilotgenp1insert;
+typedef struct {
+  int carriermode, fftsize, pilotpattern, guardinterval, numdatasyms, paprmode, version, preamble,
+      misogroup, equalization, bandwidth, vlength;
+} dvbt2ll_pilotgenp1insert_params;
+int dvbt2ll_pilotgenp1insert_create(const dvbt2ll_pilotgenp1insert_params *p, int device,
+                                    dvbt2ll_pilotgenp1insert **out);
+int dvbt2ll_pilotgenp1insert_output_multiple(const dvbt2ll_pilotgenp1insert *h);   /* Nsym*(N+GI)+2048 */
+int dvbt2ll_pilotgenp1insert_active_items(const dvbt2ll_pilotgenp1insert *h);
+int dvbt2ll_pilotgenp1insert_forecast(const dvbt2ll_pilotgenp1insert *h, int noutput_items, int *ninput_items_required);
+int dvbt2ll_pilotgenp1insert_general_work(dvbt2ll_pilotgenp1insert *h, int noutput_items, int ninput_items,
+                                          const void *in, void *out, int *consumed);
+/* test hook: the frequency-domain symbols (after EQ, before fftshift/IFFT) of one frame,
+ * num_symbols * vlength complex64 written to carriers (host). */
+int dvbt2ll_pilotgenp1insert_debug_carriers(dvbt2ll_pilotgenp1insert *h, const void *in, void *carriers);
+void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h);
+
+/* ---------------------------------------------------------------------------
+ * Fused chain: TS bytes -> IQ for whole T2 frames (BB+BCH+LDPC -> bit interleave +
+ * QAM + cell interleave -> frame/time/frequency interleave + pilots + IFFT + GI + P1).
+ * Equivalent to the five blocks above connected in the shipped flowgraph, each frame
+ * k encoded with the state the reference would hold at that point of the stream
+ * (TS offset, SYNCD count, CRC-8 of the previous packet, t2_frame_num = k % t2frames).
+ * ------------------------------------------------------------------------- */
+typedef struct dvbt2ll_chain dvbt2ll_chain;
+typedef struct {
+  dvbt2ll_framemapperfint_params fm;   /* framesize ... inband */
+  int misogroup, equalization, bandwidth;
+  int max_frames;                      /* largest nframes per run call */
+} dvbt2ll_chain_params;
+typedef struct {
+  int fec_blocks_per_frame;   /* F */
+  int payload_bytes_per_block; /* TS bytes consumed per FEC block (NM) */
+  int64_t ts_bytes_per_frame;
+  int64_t iq_samples_per_frame;
+  int cell_size, stream_items, mapped_items, num_symbols, fft_size, guard_interval;
+  int64_t cw_stride_bytes;     /* packed codeword stride in the internal buffer */
+} dvbt2ll_chain_info;
+int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, dvbt2ll_chain **out);
+int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info);
+/* ts_dev: device pointer to TS bytes whose first byte is absolute stream offset ts_base
+ * (a multiple of 188, at least one packet before the first byte the frames consume so
+ * the CRC-8 of the preceding packet can be formed); ts_len bytes valid.  iq_dev receives
+ * nframes * iq_samples_per_frame complex64.  stream: hipStream_t (NULL = the handle's
+ * own stream).  Asynchronous on that stream. */
+int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_base, int64_t ts_len,
+                             int64_t first_frame, int nframes, void *iq_dev, void *stream);
+/* host buffers, synchronous */
+int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
+                           int64_t first_frame, int nframes, void *iq);
+/* per-stage kernel timing with HIP events on the launch stream: enable, then read the
+ * accumulated milliseconds and launch counts of stages {0: fec, 1: map, 2: ofdm}. */
+int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable);
+int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages);
+/* test hooks (host outputs, synchronous): packed codewords (tempu order) and
+ * cells (time-interleaver input order) of the last run's frame 0 */
+int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes);
+int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells);
+int dvbt2ll_chain_synchronize(dvbt2ll_chain *h);
+void dvbt2ll_chain_destroy(dvbt2ll_chain *h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DVBT2LL_HIP_H */

@@ -1,0 +1,177 @@
+"""ctypes binding of the CPU oracle (TEST INFRASTRUCTURE ONLY).
+
+The oracle is a plain-C restatement of the reference blocks (oracle/dvbt2_oracle.c);
+only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load it.
+"""
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB_PATH = ROOT / "oracle" / "_build" / "libdvbt2_oracle.so"
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+        L = ctypes.CDLL(str(LIB_PATH))
+        vp, ci = ctypes.c_void_p, ctypes.c_int
+        L.orc_bb_create.restype = vp
+        L.orc_bb_create.argtypes = [ci] * 6
+        L.orc_bb_work.argtypes = [vp, ci, vp, vp, ctypes.POINTER(ci)]
+        L.orc_bb_forecast.argtypes = [vp, ci]
+        L.orc_bb_nbch.argtypes = [vp]
+        L.orc_bb_kbch.argtypes = [vp]
+        L.orc_bb_destroy.argtypes = [vp]
+        L.orc_ldpc_create.restype = vp
+        L.orc_ldpc_create.argtypes = [ci, ci]
+        L.orc_ldpc_work.argtypes = [vp, ci, vp, vp]
+        L.orc_ldpc_destroy.argtypes = [vp]
+        L.orc_im_create.restype = vp
+        L.orc_im_create.argtypes = [ci] * 4
+        L.orc_im_work.argtypes = [vp, ci, vp, vp, ctypes.POINTER(ci)]
+        L.orc_im_cell_size.argtypes = [vp]
+        L.orc_im_destroy.argtypes = [vp]
+        L.orc_fm_create.restype = vp
+        L.orc_fm_create.argtypes = [ci] * 20
+        L.orc_fm_work.argtypes = [vp, vp, vp]
+        L.orc_fm_stream_items.argtypes = [vp]
+        L.orc_fm_mapped_items.argtypes = [vp]
+        L.orc_fm_destroy.argtypes = [vp]
+        L.orc_pg_create.restype = vp
+        L.orc_pg_create.argtypes = [ci] * 12
+        for f in ("orc_pg_active_items", "orc_pg_output_items", "orc_pg_num_symbols", "orc_pg_guard"):
+            getattr(L, f).argtypes = [vp]
+        L.orc_pg_normalization.argtypes = [vp]
+        L.orc_pg_normalization.restype = ctypes.c_float
+        L.orc_pg_carriers.argtypes = [vp, vp, vp]
+        L.orc_pg_work.argtypes = [vp, vp, vp]
+        L.orc_pg_p1.argtypes = [vp, vp]
+        L.orc_pg_destroy.argtypes = [vp]
+        L.orc_crc8_dvbs2.restype = ctypes.c_uint8
+        L.orc_crc8_dvbs2.argtypes = [vp, ci]
+        L.orc_crc32_bits.restype = ctypes.c_uint32
+        L.orc_crc32_bits.argtypes = [vp, ci]
+        L.orc_bb_prbs.argtypes = [vp, ci]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class BB:
+    def __init__(self, framesize, rate, mode=0, inband=0, fecblocks=168, tsrate=4000000):
+        self.h = lib().orc_bb_create(framesize, rate, mode, inband, fecblocks, tsrate)
+        assert self.h, "oracle bbheaderbch create failed"
+        self.nbch = lib().orc_bb_nbch(self.h)
+        self.kbch = lib().orc_bb_kbch(self.h)
+
+    def forecast(self, nout):
+        return lib().orc_bb_forecast(self.h, nout)
+
+    def work(self, ts, nblocks):
+        out = np.zeros(nblocks * self.nbch, np.uint8)
+        ts = np.ascontiguousarray(ts, np.uint8)
+        c = ctypes.c_int(0)
+        lib().orc_bb_work(self.h, nblocks * self.nbch, _p(ts), _p(out), ctypes.byref(c))
+        return out, c.value
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_bb_destroy(self.h)
+
+
+class LDPC:
+    def __init__(self, framesize, rate):
+        self.h = lib().orc_ldpc_create(framesize, rate)
+        self.nldpc = 64800 if framesize == 1 else 16200
+
+    def work(self, bits, nblocks):
+        out = np.zeros(nblocks * self.nldpc, np.uint8)
+        bits = np.ascontiguousarray(bits, np.uint8)
+        lib().orc_ldpc_work(self.h, nblocks, _p(bits), _p(out))
+        return out
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_ldpc_destroy(self.h)
+
+
+class IM:
+    def __init__(self, framesize, rate, constellation, rotation):
+        self.h = lib().orc_im_create(framesize, rate, constellation, rotation)
+        self.cell_size = lib().orc_im_cell_size(self.h)
+        self.nldpc = 64800 if framesize == 1 else 16200
+
+    def work(self, bits, nblocks):
+        out = np.zeros(nblocks * self.cell_size, np.complex64)
+        bits = np.ascontiguousarray(bits, np.uint8)
+        c = ctypes.c_int(0)
+        lib().orc_im_work(self.h, nblocks * self.cell_size, _p(bits), _p(out), ctypes.byref(c))
+        return out
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_im_destroy(self.h)
+
+
+class FM:
+    def __init__(self, *params):
+        assert len(params) == 20
+        self.h = lib().orc_fm_create(*params)
+        assert self.h, "oracle framemapper create failed"
+        self.stream_items = lib().orc_fm_stream_items(self.h)
+        self.mapped_items = lib().orc_fm_mapped_items(self.h)
+
+    def work(self, cells):
+        cells = np.ascontiguousarray(cells, np.complex64)
+        out = np.zeros(self.mapped_items, np.complex64)
+        lib().orc_fm_work(self.h, _p(cells), _p(out))
+        return out
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_fm_destroy(self.h)
+
+
+class PG:
+    def __init__(self, *params):
+        assert len(params) == 12
+        self.h = lib().orc_pg_create(*params)
+        assert self.h, "oracle pilotgen create failed"
+        self.vlength = params[11]
+        self.active_items = lib().orc_pg_active_items(self.h)
+        self.output_items = lib().orc_pg_output_items(self.h)
+        self.num_symbols = lib().orc_pg_num_symbols(self.h)
+        self.guard = lib().orc_pg_guard(self.h)
+        self.normalization = lib().orc_pg_normalization(self.h)
+
+    def carriers(self, cells):
+        cells = np.ascontiguousarray(cells, np.complex64)
+        out = np.zeros(self.num_symbols * self.vlength, np.complex64)
+        lib().orc_pg_carriers(self.h, _p(cells), _p(out))
+        return out.reshape(self.num_symbols, self.vlength)
+
+    def work(self, cells):
+        cells = np.ascontiguousarray(cells, np.complex64)
+        out = np.zeros(self.output_items, np.complex64)
+        lib().orc_pg_work(self.h, _p(cells), _p(out))
+        return out
+
+    def p1(self):
+        out = np.zeros(2048, np.complex64)
+        lib().orc_pg_p1(self.h, _p(out))
+        return out
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_pg_destroy(self.h)

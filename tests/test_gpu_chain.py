@@ -1,0 +1,57 @@
+"""Fused chain (TS -> IQ) parity vs the oracle chain; frame independence (sharding basis)."""
+import numpy as np
+import pytest
+
+import dvbt2ll
+from dvbt2ll.configs import CONFIGS, ts_for_frames
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_chain(cfg, nframes):
+    ts, base = ts_for_frames(cfg, 0, nframes)
+    F = cfg.fecblocks
+    bb = O.BB(*cfg.bb_args()); ld = O.LDPC(cfg.framesize, cfg.rate); im = O.IM(*cfg.im_args())
+    fm = O.FM(*cfg.fm_args()); pg = O.PG(*cfg.pg_args())
+    off = 0
+    out = []
+    for k in range(nframes):
+        bits, cons = bb.work(ts[off:], F)
+        off += cons
+        cells = im.work(ld.work(bits, F), F)
+        mapped = fm.work(cells)
+        out.append((pg.carriers(mapped), mapped))
+    return out, pg
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg3"])
+def test_chain_iq_matches_oracle(gpu, name):
+    cfg = CONFIGS[name]
+    nframes = 3 if name == "cfg1" else 2
+    ref, pg = oracle_chain(cfg, nframes)
+    ch = dvbt2ll.Chain(cfg, max_frames=nframes)
+    iq = ch.run(0, nframes)
+    N, G = pg.vlength, pg.guard
+    per = ch.iq_per_frame
+    for k in range(nframes):
+        car = ref[k][0]
+        f = iq[k * per:(k + 1) * per]
+        for j in range(pg.num_symbols):
+            x = np.fft.ifft(np.fft.fftshift(car[j].astype(np.complex128))) * N * pg.normalization
+            want = np.concatenate([x[N - G:], x])
+            y = f[2048 + j * (N + G): 2048 + (j + 1) * (N + G)]
+            rms = np.sqrt(np.mean(np.abs(want) ** 2))
+            assert np.abs(y - want).max() <= 2e-5 * rms, (k, j, np.abs(y - want).max() / rms)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg3"])
+def test_chain_frames_independent(gpu, name):
+    """frame k computed alone (first_frame=k) equals frame k of a batched run"""
+    cfg = CONFIGS[name]
+    ch = dvbt2ll.Chain(cfg, max_frames=3)
+    batch = ch.run(0, 3)
+    per = ch.iq_per_frame
+    for k in (1, 2):
+        one = ch.run(k, 1)
+        np.testing.assert_array_equal(one.view(np.uint32), batch[k * per:(k + 1) * per].view(np.uint32))
