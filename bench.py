@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""DVB-T2 transmit-chain benchmark on MI355X (BASELINE.json metric: IQ Msamples/s for the whole
+node + FEC blocks/s, 32K-FFT 256-QAM 3/5 = cfg3).
+
+One "step" = the whole hot path (TS bytes -> BBFRAME/BCH/LDPC -> bit interleave/QAM/cell
+interleave -> time/frame/frequency interleave + pilots + IFFT + GI + P1) over a batch of
+--frames T2 frames per GPU, TS input already resident in HBM, IQ written to HBM.
+
+Multi-GPU: frame-sharded, one process per GPU (torchrun); each rank encodes its own
+disjoint T2 frames with closed-form stream state, no data-path collective ("weak" scaling).
+Rank 0 prints one JSON line.  Synthetic data: splitmix64 TS packets (dvbt2ll.configs).
+
+Extra fields: roofline (dominant kernel, HIP-event timed on the launch stream inside the
+timed region; traffic from rocprofv3 PMC passes run as child processes BEFORE this process
+touches the GPU) and cpu_baseline (the oracle C restatement, single thread, bounded sample).
+"""
+import argparse
+import glob
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "gr-dvbt2ll_amd"))
+
+RT_SPS = 8e6 * 8 / 7          # real-time IQ rate of the 8 MHz channel (apps/vv009-4kshort.grc:143)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "IQ Msamples/sec (whole node) + FEC blocks/sec, 32K-FFT 256-QAM 3/5"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=16, help="T2 frames per step per GPU")
+    ap.add_argument("--config", default="cfg3")
+    ap.add_argument("--no-pmc", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+def algorithmic_bytes(cfg, info):
+    """SURVEY.md section 8(d) per-frame algorithmic bytes of each stage."""
+    from dvbt2ll.configs import KBCH
+    F = info["fec_blocks_per_frame"]
+    nldpc = 64800 if cfg.framesize == 1 else 16200
+    kbch = KBCH[(cfg.framesize, cfg.rate)]
+    cs, S, M, IQ = info["cell_size"], info["stream_items"], info["mapped_items"], info["iq_samples_per_frame"]
+    s1 = F * ((kbch - 80) // 8 + nldpc // 8)
+    s2 = F * (nldpc // 8 + 8 * cs)
+    s3 = 8 * S + 8 * M
+    s4 = 8 * M + 8 * IQ
+    # kernel stages: fec = S1 (+ LDPC), map = S2, ofdm = S3 + S4 (fused)
+    return {"fec": s1, "map": s2, "ofdm": s3 + s4}
+
+
+def pmc_passes(args):
+    """rocprofv3 FETCH_SIZE / WRITE_SIZE of the ofdm kernel, one counter set per pass, run as child
+    processes before this process initialises the GPU.  Returns per-launch corrected bytes or None."""
+    import shutil
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not found"
+    res = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="t2pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = [rp, "--pmc", ctr, "--kernel-include-regex", "ofdm_kernel", "-T", "-f", "csv", "-d", d, "-o", "pmc",
+               "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--config", args.config,
+               "--frames", str(args.frames), "--steps", "2", "--warmup", "1"]
+        try:
+            subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        except Exception as e:  # noqa: BLE001
+            return None, "rocprofv3 %s pass failed: %s" % (ctr, e)
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        vals = []
+        for fn in files:
+            import csv
+            with open(fn) as fh:
+                for row in csv.DictReader(fh):
+                    if row.get("Counter_Name") == ctr and "ofdm_kernel" in row.get("Kernel_Name", ""):
+                        vals.append(float(row["Counter_Value"]))
+        if not vals:
+            return None, "no %s rows" % ctr
+        res[ctr] = sum(vals) / len(vals)
+    # FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE reads half of the streamed bytes
+    # (MI355X_MICROARCH.md, HBM section) -> x2 on the read side
+    fetch = res["FETCH_SIZE"] * 1024 * 2
+    write = res["WRITE_SIZE"] * 1024
+    return {"fetch_bytes": fetch, "write_bytes": write, "total": fetch + write}, None
+
+
+def cpu_baseline(cfg, seconds):
+    """Oracle C restatement (single thread) over a bounded sample of the same workload."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    from dvbt2ll.configs import ts_for_frames
+    F = cfg.fecblocks
+    bb = O.BB(*cfg.bb_args()); ld = O.LDPC(cfg.framesize, cfg.rate); im = O.IM(*cfg.im_args())
+    fm = O.FM(*cfg.fm_args()); pg = O.PG(*cfg.pg_args())
+    ts, _ = ts_for_frames(cfg, 0, 64)
+    off, frames, samples = 0, 0, 0
+    t0 = time.perf_counter()
+    while True:
+        bits, cons = bb.work(ts[off:], F)
+        off += cons
+        cells = im.work(ld.work(bits, F), F)
+        iq = pg.work(fm.work(cells))
+        frames += 1
+        samples += len(iq)
+        dt = time.perf_counter() - t0
+        if dt >= seconds or frames >= 64:
+            break
+    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
+            "sample": "%d %s T2 frames (%d FEC blocks) through the oracle C restatement of all five "
+                      "blocks, one thread, own radix-2 float IFFT (FFTW unavailable), %.1f s"
+                      % (frames, cfg.name, frames * F, dt),
+            "fec_blocks_per_sec": frames * F / dt}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic, pmc_note = None, "skipped"
+    if world == 1 and not args.pmc_child and not args.no_pmc:
+        traffic, pmc_note = pmc_passes(args)          # before any GPU initialisation here
+
+    import numpy as np
+    import torch
+    import dvbt2ll
+    from dvbt2ll.configs import CONFIGS, ts_for_frames
+
+    cfg = CONFIGS[args.config]
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    B = args.frames
+    chain = dvbt2ll.Chain(cfg, max_frames=B, device=local_rank)
+    info = chain.info
+    per = chain.iq_per_frame
+    # R distinct resident batches per rank, frames disjoint across ranks and batches
+    R = 2
+    ts_dev, ts_meta = [], []
+    for r in range(R):
+        first = (rank * R + r) * B
+        ts, base = ts_for_frames(cfg, first, B)
+        ts_dev.append(torch.from_numpy(ts).cuda())
+        ts_meta.append((first, base, len(ts)))
+    iq = torch.empty((B * per, 2), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(s):
+        first, base, n = ts_meta[s % R]
+        chain.run_device(ts_dev[s % R].data_ptr(), base, n, first, B, iq.data_ptr(), stream)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    if args.pmc_child:
+        for s in range(args.steps):
+            step(s)
+        torch.cuda.synchronize()
+        return
+    chain.set_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        step(s)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    stage_ms, launches = chain.timing()
+    chain.set_timing(False)
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    frames_total = B * args.steps * world
+    samples_total = frames_total * per
+    fec_total = frames_total * info["fec_blocks_per_frame"]
+    msps = samples_total / elapsed / 1e6
+    if rank == 0:
+        ab = algorithmic_bytes(cfg, info)
+        stages = {}
+        for k, name in enumerate(("fec", "map", "ofdm")):
+            avg_ms = stage_ms[k] / max(1, launches[k])
+            bytes_launch = ab[name] * B
+            stages[name] = {"avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": bytes_launch,
+                            "achieved_GBs": bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None}
+        dom = max(stages, key=lambda n: stages[n]["avg_launch_ms"])
+        st = stages[dom]
+        roof = {"kernel": dom + "_kernel", "bound": "hbm", "achieved": st["achieved_GBs"], "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": st["achieved_GBs"] / HBM_PEAK_GBS if st["achieved_GBs"] else None,
+                "traffic": (traffic["total"] if (traffic and dom == "ofdm") else None),
+                "traffic_note": pmc_note if traffic is None else
+                "rocprofv3 PMC passes (FETCH_SIZE x1024 x2 gfx950 read correction + WRITE_SIZE x1024), "
+                "ofdm_kernel per launch",
+                "algorithmic_bytes_per_launch": st["algorithmic_bytes_per_launch"],
+                "avg_launch_ms": st["avg_launch_ms"]}
+        out = {
+            "metric": METRIC, "value": msps, "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "%s: TS->IQ full DVB-T2 chain, %d T2 frames per step per GPU "
+                                   "(%d FEC blocks, %d IQ samples per frame)"
+                                   % (cfg.name, B, info["fec_blocks_per_frame"], per),
+                       "frames_per_step_per_gpu": B, "parallelism": "frame-sharded x%d (replicas, no collective)" % world},
+            "fec_blocks_per_sec": fec_total / elapsed,
+            "x_realtime": msps * 1e6 / RT_SPS,
+            "stages": stages,
+            "roofline": roof,
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        print(json.dumps(out))
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

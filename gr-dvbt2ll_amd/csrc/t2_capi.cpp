@@ -128,12 +128,6 @@ struct MapTables {
   }
 };
 
-int hip_status(hipError_t e) {
-  if (e == hipSuccess) return DVBT2LL_OK;
-  last_hip_error() = e;
-  return e == hipErrorOutOfMemory ? DVBT2LL_ENOMEM : DVBT2LL_EDEVICE;
-}
-
 }  // namespace
 
 // ============================================================================ common
@@ -504,12 +498,36 @@ struct dvbt2ll_chain {
   int64_t iq_per_frame = 0;
   int64_t ts_per_frame = 0;
   int pay = 0;
+  // stage timing: 4 events per run (start, after fec, after map, after ofdm) recorded on the
+  // launch stream without host synchronisation; folded into ms[] by get_timing()
   bool timing = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> evpool;
+  size_t evused = 0;
   double ms[3] = {0, 0, 0};
   int64_t launches[3] = {0, 0, 0};
+  hipEvent_t next_event() {
+    if (evused == evpool.size()) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      evpool.push_back(e);
+    }
+    return evpool[evused++];
+  }
+  int fold_timing() {
+    if (!evused) return 0;
+    HIP_TRY(hipEventSynchronize(evpool[evused - 1]));
+    for (size_t b = 0; b + 3 < evused; b += 4)
+      for (int k = 0; k < 3; k++) {
+        float t = 0;
+        HIP_TRY(hipEventElapsedTime(&t, evpool[b + k], evpool[b + k + 1]));
+        ms[k] += t;
+        launches[k] += 1;
+      }
+    evused = 0;
+    return 0;
+  }
   ~dvbt2ll_chain() {
-    for (auto &e : ev)
+    for (auto &e : evpool)
       if (e) (void)hipEventDestroy(e);
   }
 };
@@ -554,7 +572,6 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   int64_t nblk = (int64_t)h->frame.F * h->max_frames;
   if (h->cw.ensure((size_t)nblk * h->cw_stride) || h->cells.ensure((size_t)h->frame.S * 8 * h->max_frames))
     return DVBT2LL_ENOMEM;
-  for (auto &e : h->ev) HIP_TRY(hipEventCreate(&e));
   *out = h.release();
   return DVBT2LL_OK;
 }
@@ -591,7 +608,13 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   int64_t lo = start >= 188 ? (start / 188) * 188 - 188 : 0;
   if (ts_base > lo || ts_base + ts_len < end) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[0], s));
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (h->timing) {
+    if (h->evused + 4 > 4096 && h->fold_timing()) return DVBT2LL_EDEVICE;
+    for (auto &e : ev)
+      if (!(e = h->next_event())) return DVBT2LL_EDEVICE;
+    HIP_TRY(hipEventRecord(ev[0], s));
+  }
   FecIO fio{};
   fio.in = (const uint8_t *)ts_dev;
   fio.ts_base = ts_base;
@@ -601,7 +624,7 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   fio.cw_stride = h->cw_stride;
   fio.nblocks = F * nframes;
   HIP_TRY(launch_fec(FEC_TS_TO_TEMPU, h->fec.dev, fio, s));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[1], s));
+  if (h->timing) HIP_TRY(hipEventRecord(ev[1], s));
   MapIO mio{};
   mio.in = h->cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
@@ -610,7 +633,7 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   mio.packed_in = 1;
   mio.apply_ci = 1;
   HIP_TRY(launch_map(h->map.dev, mio, s));
-  if (h->timing) HIP_TRY(hipEventRecord(h->ev[2], s));
+  if (h->timing) HIP_TRY(hipEventRecord(ev[2], s));
   OfdmIO oio{};
   oio.cells = h->cells.as<float2>();
   oio.cell_stride = h->frame.S;
@@ -619,16 +642,7 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   oio.first_frame = first_frame;
   oio.nframes = nframes;
   HIP_TRY(launch_ofdm(h->ofdm.dev, oio, s));
-  if (h->timing) {
-    HIP_TRY(hipEventRecord(h->ev[3], s));
-    HIP_TRY(hipEventSynchronize(h->ev[3]));
-    for (int k = 0; k < 3; k++) {
-      float t = 0;
-      HIP_TRY(hipEventElapsedTime(&t, h->ev[k], h->ev[k + 1]));
-      h->ms[k] += t;
-      h->launches[k] += 1;
-    }
-  }
+  if (h->timing) HIP_TRY(hipEventRecord(ev[3], s));
   return DVBT2LL_OK;
 }
 
@@ -648,12 +662,14 @@ extern "C" int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t 
 
 extern "C" int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable) {
   if (!h) return DVBT2LL_EINVAL;
+  if (h->fold_timing()) return DVBT2LL_EDEVICE;
   h->timing = enable != 0;
   for (int k = 0; k < 3; k++) { h->ms[k] = 0; h->launches[k] = 0; }
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages) {
   if (!h || !ms || nstages < 1) return DVBT2LL_EINVAL;
+  if (h->fold_timing()) return DVBT2LL_EDEVICE;
   for (int k = 0; k < nstages && k < 3; k++) {
     ms[k] = h->ms[k];
     if (launches) launches[k] = h->launches[k];
