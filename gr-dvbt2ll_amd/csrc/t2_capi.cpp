@@ -397,17 +397,24 @@ static PgParams to_pg(const dvbt2ll_pilotgenp1insert_params &p) {
 }
 
 struct OfdmTables {
-  DevBuf map, aux, tw, isinc, p1;
+  DevBuf map, tw, isinc, p1;
   OfdmDev dev{};
-  int init(const PilotPlan &pp, const std::vector<int32_t> &bin_map, const std::vector<cf32> &aux_host,
-           int aux_len, int t2frames) {
+  // bin_map rows are IFFT-input ordered; for N > 16K the kernel runs two N/2 transforms over
+  // even and odd bins, so each row is stored as [even bins | odd bins]
+  int init(const PilotPlan &pp, const std::vector<int32_t> &bin_map, int aux_len, int t2frames) {
     int r;
-    if ((r = upload(map, bin_map)) || (r = upload(aux, aux_host)) || (r = upload(tw, pp.twiddle)) ||
-        (r = upload(p1, pp.p1)))
+    const int N = pp.N;
+    if (N > 16384) {
+      std::vector<int32_t> m(bin_map.size());
+      for (int j = 0; j < pp.Nsym; j++)
+        for (int k = 0; k < N; k++) m[(size_t)j * N + (k & 1) * (N / 2) + (k >> 1)] = bin_map[(size_t)j * N + k];
+      if ((r = upload(map, m))) return r;
+    } else if ((r = upload(map, bin_map))) {
       return r;
+    }
+    if ((r = upload(tw, pp.twiddle)) || (r = upload(p1, pp.p1))) return r;
     if (pp.eq && (r = upload(isinc, pp.isinc))) return r;
     dev.bin_map = map.as<int32_t>();
-    dev.aux = aux.as<float2>();
     dev.twiddle = tw.as<float2>();
     dev.isinc = pp.eq ? isinc.as<float>() : nullptr;
     dev.p1 = p1.as<float2>();
@@ -421,9 +428,10 @@ struct dvbt2ll_pilotgenp1insert {
   DeviceCtx ctx;
   PilotPlan plan;
   OfdmTables ofdm;
-  DevBuf din, dout;
+  DevBuf din, dout;    // din = [aux (pilot values) | one frame of mapped cells]
   int out_items = 0;
 };
+constexpr int PG_AUX_PAD = 16;
 extern "C" int dvbt2ll_pilotgenp1insert_create(const dvbt2ll_pilotgenp1insert_params *p, int device,
                                                dvbt2ll_pilotgenp1insert **out) {
   if (!p || !out) return DVBT2LL_EINVAL;
@@ -433,9 +441,11 @@ extern "C" int dvbt2ll_pilotgenp1insert_create(const dvbt2ll_pilotgenp1insert_pa
   if (build_pilot(to_pg(*p), h->plan)) return DVBT2LL_EINVAL;
   int r = h->ctx.init(device);
   if (r) return r;
-  std::vector<cf32> aux(AUX_L1PRE, cf32{0.f, 0.f});
+  std::vector<cf32> aux(PG_AUX_PAD, cf32{0.f, 0.f});
   for (int i = 0; i < 12; i++) aux[AUX_PILOT0 + i] = h->plan.pilot_values[i];
-  if ((r = h->ofdm.init(h->plan, h->plan.bin_map, aux, AUX_L1PRE, 1))) return r;
+  if ((r = h->ofdm.init(h->plan, h->plan.bin_map, PG_AUX_PAD, 1))) return r;
+  if (h->din.ensure((size_t)(PG_AUX_PAD + h->plan.active) * 8)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpy(h->din.p, aux.data(), PG_AUX_PAD * 8, hipMemcpyHostToDevice));
   h->out_items = h->plan.Nsym * (h->plan.N + h->plan.G) + 2048;
   *out = h.release();
   return DVBT2LL_OK;
@@ -451,11 +461,14 @@ static int pg_run(dvbt2ll_pilotgenp1insert *h, const void *in, void *out, int ca
   const PilotPlan &pp = h->plan;
   size_t out_n = carriers_only ? (size_t)pp.Nsym * pp.N : (size_t)h->out_items;
   HIP_TRY(hipSetDevice(h->ctx.device));
-  if (h->din.ensure((size_t)pp.active * 8) || h->dout.ensure(out_n * 8)) return DVBT2LL_ENOMEM;
-  HIP_TRY(hipMemcpyAsync(h->din.p, in, (size_t)pp.active * 8, hipMemcpyHostToDevice, h->ctx.stream));
+  if (h->dout.ensure(out_n * 8)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(h->din.as<float2>() + PG_AUX_PAD, in, (size_t)pp.active * 8, hipMemcpyHostToDevice,
+                         h->ctx.stream));
   OfdmIO io{};
-  io.cells = h->din.as<float2>();
-  io.cell_stride = pp.active;
+  io.data = h->din.as<float2>();
+  io.aux_off = 0;
+  io.cell_off = PG_AUX_PAD;
+  io.cell_stride = (uint32_t)pp.active;
   io.out = h->dout.as<float2>();
   io.out_stride = (int64_t)out_n;
   io.first_frame = 0;
@@ -494,6 +507,7 @@ struct dvbt2ll_chain {
   OfdmTables ofdm;
   DevBuf cw, cells, perm, shift, ts_tmp, iq_tmp;
   int max_frames = 0;
+  int64_t aux_pad = 0;       // cells buffer = [aux variants (aux_pad elements) | frame cells]
   int64_t cw_stride = 0;
   int64_t iq_per_frame = 0;
   int64_t ts_per_frame = 0;
@@ -564,14 +578,18 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   std::vector<cf32> aux = h->frame.aux;
   for (int v = 0; v < h->frame.t2frames; v++)
     for (int i = 0; i < 12; i++) aux[(size_t)v * h->frame.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
-  if ((r = h->ofdm.init(pp, cmap, aux, h->frame.aux_len, h->frame.t2frames))) return r;
+  if ((r = h->ofdm.init(pp, cmap, h->frame.aux_len, h->frame.t2frames))) return r;
+  h->aux_pad = ((int64_t)aux.size() + 63) / 64 * 64;
   h->cw_stride = ((h->fec.plan.nldpc / 8) + 255) / 256 * 256;
   h->iq_per_frame = (int64_t)pp.Nsym * (pp.N + pp.G) + 2048;
   h->pay = (h->fec.plan.kbch - 80) / 8;
   h->ts_per_frame = (int64_t)h->frame.F * h->pay;
   int64_t nblk = (int64_t)h->frame.F * h->max_frames;
-  if (h->cw.ensure((size_t)nblk * h->cw_stride) || h->cells.ensure((size_t)h->frame.S * 8 * h->max_frames))
+  if (h->cw.ensure((size_t)nblk * h->cw_stride) ||
+      h->cells.ensure((size_t)(h->aux_pad + (int64_t)h->frame.S * h->max_frames) * 8))
     return DVBT2LL_ENOMEM;
+  if ((uint64_t)(h->aux_pad + (int64_t)h->frame.S * h->max_frames) * 8 >= (1ull << 32)) return DVBT2LL_EINVAL;
+  HIP_TRY(hipMemcpy(h->cells.p, aux.data(), aux.size() * sizeof(cf32), hipMemcpyHostToDevice));
   *out = h.release();
   return DVBT2LL_OK;
 }
@@ -628,15 +646,17 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   MapIO mio{};
   mio.in = h->cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
-  mio.out = h->cells.as<float2>();
+  mio.out = h->cells.as<float2>() + h->aux_pad;
   mio.nblocks = F * nframes;
   mio.packed_in = 1;
   mio.apply_ci = 1;
   HIP_TRY(launch_map(h->map.dev, mio, s));
   if (h->timing) HIP_TRY(hipEventRecord(ev[2], s));
   OfdmIO oio{};
-  oio.cells = h->cells.as<float2>();
-  oio.cell_stride = h->frame.S;
+  oio.data = h->cells.as<float2>();
+  oio.aux_off = 0;
+  oio.cell_off = (uint32_t)h->aux_pad;
+  oio.cell_stride = (uint32_t)h->frame.S;
   oio.out = (float2 *)iq_dev;
   oio.out_stride = h->iq_per_frame;
   oio.first_frame = first_frame;
@@ -684,10 +704,10 @@ extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells) {
-  if (!h || !out || cells < 0 || (size_t)cells * 8 > h->cells.n) return DVBT2LL_EINVAL;
+  if (!h || !out || cells < 0 || (size_t)(cells + h->aux_pad) * 8 > h->cells.n) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, h->cells.p, (size_t)cells * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out, h->cells.as<float2>() + h->aux_pad, (size_t)cells * 8, hipMemcpyDeviceToHost));
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_synchronize(dvbt2ll_chain *h) {

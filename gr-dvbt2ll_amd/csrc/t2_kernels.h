@@ -54,8 +54,7 @@ struct MapIO {
 
 // ---------------------------------------------------------------- OFDM symbols
 struct OfdmDev {
-  const int32_t *bin_map;   // Nsym x N (IFFT input order)
-  const float2 *aux;        // t2frames x aux_len
+  const int32_t *bin_map;   // Nsym x N (IFFT input order): >= 0 cell index, < 0 aux entry
   const float2 *twiddle;    // N
   const float *isinc;       // N or null
   const float2 *p1;         // 2048
@@ -63,8 +62,10 @@ struct OfdmDev {
   float norm;
 };
 struct OfdmIO {
-  const float2 *cells;      // per frame: cell_stride entries
-  int64_t cell_stride;
+  const float2 *data;       // one buffer: aux variants at aux_off, frame f cells at cell_off + f*cell_stride
+  uint32_t aux_off;         // element offset of aux variant 0 (variant v at aux_off + v*aux_len)
+  uint32_t cell_off;
+  uint32_t cell_stride;
   float2 *out;              // per frame: out_stride samples
   int64_t out_stride;
   int64_t first_frame;

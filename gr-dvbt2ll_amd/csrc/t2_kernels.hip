@@ -25,6 +25,17 @@ __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
+// uniform (SGPR) base + 32-bit unsigned byte offset: lets the compiler use the global
+// saddr form (one VGPR per address instead of a 64-bit VGPR pair per element)
+template <class T>
+__device__ __forceinline__ T ld_off(const T *base, uint32_t byte_off) {
+  return *(const T *)((const char *)base + byte_off);
+}
+template <class T>
+__device__ __forceinline__ void st_off(T *base, uint32_t byte_off, T v) {
+  *(T *)((char *)base + byte_off) = v;
+}
+
 __device__ __forceinline__ uint32_t rd_lane_u32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t rd_lane_u64(uint64_t v, int l) {
   uint32_t lo = rd_lane_u32((uint32_t)v, l), hi = rd_lane_u32((uint32_t)(v >> 32), l);
@@ -470,164 +481,293 @@ __device__ constexpr float kSin32[32] = {
     -0.98078528040323043f, -1.0f, -0.98078528040323043f, -0.92387953251128674f, -0.83146961230254524f,
     -0.70710678118654757f, -0.55557023301960218f, -0.38268343236508978f, -0.19509032201612828f};
 
-// in-register inverse DFT of size R (natural order in and out), radix-2 recursion
-template <int R, int STRIDE = 1>
+__host__ __device__ constexpr int brev_c(int i, int bits) {
+  int r = 0;
+  for (int b = 0; b < bits; b++) r |= ((i >> b) & 1) << (bits - 1 - b);
+  return r;
+}
+__host__ __device__ constexpr int log2_c(int n) { return n <= 1 ? 0 : 1 + log2_c(n / 2); }
+
+// In-register inverse DFT of size R (natural order in and out): bit-reversal by register
+// renaming, then in-place radix-2 stages fenced so each stage retires before the next
+// (keeps a 32-point transform inside the 128-VGPR budget of a 1024-thread workgroup).
+template <int R>
 struct Dft {
   __device__ __forceinline__ static void run(float2 *x) {
-    float2 e[R / 2], o[R / 2];
+    constexpr int L = log2_c(R);
 #pragma unroll
-    for (int i = 0; i < R / 2; i++) { e[i] = x[2 * i]; o[i] = x[2 * i + 1]; }
-    Dft<R / 2>::run(e);
-    Dft<R / 2>::run(o);
+    for (int i = 0; i < R; i++) {
+      const int j = brev_c(i, L);
+      if (i < j) { float2 t = x[i]; x[i] = x[j]; x[j] = t; }
+    }
 #pragma unroll
-    for (int k = 0; k < R / 2; k++) {
-      float2 t;
-      constexpr int sc = 32 / R;
-      if (k == 0) t = o[k];
-      else if (4 * k == R) t = make_float2(-o[k].y, o[k].x);          // * i
-      else t = cmulf(o[k], make_float2(kCos32[k * sc], kSin32[k * sc]));
-      x[k] = cadd(e[k], t);
-      x[k + R / 2] = csub(e[k], t);
+    for (int len = 2; len <= R; len <<= 1) {
+#pragma unroll
+      for (int i = 0; i < R; i += len) {
+#pragma unroll
+        for (int k = 0; k < len / 2; k++) {
+          float2 a = x[i + k], b = x[i + k + len / 2], t;
+          if (k == 0) t = b;
+          else if (4 * k == len) t = make_float2(-b.y, b.x);                        // * i
+          else t = cmulf(b, make_float2(kCos32[k * (32 / len)], kSin32[k * (32 / len)]));
+          x[i + k] = cadd(a, t);
+          x[i + k + len / 2] = csub(a, t);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 };
-template <int STRIDE>
-struct Dft<1, STRIDE> {
-  __device__ __forceinline__ static void run(float2 *) {}
+
+// ---------------------------------------------------------------- Stockham IFFT
+// Sub-transform of NSUB <= 16384 points by NT = NSUB/16 threads, 16 complex values per thread.
+// Pass with radix R over units j (Ns = product of earlier radices, Stockham autosort):
+//   in  : A[j + r*NSUB/R]                         (r < R)
+//   out : B[(j/Ns)*Ns*R + j%Ns + r*Ns] after twiddles w^((j%Ns)*r*NSUB/(Ns*R)) and DFT_R
+// Data live in LDS between passes as float2 with one pad slot per 16 (conflict-free for the
+// stride-R writes of the first pass and the unit-stride reads).  The first pass reads the
+// gathered inputs from registers, the last writes its outputs to registers:
+// thread t ends with n = t + NT*m, m = u + (16/R_last)*r.
+__device__ __forceinline__ uint32_t lds_pad(uint32_t a) { return a + (a >> 4); }
+
+// v[r] *= w^(r * e) for r = 1..R-1 from the table tw (w = exp(2 pi i / Ntab)), index scale s:
+// 2-level table products (loads w^e .. w^3e and w^4e, w^8e, w^12e)
+template <int R>
+__device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32_t e) {
+  if (R == 1) return;
+  float2 lo[4], hi[4];
+#pragma unroll
+  for (int l = 1; l < 4 && l < R; l++) lo[l] = ld_off(tw, (uint32_t)l * e * 8u);
+#pragma unroll
+  for (int h = 1; h < 4 && 4 * h < R; h++) hi[h] = ld_off(tw, (uint32_t)(4 * h) * e * 8u);
+#pragma unroll
+  for (int r = 1; r < R; r++) {
+    const int h = r >> 2, l = r & 3;
+    float2 w = h == 0 ? lo[l] : (l == 0 ? hi[h] : cmulf(hi[h], lo[l]));
+    v[r] = cmulf(v[r], w);
+  }
+}
+
+template <int NSUB, int NT, int R, int NS>
+struct StockhamPass {
+  static constexpr int U = 16 / R;          // units per thread
+  // twiddles + DFT on the thread's U units (v laid out [u][r])
+  __device__ __forceinline__ static void compute(float2 *v, const float2 *tw, uint32_t tws, int tid) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (NS > 1) {
+        const uint32_t j = (uint32_t)(tid + NT * u);
+        twiddle_unit<R>(v + u * R, tw, (j % NS) * (uint32_t)(NSUB / (NS * R)) * tws);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      Dft<R>::run(v + u * R);
+    }
+  }
+  __device__ __forceinline__ static void store_lds(const float2 *v, float2 *lds, int tid) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t j = (uint32_t)(tid + NT * u);
+      const uint32_t base = (j / NS) * (NS * R) + (j % NS);
+#pragma unroll
+      for (int r = 0; r < R; r++) lds[lds_pad(base + (uint32_t)(r * NS))] = v[u * R + r];
+    }
+  }
+  __device__ __forceinline__ static void load_lds(float2 *v, const float2 *lds, int tid) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t j = (uint32_t)(tid + NT * u);
+#pragma unroll
+      for (int r = 0; r < R; r++) v[u * R + r] = lds[lds_pad(j + (uint32_t)(r * (NSUB / R)))];
+    }
+  }
 };
 
-// N = R1 * R2 * R3; LDS exchange through padded float arrays (re, then im)
-template <int R1, int R2, int R3>
-struct FftGeom {
-  static constexpr int N = R1 * R2 * R3, N2 = R2 * R3;
-  static constexpr int U1 = N2, U2 = R1 * R3, U3 = R1 * R2;
-  static constexpr int NT = U1 > U2 ? (U1 > U3 ? U1 : U3) : (U2 > U3 ? U2 : U3);
-  static constexpr int LDS_FLOATS = N2 * (R1 + 1);
+// remaining passes after the first, radices R2.. ; NS = product of radices already applied
+template <int NSUB, int NT, int NS, int... Rs>
+struct StockhamTail;
+template <int NSUB, int NT, int NS>
+struct StockhamTail<NSUB, NT, NS> {
+  static constexpr int RLAST = 16;   // unused
+  __device__ __forceinline__ static void run(float2 *, float2 *, const float2 *, uint32_t, int) {}
+};
+template <int NSUB, int NT, int NS, int R, int... Rs>
+struct StockhamTail<NSUB, NT, NS, R, Rs...> {
+  __device__ __forceinline__ static void run(float2 *v, float2 *lds, const float2 *tw, uint32_t tws, int tid) {
+    using P = StockhamPass<NSUB, NT, R, NS>;
+    P::load_lds(v, lds, tid);
+    __syncthreads();
+    P::compute(v, tw, tws, tid);
+    if (sizeof...(Rs) > 0) {
+      P::store_lds(v, lds, tid);
+      __syncthreads();
+      StockhamTail<NSUB, NT, NS * R, Rs...>::run(v, lds, tw, tws, tid);
+    }
+  }
 };
 
-template <int R1, int R2, int R3, int NTH>
-__global__ __launch_bounds__(NTH) void ofdm_kernel(OfdmDev d, OfdmIO io) {
-  using Gm = FftGeom<R1, R2, R3>;
-  constexpr int N = Gm::N, N2 = Gm::N2, S1 = R1 + 1;
+template <int NSUB> struct FftPlan;
+template <> struct FftPlan<1024> { static constexpr int RL = 4; template <class F> using Tail = StockhamTail<1024, 64, 16, 16, 4>; };
+template <> struct FftPlan<2048> { static constexpr int RL = 8; template <class F> using Tail = StockhamTail<2048, 128, 16, 16, 8>; };
+template <> struct FftPlan<4096> { static constexpr int RL = 16; template <class F> using Tail = StockhamTail<4096, 256, 16, 16, 16>; };
+template <> struct FftPlan<8192> { static constexpr int RL = 2; template <class F> using Tail = StockhamTail<8192, 512, 16, 16, 16, 2>; };
+template <> struct FftPlan<16384> { static constexpr int RL = 4; template <class F> using Tail = StockhamTail<16384, 1024, 16, 16, 16, 4>; };
+
+// One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split), ending with
+// v[u*RL + r] = y[t + NT*(u + (16/RL)*r)].
+template <int NSUB, bool SPLIT>
+__device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const int32_t *map, const float2 *data,
+                                         uint32_t cbase, uint32_t abase, const float *isinc,
+                                         const float2 *tw, uint32_t tws, int tid, int half) {
+  constexpr int NT = NSUB / 16, N = SPLIT ? 2 * NSUB : NSUB;
+  // first pass (R = 16, Ns = 1): gather A[tid + r*NT]; map rows are [even | odd] when SPLIT
+  const int32_t *m = map + (SPLIT ? half * NSUB : 0);
+#pragma unroll
+  for (int c0 = 0; c0 < 16; c0 += 8) {
+    uint32_t off[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      int code = ld_off(m, (uint32_t)(tid + NT * (c0 + u)) * 4u);
+      off[u] = (code >= 0 ? cbase + (uint32_t)code : abase - (uint32_t)code) * 8u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[c0 + u] = ld_off(data, off[u]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (isinc) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      uint32_t k = (uint32_t)(tid + NT * r);
+      if (SPLIT) k = 2 * k + half;
+      float sc = isinc[(k + N / 2) & (N - 1)];
+      v[r].x *= sc;
+      v[r].y *= sc;
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  Dft<16>::run(v);
+  StockhamPass<NSUB, NT, 16, 1>::store_lds(v, lds, tid);
+  __syncthreads();
+  FftPlan<NSUB>::template Tail<void>::run(v, lds, tw, tws, tid);
+}
+
+template <int N>
+struct OfdmShape {
+  static constexpr bool SPLIT = N > 16384;
+  static constexpr int NSUB = SPLIT ? N / 2 : N;
+  static constexpr int NT = NSUB / 16;
+  static constexpr int LDS_BYTES = (NSUB + NSUB / 16) * 8;
+};
+
+template <int N>
+__global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmIO io) {
+  using Sh = OfdmShape<N>;
+  constexpr int NSUB = Sh::NSUB, NT = Sh::NT, RL = FftPlan<NSUB>::RL, UL = 16 / RL;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float *lds = (float *)smem;
+  float2 *lds = (float2 *)smem;
   const int tid = threadIdx.x;
   const int j = blockIdx.x;                       // symbol
   const int f = blockIdx.y;                       // frame within launch
   const int64_t frame = io.first_frame + f;
-  const float2 *cells = io.cells + (int64_t)f * io.cell_stride;
-  const float2 *aux = d.aux + (int64_t)(frame % d.t2frames) * d.aux_len;
+  const float2 *data = io.data;                   // uniform base: all gathers are base + u32 offset
+  const uint32_t cbase = io.cell_off + (uint32_t)f * io.cell_stride;
+  const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
   const int32_t *map = d.bin_map + (int64_t)j * N;
+  const uint32_t tws = Sh::SPLIT ? 2u : 1u;       // sub-transform twiddle = table index * tws
 
-  if (j == 0 && !io.carriers_only) {            // P1 symbol (precomputed), pilotgen:2802-2810
-    float2 *p = io.out + (int64_t)f * io.out_stride;
-    for (int i = tid; i < 2048; i += Gm::NT) p[i] = d.p1[i];
-  }
-  // ---- pass 1: gather R1 inputs at stride N2, R1-point DFT, twiddle, -> LDS (k2, n1)
-  float2 x[R1 > R2 ? (R1 > R3 ? R1 : R3) : (R2 > R3 ? R2 : R3)];
-  const bool act1 = tid < Gm::U1;
-  if (act1) {
-    const int k2 = tid;
-#pragma unroll
-    for (int k1 = 0; k1 < R1; k1++) {
-      int k = k2 + N2 * k1;
-      int code = map[k];
-      float2 v = code >= 0 ? cells[code] : aux[-code - 1];
+  if (io.carriers_only) {                          // test hook: bins in natural order
+    float2 *o = io.out + (int64_t)f * io.out_stride + (int64_t)j * N;
+    for (int k = tid; k < N; k += NT) {
+      const int sub = Sh::SPLIT ? (k & 1) : 0, kk = Sh::SPLIT ? (k >> 1) : k;
+      int code = map[sub * NSUB + kk];
+      float2 v = data[code >= 0 ? cbase + (uint32_t)code : abase - (uint32_t)code];
       if (d.isinc) {
-        float s = d.isinc[(k + N / 2) & (N - 1)];
-        v.x *= s;
-        v.y *= s;
+        float sc = d.isinc[(k + N / 2) & (N - 1)];
+        v.x *= sc;
+        v.y *= sc;
       }
-      x[k1] = v;
+      o[(k + N / 2) & (N - 1)] = v;
     }
-    if (io.carriers_only) {
-      float2 *o = io.out + (int64_t)f * io.out_stride + (int64_t)j * N;
-#pragma unroll
-      for (int k1 = 0; k1 < R1; k1++) {
-        int k = k2 + N2 * k1;
-        o[(k + N / 2) & (N - 1)] = x[k1];
-      }
-    }
+    return;
   }
-  if (io.carriers_only) return;
-  if (act1) {
-    Dft<R1>::run(x);
-#pragma unroll
-    for (int n1 = 1; n1 < R1; n1++) x[n1] = cmulf(x[n1], d.twiddle[n1 * tid]);
+  if (j == 0) {                                   // P1 symbol (precomputed), pilotgen:2802-2810
+    float2 *p = io.out + (int64_t)f * io.out_stride;
+    for (int i = tid; i < 2048; i += NT) p[i] = d.p1[i];
   }
-  // exchange helpers: write component c of x[0..R) at base + i*stride, read back likewise
-#define T2_XCHG(ACT_W, WADDR, CNT_W, ACT_R, RADDR, CNT_R)                        \
-  {                                                                              \
-    float2 y[CNT_R];                                                             \
-    _Pragma("unroll") for (int comp = 0; comp < 2; comp++) {                     \
-      if (ACT_W) {                                                               \
-        _Pragma("unroll") for (int i = 0; i < CNT_W; i++) lds[WADDR] = comp ? x[i].y : x[i].x; \
-      }                                                                          \
-      __syncthreads();                                                           \
-      if (ACT_R) {                                                               \
-        _Pragma("unroll") for (int i = 0; i < CNT_R; i++) {                      \
-          float v = lds[RADDR];                                                  \
-          if (comp) y[i].y = v; else y[i].x = v;                                 \
-        }                                                                        \
-      }                                                                          \
-      __syncthreads();                                                           \
-    }                                                                            \
-    if (ACT_R) {                                                                 \
-      _Pragma("unroll") for (int i = 0; i < CNT_R; i++) x[i] = y[i];             \
-    }                                                                            \
-  }
-  // pass 1 -> 2: A[k2][n1] at k2*S1 + n1; unit (n1 = u % R1, a = u / R1) reads k2 = a + R3*b
-  const bool act2 = tid < Gm::U2;
-  const int n1b = tid % R1, ab = tid / R1;
-  T2_XCHG(act1, tid * S1 + i, R1, act2, (ab + R3 * i) * S1 + n1b, R2)
-  if (act2) {
-    Dft<R2>::run(x);
-#pragma unroll
-    for (int c = 1; c < R2; c++) x[c] = cmulf(x[c], d.twiddle[R1 * c * ab]);
-  }
-  // pass 2 -> 3: B[c][a] (n1 innermost) at (c*R3 + a)*S1 + n1; unit (n1, c = u / R1) reads a
-  const bool act3 = tid < Gm::U3;
-  const int cc = tid / R1;
-  T2_XCHG(act2, (i * R3 + ab) * S1 + n1b, R2, act3, (cc * R3 + i) * S1 + n1b, R3)
-#undef T2_XCHG
-  if (!act3) return;
-  Dft<R3>::run(x);
-  // ---- output: x[n1 + R1*(c + R2*d)] = x[tid + U3*d]; GI = last G samples first
   const int G = d.G;
   float2 *o = io.out + (int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + G);
   const float nrm = d.norm;
+  float2 v[16];
+  sub_ifft<NSUB, Sh::SPLIT>(v, lds, map, data, cbase, abase, d.isinc, d.twiddle, tws, tid, 0);
+  if (Sh::SPLIT) {
+    // x[n] = E[n] + w^n O[n], x[n + NSUB] = E[n] - w^n O[n], w = exp(2 pi i / N).
+    // E is parked in this symbol's own output slots x[n] (same thread re-reads it; the
+    // lines stay in L2) so the odd-bin transform runs within the 128-VGPR budget.
 #pragma unroll
-  for (int dd = 0; dd < R3; dd++) {
-    int n = tid + Gm::U3 * dd;
-    float2 v = make_float2(x[dd].x * nrm, x[dd].y * nrm);
-    o[G + n] = v;
-    if (n >= N - G) o[n - (N - G)] = v;
+    for (int u = 0; u < UL; u++)
+#pragma unroll
+      for (int r = 0; r < RL; r++) {
+        const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
+        st_off(o, ((uint32_t)G + n) * 8u, v[u * RL + r]);
+      }
+    __syncthreads();
+    // launder tid: stops the compiler from keeping the first transform's index/twiddle
+    // arithmetic alive (spilled) for reuse by the second
+    int tid2 = tid;
+    asm volatile("" : "+v"(tid2));
+    sub_ifft<NSUB, Sh::SPLIT>(v, lds, map, data, cbase, abase, d.isinc, d.twiddle, tws, tid2, 1);
+#pragma unroll
+    for (int u = 0; u < UL; u++)
+#pragma unroll
+      for (int r = 0; r < RL; r++) {
+        const int i = u * RL + r;
+        const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
+        const float2 e = ld_off(o, ((uint32_t)G + n) * 8u);
+        float2 t = cmulf(v[i], ld_off(d.twiddle, n * 8u));
+        float2 a = cadd(e, t), b = csub(e, t);
+        a.x *= nrm; a.y *= nrm; b.x *= nrm; b.y *= nrm;
+        st_off(o, ((uint32_t)G + n) * 8u, a);
+        const uint32_t n2 = n + (uint32_t)NSUB;
+        st_off(o, ((uint32_t)G + n2) * 8u, b);
+        if (n2 >= (uint32_t)(N - G)) st_off(o, (n2 - (uint32_t)(N - G)) * 8u, b);
+        if (n >= (uint32_t)(N - G)) st_off(o, (n - (uint32_t)(N - G)) * 8u, a);
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+  } else {
+#pragma unroll
+    for (int u = 0; u < UL; u++)
+#pragma unroll
+      for (int r = 0; r < RL; r++) {
+        const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
+        float2 a = v[u * RL + r];
+        a.x *= nrm; a.y *= nrm;
+        st_off(o, ((uint32_t)G + n) * 8u, a);
+        if (n >= (uint32_t)(N - G)) st_off(o, (n - (uint32_t)(N - G)) * 8u, a);
+      }
   }
 }
 
-template <int R1, int R2, int R3>
+template <int N>
 static hipError_t launch_ofdm_t(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
-  using Gm = FftGeom<R1, R2, R3>;
-  size_t smem = sizeof(float) * Gm::LDS_FLOATS;
+  using Sh = OfdmShape<N>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void *)ofdm_kernel<R1, R2, R3, Gm::NT>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    (void)hipFuncSetAttribute((const void *)ofdm_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Sh::LDS_BYTES);
     attr_set = true;
   }
-  hipLaunchKernelGGL((ofdm_kernel<R1, R2, R3, Gm::NT>), dim3(d.Nsym, io.nframes), dim3(Gm::NT), smem, s, d, io);
+  hipLaunchKernelGGL((ofdm_kernel<N>), dim3(d.Nsym, io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
   return hipGetLastError();
 }
 
 hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
   if (io.nframes <= 0) return hipSuccess;
   switch (d.N) {
-    case 1024: return launch_ofdm_t<8, 8, 16>(d, io, s);
-    case 2048: return launch_ofdm_t<8, 16, 16>(d, io, s);
-    case 4096: return launch_ofdm_t<16, 16, 16>(d, io, s);
-    case 8192: return launch_ofdm_t<16, 16, 32>(d, io, s);
-    case 16384: return launch_ofdm_t<16, 32, 32>(d, io, s);
-    case 32768: return launch_ofdm_t<32, 32, 32>(d, io, s);
+    case 1024: return launch_ofdm_t<1024>(d, io, s);
+    case 2048: return launch_ofdm_t<2048>(d, io, s);
+    case 4096: return launch_ofdm_t<4096>(d, io, s);
+    case 8192: return launch_ofdm_t<8192>(d, io, s);
+    case 16384: return launch_ofdm_t<16384>(d, io, s);
+    case 32768: return launch_ofdm_t<32768>(d, io, s);
     default: return hipErrorInvalidValue;
   }
 }
