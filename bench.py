@@ -148,11 +148,14 @@ def main():
     chain = dvbt2ll.Chain(cfg, max_frames=B, device=local_rank)
     info = chain.info
     per = chain.iq_per_frame
-    # R distinct resident batches per rank, frames disjoint across ranks and batches
+    # R distinct resident batches per rank; frames split contiguously across ranks
+    # (dvbt2ll.distributed.frame_range), disjoint across ranks and batches
+    from dvbt2ll.distributed import frame_range
     R = 2
+    rank_first, _ = frame_range(world * R * B, rank, world)
     ts_dev, ts_meta = [], []
     for r in range(R):
-        first = (rank * R + r) * B
+        first = rank_first + r * B
         ts, base = ts_for_frames(cfg, first, B)
         ts_dev.append(torch.from_numpy(ts).cuda())
         ts_meta.append((first, base, len(ts)))

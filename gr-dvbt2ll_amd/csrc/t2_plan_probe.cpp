@@ -1,0 +1,64 @@
+// t2_plan_probe.cpp -- host-only export of the configuration planner (t2_plan.cpp) for the
+// CPU test suite: lets tests apply the product's composed gather maps with numpy and compare
+// them with the oracle for every parameter combination without a GPU.  Not part of the
+// GPU product library (libdvbt2ll_hip.so); built as gr-dvbt2ll_amd/csrc/_obj/libt2plan_probe.so.
+#include <cstring>
+
+#include "t2_plan.h"
+
+using namespace t2;
+
+extern "C" {
+
+// info: [M, S, aux_len, t2frames, cs, F, N_P2, C_P2, C_DATA, N_FC, C_FC, Lp, D]
+int t2probe_frame(const int *p20, int *info, int32_t *gather_in, int32_t *gather_t, float *aux) {
+  FmParams p{p20[0], p20[1], p20[2], p20[3], p20[4], p20[5], p20[6], p20[7], p20[8], p20[9],
+             p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
+  FramePlan fp;
+  if (build_frame(p, fp)) return -1;
+  int v[13] = {fp.M, fp.S, fp.aux_len, fp.t2frames, fp.cs, fp.F, fp.N_P2, fp.C_P2, fp.C_DATA, fp.N_FC, fp.C_FC,
+               fp.Lp, fp.D};
+  memcpy(info, v, sizeof(v));
+  if (gather_in) memcpy(gather_in, fp.gather_in.data(), fp.gather_in.size() * 4);
+  if (gather_t) memcpy(gather_t, fp.gather_t.data(), fp.gather_t.size() * 4);
+  if (aux) memcpy(aux, fp.aux.data(), fp.aux.size() * 8);
+  return 0;
+}
+
+// info: [Nsym, N, active, G, C_PS, eq]; pilot_values 12 complex; p1 2048 complex; isinc N
+int t2probe_pilot(const int *p12, int *info, int32_t *bin_map, float *pilot_values, float *p1, float *isinc,
+                  float *norm) {
+  PgParams p{p12[0], p12[1], p12[2], p12[3], p12[4], p12[5], p12[6], p12[7], p12[8], p12[9], p12[10], p12[11]};
+  PilotPlan pp;
+  if (build_pilot(p, pp)) return -1;
+  int v[6] = {pp.Nsym, pp.N, pp.active, pp.G, pp.C_PS, pp.eq};
+  memcpy(info, v, sizeof(v));
+  if (bin_map) memcpy(bin_map, pp.bin_map.data(), pp.bin_map.size() * 4);
+  if (pilot_values) memcpy(pilot_values, pp.pilot_values, sizeof(pp.pilot_values));
+  if (p1) memcpy(p1, pp.p1.data(), pp.p1.size() * 8);
+  if (isinc && pp.eq) memcpy(isinc, pp.isinc.data(), pp.isinc.size() * 4);
+  if (norm) *norm = pp.normalization;
+  return 0;
+}
+
+// info: [mode, mod, W, R, cs]; lut 256 complex
+int t2probe_map(int framesize, int rate, int constellation, int rotation, int *info, float *lut) {
+  MapPlan mp;
+  if (build_map(framesize, rate, constellation, rotation, mp)) return -1;
+  int v[5] = {mp.mode, mp.mod, mp.W, mp.R, mp.cs};
+  memcpy(info, v, sizeof(v));
+  if (lut) memcpy(lut, mp.lut, sizeof(mp.lut));
+  return 0;
+}
+
+// info: [kbch, nbch, P, q, nent, chunk, parity_il]; ldpc entries (group << 16 | rotation)
+int t2probe_fec(int framesize, int rate, int constellation, int *info, uint32_t *ent, uint16_t *rowptr) {
+  FecPlan fp;
+  if (build_fec(framesize, rate, constellation, fp)) return -1;
+  int v[7] = {fp.kbch, fp.nbch, fp.nparity, fp.q, (int)fp.ldpc_ent.size(), fp.bch_chunk, fp.parity_interleave};
+  memcpy(info, v, sizeof(v));
+  if (ent) memcpy(ent, fp.ldpc_ent.data(), fp.ldpc_ent.size() * 4);
+  if (rowptr) memcpy(rowptr, fp.ldpc_rowptr.data(), fp.ldpc_rowptr.size() * 2);
+  return 0;
+}
+}

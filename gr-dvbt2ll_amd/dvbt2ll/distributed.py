@@ -1,0 +1,59 @@
+"""Frame sharding across GPUs (one process per GPU, torch.distributed over RCCL).
+
+The chain encodes T2 frame k from closed-form stream state (the absolute FEC-block index fixes
+the BBHEADER, the scrambler restarts per BBFRAME, the previous packet's CRC-8 is recomputed from
+the TS bytes one packet before the frame), so a contiguous run of frames splits across ranks
+with no data-path collective: each rank encodes its own frames from its own slice of the TS.
+The only collective is the optional ordered gather of the IQ to one rank (for a sink that
+wants the whole stream); the benchmark does not use it.
+"""
+import torch
+import torch.distributed as dist
+
+from .configs import ts_for_frames
+
+
+def frame_range(total_frames, rank, world, first_frame=0):
+    """contiguous, ragged-safe split of [first_frame, first_frame + total_frames): (first, count)"""
+    base, extra = divmod(int(total_frames), int(world))
+    count = base + (1 if rank < extra else 0)
+    first = first_frame + rank * base + min(rank, extra)
+    return first, count
+
+
+def gather_frames(local, total_frames, per_frame, group=None, dst=0):
+    """ordered gather of per-rank frame shards (local: [count * per_frame, ...] tensor) to rank dst.
+    Returns the [total_frames * per_frame, ...] tensor on dst, None elsewhere.  Ragged shards are
+    padded to the largest shard for the all_gather."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    counts = [frame_range(total_frames, r, world)[1] for r in range(world)]
+    assert local.shape[0] == counts[rank] * per_frame, "shard size mismatch"
+    cap = max(counts) * per_frame
+    pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    if rank != dst:
+        return None
+    return torch.cat([b[: c * per_frame] for b, c in zip(bufs, counts)], 0)
+
+
+def encode_sharded(chain, first_frame, total_frames, group=None, gather=True, seed=1):
+    """each rank encodes its contiguous share of the frames on its own GPU (synthetic TS slice
+    generated for exactly those frames); optional ordered gather of the IQ to rank 0."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    first, count = frame_range(total_frames, rank, world, first_frame)
+    per = chain.iq_per_frame
+    iq = torch.zeros((count * per, 2), dtype=torch.float32, device="cuda")
+    if count:
+        if count > chain.max_frames:
+            raise ValueError("shard of %d frames exceeds chain max_frames %d" % (count, chain.max_frames))
+        ts, base = ts_for_frames(chain.cfg, first, count, seed)
+        ts_d = torch.from_numpy(ts).cuda()
+        chain.run_device(ts_d.data_ptr(), base, len(ts), first, count, iq.data_ptr(),
+                         torch.cuda.current_stream().cuda_stream)
+    if not gather:
+        return iq
+    return gather_frames(iq, total_frames, per, group)

@@ -1,0 +1,83 @@
+"""ctypes binding of the host-only planner probe (gr-dvbt2ll_amd/csrc/t2_plan_probe.cpp).
+
+It exposes the product's configuration-time gather maps so CPU tests can check them against
+the oracle for the whole parameter space; the GPU kernels that consume them are checked by
+the -m gpu tests."""
+import ctypes
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "gr-dvbt2ll_amd" / "csrc"
+LIB = CSRC / "_obj" / "libt2plan_probe.so"
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        if not LIB.exists():
+            subprocess.run(["make", "-s", "-C", str(CSRC), "probe"], check=True)
+        L = ctypes.CDLL(str(LIB))
+        vp = ctypes.c_void_p
+        L.t2probe_frame.argtypes = [vp, vp, vp, vp, vp]
+        L.t2probe_pilot.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.t2probe_map.argtypes = [ctypes.c_int] * 4 + [vp, vp]
+        L.t2probe_fec.argtypes = [ctypes.c_int] * 3 + [vp, vp, vp]
+        _L = L
+    return _L
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def frame_plan(fm_args):
+    p = np.array(fm_args, np.int32)
+    info = np.zeros(13, np.int32)
+    if lib().t2probe_frame(_p(p), _p(info), None, None, None):
+        return None
+    M, S, aux_len, t2frames = (int(x) for x in info[:4])
+    gin = np.zeros(M, np.int32)
+    gt = np.zeros(M, np.int32)
+    aux = np.zeros(t2frames * aux_len, np.complex64)
+    assert lib().t2probe_frame(_p(p), _p(info), _p(gin), _p(gt), _p(aux)) == 0
+    keys = ["M", "S", "aux_len", "t2frames", "cs", "F", "N_P2", "C_P2", "C_DATA", "N_FC", "C_FC", "Lp", "D"]
+    d = dict(zip(keys, (int(x) for x in info)))
+    d.update(gather_in=gin, gather_t=gt, aux=aux.reshape(t2frames, aux_len))
+    return d
+
+
+def pilot_plan(pg_args):
+    p = np.array(pg_args, np.int32)
+    info = np.zeros(6, np.int32)
+    if lib().t2probe_pilot(_p(p), _p(info), None, None, None, None, None):
+        return None
+    Nsym, N = int(info[0]), int(info[1])
+    bm = np.zeros(Nsym * N, np.int32)
+    pv = np.zeros(12, np.complex64)
+    p1 = np.zeros(2048, np.complex64)
+    isinc = np.zeros(N, np.float32)
+    norm = np.zeros(1, np.float32)
+    assert lib().t2probe_pilot(_p(p), _p(info), _p(bm), _p(pv), _p(p1), _p(isinc), _p(norm)) == 0
+    return dict(Nsym=Nsym, N=N, active=int(info[2]), G=int(info[3]), C_PS=int(info[4]), eq=int(info[5]),
+                bin_map=bm.reshape(Nsym, N), pilot_values=pv, p1=p1, isinc=isinc, norm=float(norm[0]))
+
+
+def map_plan(framesize, rate, constellation, rotation):
+    info = np.zeros(5, np.int32)
+    lut = np.zeros(256, np.complex64)
+    assert lib().t2probe_map(framesize, rate, constellation, rotation, _p(info), _p(lut)) == 0
+    return dict(zip(["mode", "mod", "W", "R", "cs"], (int(x) for x in info)), lut=lut)
+
+
+def fec_plan(framesize, rate, constellation=3):
+    info = np.zeros(7, np.int32)
+    assert lib().t2probe_fec(framesize, rate, constellation, _p(info), None, None) == 0
+    kbch, nbch, P, q, nent, chunk, pil = (int(x) for x in info)
+    ent = np.zeros(nent, np.uint32)
+    rp = np.zeros(q + 1, np.uint16)
+    assert lib().t2probe_fec(framesize, rate, constellation, _p(info), _p(ent), _p(rp)) == 0
+    return dict(kbch=kbch, nbch=nbch, P=P, q=q, ent=ent, rowptr=rp, chunk=chunk, parity_il=pil)

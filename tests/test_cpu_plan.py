@@ -1,0 +1,169 @@
+"""CPU: the product's host planner (composed gather maps, L1/dummy/pilot tables, LDPC
+schedule) against the oracle, across the parameter space.  No GPU needed."""
+import itertools
+
+import numpy as np
+import pytest
+
+from dvbt2ll import enums as E
+from dvbt2ll.configs import CONFIGS, T2Config
+import oracle_lib as O
+import plan_probe as PP
+
+rng = np.random.default_rng(7)
+
+
+def rand_cells(n):
+    return (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64)
+
+
+def fitting_fecblocks(cfg):
+    """largest fecblocks the frame can carry (the reference warns and overflows beyond it)"""
+    lo, hi = 1, 4000
+    if PP.frame_plan(cfg.with_(fecblocks=1, tiblocks=min(cfg.tiblocks, 1)).fm_args()) is None:
+        return None
+    while lo < hi:
+        mid = (lo + hi + 1) // 2
+        if PP.frame_plan(cfg.with_(fecblocks=mid, tiblocks=min(cfg.tiblocks, mid)).fm_args()) is None:
+            hi = mid - 1
+        else:
+            lo = mid
+    return lo
+
+
+def _apply(gmap, src, aux):
+    out = np.where(gmap >= 0, src[np.clip(gmap, 0, None)], aux[np.clip(-gmap - 1, 0, None)])
+    return out.astype(np.complex64)
+
+
+BASE = CONFIGS["cfg1"]
+GRID = [
+    # (name, overrides)
+    ("4k_grc", {}),
+    ("4k_l1bpsk", dict(l1constellation=E.L1_MOD_BPSK)),
+    ("4k_l1qpsk_ti0", dict(l1constellation=E.L1_MOD_QPSK, tiblocks=0)),
+    ("4k_l1_16qam_pp2", dict(l1constellation=E.L1_MOD_16QAM, pilotpattern=E.PILOT_PP2, guardinterval=E.GI_1_8)),
+    ("2k_pp3_qpsk_short", dict(fftsize=E.FFTSIZE_2K, pilotpattern=E.PILOT_PP3, constellation=E.MOD_QPSK, rate=E.C1_3,
+                               guardinterval=E.GI_1_4, numdatasyms=6)),
+    ("1k_pp1_16qam", dict(fftsize=E.FFTSIZE_1K, pilotpattern=E.PILOT_PP1, constellation=E.MOD_16QAM, rate=E.C2_5,
+                          guardinterval=E.GI_1_8, numdatasyms=8)),
+    ("8k_pp8_ext_64qam", dict(fftsize=E.FFTSIZE_8K, pilotpattern=E.PILOT_PP8, carriermode=E.CARRIERS_EXTENDED,
+                              constellation=E.MOD_64QAM, guardinterval=E.GI_1_128, numdatasyms=4)),
+    ("8k_pp2_miso_tx2", dict(fftsize=E.FFTSIZE_8K, pilotpattern=E.PILOT_PP2, preamble=E.PREAMBLE_T2_MISO,
+                             misogroup=E.MISO_TX2, guardinterval=E.GI_1_8, numdatasyms=5)),
+    ("16k_pp5_tr", dict(fftsize=E.FFTSIZE_16K, pilotpattern=E.PILOT_PP5, paprmode=E.PAPR_TR, numdatasyms=3,
+                        guardinterval=E.GI_1_8)),
+    ("16k_pp6_ext_v131", dict(fftsize=E.FFTSIZE_16K, pilotpattern=E.PILOT_PP6, carriermode=E.CARRIERS_EXTENDED,
+                              version=E.VERSION_131, l1scrambled=E.L1_SCRAMBLED_ON, reservedbiasbits=E.RESERVED_ON,
+                              numdatasyms=3, guardinterval=E.GI_1_32)),
+    ("32k_pp4_ext_cfg3like", dict(fftsize=E.FFTSIZE_32K, pilotpattern=E.PILOT_PP4, carriermode=E.CARRIERS_EXTENDED,
+                                  guardinterval=E.GI_1_16, numdatasyms=3, framesize=E.FECFRAME_NORMAL, rate=E.C3_5)),
+    ("32k_pp2_miso_tx2_tr", dict(fftsize=E.FFTSIZE_32K, pilotpattern=E.PILOT_PP2, preamble=E.PREAMBLE_T2_MISO,
+                                 misogroup=E.MISO_TX2, paprmode=E.PAPR_TR, guardinterval=E.GI_1_8, numdatasyms=3,
+                                 framesize=E.FECFRAME_NORMAL, rate=E.C2_3)),
+    ("32k_pp7_eq", dict(fftsize=E.FFTSIZE_32K, pilotpattern=E.PILOT_PP7, guardinterval=E.GI_1_128, numdatasyms=2,
+                        equalization=E.EQUALIZATION_ON, bandwidth=E.BANDWIDTH_6_0_MHZ, framesize=E.FECFRAME_NORMAL,
+                        rate=E.C5_6)),
+    ("8k_t2gi_pp4_tr_ext", dict(fftsize=E.FFTSIZE_8K_T2GI, pilotpattern=E.PILOT_PP4, paprmode=E.PAPR_BOTH,
+                                carriermode=E.CARRIERS_EXTENDED, guardinterval=E.GI_19_256, numdatasyms=4)),
+]
+
+
+def grid_cfg(over):
+    cfg = BASE.with_(**over)
+    fb = fitting_fecblocks(cfg)
+    assert fb, "config cannot carry a FEC block"
+    fb = max(1, (fb * 3) // 4)
+    return cfg.with_(fecblocks=fb, tiblocks=min(cfg.tiblocks, fb))
+
+
+@pytest.mark.parametrize("name,over", GRID, ids=[g[0] for g in GRID])
+def test_framemapper_map_matches_oracle(name, over):
+    cfg = grid_cfg(over)
+    plan = PP.frame_plan(cfg.fm_args())
+    fm = O.FM(*cfg.fm_args())
+    assert (plan["M"], plan["S"]) == (fm.mapped_items, fm.stream_items)
+    for frame in range(min(3, cfg.t2frames + 1)):
+        cells = rand_cells(plan["S"])
+        want = fm.work(cells)
+        got = _apply(plan["gather_in"], cells, plan["aux"][frame % plan["t2frames"]])
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("name,over", GRID, ids=[g[0] for g in GRID])
+def test_pilot_map_matches_oracle(name, over):
+    cfg = grid_cfg(over)
+    plan = PP.pilot_plan(cfg.pg_args())
+    pg = O.PG(*cfg.pg_args())
+    assert plan["active"] == pg.active_items
+    cells = rand_cells(plan["active"])
+    want = pg.carriers(cells)
+    aux = np.zeros(16, np.complex64)
+    aux[1:13] = plan["pilot_values"]
+    N = plan["N"]
+    k = np.arange(N)
+    for j in range(plan["Nsym"]):
+        row = _apply(plan["bin_map"][j], cells, aux)       # IFFT-input order k
+        bins = np.empty(N, np.complex64)
+        bins[(k + N // 2) % N] = row
+        if plan["eq"]:
+            bins = (bins.view(np.float32).reshape(-1, 2) * plan["isinc"][:, None]).view(np.complex64).reshape(-1)
+        np.testing.assert_array_equal(bins.view(np.uint32), want[j].view(np.uint32), err_msg="symbol %d" % j)
+    assert abs(plan["norm"] - pg.normalization) == 0
+    assert np.abs(plan["p1"] - pg.p1()).max() < 2e-6
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+def test_benchmark_configs_plan(name):
+    cfg = CONFIGS[name]
+    fplan = PP.frame_plan(cfg.fm_args())
+    pplan = PP.pilot_plan(cfg.pg_args())
+    assert fplan["M"] == pplan["active"]
+    # chain composition: every mapped data cell points into the time-interleaver input once
+    t = fplan["gather_t"]
+    data = np.sort(t[t >= 0])
+    np.testing.assert_array_equal(data, np.arange(fplan["S"]))
+    gi = fplan["gather_in"]
+    np.testing.assert_array_equal(np.sort(gi[gi >= 0]), np.arange(fplan["S"]))
+
+
+ALL_CODES = [(1, r) for r in range(6)] + [(0, r) for r in range(8)]
+
+
+@pytest.mark.parametrize("framesize,rate", ALL_CODES)
+def test_ldpc_quasi_cyclic_schedule_matches_oracle(framesize, rate):
+    """the GPU formulation: parity row a = XOR of info groups rotated by b, prefix-XOR over rows,
+    exclusive bit-prefix of the column parities -> natural parity p[a + q c]"""
+    plan = PP.fec_plan(framesize, rate)
+    nbch, q = plan["nbch"], plan["q"]
+    nldpc = 64800 if framesize else 16200
+    info = rng.integers(0, 2, nbch, dtype=np.uint8)
+    want = O.LDPC(framesize, rate).work(info, 1)[nbch:]
+    groups = info.reshape(-1, 360)
+    rows = np.zeros((q, 360), np.uint8)
+    for a in range(q):
+        for e in plan["ent"][plan["rowptr"][a]:plan["rowptr"][a + 1]]:
+            g, b = int(e) >> 16, int(e) & 0xFFFF
+            rows[a] ^= np.roll(groups[g], b)          # column c <- d_g[(c - b) mod 360]
+    R = np.bitwise_xor.accumulate(rows, axis=0)
+    V = R[-1]
+    W = np.concatenate([[0], np.bitwise_xor.accumulate(V)[:-1]]).astype(np.uint8)
+    P = R ^ W[None, :]
+    got = P.T.reshape(-1)                              # natural index a + q c
+    assert got.size == nldpc - nbch
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("const,rot", list(itertools.product(range(4), range(2))))
+def test_qam_tables(const, rot):
+    """constellation LUT: unit mean energy, Gray structure, rotation angle (interleavermod:169-253)"""
+    plan = PP.map_plan(1, E.C3_5, const, rot)
+    n = 1 << plan["mod"]
+    lut = plan["lut"][:n].astype(np.complex128)
+    assert abs(np.mean(np.abs(lut) ** 2) - 1) < 1e-6
+    deg = {0: 29.0, 1: 16.8, 2: 8.6, 3: 3.576334375}[const]
+    unrot = lut * np.exp(-1j * np.deg2rad(deg)) if rot else lut
+    # axis-aligned square grid after de-rotation
+    assert np.allclose(np.abs(unrot.real), np.abs(unrot.real).round(6), atol=1e-5)
+    levels = np.unique(np.round(unrot.real * np.sqrt({0: 2, 1: 10, 2: 42, 3: 170}[const]), 4))
+    assert len(levels) == int(np.sqrt(n)) * (2 if const == 0 else 1) // (2 if const == 0 else 1)
