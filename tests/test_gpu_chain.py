@@ -25,10 +25,7 @@ def oracle_chain(cfg, nframes):
     return out, pg
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg3"])
-def test_chain_iq_matches_oracle(gpu, name):
-    cfg = CONFIGS[name]
-    nframes = 3 if name == "cfg1" else 2
+def _check_chain(cfg, nframes):
     ref, pg = oracle_chain(cfg, nframes)
     ch = dvbt2ll.Chain(cfg, max_frames=nframes)
     iq = ch.run(0, nframes)
@@ -43,6 +40,22 @@ def test_chain_iq_matches_oracle(gpu, name):
             y = f[2048 + j * (N + G): 2048 + (j + 1) * (N + G)]
             rms = np.sqrt(np.mean(np.abs(want) ** 2))
             assert np.abs(y - want).max() <= 2e-5 * rms, (k, j, np.abs(y - want).max() / rms)
+        assert np.abs(f[:2048] - pg.p1()).max() <= 1e-5
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+def test_chain_iq_matches_oracle(gpu, name):
+    _check_chain(CONFIGS[name], 3 if name == "cfg1" else (2 if name == "cfg3" else 1))
+
+
+from test_cpu_plan import GRID, grid_cfg  # noqa: E402
+
+
+@pytest.mark.parametrize("name,over", GRID, ids=[g[0] for g in GRID])
+def test_chain_feature_grid(gpu, name, over):
+    """every FFT size, N_P2 > 1, MISO TX2, PAPR TR, extended carriers, EQ, v1.3.1 L1, L1 BPSK..16QAM"""
+    cfg = grid_cfg(over)
+    _check_chain(cfg, min(2, cfg.t2frames + 1))
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg3"])
