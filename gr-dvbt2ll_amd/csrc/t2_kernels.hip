@@ -133,22 +133,25 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     if (!d.hem) {
       const int first_slot = (188 - count0) % 188;
       const int nslots = first_slot < npay ? (npay - 1 - first_slot) / 188 + 1 : 0;
-      const int m = tid >> 3, k = tid & 7;
-      uint8_t part = 0;
-      int64_t p = pos0 + first_slot + 188 * (int64_t)m;   // sync position
-      bool active = m < nslots && p > 0;
-      if (active) {
-        int64_t b0 = p - 187 + 24 * k - io.ts_base;
-        int n = min(24, 187 - 24 * k);
-        uint8_t c = 0;
-        for (int i = 0; i < n; i++) c = crc8[io.in[b0 + i] ^ c];
-        part = crcsh[k * 256 + c];
+      // up to 36 sync slots per block (5/6 normal): 32 packets per pass
+      for (int m0 = 0; m0 < nslots; m0 += FEC_THREADS / 8) {
+        const int m = m0 + (tid >> 3), k = tid & 7;
+        uint8_t part = 0;
+        int64_t p = pos0 + first_slot + 188 * (int64_t)m;   // sync position
+        bool active = m < nslots && p > 0;
+        if (active) {
+          int64_t b0 = p - 187 + 24 * k - io.ts_base;
+          int n = min(24, 187 - 24 * k);
+          uint8_t c = 0;
+          for (int i = 0; i < n; i++) c = crc8[io.in[b0 + i] ^ c];
+          part = crcsh[k * 256 + c];
+        }
+        uint32_t v = part;
+        v ^= __shfl_xor(v, 1);
+        v ^= __shfl_xor(v, 2);
+        v ^= __shfl_xor(v, 4);
+        if (k == 0 && m < nslots) syncv[m] = active ? (uint8_t)v : 0;
       }
-      uint32_t v = part;
-      v ^= __shfl_xor(v, 1);
-      v ^= __shfl_xor(v, 2);
-      v ^= __shfl_xor(v, 4);
-      if (k == 0 && m < nslots) syncv[m] = active ? (uint8_t)v : 0;
       __syncthreads();
       for (int j = tid; j < npay; j += FEC_THREADS) {
         int64_t pos = pos0 + j;

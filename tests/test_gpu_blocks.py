@@ -7,7 +7,8 @@ import numpy as np
 import pytest
 
 import dvbt2ll
-from dvbt2ll.configs import CONFIGS, ts_for_frames
+from dvbt2ll import enums as E
+from dvbt2ll.configs import CONFIGS, ts_for_frames, ts_packets
 import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
@@ -21,7 +22,7 @@ def _ts(cfg, nframes=1):
     return ts
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg3", "cfg4"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_bbheaderbch_bit_exact(gpu, name):
     cfg = CONFIGS[name]
     ts = _ts(cfg)
@@ -54,7 +55,7 @@ def test_bbheaderbch_split_calls(gpu, name):
         off += cons
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg3", "cfg2"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_ldpc_bit_exact(gpu, name):
     cfg = CONFIGS[name]
     bb = O.BB(*cfg.bb_args())
@@ -123,3 +124,45 @@ def test_pilotgen_carriers_bit_exact_and_iq(gpu, name):
         y = iq[2048 + j * (N + G): 2048 + (j + 1) * (N + G)]
         rms = np.sqrt(np.mean(np.abs(ref) ** 2))
         assert np.abs(y - ref).max() <= IQ_RTOL * rms * 10, (j, np.abs(y - ref).max() / rms)
+
+
+ALL_CODES = [(1, r) for r in range(6)] + [(0, r) for r in range(8)]
+MODES = [(E.INPUTMODE_NORMAL, E.INBAND_OFF), (E.INPUTMODE_HIEFF, E.INBAND_OFF), (E.INPUTMODE_NORMAL, E.INBAND_ON)]
+
+
+@pytest.mark.parametrize("framesize,rate", ALL_CODES)
+@pytest.mark.parametrize("mode,inband", MODES, ids=["nm", "hem", "nm-inband"])
+def test_bbheader_ldpc_all_codes(gpu, framesize, rate, mode, inband):
+    """every FECFRAME size x code rate, normal / high-efficiency mode, in-band type B:
+    BBHEADER+CRC-8+scrambler+BCH and LDPC bit-exact, state carried across two calls"""
+    cfg = CONFIGS["cfg1"].with_(framesize=framesize, rate=rate, inputmode=mode, inband=inband, fecblocks=3)
+    ts = ts_packets(0, 600)
+    ref = O.BB(*cfg.bb_args())
+    blk = dvbt2ll.bbheaderbch_bb(*cfg.bb_args())
+    off = 0
+    for calls in (2, 5):
+        want, cons = ref.work(ts[off:], calls)
+        got = np.zeros_like(want)
+        blk.general_work([ts[off:]], [got])
+        assert blk.last_consumed == cons
+        np.testing.assert_array_equal(got, want)
+        off += cons
+    cw_want = O.LDPC(framesize, rate).work(want, 5)
+    ld = dvbt2ll.ldpc_bb(framesize, rate)
+    cw = np.zeros_like(cw_want)
+    ld.general_work([want], [cw])
+    np.testing.assert_array_equal(cw, cw_want)
+
+
+@pytest.mark.parametrize("framesize,rate", ALL_CODES)
+@pytest.mark.parametrize("const", [E.MOD_QPSK, E.MOD_16QAM, E.MOD_64QAM, E.MOD_256QAM])
+def test_interleavermod_all_codes(gpu, framesize, rate, const):
+    rng = np.random.default_rng(1000 * framesize + 10 * rate + const)
+    nldpc = 64800 if framesize else 16200
+    cw = rng.integers(0, 2, 3 * nldpc, dtype=np.uint8)
+    for rot in (E.ROTATION_OFF, E.ROTATION_ON):
+        args = (framesize, rate, const, rot)
+        want = O.IM(*args).work(cw, 3)
+        got = np.zeros_like(want)
+        dvbt2ll.interleavermod_bc(*args).general_work([cw], [got])
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))

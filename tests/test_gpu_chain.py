@@ -25,6 +25,28 @@ def oracle_chain(cfg, nframes):
     return out, pg
 
 
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+def test_chain_cells_match_oracle(gpu, name):
+    """stage check inside the fused chain: the cells buffer (time-interleaver input order, after
+    FEC + bit interleave + QAM + cell interleave) equals the oracle's, via the planner's maps"""
+    import plan_probe as PP
+    cfg = CONFIGS[name]
+    ts, base = ts_for_frames(cfg, 0, 1)
+    F = cfg.fecblocks
+    bits, _ = O.BB(*cfg.bb_args()).work(ts, F)
+    cells = O.IM(*cfg.im_args()).work(O.LDPC(cfg.framesize, cfg.rate).work(bits, F), F)
+    plan = PP.frame_plan(cfg.fm_args())
+    gi, gt = plan["gather_in"], plan["gather_t"]
+    sel = gt >= 0
+    want = np.zeros(plan["S"], np.complex64)
+    want[gt[sel]] = cells[gi[sel]]
+    ch = dvbt2ll.Chain(cfg, max_frames=1)
+    ch.run(0, 1)
+    got = ch.debug_cells(plan["S"])
+    bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
+    assert bad.size == 0, (bad.size, bad[:10], bad[:10] // plan["cs"])
+
+
 def _check_chain(cfg, nframes):
     ref, pg = oracle_chain(cfg, nframes)
     ch = dvbt2ll.Chain(cfg, max_frames=nframes)
