@@ -399,19 +399,11 @@ static PgParams to_pg(const dvbt2ll_pilotgenp1insert_params &p) {
 struct OfdmTables {
   DevBuf map, tw, isinc, p1;
   OfdmDev dev{};
-  // bin_map rows are IFFT-input ordered; for N > 16K the kernel runs two N/2 transforms over
-  // even and odd bins, so each row is stored as [even bins | odd bins]
-  int init(const PilotPlan &pp, const std::vector<int32_t> &bin_map, int aux_len, int t2frames) {
+  // stored_map: per-symbol rows in the kernel's read order (ofdm_stored_rows: [even | odd]
+  // bins when N > 16K, where the kernel runs two N/2 transforms)
+  int init(const PilotPlan &pp, const std::vector<int32_t> &stored_map, int aux_len, int t2frames) {
     int r;
-    const int N = pp.N;
-    if (N > 16384) {
-      std::vector<int32_t> m(bin_map.size());
-      for (int j = 0; j < pp.Nsym; j++)
-        for (int k = 0; k < N; k++) m[(size_t)j * N + (k & 1) * (N / 2) + (k >> 1)] = bin_map[(size_t)j * N + k];
-      if ((r = upload(map, m))) return r;
-    } else if ((r = upload(map, bin_map))) {
-      return r;
-    }
+    if ((r = upload(map, stored_map))) return r;
     if ((r = upload(tw, pp.twiddle)) || (r = upload(p1, pp.p1))) return r;
     if (pp.eq && (r = upload(isinc, pp.isinc))) return r;
     dev.bin_map = map.as<int32_t>();
@@ -443,7 +435,7 @@ extern "C" int dvbt2ll_pilotgenp1insert_create(const dvbt2ll_pilotgenp1insert_pa
   if (r) return r;
   std::vector<cf32> aux(PG_AUX_PAD, cf32{0.f, 0.f});
   for (int i = 0; i < 12; i++) aux[AUX_PILOT0 + i] = h->plan.pilot_values[i];
-  if ((r = h->ofdm.init(h->plan, h->plan.bin_map, PG_AUX_PAD, 1))) return r;
+  if ((r = h->ofdm.init(h->plan, ofdm_stored_rows(h->plan.N, h->plan.Nsym, h->plan.bin_map), PG_AUX_PAD, 1))) return r;
   if (h->din.ensure((size_t)(PG_AUX_PAD + h->plan.active) * 8)) return DVBT2LL_ENOMEM;
   HIP_TRY(hipMemcpy(h->din.p, aux.data(), PG_AUX_PAD * 8, hipMemcpyHostToDevice));
   h->out_items = h->plan.Nsym * (h->plan.N + h->plan.G) + 2048;
@@ -505,7 +497,7 @@ struct dvbt2ll_chain {
   FramePlan frame;
   PilotPlan pilot;
   OfdmTables ofdm;
-  DevBuf cw, cells, perm, shift, ts_tmp, iq_tmp;
+  DevBuf cw, cells, perm, shift, inv, sym_d0, sym_n, ts_tmp, iq_tmp;
   int max_frames = 0;
   int64_t aux_pad = 0;       // cells buffer = [aux variants (aux_pad elements) | frame cells]
   int64_t cw_stride = 0;
@@ -568,17 +560,24 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   h->map.dev.ci_perm = h->perm.as<int16_t>();
   h->map.dev.ci_shift = h->shift.as<int32_t>();
   h->map.dev.F = h->frame.F;
-  // compose: IFFT bin -> mapped cell -> time-interleaver-input cell (or aux entry)
+  h->map.dev.ti_on = h->frame.ti_on;
+  h->map.dev.ti_small = h->frame.ti_small;
+  h->map.dev.ti_big = h->frame.ti_big;
+  h->map.dev.ti_nsmall = h->frame.ti_nsmall;
+  // OFDM side: aux bins from cmap, data cells streamed per symbol and scattered through inv
+  ChainLayout layout;
+  if (build_chain_layout(h->frame, h->pilot, layout)) return DVBT2LL_EINVAL;
+  if ((r = upload(h->inv, layout.inv)) || (r = upload(h->sym_d0, layout.sym_d0)) ||
+      (r = upload(h->sym_n, layout.sym_n)))
+    return r;
   const PilotPlan &pp = h->pilot;
-  std::vector<int32_t> cmap(pp.bin_map.size());
-  for (size_t i = 0; i < cmap.size(); i++) {
-    int32_t c = pp.bin_map[i];
-    cmap[i] = c >= 0 ? h->frame.gather_t[c] : c;
-  }
   std::vector<cf32> aux = h->frame.aux;
   for (int v = 0; v < h->frame.t2frames; v++)
     for (int i = 0; i < 12; i++) aux[(size_t)v * h->frame.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
-  if ((r = h->ofdm.init(pp, cmap, h->frame.aux_len, h->frame.t2frames))) return r;
+  if ((r = h->ofdm.init(pp, layout.cmap, h->frame.aux_len, h->frame.t2frames))) return r;
+  h->ofdm.dev.inv = h->inv.as<uint16_t>();
+  h->ofdm.dev.sym_d0 = h->sym_d0.as<int32_t>();
+  h->ofdm.dev.sym_n = h->sym_n.as<int32_t>();
   h->aux_pad = ((int64_t)aux.size() + 63) / 64 * 64;
   h->cw_stride = ((h->fec.plan.nldpc / 8) + 255) / 256 * 256;
   h->iq_per_frame = (int64_t)pp.Nsym * (pp.N + pp.G) + 2048;

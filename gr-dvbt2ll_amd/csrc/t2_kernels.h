@@ -41,6 +41,7 @@ struct MapDev {
   const int16_t *ci_perm;  // cs (chain only)
   const int32_t *ci_shift; // F  (chain only)
   int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
+  int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
   uint8_t twist[16], mux[16];
 };
 struct MapIO {
@@ -49,13 +50,17 @@ struct MapIO {
   float2 *out;         // cells
   int nblocks;
   int packed_in;       // 1: chain layout; 0: unpacked bits (interleavermod block)
-  int apply_ci;        // 1: write in time-interleaver input order
+  int apply_ci;        // 1 (chain): cell + time interleave into the frame data region
 };
 
 // ---------------------------------------------------------------- OFDM symbols
 struct OfdmDev {
-  const int32_t *bin_map;   // Nsym x N (IFFT input order): >= 0 cell index, < 0 aux entry
-  const float2 *twiddle;    // N
+  const int32_t *bin_map;   // Nsym x N (stored row order): >= 0 cell index, < 0 aux entry
+  // chain (scatter) mode: symbol j's cells are the slots [sym_d0[j], +sym_n[j]), slot s goes to
+  // stored bin inv[s]; null -> gather mode (bin_map >= 0 codes are read per bin)
+  const uint16_t *inv;
+  const int32_t *sym_d0, *sym_n;
+  const float2 *twiddle;    // 128 + N/128: two-level table (PilotPlan::twiddle)
   const float *isinc;       // N or null
   const float2 *p1;         // 2048
   int N, G, Nsym, aux_len, t2frames;

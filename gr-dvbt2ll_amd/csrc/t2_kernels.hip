@@ -375,10 +375,17 @@ __host__ __device__ inline int map_smem(int cs, int cw_bytes, int apply_ci) {
   return 2048 + map_idx_bytes(cs) + ((region + 15) & ~15);
 }
 
+// XCD-aware block order: the hardware deals consecutive workgroups round-robin over the 8 XCDs;
+// give each XCD a contiguous run of logical blocks so neighbours share its L2.
+__device__ __forceinline__ int xcd_major(int i, int n) {
+  const int q = n >> 3;
+  return i < (q << 3) ? (i & 7) * q + (i >> 3) : i;
+}
+
 __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
-  const int blk = blockIdx.x;
+  const int blk = xcd_major(blockIdx.x, gridDim.x);
   float2 *lut = (float2 *)smem;
   uint8_t *idx = smem + 2048;
   uint8_t *cw = smem + 2048 + map_idx_bytes(d.cs);
@@ -431,25 +438,54 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
     }
   }
   __syncthreads();
-  // ---- constellation + cyclic Q delay; optional cell interleaver via LDS
-  const int r_in_frame = blk % d.F;
-  const int shift = io.apply_ci ? d.ci_shift[r_in_frame] : 0;
-  float2 *dst = io.out + (int64_t)blk * cs;
+  // ---- constellation + cyclic Q delay; chain: cell interleaver (framemapper:1973-1998) into
+  //      LDS, then the time interleaver (framemapper:1999-2028) as the store pattern: FEC block r
+  //      of its TI block fills columns 5(r-r0)..+4 of a rows x 5nb array read row by row, so
+  //      cells land in the frame data region in transmission order.
+  if (!io.apply_ci) {
+    float2 *dst = io.out + (int64_t)blk * cs;
+    for (int j = tid; j < cs; j += MAP_THREADS) {
+      float2 v = lut[idx[j]];
+      if (d.rotation) v.y = lut[idx[j == 0 ? cs - 1 : j - 1]].y;
+      dst[j] = v;
+    }
+    return;
+  }
+  const int r = blk % d.F;
+  const int shift = d.ci_shift[r];
+  float2 *dst = io.out + (int64_t)(blk - r) * cs;      // frame data region
+  int r0 = r, nb = 1;
+  if (d.ti_on) {
+    const int ns = d.ti_nsmall * d.ti_small;
+    if (r < ns) { r0 = r - r % d.ti_small; nb = d.ti_small; }
+    else { r0 = r - (r - ns) % d.ti_big; nb = d.ti_big; }
+  }
+  const int rows = cs / 5, cols = 5 * nb;
+  const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
+  auto ti_dst = [&](int t) -> int64_t {
+    if (!d.ti_on) return (int64_t)r * cs + t;
+    const int e = t / rows, row = t - e * rows;
+    return base + (int64_t)row * cols + e;
+  };
   for (int j = tid; j < cs; j += MAP_THREADS) {
     float2 v = lut[idx[j]];
     if (d.rotation) v.y = lut[idx[j == 0 ? cs - 1 : j - 1]].y;
-    if (io.apply_ci) {
-      int t = d.ci_perm[j] + shift;
-      t -= t >= cs ? cs : 0;
-      if (lds_stage) stage[t] = v;
-      else dst[t] = v;   // QPSK normal: 259 KB of cells do not fit LDS, scatter directly
-    } else {
-      dst[j] = v;
-    }
+    int t = d.ci_perm[j] + shift;
+    t -= t >= cs ? cs : 0;
+    if (lds_stage) stage[t] = v;
+    else dst[ti_dst(t)] = v;   // QPSK normal: 259 KB of cells do not fit LDS, scatter directly
   }
-  if (io.apply_ci && lds_stage) {
+  if (lds_stage) {
     __syncthreads();
-    for (int j = tid; j < cs; j += MAP_THREADS) dst[j] = stage[j];
+    if (!d.ti_on) {
+      for (int j = tid; j < cs; j += MAP_THREADS) dst[(int64_t)r * cs + j] = stage[j];
+    } else {
+      // row-major over (row, e): 5 consecutive cells (40 B) per TI row
+      for (int j = tid; j < cs; j += MAP_THREADS) {
+        const int row = j / 5, e = j - 5 * row;
+        dst[base + (int64_t)row * cols + e] = stage[e * rows + row];
+      }
+    }
   }
 }
 
@@ -533,16 +569,20 @@ struct Dft {
 // thread t ends with n = t + NT*m, m = u + (16/R_last)*r.
 __device__ __forceinline__ uint32_t lds_pad(uint32_t a) { return a + (a >> 4); }
 
-// v[r] *= w^(r * e) for r = 1..R-1 from the table tw (w = exp(2 pi i / Ntab)), index scale s:
-// 2-level table products (loads w^e .. w^3e and w^4e, w^8e, w^12e)
+// w^i (w = exp(2 pi i / N)) from the two-level LDS table tw = [lo: w^l, l < 128][hi: w^(128 h)]
+__device__ __forceinline__ float2 tw_at(const float2 *tw, uint32_t i) {
+  return cmulf(tw[128 + (i >> 7)], tw[i & 127]);
+}
+
+// v[r] *= w^(r * e) for r = 1..R-1 (products of w^e .. w^3e and w^4e, w^8e, w^12e)
 template <int R>
 __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32_t e) {
   if (R == 1) return;
   float2 lo[4], hi[4];
 #pragma unroll
-  for (int l = 1; l < 4 && l < R; l++) lo[l] = ld_off(tw, (uint32_t)l * e * 8u);
+  for (int l = 1; l < 4 && l < R; l++) lo[l] = tw_at(tw, (uint32_t)l * e);
 #pragma unroll
-  for (int h = 1; h < 4 && 4 * h < R; h++) hi[h] = ld_off(tw, (uint32_t)(4 * h) * e * 8u);
+  for (int h = 1; h < 4 && 4 * h < R; h++) hi[h] = tw_at(tw, (uint32_t)(4 * h) * e);
 #pragma unroll
   for (int r = 1; r < R; r++) {
     const int h = r >> 2, l = r & 3;
@@ -615,26 +655,89 @@ template <> struct FftPlan<4096> { static constexpr int RL = 16; template <class
 template <> struct FftPlan<8192> { static constexpr int RL = 2; template <class F> using Tail = StockhamTail<8192, 512, 16, 16, 16, 2>; };
 template <> struct FftPlan<16384> { static constexpr int RL = 4; template <class F> using Tail = StockhamTail<16384, 1024, 16, 16, 16, 4>; };
 
+// Experiment switch for tools/ofdm_experiments.sh (product builds use 0): bit 2 = skip the
+// E parking of the split 32K transform (wrong output; measures its cost).
+#ifndef OFDM_VARIANT
+#define OFDM_VARIANT 0
+#endif
+// bit 3: phase timestamps (s_memrealtime, 100 MHz) of each workgroup written over the first
+// samples of its symbol's guard interval (wrong output; tools/ofdm_phases.py decodes them)
+#if OFDM_VARIANT & 8
+__shared__ uint64_t g_phase_ts[16];
+#define OFDM_PHASE(i) do { if (threadIdx.x == 0) g_phase_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define OFDM_PHASE(i) do { } while (0)
+#endif
+
+// Where a sub-transform's inputs come from.  Gather (pilotgen block: cells in carrier order,
+// so per-bin loads are near unit-stride): bin k reads map[k].  Scatter (fused chain: cells in
+// TI output order, randomly placed by the frequency interleaver): aux bins (map < 0) are filled
+// from the aux table, then the symbol's contiguous run of data slots is streamed with unit-stride
+// loads and each cell is written to LDS at its bin inv[slot].
+struct BinSource {
+  const int32_t *map;          // this symbol's stored row
+  const float2 *data;          // uniform base; cells at cbase + code, aux at abase - code
+  uint32_t cbase, abase;
+  const uint16_t *inv;         // scatter mode: stored bin of each data slot (null: gather mode)
+  uint32_t d0, dn;             // scatter mode: this symbol's data slots
+};
+
 // One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split), ending with
 // v[u*RL + r] = y[t + NT*(u + (16/RL)*r)].
 template <int NSUB, bool SPLIT>
-__device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const int32_t *map, const float2 *data,
-                                         uint32_t cbase, uint32_t abase, const float *isinc,
+__device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource &src, const float *isinc,
                                          const float2 *tw, uint32_t tws, int tid, int half) {
   constexpr int NT = NSUB / 16, N = SPLIT ? 2 * NSUB : NSUB;
-  // first pass (R = 16, Ns = 1): gather A[tid + r*NT]; map rows are [even | odd] when SPLIT
-  const int32_t *m = map + (SPLIT ? half * NSUB : 0);
+  // first pass (R = 16, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
+  const int32_t *m = src.map + (SPLIT ? half * NSUB : 0);
+  if (src.inv) {
+    // aux bins: all 16 codes in flight, then all aux loads (two memory round trips)
+    {
+      int code[16];
+      float2 a[16];
 #pragma unroll
-  for (int c0 = 0; c0 < 16; c0 += 8) {
-    uint32_t off[8];
+      for (int u = 0; u < 16; u++) code[u] = ld_off(m, (uint32_t)(tid + NT * u) * 4u);
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      int code = ld_off(m, (uint32_t)(tid + NT * (c0 + u)) * 4u);
-      off[u] = (code >= 0 ? cbase + (uint32_t)code : abase - (uint32_t)code) * 8u;
+      for (int u = 0; u < 16; u++)
+        if (code[u] < 0) a[u] = ld_off(src.data, (src.abase - (uint32_t)code[u]) * 8u);
+#pragma unroll
+      for (int u = 0; u < 16; u++)
+        if (code[u] < 0) lds[lds_pad((uint32_t)(tid + NT * u))] = a[u];
     }
+    OFDM_PHASE(1 + 4 * half);
+    // data cells: the symbol's slots streamed 16 per thread per round
+    const uint32_t lo = SPLIT ? (uint32_t)half * NSUB : 0u;
+    for (uint32_t s0 = 0; s0 < src.dn; s0 += 16u * NT) {
+      uint32_t b[16];
+      float2 c[16];
 #pragma unroll
-    for (int u = 0; u < 8; u++) v[c0 + u] = ld_off(data, off[u]);
-    __builtin_amdgcn_sched_barrier(0);
+      for (int u = 0; u < 16; u++) {
+        const uint32_t sl = s0 + (uint32_t)(tid + NT * u);
+        const bool ok = sl < src.dn;
+        b[u] = ok ? (uint32_t)src.inv[src.d0 + sl] - lo : 0xFFFFFFFFu;
+        if (ok) c[u] = ld_off(src.data, (src.cbase + src.d0 + sl) * 8u);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; u++)
+        if (b[u] < (uint32_t)NSUB) lds[lds_pad(b[u])] = c[u];
+    }
+    __syncthreads();
+    OFDM_PHASE(2 + 4 * half);
+    StockhamPass<NSUB, NT, 16, 1>::load_lds(v, lds, tid);
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int c0 = 0; c0 < 16; c0 += 8) {
+      uint32_t off[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        int code = ld_off(m, (uint32_t)(tid + NT * (c0 + u)) * 4u);
+        off[u] = (code >= 0 ? src.cbase + (uint32_t)code : src.abase - (uint32_t)code) * 8u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) v[c0 + u] = ld_off(src.data, off[u]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   if (isinc) {
 #pragma unroll
@@ -658,7 +761,9 @@ struct OfdmShape {
   static constexpr bool SPLIT = N > 16384;
   static constexpr int NSUB = SPLIT ? N / 2 : N;
   static constexpr int NT = NSUB / 16;
-  static constexpr int LDS_BYTES = (NSUB + NSUB / 16) * 8;
+  static constexpr int FFT_LDS = (NSUB + NSUB / 16) * 8;            // padded sub-transform buffer
+  static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
+  static constexpr int LDS_BYTES = FFT_LDS + TW_ENTRIES * 8;
 };
 
 template <int N>
@@ -667,15 +772,25 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   constexpr int NSUB = Sh::NSUB, NT = Sh::NT, RL = FftPlan<NSUB>::RL, UL = 16 / RL;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2 *lds = (float2 *)smem;
+  float2 *twl = (float2 *)(smem + Sh::FFT_LDS);
   const int tid = threadIdx.x;
-  const int j = blockIdx.x;                       // symbol
-  const int f = blockIdx.y;                       // frame within launch
+  for (int i = tid; i < Sh::TW_ENTRIES; i += NT) twl[i] = d.twiddle[i];   // visible after the first barrier
+  // one workgroup per (symbol, frame); XCD-major so each XCD walks a contiguous run of symbols
+  // for all frames of the launch at once and reads each bin_map row from its own L2
+  const int u = xcd_major(blockIdx.x, gridDim.x);
+  const int j = u / io.nframes;                   // symbol
+  const int f = u - j * io.nframes;               // frame within launch
   const int64_t frame = io.first_frame + f;
   const float2 *data = io.data;                   // uniform base: all gathers are base + u32 offset
   const uint32_t cbase = io.cell_off + (uint32_t)f * io.cell_stride;
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
   const int32_t *map = d.bin_map + (int64_t)j * N;
   const uint32_t tws = Sh::SPLIT ? 2u : 1u;       // sub-transform twiddle = table index * tws
+  BinSource src{map, data, cbase, abase, d.inv, 0u, 0u};
+  if (d.inv) {
+    src.d0 = (uint32_t)d.sym_d0[j];
+    src.dn = (uint32_t)d.sym_n[j];
+  }
 
   if (io.carriers_only) {                          // test hook: bins in natural order
     float2 *o = io.out + (int64_t)f * io.out_stride + (int64_t)j * N;
@@ -683,6 +798,7 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
       const int sub = Sh::SPLIT ? (k & 1) : 0, kk = Sh::SPLIT ? (k >> 1) : k;
       int code = map[sub * NSUB + kk];
       float2 v = data[code >= 0 ? cbase + (uint32_t)code : abase - (uint32_t)code];
+      (void)src;
       if (d.isinc) {
         float sc = d.isinc[(k + N / 2) & (N - 1)];
         v.x *= sc;
@@ -700,7 +816,9 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   float2 *o = io.out + (int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + G);
   const float nrm = d.norm;
   float2 v[16];
-  sub_ifft<NSUB, Sh::SPLIT>(v, lds, map, data, cbase, abase, d.isinc, d.twiddle, tws, tid, 0);
+  OFDM_PHASE(0);
+  sub_ifft<NSUB, Sh::SPLIT>(v, lds, src, d.isinc, twl, tws, tid, 0);
+  OFDM_PHASE(3);
   if (Sh::SPLIT) {
     // x[n] = E[n] + w^n O[n], x[n + NSUB] = E[n] - w^n O[n], w = exp(2 pi i / N).
     // E is parked in this symbol's own output slots x[n] (same thread re-reads it; the
@@ -710,22 +828,30 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
 #pragma unroll
       for (int r = 0; r < RL; r++) {
         const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
+#if !(OFDM_VARIANT & 4)
         st_off(o, ((uint32_t)G + n) * 8u, v[u * RL + r]);
+#endif
       }
     __syncthreads();
     // launder tid: stops the compiler from keeping the first transform's index/twiddle
     // arithmetic alive (spilled) for reuse by the second
     int tid2 = tid;
     asm volatile("" : "+v"(tid2));
-    sub_ifft<NSUB, Sh::SPLIT>(v, lds, map, data, cbase, abase, d.isinc, d.twiddle, tws, tid2, 1);
+    OFDM_PHASE(4);
+    sub_ifft<NSUB, Sh::SPLIT>(v, lds, src, d.isinc, twl, tws, tid2, 1);
+    OFDM_PHASE(7);
 #pragma unroll
     for (int u = 0; u < UL; u++)
 #pragma unroll
       for (int r = 0; r < RL; r++) {
         const int i = u * RL + r;
         const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
+#if OFDM_VARIANT & 4
+        const float2 e = v[i ^ 1];
+#else
         const float2 e = ld_off(o, ((uint32_t)G + n) * 8u);
-        float2 t = cmulf(v[i], ld_off(d.twiddle, n * 8u));
+#endif
+        float2 t = cmulf(v[i], tw_at(twl, n));
         float2 a = cadd(e, t), b = csub(e, t);
         a.x *= nrm; a.y *= nrm; b.x *= nrm; b.y *= nrm;
         st_off(o, ((uint32_t)G + n) * 8u, a);
@@ -747,6 +873,16 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
         if (n >= (uint32_t)(N - G)) st_off(o, (n - (uint32_t)(N - G)) * 8u, a);
       }
   }
+#if OFDM_VARIANT & 8
+  __syncthreads();
+  OFDM_PHASE(8);
+  if (tid == 0) {
+    uint32_t *w = (uint32_t *)o;
+    w[0] = (uint32_t)(g_phase_ts[0] & 0xFFFFFFFFu);
+    for (int i = 1; i < 9; i++) w[i] = (uint32_t)(g_phase_ts[i] - g_phase_ts[0]);
+    w[9] = __smid();
+  }
+#endif
 }
 
 template <int N>
@@ -758,7 +894,7 @@ static hipError_t launch_ofdm_t(const OfdmDev &d, const OfdmIO &io, hipStream_t 
                               Sh::LDS_BYTES);
     attr_set = true;
   }
-  hipLaunchKernelGGL((ofdm_kernel<N>), dim3(d.Nsym, io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
+  hipLaunchKernelGGL((ofdm_kernel<N>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
   return hipGetLastError();
 }
 

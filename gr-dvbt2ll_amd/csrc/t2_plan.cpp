@@ -486,6 +486,10 @@ int build_frame(const FmParams &p, FramePlan &fp) {
     n_big = p.fecblocks % p.tiblocks;
     n_small = p.tiblocks - n_big;
   }
+  fp.ti_on = p.tiblocks != 0;
+  fp.ti_small = small_fec;
+  fp.ti_big = big_fec;
+  fp.ti_nsmall = n_small;
   fp.ci_shift.clear();
   std::vector<int> ti_first, ti_count;           // FEC blocks per TI block
   for (int s = 0, r0 = 0; s < n_small + n_big; s++) {
@@ -544,23 +548,23 @@ int build_frame(const FmParams &p, FramePlan &fp) {
   fi_tables(N, fp.C_P2, HeP, HoP);
   if (fp.N_FC) fi_tables(N, fp.N_FC, HeF, HoF);
   if ((int)He.size() != fp.C_DATA || (int)HeP.size() != fp.C_P2) return -1;
-  fp.gather_t.assign(M, 0);
+  fp.gather_d.assign(M, 0);
   fp.gather_in.assign(M, 0);
   const int aux_dummy = AUX_L1PRE + 1840 + Lp;
   auto resolve = [&](int o, int f) {
     int v = zz[f];
-    int code_t, code_in;
-    if (v < 1840) code_t = code_in = -(AUX_L1PRE + v) - 1;
-    else if (v < 1840 + Lp) code_t = code_in = -(AUX_L1PRE + v) - 1;
+    int code_d, code_in;
+    if (v < 1840) code_d = code_in = -(AUX_L1PRE + v) - 1;
+    else if (v < 1840 + Lp) code_d = code_in = -(AUX_L1PRE + v) - 1;
     else if (v < 1840 + Lp + fp.S) {
       int t = ti_src[v - 1840 - Lp];
       int r = t / fp.cs, pos = t % fp.cs;
       int w = perm_inv[((pos - fp.ci_shift[r]) % fp.cs + fp.cs) % fp.cs];
-      code_t = t;
+      code_d = v - 1840 - Lp;
       code_in = r * fp.cs + w;
-    } else if (v < 1840 + Lp + fp.S + fp.D) code_t = code_in = -(aux_dummy + (v - 1840 - Lp - fp.S)) - 1;
-    else code_t = code_in = -AUX_ZERO - 1;
-    fp.gather_t[o] = code_t;
+    } else if (v < 1840 + Lp + fp.S + fp.D) code_d = code_in = -(aux_dummy + (v - 1840 - Lp - fp.S)) - 1;
+    else code_d = code_in = -AUX_ZERO - 1;
+    fp.gather_d[o] = code_d;
     fp.gather_in[o] = code_in;
   };
   int o = 0, base = 0, symbol = 0;
@@ -928,11 +932,69 @@ int build_pilot(const PgParams &p, PilotPlan &pp) {
     float r = (float)std::sqrt(rms / (N / 2));
     for (int i = 0; i < N; i++) pp.isinc[i] *= r;
   }
-  pp.twiddle.resize(N);
-  for (int e = 0; e < N; e++) {
+  // two-level twiddle table (kept in LDS by the OFDM kernel): w^i = hi[i >> 7] * lo[i & 127]
+  pp.twiddle.resize(128 + N / 128);
+  for (int e = 0; e < 128; e++) {
     double a = 2.0 * M_PI * (double)e / (double)N;
     pp.twiddle[e] = cf32{(float)std::cos(a), (float)std::sin(a)};
   }
+  for (int h = 0; h < N / 128; h++) {
+    double a = 2.0 * M_PI * (double)(128 * h) / (double)N;
+    pp.twiddle[128 + h] = cf32{(float)std::cos(a), (float)std::sin(a)};
+  }
+  return 0;
+}
+
+std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t> &bin_map) {
+  if (!ofdm_split(N)) return bin_map;
+  std::vector<int32_t> m(bin_map.size());
+  for (int j = 0; j < Nsym; j++)
+    for (int k = 0; k < N; k++) m[(size_t)j * N + (k & 1) * (N / 2) + (k >> 1)] = bin_map[(size_t)j * N + k];
+  return m;
+}
+
+int64_t ti_dest(const FramePlan &fp, int r, int t) {
+  const int cs = fp.cs;
+  if (!fp.ti_on) return (int64_t)r * cs + t;
+  const int ns = fp.ti_nsmall * fp.ti_small;
+  int r0, nb;
+  if (r < ns) { r0 = r - r % fp.ti_small; nb = fp.ti_small; }
+  else { r0 = r - (r - ns) % fp.ti_big; nb = fp.ti_big; }
+  const int rows = cs / 5, e = t / rows, row = t - e * rows;
+  return (int64_t)r0 * cs + (int64_t)row * (5 * nb) + 5 * (r - r0) + e;
+}
+
+int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl) {
+  if (pp.active != fp.M || pp.N > 32768) return -1;
+  // bins -> frame data order (TI output) via the framemapper's composed map
+  std::vector<int32_t> nat(pp.bin_map.size());
+  for (size_t i = 0; i < nat.size(); i++) {
+    int32_t c = pp.bin_map[i];
+    nat[i] = c >= 0 ? fp.gather_d[c] : c;
+  }
+  cl.cmap = ofdm_stored_rows(pp.N, pp.Nsym, nat);
+  cl.inv.assign(fp.S, 0);
+  cl.sym_d0.assign(pp.Nsym, 0);
+  cl.sym_n.assign(pp.Nsym, 0);
+  std::vector<char> seen(fp.S, 0);
+  for (int j = 0; j < pp.Nsym; j++) {
+    int lo = fp.S, hi = -1, n = 0;
+    for (int k = 0; k < pp.N; k++) {
+      int32_t c = cl.cmap[(size_t)j * pp.N + k];
+      if (c < 0) continue;
+      if (c >= fp.S || seen[c]) return -1;
+      seen[c] = 1;
+      cl.inv[c] = (uint16_t)k;
+      lo = std::min(lo, c);
+      hi = std::max(hi, c);
+      n++;
+    }
+    if (n && hi - lo + 1 != n) return -1;   // a symbol's data slots must be one contiguous run
+    cl.sym_d0[j] = n ? lo : 0;
+    cl.sym_n[j] = n;
+  }
+  for (int s = 0; s < fp.S; s++)
+    if (!seen[s]) return -1;
   return 0;
 }
 

@@ -68,7 +68,8 @@ struct FramePlan {
   int aux_len = 0;                       // entries per variant
   std::vector<int16_t> ci_perm;          // cs
   std::vector<int32_t> ci_shift;         // F (per FEC block of a frame)
-  std::vector<int32_t> gather_t;         // M: mapped cell -> time-interleaver-input index | aux
+  std::vector<int32_t> gather_d;         // M: mapped cell -> frame data-region index (TI output order) | aux
+  int ti_on = 0, ti_small = 1, ti_big = 1, ti_nsmall = 0;   // TI blocks: ti_nsmall of ti_small FEC blocks, then ti_big
   std::vector<int32_t> gather_in;        // M: mapped cell -> framemapper input index | aux
   std::vector<cf32> aux;                 // t2frames x aux_len
 };
@@ -87,10 +88,30 @@ struct PilotPlan {
   std::vector<int32_t> bin_map;          // Nsym x N, indexed by IFFT input position k (fftshifted)
   std::vector<float> isinc;              // N (pre-shift bin order), only if eq
   std::vector<cf32> p1;                  // 2048
-  std::vector<cf32> twiddle;             // N: exp(+2 pi i e / N)
+  std::vector<cf32> twiddle;             // 128 + N/128: [lo: w^l, l < 128][hi: w^(128 h)], w = exp(2 pi i / N)
 };
 int build_pilot(const PgParams &p, PilotPlan &pp);
 
 int fft_points(int fftsize);
+
+// ----------------------------------------------------------------------------- fused chain layout
+// The OFDM kernel transforms N > 16384 as two N/2 sub-transforms (even / odd bins), so its
+// per-symbol map rows are stored [even | odd]; otherwise in IFFT-input order k.
+inline bool ofdm_split(int N) { return N > 16384; }
+std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t> &bin_map);
+
+// Fused chain layout.  The map kernel writes each FEC block's cells through the cell and time
+// interleavers into the frame data region, which is then in transmission (TI output) order:
+// symbol j's data cells are the contiguous slots [sym_d0[j], sym_d0[j] + sym_n[j]).  The OFDM
+// kernel streams that range with unit-stride loads and scatters each cell into its IFFT bin in
+// LDS (inv), after filling pilot / null / L1 / dummy bins from the aux table (cmap < 0).
+struct ChainLayout {
+  std::vector<int32_t> cmap;     // Nsym x N, stored row order: >= 0 data slot, < 0 aux (-code - 1)
+  std::vector<uint16_t> inv;     // S: data slot -> stored bin index within its symbol's row
+  std::vector<int32_t> sym_d0, sym_n;   // Nsym
+};
+int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl);
+// time-interleaver output index (frame data order) of cell-interleaved cell t of FEC block r
+int64_t ti_dest(const FramePlan &fp, int r, int t);
 
 }  // namespace t2

@@ -10,17 +10,21 @@ using namespace t2;
 
 extern "C" {
 
-// info: [M, S, aux_len, t2frames, cs, F, N_P2, C_P2, C_DATA, N_FC, C_FC, Lp, D]
-int t2probe_frame(const int *p20, int *info, int32_t *gather_in, int32_t *gather_t, float *aux) {
+// info: [M, S, aux_len, t2frames, cs, F, N_P2, C_P2, C_DATA, N_FC, C_FC, Lp, D,
+//        ti_on, ti_small, ti_big, ti_nsmall]
+int t2probe_frame(const int *p20, int *info, int32_t *gather_in, int32_t *gather_d, float *aux, int16_t *ci_perm,
+                  int32_t *ci_shift) {
   FmParams p{p20[0], p20[1], p20[2], p20[3], p20[4], p20[5], p20[6], p20[7], p20[8], p20[9],
              p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
   FramePlan fp;
   if (build_frame(p, fp)) return -1;
-  int v[13] = {fp.M, fp.S, fp.aux_len, fp.t2frames, fp.cs, fp.F, fp.N_P2, fp.C_P2, fp.C_DATA, fp.N_FC, fp.C_FC,
-               fp.Lp, fp.D};
+  int v[17] = {fp.M, fp.S, fp.aux_len, fp.t2frames, fp.cs, fp.F, fp.N_P2, fp.C_P2, fp.C_DATA, fp.N_FC, fp.C_FC,
+               fp.Lp, fp.D, fp.ti_on, fp.ti_small, fp.ti_big, fp.ti_nsmall};
   memcpy(info, v, sizeof(v));
   if (gather_in) memcpy(gather_in, fp.gather_in.data(), fp.gather_in.size() * 4);
-  if (gather_t) memcpy(gather_t, fp.gather_t.data(), fp.gather_t.size() * 4);
+  if (gather_d) memcpy(gather_d, fp.gather_d.data(), fp.gather_d.size() * 4);
+  if (ci_perm) memcpy(ci_perm, fp.ci_perm.data(), fp.ci_perm.size() * 2);
+  if (ci_shift) memcpy(ci_shift, fp.ci_shift.data(), fp.ci_shift.size() * 4);
   if (aux) memcpy(aux, fp.aux.data(), fp.aux.size() * 8);
   return 0;
 }
@@ -59,6 +63,26 @@ int t2probe_fec(int framesize, int rate, int constellation, int *info, uint32_t 
   memcpy(info, v, sizeof(v));
   if (ent) memcpy(ent, fp.ldpc_ent.data(), fp.ldpc_ent.size() * 4);
   if (rowptr) memcpy(rowptr, fp.ldpc_rowptr.data(), fp.ldpc_rowptr.size() * 2);
+  return 0;
+}
+
+// fused-chain layout: cmap Nsym x N (stored row order), inv S, sym_d0/sym_n Nsym;
+// info [Nsym, N, S, split]
+int t2probe_chain(const int *p20, const int *pg3, int *info, int32_t *cmap, uint16_t *inv, int32_t *d0,
+                  int32_t *dn) {
+  FmParams f{p20[0], p20[1], p20[2], p20[3], p20[4], p20[5], p20[6], p20[7], p20[8], p20[9],
+             p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
+  PgParams g{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
+             f.preamble, pg3[0], pg3[1], pg3[2], fft_points(f.fftsize)};
+  FramePlan fp;
+  PilotPlan pp;
+  ChainLayout cl;
+  if (build_frame(f, fp) || build_pilot(g, pp) || build_chain_layout(fp, pp, cl)) return -1;
+  info[0] = pp.Nsym; info[1] = pp.N; info[2] = fp.S; info[3] = ofdm_split(pp.N) ? 1 : 0;
+  if (cmap) memcpy(cmap, cl.cmap.data(), cl.cmap.size() * 4);
+  if (inv) memcpy(inv, cl.inv.data(), cl.inv.size() * 2);
+  if (d0) memcpy(d0, cl.sym_d0.data(), cl.sym_d0.size() * 4);
+  if (dn) memcpy(dn, cl.sym_n.data(), cl.sym_n.size() * 4);
   return 0;
 }
 }

@@ -173,7 +173,7 @@ int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, in
 int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable);
 int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages);
 /* test hooks (host outputs, synchronous): packed codewords (tempu order) and
- * cells (time-interleaver input order) of the last run's frame 0 */
+ * cells (frame data region, in the slot order the OFDM kernel reads) of the last run's frame 0 */
 int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes);
 int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells);
 int dvbt2ll_chain_synchronize(dvbt2ll_chain *h);

@@ -22,10 +22,11 @@ def lib():
             subprocess.run(["make", "-s", "-C", str(CSRC), "probe"], check=True)
         L = ctypes.CDLL(str(LIB))
         vp = ctypes.c_void_p
-        L.t2probe_frame.argtypes = [vp, vp, vp, vp, vp]
+        L.t2probe_frame.argtypes = [vp] * 7
         L.t2probe_pilot.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.t2probe_map.argtypes = [ctypes.c_int] * 4 + [vp, vp]
         L.t2probe_fec.argtypes = [ctypes.c_int] * 3 + [vp, vp, vp]
+        L.t2probe_chain.argtypes = [vp] * 7
         _L = L
     return _L
 
@@ -36,17 +37,22 @@ def _p(a):
 
 def frame_plan(fm_args):
     p = np.array(fm_args, np.int32)
-    info = np.zeros(13, np.int32)
-    if lib().t2probe_frame(_p(p), _p(info), None, None, None):
+    info = np.zeros(17, np.int32)
+    if lib().t2probe_frame(_p(p), _p(info), None, None, None, None, None):
         return None
     M, S, aux_len, t2frames = (int(x) for x in info[:4])
     gin = np.zeros(M, np.int32)
-    gt = np.zeros(M, np.int32)
+    gd = np.zeros(M, np.int32)
     aux = np.zeros(t2frames * aux_len, np.complex64)
-    assert lib().t2probe_frame(_p(p), _p(info), _p(gin), _p(gt), _p(aux)) == 0
-    keys = ["M", "S", "aux_len", "t2frames", "cs", "F", "N_P2", "C_P2", "C_DATA", "N_FC", "C_FC", "Lp", "D"]
+    cs, F = int(info[4]), int(info[5])
+    perm = np.zeros(cs, np.int16)
+    shift = np.zeros(F, np.int32)
+    assert lib().t2probe_frame(_p(p), _p(info), _p(gin), _p(gd), _p(aux), _p(perm), _p(shift)) == 0
+    keys = ["M", "S", "aux_len", "t2frames", "cs", "F", "N_P2", "C_P2", "C_DATA", "N_FC", "C_FC", "Lp", "D",
+            "ti_on", "ti_small", "ti_big", "ti_nsmall"]
     d = dict(zip(keys, (int(x) for x in info)))
-    d.update(gather_in=gin, gather_t=gt, aux=aux.reshape(t2frames, aux_len))
+    d.update(gather_in=gin, gather_d=gd, aux=aux.reshape(t2frames, aux_len), ci_perm=perm.astype(np.int64),
+             ci_shift=shift.astype(np.int64))
     return d
 
 
@@ -81,3 +87,45 @@ def fec_plan(framesize, rate, constellation=3):
     rp = np.zeros(q + 1, np.uint16)
     assert lib().t2probe_fec(framesize, rate, constellation, _p(info), _p(ent), _p(rp)) == 0
     return dict(kbch=kbch, nbch=nbch, P=P, q=q, ent=ent, rowptr=rp, chunk=chunk, parity_il=pil)
+
+
+def ti_dest(plan, r, t):
+    """frame data-region index of cell t (cell-interleaved position) of FEC block r: the
+    time-interleaver write the chain's map kernel performs (t2_kernels.hip map_kernel)"""
+    cs = plan["cs"]
+    if not plan["ti_on"]:
+        return r * cs + t
+    small, big, ns = plan["ti_small"], plan["ti_big"], plan["ti_nsmall"]
+    r = np.asarray(r)
+    in_small = r < ns * small
+    r0 = np.where(in_small, (r // small) * small, ns * small + ((r - ns * small) // big) * big)
+    nb = np.where(in_small, small, big)
+    rows = cs // 5
+    return r0 * cs + (t % rows) * (5 * nb) + 5 * (r - r0) + t // rows
+
+
+def chain_layout(cfg):
+    """the fused chain's layout: cmap (Nsym x N, stored row order: [even | odd] bins when split;
+    data codes are frame data slots in TI output order), inv (slot -> stored bin), and each
+    symbol's contiguous slot range [d0, d0 + n)"""
+    p = np.array(cfg.fm_args(), np.int32)
+    g = np.array([cfg.misogroup, cfg.equalization, cfg.bandwidth], np.int32)
+    info = np.zeros(4, np.int32)
+    assert lib().t2probe_chain(_p(p), _p(g), _p(info), None, None, None, None) == 0
+    Nsym, N, S, split = (int(x) for x in info)
+    cmap = np.zeros(Nsym * N, np.int32)
+    inv = np.zeros(S, np.uint16)
+    d0 = np.zeros(Nsym, np.int32)
+    dn = np.zeros(Nsym, np.int32)
+    assert lib().t2probe_chain(_p(p), _p(g), _p(info), _p(cmap), _p(inv), _p(d0), _p(dn)) == 0
+    return dict(Nsym=Nsym, N=N, S=S, split=split, cmap_stored=cmap.reshape(Nsym, N), inv=inv.astype(np.int64),
+                d0=d0, n=dn)
+
+
+def stored_to_natural(row, N, split):
+    if not split:
+        return row
+    nat = np.empty_like(row)
+    nat[0::2] = row[: N // 2]
+    nat[1::2] = row[N // 2:]
+    return nat

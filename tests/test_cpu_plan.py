@@ -90,6 +90,46 @@ def test_framemapper_map_matches_oracle(name, over):
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+@pytest.mark.parametrize("name,over", GRID + [("cfg%d" % i, None) for i in range(1, 6)],
+                         ids=[g[0] for g in GRID] + ["cfg%d" % i for i in range(1, 6)])
+def test_chain_cell_layout_matches_oracle(name, over):
+    """the fused chain's indexing, as the kernels apply it: the map kernel stores QAM cell (r, j)
+    at ti_dest(r, (perm[j] + shift[r]) mod cs); the OFDM kernel fills aux bins from cmap < 0 and
+    scatters its symbol's contiguous data slots into bins through inv.  The carriers equal the
+    oracle's framemapper + pilotgen for every parameter combination."""
+    cfg = CONFIGS[name] if over is None else grid_cfg(over)
+    lay = PP.chain_layout(cfg)
+    fplan = PP.frame_plan(cfg.fm_args())
+    pplan = PP.pilot_plan(cfg.pg_args())
+    fm = O.FM(*cfg.fm_args())
+    pg = O.PG(*cfg.pg_args())
+    cs, F = fplan["cs"], fplan["F"]
+    cells = rand_cells(lay["S"])
+    r = np.repeat(np.arange(F), cs)
+    jj = np.tile(np.arange(cs), F)
+    t = (fplan["ci_perm"][jj] + fplan["ci_shift"][r]) % cs
+    data = np.zeros(lay["S"], np.complex64)
+    data[PP.ti_dest(fplan, r, t)] = cells
+    want = pg.carriers(fm.work(cells))
+    aux = fplan["aux"][0].copy()
+    aux[1:13] = pplan["pilot_values"]
+    N = lay["N"]
+    k = np.arange(N)
+    assert lay["n"].sum() == lay["S"]
+    for j in range(lay["Nsym"]):
+        code = lay["cmap_stored"][j]
+        row = np.where(code < 0, aux[np.clip(-code - 1, 0, None)], 0).astype(np.complex64)
+        sl = np.arange(lay["d0"][j], lay["d0"][j] + lay["n"][j])
+        assert (code[lay["inv"][sl]] >= 0).all()
+        row[lay["inv"][sl]] = data[sl]
+        row = PP.stored_to_natural(row, N, lay["split"])
+        bins = np.empty(N, np.complex64)
+        bins[(k + N // 2) % N] = row
+        if pplan["eq"]:
+            bins = (bins.view(np.float32).reshape(-1, 2) * pplan["isinc"][:, None]).view(np.complex64).reshape(-1)
+        np.testing.assert_array_equal(bins.view(np.uint32), want[j].view(np.uint32), err_msg="symbol %d" % j)
+
+
 @pytest.mark.parametrize("name,over", GRID, ids=[g[0] for g in GRID])
 def test_pilot_map_matches_oracle(name, over):
     cfg = grid_cfg(over)
@@ -119,8 +159,8 @@ def test_benchmark_configs_plan(name):
     fplan = PP.frame_plan(cfg.fm_args())
     pplan = PP.pilot_plan(cfg.pg_args())
     assert fplan["M"] == pplan["active"]
-    # chain composition: every mapped data cell points into the time-interleaver input once
-    t = fplan["gather_t"]
+    # chain composition: every mapped data cell points into the frame data region once
+    t = fplan["gather_d"]
     data = np.sort(t[t >= 0])
     np.testing.assert_array_equal(data, np.arange(fplan["S"]))
     gi = fplan["gather_in"]

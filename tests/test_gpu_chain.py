@@ -27,8 +27,8 @@ def oracle_chain(cfg, nframes):
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_chain_cells_match_oracle(gpu, name):
-    """stage check inside the fused chain: the cells buffer (time-interleaver input order, after
-    FEC + bit interleave + QAM + cell interleave) equals the oracle's, via the planner's maps"""
+    """stage check inside the fused chain: the cells buffer (FEC + bit interleave + QAM + cell
+    and time interleaving = the frame data region in transmission order) equals the oracle's"""
     import plan_probe as PP
     cfg = CONFIGS[name]
     ts, base = ts_for_frames(cfg, 0, 1)
@@ -36,15 +36,17 @@ def test_chain_cells_match_oracle(gpu, name):
     bits, _ = O.BB(*cfg.bb_args()).work(ts, F)
     cells = O.IM(*cfg.im_args()).work(O.LDPC(cfg.framesize, cfg.rate).work(bits, F), F)
     plan = PP.frame_plan(cfg.fm_args())
-    gi, gt = plan["gather_in"], plan["gather_t"]
-    sel = gt >= 0
+    cs = plan["cs"]
+    r = np.repeat(np.arange(F), cs)
+    jj = np.tile(np.arange(cs), F)
+    t = (plan["ci_perm"][jj] + plan["ci_shift"][r]) % cs
     want = np.zeros(plan["S"], np.complex64)
-    want[gt[sel]] = cells[gi[sel]]
+    want[PP.ti_dest(plan, r, t)] = cells
     ch = dvbt2ll.Chain(cfg, max_frames=1)
     ch.run(0, 1)
     got = ch.debug_cells(plan["S"])
     bad = np.nonzero(got.view(np.uint64) != want.view(np.uint64))[0]
-    assert bad.size == 0, (bad.size, bad[:10], bad[:10] // plan["cs"])
+    assert bad.size == 0, (bad.size, bad[:10], bad[:10] // cs)
 
 
 def _check_chain(cfg, nframes):

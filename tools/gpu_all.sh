@@ -1,14 +1,15 @@
 # One GPU-box session: parity tests, smoke, bench, rocprofv3 kernel trace + PMC passes.
 # Each GPU step has its own time limit; a crash/abort/timeout ends the script (no further GPU work).
 set -o pipefail
+exec 3>&1
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 TAG=${1:-run}
 step() {  # step <name> <seconds> <cmd...>; stops the script on a crash-class exit code
   local name=$1 secs=$2; shift 2
   timeout -k 10 $secs "$@"; local rc=$?
-  echo "STEP $name EXIT $rc"
-  case $rc in 124|134|137|139) echo "STOP after $name"; exit $rc;; esac
+  echo "STEP $name EXIT $rc" >&3
+  case $rc in 124|134|137|139) echo "STOP after $name" >&3; exit $rc;; esac
   return 0
 }
 step tests 600 python -m pytest tests -m gpu -q --tb=short -x -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1
