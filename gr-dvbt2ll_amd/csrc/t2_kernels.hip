@@ -36,6 +36,13 @@ __device__ __forceinline__ void st_off(T *base, uint32_t byte_off, T v) {
   *(T *)((char *)base + byte_off) = v;
 }
 
+// streaming store (nontemporal): final IQ samples are never re-read by the chain
+__device__ __forceinline__ void st_nt(float2 *base, uint32_t byte_off, float2 v) {
+  float2 *p = (float2 *)((char *)base + byte_off);
+  __builtin_nontemporal_store(v.x, &p->x);
+  __builtin_nontemporal_store(v.y, &p->y);
+}
+
 __device__ __forceinline__ uint32_t rd_lane_u32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
 __device__ __forceinline__ uint64_t rd_lane_u64(uint64_t v, int l) {
   uint32_t lo = rd_lane_u32((uint32_t)v, l), hi = rd_lane_u32((uint32_t)(v >> 32), l);
@@ -574,15 +581,22 @@ __device__ __forceinline__ float2 tw_at(const float2 *tw, uint32_t i) {
   return cmulf(tw[128 + (i >> 7)], tw[i & 127]);
 }
 
-// v[r] *= w^(r * e) for r = 1..R-1 (products of w^e .. w^3e and w^4e, w^8e, w^12e)
+// v[r] *= w^(r * e) for r = 1..R-1: one table lookup for w^e, the other powers by products
+// of depth <= 4 (w^2e, w^3e, w^4e, w^8e, w^12e, then hi * lo)
 template <int R>
 __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32_t e) {
   if (R == 1) return;
   float2 lo[4], hi[4];
-#pragma unroll
-  for (int l = 1; l < 4 && l < R; l++) lo[l] = tw_at(tw, (uint32_t)l * e);
-#pragma unroll
-  for (int h = 1; h < 4 && 4 * h < R; h++) hi[h] = tw_at(tw, (uint32_t)(4 * h) * e);
+  lo[1] = tw_at(tw, e);
+  if (R > 2) {
+    lo[2] = cmulf(lo[1], lo[1]);
+    lo[3] = cmulf(lo[2], lo[1]);
+  }
+  if (R > 4) hi[1] = cmulf(lo[2], lo[2]);
+  if (R > 8) {
+    hi[2] = cmulf(hi[1], hi[1]);
+    hi[3] = cmulf(hi[2], hi[1]);
+  }
 #pragma unroll
   for (int r = 1; r < R; r++) {
     const int h = r >> 2, l = r & 3;
@@ -594,6 +608,9 @@ __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32
 template <int NSUB, int NT, int R, int NS>
 struct StockhamPass {
   static constexpr int U = 16 / R;          // units per thread
+  // every LDS address below is lds_pad(thread base) + a compile-time offset (immediate field)
+  static_assert((NS == 1 && R == 16) || NS % 16 == 0, "pad offsets need NS == 1 (R == 16) or 16 | NS");
+  static_assert((NSUB / R) % 16 == 0, "pad offsets need 16 | NSUB / R");
   // twiddles + DFT on the thread's U units (v laid out [u][r])
   __device__ __forceinline__ static void compute(float2 *v, const float2 *tw, uint32_t tws, int tid) {
 #pragma unroll
@@ -610,17 +627,17 @@ struct StockhamPass {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t j = (uint32_t)(tid + NT * u);
-      const uint32_t base = (j / NS) * (NS * R) + (j % NS);
+      float2 *b = lds + lds_pad((j / NS) * (NS * R) + (j % NS));
 #pragma unroll
-      for (int r = 0; r < R; r++) lds[lds_pad(base + (uint32_t)(r * NS))] = v[u * R + r];
+      for (int r = 0; r < R; r++) b[r * NS + ((r * NS) >> 4)] = v[u * R + r];
     }
   }
   __device__ __forceinline__ static void load_lds(float2 *v, const float2 *lds, int tid) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const uint32_t j = (uint32_t)(tid + NT * u);
+      const float2 *b = lds + lds_pad((uint32_t)(tid + NT * u));
 #pragma unroll
-      for (int r = 0; r < R; r++) v[u * R + r] = lds[lds_pad(j + (uint32_t)(r * (NSUB / R)))];
+      for (int r = 0; r < R; r++) v[u * R + r] = b[r * (NSUB / R) * 17 / 16];
     }
   }
 };
@@ -691,35 +708,39 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   // first pass (R = 16, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
   const int32_t *m = src.map + (SPLIT ? half * NSUB : 0);
   if (src.inv) {
-    // aux bins: all 16 codes in flight, then all aux loads (two memory round trips)
+    // every bin: aux value, or zero for data bins (aux entry 0); branch-free, all 16 codes in
+    // flight, then all 16 aux loads (two memory round trips)
     {
       int code[16];
-      float2 a[16];
 #pragma unroll
       for (int u = 0; u < 16; u++) code[u] = ld_off(m, (uint32_t)(tid + NT * u) * 4u);
+      float2 a[16];
 #pragma unroll
       for (int u = 0; u < 16; u++)
-        if (code[u] < 0) a[u] = ld_off(src.data, (src.abase - (uint32_t)code[u]) * 8u);
+        a[u] = ld_off(src.data, (src.abase + (code[u] < 0 ? (uint32_t)(-code[u]) : 1u)) * 8u);
+      float2 *b = lds + lds_pad((uint32_t)tid);
 #pragma unroll
-      for (int u = 0; u < 16; u++)
-        if (code[u] < 0) lds[lds_pad((uint32_t)(tid + NT * u))] = a[u];
+      for (int u = 0; u < 16; u++) b[u * NT * 17 / 16] = a[u];
     }
+    __syncthreads();
     OFDM_PHASE(1 + 4 * half);
-    // data cells: the symbol's slots streamed 16 per thread per round
+    // data cells: the symbol's slots streamed with unit-stride loads, written to their bins;
+    // cells of the other half go to a per-lane dummy slot past the buffer (branch-free)
     const uint32_t lo = SPLIT ? (uint32_t)half * NSUB : 0u;
-    for (uint32_t s0 = 0; s0 < src.dn; s0 += 16u * NT) {
-      uint32_t b[16];
-      float2 c[16];
+    const uint32_t dummy = (uint32_t)(NSUB + NSUB / 16) + (uint32_t)(tid & 63);
+    constexpr int SC = NSUB >= 16384 ? 32 : 16;   // slots per thread per round (32K: one round)
+    const uint32_t last = src.dn - 1u;
+    for (uint32_t s0 = 0; s0 < src.dn; s0 += (uint32_t)SC * NT) {
+      uint32_t b[SC];
+      float2 c[SC];
 #pragma unroll
-      for (int u = 0; u < 16; u++) {
-        const uint32_t sl = s0 + (uint32_t)(tid + NT * u);
-        const bool ok = sl < src.dn;
-        b[u] = ok ? (uint32_t)src.inv[src.d0 + sl] - lo : 0xFFFFFFFFu;
-        if (ok) c[u] = ld_off(src.data, (src.cbase + src.d0 + sl) * 8u);
+      for (int u = 0; u < SC; u++) {
+        const uint32_t sl = min(s0 + (uint32_t)(tid + NT * u), last);
+        b[u] = (uint32_t)src.inv[src.d0 + sl] - lo;
+        c[u] = ld_off(src.data, (src.cbase + src.d0 + sl) * 8u);
       }
 #pragma unroll
-      for (int u = 0; u < 16; u++)
-        if (b[u] < (uint32_t)NSUB) lds[lds_pad(b[u])] = c[u];
+      for (int u = 0; u < SC; u++) lds[b[u] < (uint32_t)NSUB ? lds_pad(b[u]) : dummy] = c[u];
     }
     __syncthreads();
     OFDM_PHASE(2 + 4 * half);
@@ -761,7 +782,7 @@ struct OfdmShape {
   static constexpr bool SPLIT = N > 16384;
   static constexpr int NSUB = SPLIT ? N / 2 : N;
   static constexpr int NT = NSUB / 16;
-  static constexpr int FFT_LDS = (NSUB + NSUB / 16) * 8;            // padded sub-transform buffer
+  static constexpr int FFT_LDS = (NSUB + NSUB / 16 + 64) * 8;       // padded buffer + 64 dummy slots
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
   static constexpr int LDS_BYTES = FFT_LDS + TW_ENTRIES * 8;
 };
@@ -854,11 +875,11 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
         float2 t = cmulf(v[i], tw_at(twl, n));
         float2 a = cadd(e, t), b = csub(e, t);
         a.x *= nrm; a.y *= nrm; b.x *= nrm; b.y *= nrm;
-        st_off(o, ((uint32_t)G + n) * 8u, a);
+        st_nt(o, ((uint32_t)G + n) * 8u, a);
         const uint32_t n2 = n + (uint32_t)NSUB;
-        st_off(o, ((uint32_t)G + n2) * 8u, b);
-        if (n2 >= (uint32_t)(N - G)) st_off(o, (n2 - (uint32_t)(N - G)) * 8u, b);
-        if (n >= (uint32_t)(N - G)) st_off(o, (n - (uint32_t)(N - G)) * 8u, a);
+        st_nt(o, ((uint32_t)G + n2) * 8u, b);
+        if (n2 >= (uint32_t)(N - G)) st_nt(o, (n2 - (uint32_t)(N - G)) * 8u, b);
+        if (n >= (uint32_t)(N - G)) st_nt(o, (n - (uint32_t)(N - G)) * 8u, a);
         if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
   } else {
@@ -869,8 +890,8 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
         const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
         float2 a = v[u * RL + r];
         a.x *= nrm; a.y *= nrm;
-        st_off(o, ((uint32_t)G + n) * 8u, a);
-        if (n >= (uint32_t)(N - G)) st_off(o, (n - (uint32_t)(N - G)) * 8u, a);
+        st_nt(o, ((uint32_t)G + n) * 8u, a);
+        if (n >= (uint32_t)(N - G)) st_nt(o, (n - (uint32_t)(N - G)) * 8u, a);
       }
   }
 #if OFDM_VARIANT & 8
