@@ -50,26 +50,42 @@ __device__ __forceinline__ uint64_t rd_lane_u64(uint64_t v, int l) {
 }
 
 // ============================================================================ FEC kernel
+// experiment switch (product builds: 0): bit 0 = phase timestamps of each block written over
+// the first 40 bytes of its codeword (wrong output; tools/fec_phases.py decodes them)
+#ifndef FEC_VARIANT
+#define FEC_VARIANT 0
+#endif
+#if FEC_VARIANT & 1
+__shared__ uint64_t g_fec_ts[12];
+#define FEC_PHASE(i) do { if (threadIdx.x == 0) g_fec_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define FEC_PHASE(i) do { } while (0)
+#endif
 constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
 constexpr int FEC_MAX_GROUPS = 150;     // nbch / 360 (5/6 normal)
 constexpr int FEC_MAX_Q = 90;
 constexpr int FEC_MAX_ENT = 656;
-// dynamic LDS carve (bytes)
+// dynamic LDS carve (bytes): a persistent part, then one region reused by phase
+//   BB/CRC phase: [btab | crc8 | crcsh | raw TS bytes]   BCH: [btab]   LDPC: [D | rows]
 constexpr int SM_FRAME = 0;
-constexpr int SM_CRC8 = SM_FRAME + FEC_FRAME_BYTES;          // 256
-constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
-constexpr int SM_SYNC = SM_CRCSH + 2048;                     // 64
-constexpr int SM_BTAB = SM_SYNC + 64;                        // 256*3*8 = 6144
-constexpr int SM_WACC = SM_BTAB + 6144;                      // 4*3*8 = 96
-constexpr int SM_D = SM_WACC + 96;                           // 150*24*4 = 14400
-constexpr int SM_ROWA = SM_D + FEC_MAX_GROUPS * 24 * 4;      // 90*12*4 = 4320
-constexpr int SM_ROWB = SM_ROWA + FEC_MAX_Q * 12 * 4;
-constexpr int SM_W = SM_ROWB + FEC_MAX_Q * 12 * 4;           // 16*4
+constexpr int SM_SYNC = SM_FRAME + FEC_FRAME_BYTES;          // 64
+constexpr int SM_WACC = SM_SYNC + 64;                        // 4*3*8 = 96
+constexpr int SM_W = SM_WACC + 96;                           // 16*4
 constexpr int SM_ENT = SM_W + 64;                            // 656*4
 constexpr int SM_RP = SM_ENT + FEC_MAX_ENT * 4;              // 96*2
-constexpr int FEC_SMEM = SM_RP + 96 * 2;
+constexpr int SM_PHASE = (SM_RP + 96 * 2 + 15) & ~15;
+constexpr int SM_BTAB = SM_PHASE;                            // 256*3*8 = 6144
+constexpr int SM_CRC8 = SM_BTAB + 6144;                      // 256
+constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
+constexpr int SM_RAW = SM_CRCSH + 2048;                      // raw TS bytes of the block (NM)
+constexpr int FEC_RAW_BYTES = 188 + 6720 + 16;               // one packet before + max payload
+constexpr int SM_D = SM_PHASE;                               // 150*24*4 = 14400 (after BCH)
+constexpr int SM_ROWA = SM_D + FEC_MAX_GROUPS * 24 * 4;      // 90*12*4 = 4320
+constexpr int FEC_SMEM = (SM_RAW + FEC_RAW_BYTES > SM_ROWA + FEC_MAX_Q * 12 * 4 ? SM_RAW + FEC_RAW_BYTES
+                                                                                : SM_ROWA + FEC_MAX_Q * 12 * 4);
 static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0, "LDS carve alignment");
+static_assert(FEC_SMEM <= 160 * 1024 / 5, "five FEC workgroups per CU");
 
 // stream position of payload byte J (counted over the payload bytes of the whole stream)
 __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
@@ -97,12 +113,12 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
   uint64_t *wacc = (uint64_t *)(smem + SM_WACC);
   uint32_t *D = (uint32_t *)(smem + SM_D);
   uint32_t *rowA = (uint32_t *)(smem + SM_ROWA);
-  uint32_t *rowB = (uint32_t *)(smem + SM_ROWB);
   uint32_t *Wv = (uint32_t *)(smem + SM_W);
   uint32_t *ents = (uint32_t *)(smem + SM_ENT);
   uint16_t *rp = (uint16_t *)(smem + SM_RP);
 
   // ---- stage constant tables into LDS
+  FEC_PHASE(0);
   for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
   for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
   for (int i = tid; i <= d.q; i += FEC_THREADS) rp[i] = d.ldpc_rowptr[i];
@@ -135,9 +151,33 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     if (d.hem) count0 = J0 == 0 ? 0 : (int)((payload_pos(J0 - 1, 1) + 1) % 188);
     else count0 = (int)(pos0 % 188);
     __syncthreads();
+    FEC_PHASE(1);
     // ---- CRC-8 of each packet whose sync slot falls in this block (NM only):
     //      8 lanes per packet, 24-byte chunks combined with zero-extension tables
     if (!d.hem) {
+      // stage the raw stream bytes [pos0 - 188, pos0 + npay) once (independent loads); the CRC
+      // chains and the payload copy then read LDS
+      // (dword loads; raw[i] = stream byte rs + i lives at rawb[i + delta])
+      const int64_t rs = pos0 - 188;
+      const int64_t rel = rs - io.ts_base;                 // >= -188
+      const int64_t w0 = (rel >= 0 ? rel : rel - 3) / 4;   // floor
+      const int delta = (int)(rel - 4 * w0);
+      const int nw = (delta + npay + 188 + 3) >> 2;
+      uint32_t *raww = (uint32_t *)(smem + SM_RAW);
+      const bool aligned = (((uintptr_t)io.in) & 3) == 0;
+      for (int i = tid; i < nw; i += FEC_THREADS) {
+        const int64_t b = 4 * (w0 + i);
+        uint32_t v = 0;
+        if (aligned && b >= 0 && b + 4 <= io.ts_len) {
+          v = *(const uint32_t *)(io.in + b);
+        } else {
+          for (int e = 0; e < 4; e++)
+            if (b + e >= 0 && b + e < io.ts_len) v |= (uint32_t)io.in[b + e] << (8 * e);
+        }
+        raww[i] = v;
+      }
+      const uint8_t *raw = smem + SM_RAW + delta;
+      __syncthreads();
       const int first_slot = (188 - count0) % 188;
       const int nslots = first_slot < npay ? (npay - 1 - first_slot) / 188 + 1 : 0;
       // up to 36 sync slots per block (5/6 normal): 32 packets per pass
@@ -147,10 +187,15 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
         int64_t p = pos0 + first_slot + 188 * (int64_t)m;   // sync position
         bool active = m < nslots && p > 0;
         if (active) {
-          int64_t b0 = p - 187 + 24 * k - io.ts_base;
-          int n = min(24, 187 - 24 * k);
-          uint8_t c = 0;
-          for (int i = 0; i < n; i++) c = crc8[io.in[b0 + i] ^ c];
+          const uint8_t *b0 = raw + (p - 187 + 24 * k - rs);
+          const int n = k == 7 ? 19 : 24;            // 187 = 7 x 24 + 19
+          uint8_t by[24];
+#pragma unroll
+          for (int i = 0; i < 24; i++) by[i] = i < n ? b0[i] : 0;
+          uint32_t c = 0;
+#pragma unroll
+          for (int i = 0; i < 24; i++)
+            if (i < n) c = crc8[by[i] ^ c];
           part = crcsh[k * 256 + c];
         }
         uint32_t v = part;
@@ -161,9 +206,8 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
       }
       __syncthreads();
       for (int j = tid; j < npay; j += FEC_THREADS) {
-        int64_t pos = pos0 + j;
         int r = (int)((count0 + j) % 188);
-        frame[10 + j] = r == 0 ? syncv[(j - first_slot) / 188] : io.in[pos - io.ts_base];
+        frame[10 + j] = r == 0 ? syncv[(j - first_slot) / 188] : raw[188 + j];
       }
     } else {
       for (int j = tid; j < npay; j += FEC_THREADS) frame[10 + j] = io.in[payload_pos(J0 + j, 1) - io.ts_base];
@@ -203,15 +247,26 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
       }
     }
     __syncthreads();
+    FEC_PHASE(2);
     for (int i = tid; i < L; i += FEC_THREADS) frame[i] ^= d.prbs[i];   // BB scrambling
     __syncthreads();
 
     // ---- BCH: lane t divides its chunk; Horner across lanes then waves
     {
       const int C = d.chunk;
-      const int lo = L - (FEC_THREADS - tid) * C, hi = L - (FEC_THREADS - 1 - tid) * C;
+      // 128 chunks of C bytes: chunk t = 32 wave + lane on lanes 0..31 (t2_plan: bch_chunk)
+      const int t = 32 * wave + lane;
+      const int lo = L - (128 - t) * C, hi = lane < 32 ? L - (127 - t) * C : 0;
       const int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
+      // per-lane rows of M1 (v -> v x^(8C)) and M2 (v -> v x^(8*32*C)), loaded up front
+      uint64_t m1[3][3], m2[3][3];
+      for (int s = 0; s < 3; s++)
+        for (int k = 0; k < 3; k++) {
+          m1[s][k] = d.bch_m1[(lane + 64 * s) * 3 + k];
+          m2[s][k] = d.bch_m2[(lane + 64 * s) * 3 + k];
+        }
       uint64_t r0 = 0, r1 = 0, r2 = 0;
+#pragma unroll 4
       for (int i = max(lo, 0); i < hi; i++) {
         uint32_t top = (uint32_t)(((tw == 0 ? r0 : tw == 1 ? r1 : r2) >> tsft) & 0xFF);
         uint32_t idx = top ^ frame[i];
@@ -226,15 +281,8 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
         r1 ^= btab[idx * 3 + 1];
         r2 ^= btab[idx * 3 + 2];
       }
-      // per-lane rows of M1 (v -> v x^(8C)) and M2 (v -> v x^(8*64*C))
-      uint64_t m1[3][3], m2[3][3];
-      for (int s = 0; s < 3; s++)
-        for (int k = 0; k < 3; k++) {
-          m1[s][k] = d.bch_m1[(lane + 64 * s) * 3 + k];
-          m2[s][k] = d.bch_m2[(lane + 64 * s) * 3 + k];
-        }
       uint64_t a0 = rd_lane_u64(r0, 0), a1 = rd_lane_u64(r1, 0), a2 = rd_lane_u64(r2, 0);
-      for (int l = 1; l < 64; l++) {
+      for (int l = 1; l < 32; l++) {
         uint64_t n0 = __ballot(__popcll((m1[0][0] & a0) ^ (m1[0][1] & a1) ^ (m1[0][2] & a2)) & 1);
         uint64_t n1 = __ballot(__popcll((m1[1][0] & a0) ^ (m1[1][1] & a1) ^ (m1[1][2] & a2)) & 1);
         uint64_t n2 = __ballot(__popcll((m1[2][0] & a0) ^ (m1[2][1] & a1) ^ (m1[2][2] & a2)) & 1);
@@ -259,6 +307,7 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
         for (int k = lane; k < P / 8; k += 64) frame[L + k] = get_byte192(acc, P - 8 - 8 * k);
       }
       __syncthreads();
+      FEC_PHASE(3);
     }
     if (MODE == FEC_TS_TO_BITS) {
       uint8_t *dst = io.out + (int64_t)blockIdx.x * d.nbch;
@@ -278,6 +327,7 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     D[it] = w;
   }
   __syncthreads();
+  FEC_PHASE(4);
   // row a, word w of p[a][c] = XOR over entries (g, b) of d_g[(c - b) mod 360]
   const int q = d.q;
   for (int it = tid; it < q * 12; it += FEC_THREADS) {
@@ -295,18 +345,26 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     rowA[it] = acc;
   }
   __syncthreads();
-  // inclusive prefix XOR over rows a (Hillis-Steele)
-  uint32_t *cur = rowA, *nxt = rowB;
-  for (int dd = 1; dd < q; dd <<= 1) {
-    for (int it = tid; it < q * 12; it += FEC_THREADS) {
-      int a = it / 12;
-      uint32_t v = cur[it];
-      if (a >= dd) v ^= cur[it - 12 * dd];
-      nxt[it] = v;
+  FEC_PHASE(5);
+  // inclusive prefix XOR over rows a, in place: wave w scans word columns 3w..3w+2, 64 rows
+  // per wave-level shuffle scan plus the carry of the previous 64
+  uint32_t *cur = rowA;
+  for (int col = 3 * wave; col < 3 * wave + 3; col++) {
+    uint32_t carry = 0;
+    for (int a0 = 0; a0 < q; a0 += 64) {
+      const int a = a0 + lane;
+      uint32_t v = a < q ? cur[a * 12 + col] : 0u;
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        uint32_t t = __shfl_up(v, dd);
+        if (lane >= dd) v ^= t;
+      }
+      v ^= carry;
+      if (a < q) cur[a * 12 + col] = v;
+      carry = __shfl(v, 63);
     }
-    __syncthreads();
-    uint32_t *t = cur; cur = nxt; nxt = t;
   }
+  __syncthreads();
   // exclusive bit-prefix XOR of the last row (the column parities) along c
   if (tid == 0) {
     uint32_t carry = 0;
@@ -324,6 +382,7 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
   __syncthreads();
   for (int it = tid; it < q * 12; it += FEC_THREADS) cur[it] ^= Wv[it % 12];
   __syncthreads();
+  FEC_PHASE(6);
   // parity bit of row a (interleaved position 360 a + c) / natural index a + q c
   auto pbit = [&](int a, int c) -> uint32_t { return (cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1; };
 
@@ -357,6 +416,14 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
   uint32_t *dstw = (uint32_t *)(io.out + (int64_t)blockIdx.x * io.cw_stride);
   const uint32_t *srcw = (const uint32_t *)stage;
   for (int i = tid; i < cwb / 4 + (cwb & 3 ? 1 : 0); i += FEC_THREADS) dstw[i] = srcw[i];
+#if FEC_VARIANT & 1
+  __syncthreads();
+  FEC_PHASE(7);
+  if (tid == 0) {
+    dstw[0] = (uint32_t)g_fec_ts[0];
+    for (int i = 1; i < 8; i++) dstw[i] = (uint32_t)(g_fec_ts[i] - g_fec_ts[0]);
+  }
+#endif
 }
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {

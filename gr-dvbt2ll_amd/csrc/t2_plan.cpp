@@ -159,9 +159,10 @@ int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
     for (int k = 0; k < 3; k++) fp.bch_tab[d * 3 + k] = v.w[k];
   }
   const int L = fp.kbch / 8;
-  fp.bch_chunk = (L + 255) / 256;
+  // 128 chunks: lanes 0..31 of each of the 4 waves of the FEC kernel (BCH_CHUNKS)
+  fp.bch_chunk = (L + 127) / 128;
   fp.bch_m1 = shift_matrix(g, P, 8L * fp.bch_chunk);
-  fp.bch_m2 = shift_matrix(g, P, 8L * fp.bch_chunk * 64);
+  fp.bch_m2 = shift_matrix(g, P, 8L * fp.bch_chunk * 32);
   // LDPC: info group gidx (360 bits) with address x lands in parity row a = x mod q with
   // cyclic offset b = x div q (columns c = (b + n) mod 360, since pbits = 360 q)
   const t2_ldpc_code_t *c = find_code(normal, rate);
