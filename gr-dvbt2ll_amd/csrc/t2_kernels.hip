@@ -439,13 +439,13 @@ hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s)
 
 // ============================================================================ map kernel
 constexpr int MAP_THREADS = 512;
-constexpr int MAP_LDS_MAX = 160 * 1024;
-// LDS: [LUT 2 KB][cell indices, cs bytes][codeword bytes | cell-interleave staging (8 cs)]
+constexpr int MAP_LDS_MAX = 160 * 1024 - 256;   // leaves room for static LDS of experiment builds
+// LDS: [LUT 2 KB][cell indices, cs bytes][codeword bytes | cell-interleaved index pairs (2 cs)]
+// (<= 99 KB for QPSK normal, 26 KB for 256-QAM normal)
 __host__ __device__ inline int map_idx_bytes(int cs) { return (cs + 15) & ~15; }
-__host__ __device__ inline bool map_stage_in_lds(int cs) { return 2048 + map_idx_bytes(cs) + 8 * cs <= MAP_LDS_MAX; }
 __host__ __device__ inline int map_smem(int cs, int cw_bytes, int apply_ci) {
   int region = cw_bytes;
-  if (apply_ci && map_stage_in_lds(cs) && 8 * cs > region) region = 8 * cs;
+  if (apply_ci && 2 * cs > region) region = 2 * cs;
   return 2048 + map_idx_bytes(cs) + ((region + 15) & ~15);
 }
 
@@ -456,6 +456,18 @@ __device__ __forceinline__ int xcd_major(int i, int n) {
   return i < (q << 3) ? (i & 7) * q + (i >> 3) : i;
 }
 
+// experiment switch (product builds: 0): bit 0 = phase timestamps of each chain block written
+// over its first three cell-interleaved cells (wrong output; tools/map_phases.py decodes them)
+#ifndef MAP_VARIANT
+#define MAP_VARIANT 0
+#endif
+#if MAP_VARIANT & 1
+__shared__ uint64_t g_map_ts[8];
+#define MAP_PHASE(i) do { if (threadIdx.x == 0) g_map_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define MAP_PHASE(i) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -463,9 +475,9 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   float2 *lut = (float2 *)smem;
   uint8_t *idx = smem + 2048;
   uint8_t *cw = smem + 2048 + map_idx_bytes(d.cs);
-  float2 *stage = (float2 *)cw;
-  const bool lds_stage = map_stage_in_lds(d.cs);
+  uint16_t *stage = (uint16_t *)cw;    // chain: (idx[j], idx[j-1]) at cell-interleaved position t
   const int cs = d.cs, nl = d.nldpc;
+  MAP_PHASE(0);
   for (int i = tid; i < 256; i += MAP_THREADS) lut[i] = d.lut[i];
   // ---- interleaver input bits (tempu) into LDS
   if (io.packed_in) {
@@ -490,6 +502,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
     }
   }
   __syncthreads();
+  MAP_PHASE(1);
   auto bit = [&](int i) -> uint32_t { return (cw[i >> 3] >> (7 - (i & 7))) & 1; };
   // ---- cell indices: column-twist write / row read / demux (interleavermod:351-403 ...)
   if (d.mode == 0) {
@@ -512,10 +525,11 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
     }
   }
   __syncthreads();
-  // ---- constellation + cyclic Q delay; chain: cell interleaver (framemapper:1973-1998) into
-  //      LDS, then the time interleaver (framemapper:1999-2028) as the store pattern: FEC block r
-  //      of its TI block fills columns 5(r-r0)..+4 of a rows x 5nb array read row by row, so
-  //      cells land in the frame data region in transmission order.
+  MAP_PHASE(2);
+  // ---- constellation + cyclic Q delay; chain: cell interleaver (framemapper:1973-1998) on the
+  //      cell indices in LDS, then QAM fused into the time-interleaver (framemapper:1999-2028)
+  //      store pattern: FEC block r of its TI block fills columns 5(r-r0)..+4 of a rows x 5nb
+  //      array read row by row, so cells land in the frame data region in transmission order.
   if (!io.apply_ci) {
     float2 *dst = io.out + (int64_t)blk * cs;
     for (int j = tid; j < cs; j += MAP_THREADS) {
@@ -536,36 +550,58 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   }
   const int rows = cs / 5, cols = 5 * nb;
   const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
+#if MAP_VARIANT & 1
   auto ti_dst = [&](int t) -> int64_t {
     if (!d.ti_on) return (int64_t)r * cs + t;
     const int e = t / rows, row = t - e * rows;
     return base + (int64_t)row * cols + e;
   };
+#endif
+  // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
   for (int j = tid; j < cs; j += MAP_THREADS) {
-    float2 v = lut[idx[j]];
-    if (d.rotation) v.y = lut[idx[j == 0 ? cs - 1 : j - 1]].y;
     int t = d.ci_perm[j] + shift;
     t -= t >= cs ? cs : 0;
-    if (lds_stage) stage[t] = v;
-    else dst[ti_dst(t)] = v;   // QPSK normal: 259 KB of cells do not fit LDS, scatter directly
+    stage[t] = (uint16_t)(idx[j] | (idx[j == 0 ? cs - 1 : j - 1] << 8));
   }
-  if (lds_stage) {
-    __syncthreads();
-    if (!d.ti_on) {
-      for (int j = tid; j < cs; j += MAP_THREADS) dst[(int64_t)r * cs + j] = stage[j];
+  __syncthreads();
+  MAP_PHASE(3);
+  // QAM (+ rotated-constellation Q delay) fused into the time-interleaver store: row-major over
+  // (row, e), 5 consecutive cells (40 B) per TI row
+  for (int j = tid; j < cs; j += MAP_THREADS) {
+    int t, o;
+    if (d.ti_on) {
+      const int row = j / 5, e = j - 5 * row;
+      t = e * rows + row;
+      o = row * cols + e;
     } else {
-      // row-major over (row, e): 5 consecutive cells (40 B) per TI row
-      for (int j = tid; j < cs; j += MAP_THREADS) {
-        const int row = j / 5, e = j - 5 * row;
-        dst[base + (int64_t)row * cols + e] = stage[e * rows + row];
-      }
+      t = j;
+      o = j;
+    }
+    const uint32_t pr = stage[t];
+    float2 v = lut[pr & 0xFF];
+    if (d.rotation) v.y = lut[pr >> 8].y;
+    dst[(d.ti_on ? base : (int64_t)r * cs) + o] = v;
+  }
+#if MAP_VARIANT & 1
+  __syncthreads();
+  MAP_PHASE(4);
+  if (tid == 0) {
+    uint32_t v[6] = {(uint32_t)g_map_ts[0], (uint32_t)(g_map_ts[1] - g_map_ts[0]), (uint32_t)(g_map_ts[2] - g_map_ts[0]),
+                     (uint32_t)(g_map_ts[3] - g_map_ts[0]), (uint32_t)(g_map_ts[4] - g_map_ts[0]), 0u};
+    for (int c = 0; c < 3; c++) {
+      float2 x;
+      x.x = __uint_as_float(v[2 * c]);
+      x.y = __uint_as_float(v[2 * c + 1]);
+      dst[ti_dst(c)] = x;
     }
   }
+#endif
 }
 
 hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
   int smem = map_smem(d.cs, d.nldpc / 8 + 4, io.apply_ci);
+  if (smem > MAP_LDS_MAX) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void *)map_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, MAP_LDS_MAX);

@@ -1,0 +1,39 @@
+"""Decode per-block phase timestamps from a MAP_VARIANT=1 build (experiment only)."""
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "gr-dvbt2ll_amd"), str(ROOT / "tests")]
+import dvbt2ll  # noqa: E402
+from dvbt2ll.configs import CONFIGS, ts_for_frames  # noqa: E402
+import plan_probe as PP  # noqa: E402
+
+cfg = CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "cfg3"]
+B = 16
+ch = dvbt2ll.Chain(cfg, max_frames=B)
+ts, base = ts_for_frames(cfg, 0, B)
+ts_d = torch.from_numpy(ts).cuda()
+iq = torch.empty((B * ch.iq_per_frame, 2), dtype=torch.float32, device="cuda")
+for _ in range(3):
+    ch.run_device(ts_d.data_ptr(), base, len(ts), 0, B, iq.data_ptr(), torch.cuda.current_stream().cuda_stream)
+torch.cuda.synchronize()
+plan = PP.frame_plan(cfg.fm_args())
+F = plan["F"]
+cells = ch.debug_cells(plan["S"]).view(np.uint32).reshape(-1, 2)
+rows = []
+for r in range(F):
+    pos = [int(PP.ti_dest(plan, np.array([r]), np.array([c]))[0]) for c in range(3)]
+    w = np.concatenate([cells[p] for p in pos]).astype(np.int64)
+    rows.append(w)
+a = np.array(rows)
+names = ["cw load", "cell idx", "qam+ci", "ti store"]
+prev = np.zeros(len(a), np.int64)
+print("map phases (us), median / p90 over %d blocks of frame 0" % len(a))
+for i, n in enumerate(names):
+    cur = a[:, i + 1]
+    print("  %-9s %7.2f %7.2f" % (n, np.median((cur - prev) * 0.01), np.percentile((cur - prev) * 0.01, 90)))
+    prev = cur
+print("  total     %7.2f" % np.median(a[:, 4] * 0.01))
