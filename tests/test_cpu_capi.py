@@ -34,3 +34,15 @@ def test_reference_block_names():
         assert hasattr(dvbt2ll, n)
         assert hasattr(getattr(dvbt2ll, n), "make")
     assert dvbt2ll.FFTSIZE_16K_T2GI == 11 and dvbt2ll.C2_5 == 7 and dvbt2ll.PREAMBLE_T2_LITE_MISO == 4
+
+
+def test_no_cpu_fallback_without_gpu():
+    """the product fails loudly when no gfx950 device is visible (no silent CPU path)"""
+    import pytest
+    lib = dvbt2ll.lib()
+    if lib.dvbt2ll_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(dvbt2ll.DVBT2Error):
+        dvbt2ll.bbheaderbch_bb(0, 4, 0, 0, 8, 4000000)
+    with pytest.raises(dvbt2ll.DVBT2Error):
+        dvbt2ll.Chain(dvbt2ll.CONFIGS["cfg1"], max_frames=1)
