@@ -684,8 +684,8 @@ __device__ __forceinline__ float2 tw_at(const float2 *tw, uint32_t i) {
   return cmulf(tw[128 + (i >> 7)], tw[i & 127]);
 }
 
-// v[r] *= w^(r * e) for r = 1..R-1: one table lookup for w^e, the other powers by products
-// of depth <= 4 (w^2e, w^3e, w^4e, w^8e, w^12e, then hi * lo)
+// v[r] *= w^(r * e) for r = 1..R-1 (R <= 32): one table lookup for w^e, the other powers by
+// products of depth <= 5 (w^2e, w^3e, w^4e, w^8e, w^12e, w^16e, then top * hi * lo)
 template <int R>
 __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32_t e) {
   if (R == 1) return;
@@ -700,19 +700,23 @@ __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32
     hi[2] = cmulf(hi[1], hi[1]);
     hi[3] = cmulf(hi[2], hi[1]);
   }
+  float2 top = make_float2(1.f, 0.f);
+  if (R > 16) top = cmulf(hi[2], hi[2]);                  // w^16e
 #pragma unroll
   for (int r = 1; r < R; r++) {
-    const int h = r >> 2, l = r & 3;
+    const int t = r >> 4, h = (r >> 2) & 3, l = r & 3;
     float2 w = h == 0 ? lo[l] : (l == 0 ? hi[h] : cmulf(hi[h], lo[l]));
+    if (t) w = (h == 0 && l == 0) ? top : cmulf(top, w);
     v[r] = cmulf(v[r], w);
   }
 }
 
 template <int NSUB, int NT, int R, int NS>
 struct StockhamPass {
-  static constexpr int U = 16 / R;          // units per thread
+  static constexpr int V = NSUB / NT;       // values per thread
+  static constexpr int U = V / R;           // units per thread
   // every LDS address below is lds_pad(thread base) + a compile-time offset (immediate field)
-  static_assert((NS == 1 && R == 16) || NS % 16 == 0, "pad offsets need NS == 1 (R == 16) or 16 | NS");
+  static_assert((NS == 1 && R % 16 == 0) || NS % 16 == 0, "pad offsets need NS == 1 (16 | R) or 16 | NS");
   static_assert((NSUB / R) % 16 == 0, "pad offsets need 16 | NSUB / R");
   // twiddles + DFT on the thread's U units (v laid out [u][r])
   __device__ __forceinline__ static void compute(float2 *v, const float2 *tw, uint32_t tws, int tid) {
@@ -768,20 +772,23 @@ struct StockhamTail<NSUB, NT, NS, R, Rs...> {
   }
 };
 
-template <int NSUB> struct FftPlan;
-template <> struct FftPlan<1024> { static constexpr int RL = 4; template <class F> using Tail = StockhamTail<1024, 64, 16, 16, 4>; };
-template <> struct FftPlan<2048> { static constexpr int RL = 8; template <class F> using Tail = StockhamTail<2048, 128, 16, 16, 8>; };
-template <> struct FftPlan<4096> { static constexpr int RL = 16; template <class F> using Tail = StockhamTail<4096, 256, 16, 16, 16>; };
-template <> struct FftPlan<8192> { static constexpr int RL = 2; template <class F> using Tail = StockhamTail<8192, 512, 16, 16, 16, 2>; };
-template <> struct FftPlan<16384> { static constexpr int RL = 4; template <class F> using Tail = StockhamTail<16384, 1024, 16, 16, 16, 4>; };
+// FFT plans: first pass radix V (values per thread) from LDS or registers, then the tail.
+// RL = radix of the last pass; thread t ends with n = t + NT*(u + (V/RL)*r).
+template <int NSUB, int V> struct FftPlan;
+template <> struct FftPlan<1024, 16> { static constexpr int RL = 4; using Tail = StockhamTail<1024, 64, 16, 16, 4>; };
+template <> struct FftPlan<2048, 16> { static constexpr int RL = 8; using Tail = StockhamTail<2048, 128, 16, 16, 8>; };
+template <> struct FftPlan<4096, 16> { static constexpr int RL = 16; using Tail = StockhamTail<4096, 256, 16, 16, 16>; };
+template <> struct FftPlan<8192, 16> { static constexpr int RL = 2; using Tail = StockhamTail<8192, 512, 16, 16, 16, 2>; };
+template <> struct FftPlan<16384, 16> { static constexpr int RL = 4; using Tail = StockhamTail<16384, 1024, 16, 16, 16, 4>; };
+// 32K halves: 512 threads x 32 values, radices 32 x 32 x 16 (three LDS passes)
+template <> struct FftPlan<16384, 32> { static constexpr int RL = 16; using Tail = StockhamTail<16384, 512, 32, 32, 16>; };
 
-// Experiment switch for tools/ofdm_experiments.sh (product builds use 0): bit 2 = skip the
-// E parking of the split 32K transform (wrong output; measures its cost).
+// experiment switch (product builds: 0): bit 3 = phase timestamps (s_memrealtime, 100 MHz) of
+// each workgroup written over the first samples of its symbol's guard interval (wrong output;
+// tools/ofdm_phases.py decodes them)
 #ifndef OFDM_VARIANT
 #define OFDM_VARIANT 0
 #endif
-// bit 3: phase timestamps (s_memrealtime, 100 MHz) of each workgroup written over the first
-// samples of its symbol's guard interval (wrong output; tools/ofdm_phases.py decodes them)
 #if OFDM_VARIANT & 8
 __shared__ uint64_t g_phase_ts[16];
 #define OFDM_PHASE(i) do { if (threadIdx.x == 0) g_phase_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -802,28 +809,29 @@ struct BinSource {
   uint32_t d0, dn;             // scatter mode: this symbol's data slots
 };
 
-// One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split), ending with
-// v[u*RL + r] = y[t + NT*(u + (16/RL)*r)].
-template <int NSUB, bool SPLIT>
+// One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split) by NT = NSUB/V
+// threads, ending with v[u*RL + r] = y[t + NT*(u + (V/RL)*r)].
+template <int NSUB, bool SPLIT, int V>
 __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource &src, const float *isinc,
                                          const float2 *tw, uint32_t tws, int tid, int half) {
-  constexpr int NT = NSUB / 16, N = SPLIT ? 2 * NSUB : NSUB;
-  // first pass (R = 16, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
+  constexpr int NT = NSUB / V, N = SPLIT ? 2 * NSUB : NSUB;
+  // first pass (R = V, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
   const int32_t *m = src.map + (SPLIT ? half * NSUB : 0);
   if (src.inv) {
-    // every bin: aux value, or zero for data bins (aux entry 0); branch-free, all 16 codes in
-    // flight, then all 16 aux loads (two memory round trips)
-    {
+    // every bin: aux value, or zero for data bins (aux entry 0); branch-free, all V codes in
+    // flight, then all V aux loads (two memory round trips)
+#pragma unroll
+    for (int c0 = 0; c0 < V; c0 += 16) {
       int code[16];
 #pragma unroll
-      for (int u = 0; u < 16; u++) code[u] = ld_off(m, (uint32_t)(tid + NT * u) * 4u);
+      for (int u = 0; u < 16; u++) code[u] = ld_off(m, (uint32_t)(tid + NT * (c0 + u)) * 4u);
       float2 a[16];
 #pragma unroll
       for (int u = 0; u < 16; u++)
         a[u] = ld_off(src.data, (src.abase + (code[u] < 0 ? (uint32_t)(-code[u]) : 1u)) * 8u);
       float2 *b = lds + lds_pad((uint32_t)tid);
 #pragma unroll
-      for (int u = 0; u < 16; u++) b[u * NT * 17 / 16] = a[u];
+      for (int u = 0; u < 16; u++) b[(c0 + u) * NT * 17 / 16] = a[u];
     }
     __syncthreads();
     OFDM_PHASE(1 + 4 * half);
@@ -831,7 +839,7 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     // cells of the other half go to a per-lane dummy slot past the buffer (branch-free)
     const uint32_t lo = SPLIT ? (uint32_t)half * NSUB : 0u;
     const uint32_t dummy = (uint32_t)(NSUB + NSUB / 16) + (uint32_t)(tid & 63);
-    constexpr int SC = NSUB >= 16384 ? 32 : 16;   // slots per thread per round (32K: one round)
+    constexpr int SC = V == 32 ? 16 : 32;        // slots per thread per round
     const uint32_t last = src.dn - 1u;
     for (uint32_t s0 = 0; s0 < src.dn; s0 += (uint32_t)SC * NT) {
       uint32_t b[SC];
@@ -847,11 +855,11 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     }
     __syncthreads();
     OFDM_PHASE(2 + 4 * half);
-    StockhamPass<NSUB, NT, 16, 1>::load_lds(v, lds, tid);
+    StockhamPass<NSUB, NT, V, 1>::load_lds(v, lds, tid);
     __syncthreads();
   } else {
 #pragma unroll
-    for (int c0 = 0; c0 < 16; c0 += 8) {
+    for (int c0 = 0; c0 < V; c0 += 8) {
       uint32_t off[8];
 #pragma unroll
       for (int u = 0; u < 8; u++) {
@@ -865,7 +873,7 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   }
   if (isinc) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
+    for (int r = 0; r < V; r++) {
       uint32_t k = (uint32_t)(tid + NT * r);
       if (SPLIT) k = 2 * k + half;
       float sc = isinc[(k + N / 2) & (N - 1)];
@@ -874,17 +882,18 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     }
   }
   __builtin_amdgcn_sched_barrier(0);
-  Dft<16>::run(v);
-  StockhamPass<NSUB, NT, 16, 1>::store_lds(v, lds, tid);
+  Dft<V>::run(v);
+  StockhamPass<NSUB, NT, V, 1>::store_lds(v, lds, tid);
   __syncthreads();
-  FftPlan<NSUB>::template Tail<void>::run(v, lds, tw, tws, tid);
+  FftPlan<NSUB, V>::Tail::run(v, lds, tw, tws, tid);
 }
 
 template <int N>
 struct OfdmShape {
   static constexpr bool SPLIT = N > 16384;
   static constexpr int NSUB = SPLIT ? N / 2 : N;
-  static constexpr int NT = NSUB / 16;
+  static constexpr int V = SPLIT ? 32 : 16;                           // values per thread
+  static constexpr int NT = NSUB / V;
   static constexpr int FFT_LDS = (NSUB + NSUB / 16 + 64) * 8;       // padded buffer + 64 dummy slots
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
   static constexpr int LDS_BYTES = FFT_LDS + TW_ENTRIES * 8;
@@ -893,7 +902,7 @@ struct OfdmShape {
 template <int N>
 __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmIO io) {
   using Sh = OfdmShape<N>;
-  constexpr int NSUB = Sh::NSUB, NT = Sh::NT, RL = FftPlan<NSUB>::RL, UL = 16 / RL;
+  constexpr int NSUB = Sh::NSUB, NT = Sh::NT, V = Sh::V, RL = FftPlan<NSUB, V>::RL, UL = V / RL;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2 *lds = (float2 *)smem;
   float2 *twl = (float2 *)(smem + Sh::FFT_LDS);
@@ -922,7 +931,6 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
       const int sub = Sh::SPLIT ? (k & 1) : 0, kk = Sh::SPLIT ? (k >> 1) : k;
       int code = map[sub * NSUB + kk];
       float2 v = data[code >= 0 ? cbase + (uint32_t)code : abase - (uint32_t)code];
-      (void)src;
       if (d.isinc) {
         float sc = d.isinc[(k + N / 2) & (N - 1)];
         v.x *= sc;
@@ -939,44 +947,31 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const int G = d.G;
   float2 *o = io.out + (int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + G);
   const float nrm = d.norm;
-  float2 v[16];
+  float2 v[V];
   OFDM_PHASE(0);
-  sub_ifft<NSUB, Sh::SPLIT>(v, lds, src, d.isinc, twl, tws, tid, 0);
+  sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid, 0);
   OFDM_PHASE(3);
   if (Sh::SPLIT) {
-    // x[n] = E[n] + w^n O[n], x[n + NSUB] = E[n] - w^n O[n], w = exp(2 pi i / N).
-    // E is parked in this symbol's own output slots x[n] (same thread re-reads it; the
-    // lines stay in L2) so the odd-bin transform runs within the 128-VGPR budget.
+    // x[n] = E[n] + w^n O[n], x[n + NSUB] = E[n] - w^n O[n], w = exp(2 pi i / N): the even-bin
+    // transform E stays in registers (32 values per thread) while the odd-bin one runs
+    float2 e[V];
 #pragma unroll
-    for (int u = 0; u < UL; u++)
-#pragma unroll
-      for (int r = 0; r < RL; r++) {
-        const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
-#if !(OFDM_VARIANT & 4)
-        st_off(o, ((uint32_t)G + n) * 8u, v[u * RL + r]);
-#endif
-      }
-    __syncthreads();
+    for (int i = 0; i < V; i++) e[i] = v[i];
+    OFDM_PHASE(4);
     // launder tid: stops the compiler from keeping the first transform's index/twiddle
-    // arithmetic alive (spilled) for reuse by the second
+    // arithmetic alive for reuse by the second
     int tid2 = tid;
     asm volatile("" : "+v"(tid2));
-    OFDM_PHASE(4);
-    sub_ifft<NSUB, Sh::SPLIT>(v, lds, src, d.isinc, twl, tws, tid2, 1);
+    sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid2, 1);
     OFDM_PHASE(7);
 #pragma unroll
-    for (int u = 0; u < UL; u++)
+    for (int uu = 0; uu < UL; uu++)
 #pragma unroll
       for (int r = 0; r < RL; r++) {
-        const int i = u * RL + r;
-        const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
-#if OFDM_VARIANT & 4
-        const float2 e = v[i ^ 1];
-#else
-        const float2 e = ld_off(o, ((uint32_t)G + n) * 8u);
-#endif
+        const int i = uu * RL + r;
+        const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
         float2 t = cmulf(v[i], tw_at(twl, n));
-        float2 a = cadd(e, t), b = csub(e, t);
+        float2 a = cadd(e[i], t), b = csub(e[i], t);
         a.x *= nrm; a.y *= nrm; b.x *= nrm; b.y *= nrm;
         st_nt(o, ((uint32_t)G + n) * 8u, a);
         const uint32_t n2 = n + (uint32_t)NSUB;
@@ -987,11 +982,11 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
       }
   } else {
 #pragma unroll
-    for (int u = 0; u < UL; u++)
+    for (int uu = 0; uu < UL; uu++)
 #pragma unroll
       for (int r = 0; r < RL; r++) {
-        const uint32_t n = (uint32_t)(tid + NT * (u + UL * r));
-        float2 a = v[u * RL + r];
+        const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
+        float2 a = v[uu * RL + r];
         a.x *= nrm; a.y *= nrm;
         st_nt(o, ((uint32_t)G + n) * 8u, a);
         if (n >= (uint32_t)(N - G)) st_nt(o, (n - (uint32_t)(N - G)) * 8u, a);

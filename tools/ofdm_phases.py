@@ -12,7 +12,7 @@ import dvbt2ll  # noqa: E402
 from dvbt2ll.configs import CONFIGS, ts_for_frames  # noqa: E402
 
 cfg = CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "cfg3"]
-B = 16
+B = 64
 ch = dvbt2ll.Chain(cfg, max_frames=B)
 ts, base = ts_for_frames(cfg, 0, B)
 ts_d = torch.from_numpy(ts).cuda()
@@ -33,7 +33,7 @@ a = np.array(rows)
 t0 = a[:, 0]
 t0 = (t0 - t0.min()) & 0xFFFFFFFF
 d = a[:, 1:9]
-names = ["fill0", "scatter0", "fft0", "park", "fill1", "scatter1", "fft1", "combine"]
+names = ["fill0", "scatter0", "fft0", "hold E", "fill1", "scatter1", "fft1", "combine"]
 prev = np.zeros(len(a), np.int64)
 print("phase durations (us), median / p90 over %d workgroups" % len(a))
 for i, n in enumerate(names):
