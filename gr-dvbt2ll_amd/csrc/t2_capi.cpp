@@ -497,7 +497,7 @@ struct dvbt2ll_chain {
   FramePlan frame;
   PilotPlan pilot;
   OfdmTables ofdm;
-  DevBuf cw, cells, perm, shift, inv, sym_d0, sym_n, ts_tmp, iq_tmp;
+  DevBuf cw, cells, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
   int max_frames = 0;
   int64_t aux_pad = 0;       // cells buffer = [aux variants (aux_pad elements) | frame cells]
   int64_t cw_stride = 0;
@@ -568,8 +568,12 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   ChainLayout layout;
   if (build_chain_layout(h->frame, h->pilot, layout)) return DVBT2LL_EINVAL;
   if ((r = upload(h->inv, layout.inv)) || (r = upload(h->sym_d0, layout.sym_d0)) ||
-      (r = upload(h->sym_n, layout.sym_n)))
+      (r = upload(h->sym_n, layout.sym_n)) || (r = upload(h->sym_n0, layout.sym_n0)))
     return r;
+  if (!layout.part.empty()) {
+    if ((r = upload(h->part, layout.part))) return r;
+    h->map.dev.part = h->part.as<int32_t>();
+  }
   const PilotPlan &pp = h->pilot;
   std::vector<cf32> aux = h->frame.aux;
   for (int v = 0; v < h->frame.t2frames; v++)
@@ -578,6 +582,7 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   h->ofdm.dev.inv = h->inv.as<uint16_t>();
   h->ofdm.dev.sym_d0 = h->sym_d0.as<int32_t>();
   h->ofdm.dev.sym_n = h->sym_n.as<int32_t>();
+  h->ofdm.dev.sym_n0 = h->sym_n0.as<int32_t>();
   h->aux_pad = ((int64_t)aux.size() + 63) / 64 * 64;
   h->cw_stride = ((h->fec.plan.nldpc / 8) + 255) / 256 * 256;
   h->iq_per_frame = (int64_t)pp.Nsym * (pp.N + pp.G) + 2048;

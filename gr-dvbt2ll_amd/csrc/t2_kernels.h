@@ -42,6 +42,7 @@ struct MapDev {
   const int32_t *ci_shift; // F  (chain only)
   int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
+  const int32_t *part;     // chain, 32K only: TI output index -> data slot (ChainLayout::part)
   uint8_t twist[16], mux[16];
 };
 struct MapIO {
@@ -59,7 +60,7 @@ struct OfdmDev {
   // chain (scatter) mode: symbol j's cells are the slots [sym_d0[j], +sym_n[j]), slot s goes to
   // stored bin inv[s]; null -> gather mode (bin_map >= 0 codes are read per bin)
   const uint16_t *inv;
-  const int32_t *sym_d0, *sym_n;
+  const int32_t *sym_d0, *sym_n, *sym_n0;   // sym_n0: slots of the even-bin half (split)
   const float2 *twiddle;    // 128 + N/128: two-level table (PilotPlan::twiddle)
   const float *isinc;       // N or null
   const float2 *p1;         // 2048

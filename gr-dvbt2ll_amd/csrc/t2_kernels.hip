@@ -580,7 +580,8 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
     const uint32_t pr = stage[t];
     float2 v = lut[pr & 0xFF];
     if (d.rotation) v.y = lut[pr >> 8].y;
-    dst[(d.ti_on ? base : (int64_t)r * cs) + o] = v;
+    const int64_t sidx = (d.ti_on ? base : (int64_t)r * cs) + o;
+    dst[d.part ? (int64_t)d.part[sidx] : sidx] = v;
   }
 #if MAP_VARIANT & 1
   __syncthreads();
@@ -806,7 +807,7 @@ struct BinSource {
   const float2 *data;          // uniform base; cells at cbase + code, aux at abase - code
   uint32_t cbase, abase;
   const uint16_t *inv;         // scatter mode: stored bin of each data slot (null: gather mode)
-  uint32_t d0, dn;             // scatter mode: this symbol's data slots
+  uint32_t d0, dn, dn0;        // scatter mode: this symbol's data slots; the first dn0 feed half 0
 };
 
 // One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split) by NT = NSUB/V
@@ -820,35 +821,37 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   if (src.inv) {
     // every bin: aux value, or zero for data bins (aux entry 0); branch-free, all V codes in
     // flight, then all V aux loads (two memory round trips)
+    {
+      int code[V];
 #pragma unroll
-    for (int c0 = 0; c0 < V; c0 += 16) {
-      int code[16];
+      for (int u = 0; u < V; u++) code[u] = ld_off(m, (uint32_t)(tid + NT * u) * 4u);
+      float2 a[V];
 #pragma unroll
-      for (int u = 0; u < 16; u++) code[u] = ld_off(m, (uint32_t)(tid + NT * (c0 + u)) * 4u);
-      float2 a[16];
-#pragma unroll
-      for (int u = 0; u < 16; u++)
+      for (int u = 0; u < V; u++)
         a[u] = ld_off(src.data, (src.abase + (code[u] < 0 ? (uint32_t)(-code[u]) : 1u)) * 8u);
       float2 *b = lds + lds_pad((uint32_t)tid);
 #pragma unroll
-      for (int u = 0; u < 16; u++) b[(c0 + u) * NT * 17 / 16] = a[u];
+      for (int u = 0; u < V; u++) b[u * NT * 17 / 16] = a[u];
     }
     __syncthreads();
     OFDM_PHASE(1 + 4 * half);
     // data cells: the symbol's slots streamed with unit-stride loads, written to their bins;
     // cells of the other half go to a per-lane dummy slot past the buffer (branch-free)
+    // (split: the run is partitioned, so half h streams only its own slots)
     const uint32_t lo = SPLIT ? (uint32_t)half * NSUB : 0u;
     const uint32_t dummy = (uint32_t)(NSUB + NSUB / 16) + (uint32_t)(tid & 63);
-    constexpr int SC = V == 32 ? 16 : 32;        // slots per thread per round
-    const uint32_t last = src.dn - 1u;
-    for (uint32_t s0 = 0; s0 < src.dn; s0 += (uint32_t)SC * NT) {
+    const uint32_t r0 = src.d0 + (SPLIT && half ? src.dn0 : 0u);
+    const uint32_t rn = SPLIT ? (half ? src.dn - src.dn0 : src.dn0) : src.dn;
+    constexpr int SC = 32;                       // slots per thread per round
+    const uint32_t last = rn - 1u;
+    for (uint32_t s0 = 0; s0 < rn; s0 += (uint32_t)SC * NT) {
       uint32_t b[SC];
       float2 c[SC];
 #pragma unroll
       for (int u = 0; u < SC; u++) {
         const uint32_t sl = min(s0 + (uint32_t)(tid + NT * u), last);
-        b[u] = (uint32_t)src.inv[src.d0 + sl] - lo;
-        c[u] = ld_off(src.data, (src.cbase + src.d0 + sl) * 8u);
+        b[u] = (uint32_t)src.inv[r0 + sl] - lo;
+        c[u] = ld_off(src.data, (src.cbase + r0 + sl) * 8u);
       }
 #pragma unroll
       for (int u = 0; u < SC; u++) lds[b[u] < (uint32_t)NSUB ? lds_pad(b[u]) : dummy] = c[u];
@@ -919,10 +922,11 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
   const int32_t *map = d.bin_map + (int64_t)j * N;
   const uint32_t tws = Sh::SPLIT ? 2u : 1u;       // sub-transform twiddle = table index * tws
-  BinSource src{map, data, cbase, abase, d.inv, 0u, 0u};
+  BinSource src{map, data, cbase, abase, d.inv, 0u, 0u, 0u};
   if (d.inv) {
     src.d0 = (uint32_t)d.sym_d0[j];
     src.dn = (uint32_t)d.sym_n[j];
+    src.dn0 = (uint32_t)d.sym_n0[j];
   }
 
   if (io.carriers_only) {                          // test hook: bins in natural order

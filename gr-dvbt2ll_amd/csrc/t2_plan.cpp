@@ -996,6 +996,25 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
   }
   for (int s = 0; s < fp.S; s++)
     if (!seen[s]) return -1;
+  cl.sym_n0 = cl.sym_n;
+  cl.part.clear();
+  if (ofdm_split(pp.N)) {
+    const int half = pp.N / 2;
+    cl.part.assign(fp.S, 0);
+    std::vector<uint16_t> inv2(fp.S);
+    for (int j = 0; j < pp.Nsym; j++) {
+      const int d0 = cl.sym_d0[j], n = cl.sym_n[j];
+      int n0 = 0;
+      for (int s = d0; s < d0 + n; s++) n0 += cl.inv[s] < half;
+      int a = d0, b = d0 + n0;
+      for (int s = d0; s < d0 + n; s++) cl.part[s] = cl.inv[s] < half ? a++ : b++;
+      cl.sym_n0[j] = n0;
+    }
+    for (int s = 0; s < fp.S; s++) inv2[cl.part[s]] = cl.inv[s];
+    cl.inv.swap(inv2);
+    for (auto &c : cl.cmap)
+      if (c >= 0) c = cl.part[c];
+  }
   return 0;
 }
 

@@ -105,10 +105,14 @@ std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t
 // symbol j's data cells are the contiguous slots [sym_d0[j], sym_d0[j] + sym_n[j]).  The OFDM
 // kernel streams that range with unit-stride loads and scatters each cell into its IFFT bin in
 // LDS (inv), after filling pilot / null / L1 / dummy bins from the aux table (cmap < 0).
+// When the OFDM kernel splits N = 32K into even / odd-bin halves, each symbol's run is further
+// partitioned [cells of even bins | cells of odd bins] (each part in TI output order), so a half
+// streams only its own cells; `part` maps the TI output index to that slot (empty: identity).
 struct ChainLayout {
   std::vector<int32_t> cmap;     // Nsym x N, stored row order: >= 0 data slot, < 0 aux (-code - 1)
   std::vector<uint16_t> inv;     // S: data slot -> stored bin index within its symbol's row
-  std::vector<int32_t> sym_d0, sym_n;   // Nsym
+  std::vector<int32_t> sym_d0, sym_n, sym_n0;   // Nsym: run start, length, cells of the first half
+  std::vector<int32_t> part;     // S: TI output index -> data slot (split only)
 };
 int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl);
 // time-interleaver output index (frame data order) of cell-interleaved cell t of FEC block r

@@ -69,7 +69,7 @@ int t2probe_fec(int framesize, int rate, int constellation, int *info, uint32_t 
 // fused-chain layout: cmap Nsym x N (stored row order), inv S, sym_d0/sym_n Nsym;
 // info [Nsym, N, S, split]
 int t2probe_chain(const int *p20, const int *pg3, int *info, int32_t *cmap, uint16_t *inv, int32_t *d0,
-                  int32_t *dn) {
+                  int32_t *dn, int32_t *dn0, int32_t *part) {
   FmParams f{p20[0], p20[1], p20[2], p20[3], p20[4], p20[5], p20[6], p20[7], p20[8], p20[9],
              p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
   PgParams g{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
@@ -83,6 +83,13 @@ int t2probe_chain(const int *p20, const int *pg3, int *info, int32_t *cmap, uint
   if (inv) memcpy(inv, cl.inv.data(), cl.inv.size() * 2);
   if (d0) memcpy(d0, cl.sym_d0.data(), cl.sym_d0.size() * 4);
   if (dn) memcpy(dn, cl.sym_n.data(), cl.sym_n.size() * 4);
+  if (dn0) memcpy(dn0, cl.sym_n0.data(), cl.sym_n0.size() * 4);
+  if (part) {
+    if (cl.part.empty())
+      for (int s = 0; s < fp.S; s++) part[s] = s;
+    else
+      memcpy(part, cl.part.data(), cl.part.size() * 4);
+  }
   return 0;
 }
 }

@@ -26,7 +26,7 @@ def lib():
         L.t2probe_pilot.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.t2probe_map.argtypes = [ctypes.c_int] * 4 + [vp, vp]
         L.t2probe_fec.argtypes = [ctypes.c_int] * 3 + [vp, vp, vp]
-        L.t2probe_chain.argtypes = [vp] * 7
+        L.t2probe_chain.argtypes = [vp] * 9
         _L = L
     return _L
 
@@ -106,20 +106,23 @@ def ti_dest(plan, r, t):
 
 def chain_layout(cfg):
     """the fused chain's layout: cmap (Nsym x N, stored row order: [even | odd] bins when split;
-    data codes are frame data slots in TI output order), inv (slot -> stored bin), and each
-    symbol's contiguous slot range [d0, d0 + n)"""
+    data codes are frame data slots), inv (slot -> stored bin), each symbol's contiguous slot
+    range [d0, d0 + n) with its first n0 slots feeding the even half when split, and part
+    (TI output index -> slot)"""
     p = np.array(cfg.fm_args(), np.int32)
     g = np.array([cfg.misogroup, cfg.equalization, cfg.bandwidth], np.int32)
     info = np.zeros(4, np.int32)
-    assert lib().t2probe_chain(_p(p), _p(g), _p(info), None, None, None, None) == 0
+    assert lib().t2probe_chain(_p(p), _p(g), _p(info), None, None, None, None, None, None) == 0
     Nsym, N, S, split = (int(x) for x in info)
     cmap = np.zeros(Nsym * N, np.int32)
     inv = np.zeros(S, np.uint16)
     d0 = np.zeros(Nsym, np.int32)
     dn = np.zeros(Nsym, np.int32)
-    assert lib().t2probe_chain(_p(p), _p(g), _p(info), _p(cmap), _p(inv), _p(d0), _p(dn)) == 0
+    dn0 = np.zeros(Nsym, np.int32)
+    part = np.zeros(S, np.int32)
+    assert lib().t2probe_chain(_p(p), _p(g), _p(info), _p(cmap), _p(inv), _p(d0), _p(dn), _p(dn0), _p(part)) == 0
     return dict(Nsym=Nsym, N=N, S=S, split=split, cmap_stored=cmap.reshape(Nsym, N), inv=inv.astype(np.int64),
-                d0=d0, n=dn)
+                d0=d0, n=dn, n0=dn0, part=part.astype(np.int64))
 
 
 def stored_to_natural(row, N, split):

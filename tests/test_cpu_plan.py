@@ -109,7 +109,7 @@ def test_chain_cell_layout_matches_oracle(name, over):
     jj = np.tile(np.arange(cs), F)
     t = (fplan["ci_perm"][jj] + fplan["ci_shift"][r]) % cs
     data = np.zeros(lay["S"], np.complex64)
-    data[PP.ti_dest(fplan, r, t)] = cells
+    data[lay["part"][PP.ti_dest(fplan, r, t)]] = cells
     want = pg.carriers(fm.work(cells))
     aux = fplan["aux"][0].copy()
     aux[1:13] = pplan["pilot_values"]
@@ -121,6 +121,9 @@ def test_chain_cell_layout_matches_oracle(name, over):
         row = np.where(code < 0, aux[np.clip(-code - 1, 0, None)], 0).astype(np.complex64)
         sl = np.arange(lay["d0"][j], lay["d0"][j] + lay["n"][j])
         assert (code[lay["inv"][sl]] >= 0).all()
+        if lay["split"]:   # the first n0 slots feed the even-bin half, the rest the odd half
+            n0 = lay["n0"][j]
+            assert (lay["inv"][sl[:n0]] < N // 2).all() and (lay["inv"][sl[n0:]] >= N // 2).all()
         row[lay["inv"][sl]] = data[sl]
         row = PP.stored_to_natural(row, N, lay["split"])
         bins = np.empty(N, np.complex64)

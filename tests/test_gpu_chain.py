@@ -40,8 +40,9 @@ def test_chain_cells_match_oracle(gpu, name):
     r = np.repeat(np.arange(F), cs)
     jj = np.tile(np.arange(cs), F)
     t = (plan["ci_perm"][jj] + plan["ci_shift"][r]) % cs
+    lay = PP.chain_layout(cfg)
     want = np.zeros(plan["S"], np.complex64)
-    want[PP.ti_dest(plan, r, t)] = cells
+    want[lay["part"][PP.ti_dest(plan, r, t)]] = cells
     ch = dvbt2ll.Chain(cfg, max_frames=1)
     ch.run(0, 1)
     got = ch.debug_cells(plan["S"])
