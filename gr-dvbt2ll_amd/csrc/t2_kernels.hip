@@ -899,7 +899,7 @@ struct OfdmShape {
   static constexpr int NT = NSUB / V;
   static constexpr int FFT_LDS = (NSUB + NSUB / 16 + 64) * 8;       // padded buffer + 64 dummy slots
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
-  static constexpr int LDS_BYTES = FFT_LDS + TW_ENTRIES * 8;
+  static constexpr int LDS_BYTES = FFT_LDS + (TW_ENTRIES + 32) * 8;  // + w^(NT m), m < 32 (combine)
 };
 
 template <int N>
@@ -911,6 +911,11 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   float2 *twl = (float2 *)(smem + Sh::FFT_LDS);
   const int tid = threadIdx.x;
   for (int i = tid; i < Sh::TW_ENTRIES; i += NT) twl[i] = d.twiddle[i];   // visible after the first barrier
+  float2 *wcomb = twl + Sh::TW_ENTRIES;            // split combine: w^(NT m), uniform across lanes
+  if (Sh::SPLIT && tid < 32) {
+    const uint32_t e = (uint32_t)(NT * tid);
+    wcomb[tid] = cmulf(d.twiddle[128 + (e >> 7)], d.twiddle[e & 127]);
+  }
   // one workgroup per (symbol, frame); XCD-major so each XCD walks a contiguous run of symbols
   // for all frames of the launch at once and reads each bin_map row from its own L2
   const int u = xcd_major(blockIdx.x, gridDim.x);
@@ -968,13 +973,14 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
     asm volatile("" : "+v"(tid2));
     sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid2, 1);
     OFDM_PHASE(7);
+    const float2 wt = tw_at(twl, (uint32_t)tid);   // w^n = w^tid * w^(NT m)
 #pragma unroll
     for (int uu = 0; uu < UL; uu++)
 #pragma unroll
       for (int r = 0; r < RL; r++) {
         const int i = uu * RL + r;
         const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
-        float2 t = cmulf(v[i], tw_at(twl, n));
+        float2 t = cmulf(v[i], cmulf(wt, wcomb[uu + UL * r]));
         float2 a = cadd(e[i], t), b = csub(e[i], t);
         a.x *= nrm; a.y *= nrm; b.x *= nrm; b.y *= nrm;
         st_nt(o, ((uint32_t)G + n) * 8u, a);
