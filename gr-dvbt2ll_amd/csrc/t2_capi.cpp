@@ -571,8 +571,19 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
       (r = upload(h->sym_n, layout.sym_n)) || (r = upload(h->sym_n0, layout.sym_n0)))
     return r;
   if (!layout.part.empty()) {
-    if ((r = upload(h->part, layout.part))) return r;
-    h->map.dev.part = h->part.as<int32_t>();
+    // reorder to the map kernel's store order: block r, index j = 5 row + e (TI on) or t
+    const FramePlan &fp = h->frame;
+    // stored as int16 deltas from the TI position (a cell only moves within its symbol)
+    std::vector<int16_t> pb((size_t)fp.S);
+    for (int rr = 0; rr < fp.F; rr++)
+      for (int jj = 0; jj < fp.cs; jj++) {
+        const int t = fp.ti_on ? (jj % 5) * (fp.cs / 5) + jj / 5 : jj;
+        const int64_t s = ti_dest(fp, rr, t), delta = layout.part[s] - s;
+        if (delta < INT16_MIN || delta > INT16_MAX) return DVBT2LL_EINVAL;
+        pb[(size_t)rr * fp.cs + jj] = (int16_t)delta;
+      }
+    if ((r = upload(h->part, pb))) return r;
+    h->map.dev.part = h->part.as<int16_t>();
   }
   const PilotPlan &pp = h->pilot;
   std::vector<cf32> aux = h->frame.aux;

@@ -42,7 +42,7 @@ struct MapDev {
   const int32_t *ci_shift; // F  (chain only)
   int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
-  const int32_t *part;     // chain, 32K only: TI output index -> data slot (ChainLayout::part)
+  const int16_t *part;     // chain, 32K only: slot - TI position of (block r, TI-store index j), at r*cs + j
   uint8_t twist[16], mux[16];
 };
 struct MapIO {

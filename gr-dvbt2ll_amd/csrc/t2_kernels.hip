@@ -558,30 +558,55 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   };
 #endif
   // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
-  for (int j = tid; j < cs; j += MAP_THREADS) {
-    int t = d.ci_perm[j] + shift;
-    t -= t >= cs ? cs : 0;
-    stage[t] = (uint16_t)(idx[j] | (idx[j == 0 ? cs - 1 : j - 1] << 8));
+  // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
+  constexpr int MB = 8;
+  for (int j0 = tid; j0 < cs; j0 += MB * MAP_THREADS) {
+    int t[MB];
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+      const int j = min(j0 + u * MAP_THREADS, cs - 1);
+      t[u] = d.ci_perm[j] + shift;
+    }
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+      const int j = j0 + u * MAP_THREADS;
+      if (j < cs) {
+        const int tt = t[u] >= cs ? t[u] - cs : t[u];
+        stage[tt] = (uint16_t)(idx[j] | (idx[j == 0 ? cs - 1 : j - 1] << 8));
+      }
+    }
   }
   __syncthreads();
   MAP_PHASE(3);
   // QAM (+ rotated-constellation Q delay) fused into the time-interleaver store: row-major over
-  // (row, e), 5 consecutive cells (40 B) per TI row
-  for (int j = tid; j < cs; j += MAP_THREADS) {
-    int t, o;
-    if (d.ti_on) {
-      const int row = j / 5, e = j - 5 * row;
-      t = e * rows + row;
-      o = row * cols + e;
-    } else {
-      t = j;
-      o = j;
+  // (row, e), 5 consecutive cells (40 B) per TI row (32K: through the half partition)
+  const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
+  for (int j0 = tid; j0 < cs; j0 += MB * MAP_THREADS) {
+    int64_t dsl[MB];
+    int tt[MB];
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+      const int j = min(j0 + u * MAP_THREADS, cs - 1);
+      int o;
+      if (d.ti_on) {
+        const int row = j / 5, e = j - 5 * row;
+        tt[u] = e * rows + row;
+        o = row * cols + e;
+      } else {
+        tt[u] = j;
+        o = j;
+      }
+      dsl[u] = fbase + o + (d.part ? d.part[(int64_t)r * cs + j] : 0);   // block-major int16 table
     }
-    const uint32_t pr = stage[t];
-    float2 v = lut[pr & 0xFF];
-    if (d.rotation) v.y = lut[pr >> 8].y;
-    const int64_t sidx = (d.ti_on ? base : (int64_t)r * cs) + o;
-    dst[d.part ? (int64_t)d.part[sidx] : sidx] = v;
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+      if (j0 + u * MAP_THREADS < cs) {
+        const uint32_t pr = stage[tt[u]];
+        float2 v = lut[pr & 0xFF];
+        if (d.rotation) v.y = lut[pr >> 8].y;
+        dst[dsl[u]] = v;
+      }
+    }
   }
 #if MAP_VARIANT & 1
   __syncthreads();
@@ -593,7 +618,8 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
       float2 x;
       x.x = __uint_as_float(v[2 * c]);
       x.y = __uint_as_float(v[2 * c + 1]);
-      dst[ti_dst(c)] = x;
+      const int64_t sidx = ti_dst(c);
+      dst[d.part ? (int64_t)d.part[sidx] : sidx] = x;
     }
   }
 #endif

@@ -11,7 +11,7 @@ import dvbt2ll  # noqa: E402
 from dvbt2ll.configs import CONFIGS, ts_for_frames  # noqa: E402
 
 cfg = CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "cfg3"]
-B = 16
+B = 64
 ch = dvbt2ll.Chain(cfg, max_frames=B)
 ts, base = ts_for_frames(cfg, 0, B)
 ts_d = torch.from_numpy(ts).cuda()

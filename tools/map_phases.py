@@ -12,7 +12,7 @@ from dvbt2ll.configs import CONFIGS, ts_for_frames  # noqa: E402
 import plan_probe as PP  # noqa: E402
 
 cfg = CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "cfg3"]
-B = 16
+B = 64
 ch = dvbt2ll.Chain(cfg, max_frames=B)
 ts, base = ts_for_frames(cfg, 0, B)
 ts_d = torch.from_numpy(ts).cuda()
@@ -21,11 +21,12 @@ for _ in range(3):
     ch.run_device(ts_d.data_ptr(), base, len(ts), 0, B, iq.data_ptr(), torch.cuda.current_stream().cuda_stream)
 torch.cuda.synchronize()
 plan = PP.frame_plan(cfg.fm_args())
+part = PP.chain_layout(cfg)["part"]
 F = plan["F"]
 cells = ch.debug_cells(plan["S"]).view(np.uint32).reshape(-1, 2)
 rows = []
 for r in range(F):
-    pos = [int(PP.ti_dest(plan, np.array([r]), np.array([c]))[0]) for c in range(3)]
+    pos = [int(part[PP.ti_dest(plan, np.array([r]), np.array([c]))[0]]) for c in range(3)]
     w = np.concatenate([cells[p] for p in pos]).astype(np.int64)
     rows.append(w)
 a = np.array(rows)
