@@ -497,9 +497,9 @@ struct dvbt2ll_chain {
   FramePlan frame;
   PilotPlan pilot;
   OfdmTables ofdm;
-  DevBuf cw, cells, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
+  DevBuf cw, aux, pairs, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
   int max_frames = 0;
-  int64_t aux_pad = 0;       // cells buffer = [aux variants (aux_pad elements) | frame cells]
+  int64_t pair_stride = 0;   // pairs buffer: frame k's slots at k * pair_stride (multiple of 8)
   int64_t cw_stride = 0;
   int64_t iq_per_frame = 0;
   int64_t ts_per_frame = 0;
@@ -567,7 +567,9 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   // OFDM side: aux bins from cmap, data cells streamed per symbol and scattered through inv
   ChainLayout layout;
   if (build_chain_layout(h->frame, h->pilot, layout)) return DVBT2LL_EINVAL;
-  if ((r = upload(h->inv, layout.inv)) || (r = upload(h->sym_d0, layout.sym_d0)) ||
+  std::vector<uint16_t> inv_pad(layout.inv);
+  inv_pad.resize(((layout.inv.size() + 7) & ~(size_t)7) + 8, 0);   // the kernel reads aligned quads
+  if ((r = upload(h->inv, inv_pad)) || (r = upload(h->sym_d0, layout.sym_d0)) ||
       (r = upload(h->sym_n, layout.sym_n)) || (r = upload(h->sym_n0, layout.sym_n0)))
     return r;
   if (!layout.part.empty()) {
@@ -586,25 +588,27 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
     h->map.dev.part = h->part.as<int16_t>();
   }
   const PilotPlan &pp = h->pilot;
-  std::vector<cf32> aux = h->frame.aux;
+  std::vector<cf32> auxv = h->frame.aux;
   for (int v = 0; v < h->frame.t2frames; v++)
-    for (int i = 0; i < 12; i++) aux[(size_t)v * h->frame.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
+    for (int i = 0; i < 12; i++) auxv[(size_t)v * h->frame.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
   if ((r = h->ofdm.init(pp, layout.cmap, h->frame.aux_len, h->frame.t2frames))) return r;
   h->ofdm.dev.inv = h->inv.as<uint16_t>();
   h->ofdm.dev.sym_d0 = h->sym_d0.as<int32_t>();
   h->ofdm.dev.sym_n = h->sym_n.as<int32_t>();
   h->ofdm.dev.sym_n0 = h->sym_n0.as<int32_t>();
-  h->aux_pad = ((int64_t)aux.size() + 63) / 64 * 64;
+  h->ofdm.dev.qam = h->map.dev.lut;
+  h->pair_stride = ((int64_t)h->frame.S + 7) / 8 * 8;
   h->cw_stride = ((h->fec.plan.nldpc / 8) + 255) / 256 * 256;
   h->iq_per_frame = (int64_t)pp.Nsym * (pp.N + pp.G) + 2048;
   h->pay = (h->fec.plan.kbch - 80) / 8;
   h->ts_per_frame = (int64_t)h->frame.F * h->pay;
   int64_t nblk = (int64_t)h->frame.F * h->max_frames;
-  if (h->cw.ensure((size_t)nblk * h->cw_stride) ||
-      h->cells.ensure((size_t)(h->aux_pad + (int64_t)h->frame.S * h->max_frames) * 8))
+  // the OFDM kernel addresses index pairs and aux cells with 32-bit byte offsets
+  if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32))
+    return DVBT2LL_EINVAL;
+  if (h->cw.ensure((size_t)nblk * h->cw_stride) || h->pairs.ensure((size_t)h->pair_stride * h->max_frames * 2))
     return DVBT2LL_ENOMEM;
-  if ((uint64_t)(h->aux_pad + (int64_t)h->frame.S * h->max_frames) * 8 >= (1ull << 32)) return DVBT2LL_EINVAL;
-  HIP_TRY(hipMemcpy(h->cells.p, aux.data(), aux.size() * sizeof(cf32), hipMemcpyHostToDevice));
+  if ((r = upload(h->aux, auxv))) return r;
   *out = h.release();
   return DVBT2LL_OK;
 }
@@ -661,17 +665,19 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   MapIO mio{};
   mio.in = h->cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
-  mio.out = h->cells.as<float2>() + h->aux_pad;
+  mio.out_pairs = h->pairs.as<uint16_t>();
+  mio.frame_stride = h->pair_stride;
   mio.nblocks = F * nframes;
   mio.packed_in = 1;
   mio.apply_ci = 1;
   HIP_TRY(launch_map(h->map.dev, mio, s));
   if (h->timing) HIP_TRY(hipEventRecord(ev[2], s));
   OfdmIO oio{};
-  oio.data = h->cells.as<float2>();
+  oio.data = h->aux.as<float2>();
   oio.aux_off = 0;
-  oio.cell_off = (uint32_t)h->aux_pad;
-  oio.cell_stride = (uint32_t)h->frame.S;
+  oio.cell_off = 0;
+  oio.cell_stride = (uint32_t)h->pair_stride;
+  oio.pairs = h->pairs.as<uint16_t>();
   oio.out = (float2 *)iq_dev;
   oio.out_stride = h->iq_per_frame;
   oio.first_frame = first_frame;
@@ -718,11 +724,23 @@ extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_
   HIP_TRY(hipMemcpy(out, h->cw.p, (size_t)bytes, hipMemcpyDeviceToHost));
   return DVBT2LL_OK;
 }
-extern "C" int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells) {
-  if (!h || !out || cells < 0 || (size_t)(cells + h->aux_pad) * 8 > h->cells.n) return DVBT2LL_EINVAL;
+extern "C" int dvbt2ll_chain_debug_cell_pairs(dvbt2ll_chain *h, void *out, int64_t cells) {
+  if (!h || !out || cells < 0 || (size_t)cells * 2 > h->pairs.n) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, h->cells.as<float2>() + h->aux_pad, (size_t)cells * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out, h->pairs.p, (size_t)cells * 2, hipMemcpyDeviceToHost));
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells) {
+  // frame 0's data cells: index pairs expanded through the constellation exactly as the OFDM
+  // kernel does, (lut[lo].re, lut[hi].im)
+  if (!h || !out || cells < 0 || (size_t)cells * 2 > h->pairs.n) return DVBT2LL_EINVAL;
+  std::vector<uint16_t> pr((size_t)cells);
+  int r = dvbt2ll_chain_debug_cell_pairs(h, pr.data(), cells);
+  if (r) return r;
+  cf32 *o = (cf32 *)out;
+  const cf32 *lut = h->map.plan.lut;
+  for (int64_t i = 0; i < cells; i++) o[i] = cf32{lut[pr[i] & 0xFF].re, lut[pr[i] >> 8].im};
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_synchronize(dvbt2ll_chain *h) {

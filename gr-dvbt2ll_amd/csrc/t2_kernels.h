@@ -48,7 +48,11 @@ struct MapDev {
 struct MapIO {
   const uint8_t *in;   // packed tempu codewords (stride cw_stride) or unpacked natural bits
   int64_t cw_stride;
-  float2 *out;         // cells
+  float2 *out;         // cells (apply_ci = 0)
+  // apply_ci = 1 (chain): per cell the constellation index pair lo = idx[j], hi = idx[j-1]
+  // (rotation) or idx[j], frame k's data region at out_pairs + k * frame_stride
+  uint16_t *out_pairs;
+  int64_t frame_stride;
   int nblocks;
   int packed_in;       // 1: chain layout; 0: unpacked bits (interleavermod block)
   int apply_ci;        // 1 (chain): cell + time interleave into the frame data region
@@ -64,14 +68,17 @@ struct OfdmDev {
   const float2 *twiddle;    // 128 + N/128: two-level table (PilotPlan::twiddle)
   const float *isinc;       // N or null
   const float2 *p1;         // 2048
+  const float2 *qam;        // scatter mode: 256-entry constellation; cell = (qam[lo].x, qam[hi].y)
   int N, G, Nsym, aux_len, t2frames;
   float norm;
 };
 struct OfdmIO {
-  const float2 *data;       // one buffer: aux variants at aux_off, frame f cells at cell_off + f*cell_stride
+  const float2 *data;       // gather mode: aux variants at aux_off, frame f cells at cell_off + f*cell_stride
+                            // scatter mode: aux variants only
   uint32_t aux_off;         // element offset of aux variant 0 (variant v at aux_off + v*aux_len)
   uint32_t cell_off;
-  uint32_t cell_stride;
+  uint32_t cell_stride;     // elements; scatter mode: a multiple of 4
+  const uint16_t *pairs;    // scatter mode: frame f's constellation index pairs at f*cell_stride
   float2 *out;              // per frame: out_stride samples
   int64_t out_stride;
   int64_t first_frame;

@@ -541,7 +541,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   }
   const int r = blk % d.F;
   const int shift = d.ci_shift[r];
-  float2 *dst = io.out + (int64_t)(blk - r) * cs;      // frame data region
+  uint16_t *dst = io.out_pairs + (int64_t)(blk / d.F) * io.frame_stride;   // frame data region
   int r0 = r, nb = 1;
   if (d.ti_on) {
     const int ns = d.ti_nsmall * d.ti_small;
@@ -550,13 +550,6 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   }
   const int rows = cs / 5, cols = 5 * nb;
   const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
-#if MAP_VARIANT & 1
-  auto ti_dst = [&](int t) -> int64_t {
-    if (!d.ti_on) return (int64_t)r * cs + t;
-    const int e = t / rows, row = t - e * rows;
-    return base + (int64_t)row * cols + e;
-  };
-#endif
   // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
   // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
   constexpr int MB = 8;
@@ -572,14 +565,16 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
       const int j = j0 + u * MAP_THREADS;
       if (j < cs) {
         const int tt = t[u] >= cs ? t[u] - cs : t[u];
-        stage[tt] = (uint16_t)(idx[j] | (idx[j == 0 ? cs - 1 : j - 1] << 8));
+        const uint32_t lo = idx[j], hi = d.rotation ? idx[j == 0 ? cs - 1 : j - 1] : lo;
+        stage[tt] = (uint16_t)(lo | (hi << 8));
       }
     }
   }
   __syncthreads();
   MAP_PHASE(3);
-  // QAM (+ rotated-constellation Q delay) fused into the time-interleaver store: row-major over
-  // (row, e), 5 consecutive cells (40 B) per TI row (32K: through the half partition)
+  // time-interleaver store of the index pairs: row-major over (row, e), 5 consecutive cells
+  // (10 B) per TI row (32K: through the half partition); the constellation lookup (QAM +
+  // rotated-constellation Q delay) is fused into the OFDM kernel's bin scatter
   const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
   for (int j0 = tid; j0 < cs; j0 += MB * MAP_THREADS) {
     int64_t dsl[MB];
@@ -600,12 +595,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
     }
 #pragma unroll
     for (int u = 0; u < MB; u++) {
-      if (j0 + u * MAP_THREADS < cs) {
-        const uint32_t pr = stage[tt[u]];
-        float2 v = lut[pr & 0xFF];
-        if (d.rotation) v.y = lut[pr >> 8].y;
-        dst[dsl[u]] = v;
-      }
+      if (j0 + u * MAP_THREADS < cs) dst[dsl[u]] = stage[tt[u]];
     }
   }
 #if MAP_VARIANT & 1
@@ -614,12 +604,9 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   if (tid == 0) {
     uint32_t v[6] = {(uint32_t)g_map_ts[0], (uint32_t)(g_map_ts[1] - g_map_ts[0]), (uint32_t)(g_map_ts[2] - g_map_ts[0]),
                      (uint32_t)(g_map_ts[3] - g_map_ts[0]), (uint32_t)(g_map_ts[4] - g_map_ts[0]), 0u};
-    for (int c = 0; c < 3; c++) {
-      float2 x;
-      x.x = __uint_as_float(v[2 * c]);
-      x.y = __uint_as_float(v[2 * c + 1]);
-      const int64_t sidx = ti_dst(c);
-      dst[d.part ? (int64_t)d.part[sidx] : sidx] = x;
+    for (int c = 0; c < 12; c++) {     // uint32 v[c/2], 16 bits per slot of TI-store index c
+      const int o = d.ti_on ? (c / 5) * cols + c % 5 : c;
+      dst[fbase + o + (d.part ? d.part[(int64_t)r * cs + c] : 0)] = (uint16_t)(v[c >> 1] >> (16 * (c & 1)));
     }
   }
 #endif
@@ -830,9 +817,11 @@ __shared__ uint64_t g_phase_ts[16];
 // loads and each cell is written to LDS at its bin inv[slot].
 struct BinSource {
   const int32_t *map;          // this symbol's stored row
-  const float2 *data;          // uniform base; cells at cbase + code, aux at abase - code
+  const float2 *data;          // uniform base; cells at cbase + code (gather), aux at abase - code
   uint32_t cbase, abase;
   const uint16_t *inv;         // scatter mode: stored bin of each data slot (null: gather mode)
+  const uint16_t *pairs;       // scatter mode: constellation index pair of each slot at cbase + slot
+  const float *qre, *qim;      // scatter mode: constellation real / imaginary parts in LDS
   uint32_t d0, dn, dn0;        // scatter mode: this symbol's data slots; the first dn0 feed half 0
 };
 
@@ -861,26 +850,38 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     }
     __syncthreads();
     OFDM_PHASE(1 + 4 * half);
-    // data cells: the symbol's slots streamed with unit-stride loads, written to their bins;
-    // cells of the other half go to a per-lane dummy slot past the buffer (branch-free)
+    // data cells: the symbol's slots streamed as aligned quads (8-byte loads of 4 index pairs
+    // and 4 stored bins), looked up in the constellation and written to their bins; slots
+    // outside the run (quad edges) go to a per-lane dummy slot past the buffer (branch-free)
     // (split: the run is partitioned, so half h streams only its own slots)
     const uint32_t lo = SPLIT ? (uint32_t)half * NSUB : 0u;
     const uint32_t dummy = (uint32_t)(NSUB + NSUB / 16) + (uint32_t)(tid & 63);
     const uint32_t r0 = src.d0 + (SPLIT && half ? src.dn0 : 0u);
     const uint32_t rn = SPLIT ? (half ? src.dn - src.dn0 : src.dn0) : src.dn;
-    constexpr int SC = 32;                       // slots per thread per round
-    const uint32_t last = rn - 1u;
-    for (uint32_t s0 = 0; s0 < rn; s0 += (uint32_t)SC * NT) {
-      uint32_t b[SC];
-      float2 c[SC];
+    const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
+    const uint32_t lastq = nq - 1u;
+    constexpr int SQ = 8;                        // quads per thread per round
+    for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
+      uint2 b[SQ], c[SQ];
 #pragma unroll
-      for (int u = 0; u < SC; u++) {
-        const uint32_t sl = min(s0 + (uint32_t)(tid + NT * u), last);
-        b[u] = (uint32_t)src.inv[r0 + sl] - lo;
-        c[u] = ld_off(src.data, (src.cbase + r0 + sl) * 8u);
+      for (int u = 0; u < SQ; u++) {
+        const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
+        b[u] = ld_off((const uint2 *)src.inv, s * 2u);
+        c[u] = ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u);
       }
 #pragma unroll
-      for (int u = 0; u < SC; u++) lds[b[u] < (uint32_t)NSUB ? lds_pad(b[u]) : dummy] = c[u];
+      for (int u = 0; u < SQ; u++) {
+        const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
+          const uint32_t bin = ((bw >> (16 * (e & 1))) & 0xFFFFu) - lo;
+          const uint32_t pr = cw >> (16 * (e & 1));
+          const bool in_run = s + (uint32_t)e - r0 < rn;
+          const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+          lds[in_run && bin < (uint32_t)NSUB ? lds_pad(bin) : dummy] = v;
+        }
+      }
     }
     __syncthreads();
     OFDM_PHASE(2 + 4 * half);
@@ -925,7 +926,8 @@ struct OfdmShape {
   static constexpr int NT = NSUB / V;
   static constexpr int FFT_LDS = (NSUB + NSUB / 16 + 64) * 8;       // padded buffer + 64 dummy slots
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
-  static constexpr int LDS_BYTES = FFT_LDS + (TW_ENTRIES + 32) * 8;  // + w^(NT m), m < 32 (combine)
+  static constexpr int QAM_OFF = FFT_LDS + (TW_ENTRIES + 32) * 8;    // + w^(NT m), m < 32 (combine)
+  static constexpr int LDS_BYTES = QAM_OFF + 256 * 8;                // + constellation re[256], im[256]
 };
 
 template <int N>
@@ -942,6 +944,13 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
     const uint32_t e = (uint32_t)(NT * tid);
     wcomb[tid] = cmulf(d.twiddle[128 + (e >> 7)], d.twiddle[e & 127]);
   }
+  float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + 256;
+  if (d.inv)
+    for (int i = tid; i < 256; i += NT) {
+      const float2 c = d.qam[i];
+      qre[i] = c.x;
+      qim[i] = c.y;
+    }
   // one workgroup per (symbol, frame); XCD-major so each XCD walks a contiguous run of symbols
   // for all frames of the launch at once and reads each bin_map row from its own L2
   const int u = xcd_major(blockIdx.x, gridDim.x);
@@ -953,14 +962,15 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
   const int32_t *map = d.bin_map + (int64_t)j * N;
   const uint32_t tws = Sh::SPLIT ? 2u : 1u;       // sub-transform twiddle = table index * tws
-  BinSource src{map, data, cbase, abase, d.inv, 0u, 0u, 0u};
+  BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u};
   if (d.inv) {
     src.d0 = (uint32_t)d.sym_d0[j];
     src.dn = (uint32_t)d.sym_n[j];
     src.dn0 = (uint32_t)d.sym_n0[j];
   }
 
-  if (io.carriers_only) {                          // test hook: bins in natural order
+  if (io.carriers_only) {                          // test hook (gather mode): bins in natural order
+    if (d.inv) return;
     float2 *o = io.out + (int64_t)f * io.out_stride + (int64_t)j * N;
     for (int k = tid; k < N; k += NT) {
       const int sub = Sh::SPLIT ? (k & 1) : 0, kk = Sh::SPLIT ? (k >> 1) : k;

@@ -65,7 +65,8 @@ for _b in BLOCKS:
 EXPORTS += ["dvbt2ll_framemapperfint_stream_items", "dvbt2ll_pilotgenp1insert_active_items",
             "dvbt2ll_pilotgenp1insert_debug_carriers"]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_host", "set_timing",
-                                           "get_timing", "debug_codewords", "debug_cells", "synchronize",
+                                           "get_timing", "debug_codewords", "debug_cell_pairs", "debug_cells",
+                                           "synchronize",
                                            "destroy")]
 
 
@@ -98,6 +99,7 @@ def lib():
     L.dvbt2ll_chain_set_timing.argtypes = [vp, ci]
     L.dvbt2ll_chain_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), ci]
     L.dvbt2ll_chain_debug_codewords.argtypes = [vp, vp, i64]
+    L.dvbt2ll_chain_debug_cell_pairs.argtypes = [vp, vp, i64]
     L.dvbt2ll_chain_debug_cells.argtypes = [vp, vp, i64]
     L.dvbt2ll_chain_synchronize.argtypes = [vp]
     L.dvbt2ll_chain_destroy.argtypes = [vp]

@@ -62,6 +62,11 @@ class Chain:
         check(lib().dvbt2ll_chain_debug_codewords(self._h, out.ctypes.data_as(ctypes.c_void_p), len(out)), "cw")
         return out.reshape(nblocks, stride)
 
+    def debug_cell_pairs(self, ncells):
+        out = np.zeros(ncells, np.uint16)
+        check(lib().dvbt2ll_chain_debug_cell_pairs(self._h, out.ctypes.data_as(ctypes.c_void_p), ncells), "pairs")
+        return out
+
     def debug_cells(self, ncells):
         out = np.zeros(ncells, np.complex64)
         check(lib().dvbt2ll_chain_debug_cells(self._h, out.ctypes.data_as(ctypes.c_void_p), ncells), "cells")

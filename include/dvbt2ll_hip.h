@@ -172,9 +172,12 @@ int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, in
  * accumulated milliseconds and launch counts of stages {0: fec, 1: map, 2: ofdm}. */
 int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable);
 int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages);
-/* test hooks (host outputs, synchronous): packed codewords (tempu order) and
- * cells (frame data region, in the slot order the OFDM kernel reads) of the last run's frame 0 */
+/* test hooks (host outputs, synchronous), last run's frame 0: packed codewords (tempu
+ * order); the frame data region in the slot order the OFDM kernel reads, as stored
+ * (uint16 constellation index pairs: lo = the cell's index, hi = the index whose Q part
+ * it carries, i.e. the previous cell's under rotation) and as complex64 cells */
 int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes);
+int dvbt2ll_chain_debug_cell_pairs(dvbt2ll_chain *h, void *out, int64_t cells);
 int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells);
 int dvbt2ll_chain_synchronize(dvbt2ll_chain *h);
 void dvbt2ll_chain_destroy(dvbt2ll_chain *h);

@@ -23,12 +23,15 @@ torch.cuda.synchronize()
 plan = PP.frame_plan(cfg.fm_args())
 part = PP.chain_layout(cfg)["part"]
 F = plan["F"]
-cells = ch.debug_cells(plan["S"]).view(np.uint32).reshape(-1, 2)
+pairs = ch.debug_cell_pairs(plan["S"]).astype(np.int64)
+cs = plan["cs"]
 rows = []
 for r in range(F):
-    pos = [int(part[PP.ti_dest(plan, np.array([r]), np.array([c]))[0]]) for c in range(3)]
-    w = np.concatenate([cells[p] for p in pos]).astype(np.int64)
-    rows.append(w)
+    # TI-store index c (row c // 5, column c % 5) = cell-interleaved position (c % 5) * cs/5 + c // 5
+    t = [(c % 5) * (cs // 5) + c // 5 for c in range(12)]
+    pos = [int(part[PP.ti_dest(plan, np.array([r]), np.array([tt]))[0]]) for tt in t]
+    h = [pairs[p] for p in pos]
+    rows.append(np.array([h[2 * i] | (h[2 * i + 1] << 16) for i in range(6)], np.int64))
 a = np.array(rows)
 names = ["cw load", "cell idx", "qam+ci", "ti store"]
 prev = np.zeros(len(a), np.int64)
