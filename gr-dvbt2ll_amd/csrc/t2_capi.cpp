@@ -498,6 +498,7 @@ struct dvbt2ll_chain {
   PilotPlan pilot;
   OfdmTables ofdm;
   DevBuf cw, aux, pairs, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
+  DevBuf abin, aval, aind, agrp;   // non-data bins as compact lists (t2_plan.h AuxLists)
   int max_frames = 0;
   int64_t pair_stride = 0;   // pairs buffer: frame k's slots at k * pair_stride (multiple of 8)
   int64_t cw_stride = 0;
@@ -592,6 +593,18 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   for (int v = 0; v < h->frame.t2frames; v++)
     for (int i = 0; i < 12; i++) auxv[(size_t)v * h->frame.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
   if ((r = h->ofdm.init(pp, layout.cmap, h->frame.aux_len, h->frame.t2frames))) return r;
+  AuxLists al;
+  if (build_aux_lists(layout, pp.N, pp.Nsym, auxv, h->frame.aux_len, h->frame.t2frames, al)) return DVBT2LL_EINVAL;
+  al.ind.push_back(0);   // never empty (device pointer)
+  al.dbin.resize(al.dbin.size() + 4, 0xFFFF);
+  al.dval.resize(al.dval.size() + 4, cf32{0.f, 0.f});
+  if ((r = upload(h->abin, al.dbin)) || (r = upload(h->aval, al.dval)) || (r = upload(h->aind, al.ind)) ||
+      (r = upload(h->agrp, al.grp)))
+    return r;
+  h->ofdm.dev.abin = h->abin.as<uint16_t>();
+  h->ofdm.dev.aval = h->aval.as<float2>();
+  h->ofdm.dev.aind = h->aind.as<uint32_t>();
+  h->ofdm.dev.agrp = h->agrp.as<int4>();
   h->ofdm.dev.inv = h->inv.as<uint16_t>();
   h->ofdm.dev.sym_d0 = h->sym_d0.as<int32_t>();
   h->ofdm.dev.sym_n = h->sym_n.as<int32_t>();

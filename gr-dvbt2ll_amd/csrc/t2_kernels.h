@@ -69,6 +69,12 @@ struct OfdmDev {
   const float *isinc;       // N or null
   const float2 *p1;         // 2048
   const float2 *qam;        // scatter mode: 256-entry constellation; cell = (qam[lo].x, qam[hi].y)
+  // scatter mode: non-data bins as compact lists per (symbol, half) group 2 j + h (t2_plan.h
+  // AuxLists): agrp[g] = {direct offset, direct count, indirect offset, indirect count}
+  const uint16_t *abin;     // direct bins, quads (0xFFFF = padding)
+  const float2 *aval;       // direct values
+  const uint32_t *aind;     // indirect: bin | code << 15, value at aux abase + code
+  const int4 *agrp;
   int N, G, Nsym, aux_len, t2frames;
   float norm;
 };

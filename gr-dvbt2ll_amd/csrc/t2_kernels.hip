@@ -37,10 +37,20 @@ __device__ __forceinline__ void st_off(T *base, uint32_t byte_off, T v) {
 }
 
 // streaming store (nontemporal): final IQ samples are never re-read by the chain
+// (experiment switch OFDM_STORE: 0 = one 64-bit nontemporal store, 1 = two 32-bit, 2 = plain)
+#ifndef OFDM_STORE
+#define OFDM_STORE 0
+#endif
 __device__ __forceinline__ void st_nt(float2 *base, uint32_t byte_off, float2 v) {
   float2 *p = (float2 *)((char *)base + byte_off);
+#if OFDM_STORE == 0
+  __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, v), (uint64_t *)p);
+#elif OFDM_STORE == 1
   __builtin_nontemporal_store(v.x, &p->x);
   __builtin_nontemporal_store(v.y, &p->y);
+#else
+  *p = v;
+#endif
 }
 
 __device__ __forceinline__ uint32_t rd_lane_u32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -823,6 +833,10 @@ struct BinSource {
   const uint16_t *pairs;       // scatter mode: constellation index pair of each slot at cbase + slot
   const float *qre, *qim;      // scatter mode: constellation real / imaginary parts in LDS
   uint32_t d0, dn, dn0;        // scatter mode: this symbol's data slots; the first dn0 feed half 0
+  const uint16_t *abin;        // scatter mode: aux lists (OfdmDev)
+  const float2 *aval;
+  const uint32_t *aind;
+  const int4 *agrp;            // this symbol's two groups (halves)
 };
 
 // One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split) by NT = NSUB/V
@@ -834,28 +848,41 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   // first pass (R = V, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
   const int32_t *m = src.map + (SPLIT ? half * NSUB : 0);
   if (src.inv) {
-    // every bin: aux value, or zero for data bins (aux entry 0); branch-free, all V codes in
-    // flight, then all V aux loads (two memory round trips)
+    // zero every bin (and pad slot), then write the non-data bins from the compact aux lists and
+    // the data cells from the symbol's slot run (disjoint bins: one phase, no barrier between)
     {
-      int code[V];
-#pragma unroll
-      for (int u = 0; u < V; u++) code[u] = ld_off(m, (uint32_t)(tid + NT * u) * 4u);
-      float2 a[V];
-#pragma unroll
-      for (int u = 0; u < V; u++)
-        a[u] = ld_off(src.data, (src.abase + (code[u] < 0 ? (uint32_t)(-code[u]) : 1u)) * 8u);
-      float2 *b = lds + lds_pad((uint32_t)tid);
-#pragma unroll
-      for (int u = 0; u < V; u++) b[u * NT * 17 / 16] = a[u];
+      float4 *z = (float4 *)lds;
+      constexpr int NZ = (NSUB + NSUB / 16) / 2;
+      for (int i = tid; i < NZ; i += NT) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
     OFDM_PHASE(1 + 4 * half);
+    const uint32_t dummy = (uint32_t)(NSUB + NSUB / 16) + (uint32_t)(tid & 63);
+    {
+      const int4 g = src.agrp[half];
+      // direct entries: quads of (bin, value); padding bins (0xFFFF) go to the dummy slot
+      for (uint32_t q = (uint32_t)tid; q < (uint32_t)g.y >> 2; q += NT) {
+        const uint32_t e0 = (uint32_t)g.x + 4u * q;
+        const uint2 b = ld_off((const uint2 *)src.abin, e0 * 2u);
+        const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
+        const float4 v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
+        const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
+        lds[k0 < (uint32_t)NSUB ? lds_pad(k0) : dummy] = make_float2(v01.x, v01.y);
+        lds[k1 < (uint32_t)NSUB ? lds_pad(k1) : dummy] = make_float2(v01.z, v01.w);
+        lds[k2 < (uint32_t)NSUB ? lds_pad(k2) : dummy] = make_float2(v23.x, v23.y);
+        lds[k3 < (uint32_t)NSUB ? lds_pad(k3) : dummy] = make_float2(v23.z, v23.w);
+      }
+      // indirect entries (per-frame L1-post cells): through the frame's aux variant
+      for (uint32_t i = (uint32_t)tid; i < (uint32_t)g.w; i += NT) {
+        const uint32_t e = src.aind[(uint32_t)g.z + i];
+        lds[lds_pad(e & 0x7FFFu)] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
+      }
+    }
     // data cells: the symbol's slots streamed as aligned quads (8-byte loads of 4 index pairs
     // and 4 stored bins), looked up in the constellation and written to their bins; slots
     // outside the run (quad edges) go to a per-lane dummy slot past the buffer (branch-free)
     // (split: the run is partitioned, so half h streams only its own slots)
     const uint32_t lo = SPLIT ? (uint32_t)half * NSUB : 0u;
-    const uint32_t dummy = (uint32_t)(NSUB + NSUB / 16) + (uint32_t)(tid & 63);
     const uint32_t r0 = src.d0 + (SPLIT && half ? src.dn0 : 0u);
     const uint32_t rn = SPLIT ? (half ? src.dn - src.dn0 : src.dn0) : src.dn;
     const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
@@ -962,11 +989,12 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
   const int32_t *map = d.bin_map + (int64_t)j * N;
   const uint32_t tws = Sh::SPLIT ? 2u : 1u;       // sub-transform twiddle = table index * tws
-  BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u};
+  BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u, d.abin, d.aval, d.aind, nullptr};
   if (d.inv) {
     src.d0 = (uint32_t)d.sym_d0[j];
     src.dn = (uint32_t)d.sym_n[j];
     src.dn0 = (uint32_t)d.sym_n0[j];
+    src.agrp = d.agrp + 2 * j;
   }
 
   if (io.carriers_only) {                          // test hook (gather mode): bins in natural order

@@ -1018,4 +1018,51 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
   return 0;
 }
 
+int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf32> &auxv, int aux_len,
+                    int t2frames, AuxLists &al) {
+  const bool split = ofdm_split(N);
+  const int nsub = split ? N / 2 : N, ngrp = 2 * Nsym;
+  if ((int64_t)aux_len * t2frames > (int64_t)auxv.size() || nsub > 32768) return -1;
+  al.dbin.clear(); al.dval.clear(); al.ind.clear();
+  al.grp.assign((size_t)4 * ngrp, 0);
+  auto same_in_all = [&](int a) {
+    for (int v = 1; v < t2frames; v++) {
+      const cf32 x = auxv[a], y = auxv[(size_t)v * aux_len + a];
+      if (std::memcmp(&x, &y, sizeof(cf32))) return false;
+    }
+    return true;
+  };
+  for (int g = 0; g < ngrp; g++) {
+    const int j = g >> 1, h = g & 1;
+    al.grp[4 * g + 0] = (int32_t)al.dbin.size();
+    al.grp[4 * g + 2] = (int32_t)al.ind.size();
+    if (h && !split) continue;
+    const int32_t *row = &cl.cmap[(size_t)j * N + (size_t)h * nsub];
+    for (int k = 0; k < nsub; k++) {
+      const int32_t c = row[k];
+      if (c >= 0 || c == -AUX_ZERO - 1) continue;
+      const int a = -c - 1;
+      if (a >= aux_len) return -1;
+      if (same_in_all(a)) {
+        const cf32 v = auxv[a];
+        uint64_t bits;
+        std::memcpy(&bits, &v, sizeof(bits));
+        if (bits == 0) continue;   // +0: covered by the zero fill
+        al.dbin.push_back((uint16_t)k);
+        al.dval.push_back(v);
+      } else {
+        if (-c >= (1 << 17)) return -1;
+        al.ind.push_back((uint32_t)k | ((uint32_t)(-c) << 15));
+      }
+    }
+    while (al.dbin.size() & 3) {   // pad to a quad: bin 0xFFFF goes to the kernel's dummy slot
+      al.dbin.push_back(0xFFFF);
+      al.dval.push_back(cf32{0.f, 0.f});
+    }
+    al.grp[4 * g + 1] = (int32_t)al.dbin.size() - al.grp[4 * g + 0];
+    al.grp[4 * g + 3] = (int32_t)al.ind.size() - al.grp[4 * g + 2];
+  }
+  return 0;
+}
+
 }  // namespace t2

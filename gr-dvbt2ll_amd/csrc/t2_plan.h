@@ -115,6 +115,23 @@ struct ChainLayout {
   std::vector<int32_t> part;     // S: TI output index -> data slot (split only)
 };
 int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl);
+
+// Non-data bins of the fused chain as compact per-(symbol, half) lists, group g = 2 j + h
+// (h = 0 when N is not split), bins relative to the half.  The OFDM kernel zero-fills its
+// LDS buffer, then writes:
+//   direct entries (bin, value): aux cells equal in every t2_frame_num variant (pilots,
+//     L1-pre, dummy cells), each group padded to a multiple of 4 with bin 0xFFFF;
+//   indirect entries bin | code << 15: the rest (L1-post), read from the per-variant aux
+//     table at abase + code (code = -cmap).
+// Null bins and +0 aux values are left out (the zero fill covers them).
+struct AuxLists {
+  std::vector<uint16_t> dbin;
+  std::vector<cf32> dval;
+  std::vector<uint32_t> ind;
+  std::vector<int32_t> grp;   // 4 per group: direct offset, direct count, indirect offset, count
+};
+int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf32> &auxv, int aux_len,
+                    int t2frames, AuxLists &al);
 // time-interleaver output index (frame data order) of cell-interleaved cell t of FEC block r
 int64_t ti_dest(const FramePlan &fp, int r, int t);
 
