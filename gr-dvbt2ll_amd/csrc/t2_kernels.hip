@@ -43,6 +43,9 @@ __device__ __forceinline__ void st_off(T *base, uint32_t byte_off, T v) {
 #endif
 __device__ __forceinline__ void st_nt(float2 *base, uint32_t byte_off, float2 v) {
   float2 *p = (float2 *)((char *)base + byte_off);
+#if defined(OFDM_NOSTORE)
+  if (v.x == v.x) return;   // experiment: drop (nearly) every IQ store, keep the arithmetic
+#endif
 #if OFDM_STORE == 0
   __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, v), (uint64_t *)p);
 #elif OFDM_STORE == 1
@@ -61,41 +64,43 @@ __device__ __forceinline__ uint64_t rd_lane_u64(uint64_t v, int l) {
 
 // ============================================================================ FEC kernel
 // experiment switch (product builds: 0): bit 0 = phase timestamps of each block written over
-// the first 40 bytes of its codeword (wrong output; tools/fec_phases.py decodes them)
+// the first 44 bytes of its codeword (wrong output; tools/fec_phases.py decodes them)
 #ifndef FEC_VARIANT
 #define FEC_VARIANT 0
 #endif
 #if FEC_VARIANT & 1
-__shared__ uint64_t g_fec_ts[12];
+__shared__ uint64_t g_fec_ts[16];
 #define FEC_PHASE(i) do { if (threadIdx.x == 0) g_fec_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define FEC_PHASE(i) do { } while (0)
 #endif
 constexpr int FEC_THREADS = 256;
-constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
+constexpr int FEC_FRAME_BYTES = 8112;   // >= max nldpc/8 (8100): info bytes, then the output parity bytes
 constexpr int FEC_MAX_GROUPS = 150;     // nbch / 360 (5/6 normal)
 constexpr int FEC_MAX_Q = 90;
 constexpr int FEC_MAX_ENT = 656;
-// dynamic LDS carve (bytes): a persistent part, then one region reused by phase
-//   BB/CRC phase: [btab | crc8 | crcsh | raw TS bytes]   BCH: [btab]   LDPC: [D | rows]
+constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g || d_g[0..56)
+constexpr int FEC_WG_PER_CU = 5;
+// dynamic LDS carve (bytes): a persistent part (the workgroup loops over FEC blocks; tables are
+// staged once), then one region reused by phase:  BB/CRC phase: [raw TS bytes]   LDPC: [D | rows]
 constexpr int SM_FRAME = 0;
 constexpr int SM_SYNC = SM_FRAME + FEC_FRAME_BYTES;          // 64
 constexpr int SM_WACC = SM_SYNC + 64;                        // 4*3*8 = 96
 constexpr int SM_W = SM_WACC + 96;                           // 16*4
 constexpr int SM_ENT = SM_W + 64;                            // 656*4
 constexpr int SM_RP = SM_ENT + FEC_MAX_ENT * 4;              // 96*2
-constexpr int SM_PHASE = (SM_RP + 96 * 2 + 15) & ~15;
-constexpr int SM_BTAB = SM_PHASE;                            // 256*3*8 = 6144
+constexpr int SM_BTAB = (SM_RP + 96 * 2 + 15) & ~15;         // 256*3*8 = 6144
 constexpr int SM_CRC8 = SM_BTAB + 6144;                      // 256
 constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
-constexpr int SM_RAW = SM_CRCSH + 2048;                      // raw TS bytes of the block (NM)
+constexpr int SM_PHASE = SM_CRCSH + 2048;
+constexpr int SM_RAW = SM_PHASE;                             // raw TS bytes of the block (NM)
 constexpr int FEC_RAW_BYTES = 188 + 6720 + 16;               // one packet before + max payload
-constexpr int SM_D = SM_PHASE;                               // 150*24*4 = 14400 (after BCH)
-constexpr int SM_ROWA = SM_D + FEC_MAX_GROUPS * 24 * 4;      // 90*12*4 = 4320
+constexpr int SM_D = SM_PHASE;                               // 150*13*4 = 7800 (after BCH)
+constexpr int SM_ROWA = SM_D + FEC_MAX_GROUPS * FEC_DW * 4;  // 90*12*4 = 4320
 constexpr int FEC_SMEM = (SM_RAW + FEC_RAW_BYTES > SM_ROWA + FEC_MAX_Q * 12 * 4 ? SM_RAW + FEC_RAW_BYTES
                                                                                 : SM_ROWA + FEC_MAX_Q * 12 * 4);
-static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0, "LDS carve alignment");
-static_assert(FEC_SMEM <= 160 * 1024 / 5, "five FEC workgroups per CU");
+static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0 && SM_WACC % 8 == 0, "LDS carve alignment");
+static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "five FEC workgroups per CU");
 
 // stream position of payload byte J (counted over the payload bytes of the whole stream)
 __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
@@ -108,10 +113,9 @@ __device__ __forceinline__ uint8_t get_byte192(const uint64_t w[3], int lowbit) 
 }
 
 template <int MODE>
-__global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
+__global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t B = io.first_block + blockIdx.x;
   const int L = d.kbch >> 3;           // BBFRAME bytes
   const int NB = d.nbch >> 3;          // info bytes (BBFRAME + BCH parity)
   const int P = d.P;
@@ -127,15 +131,23 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
   uint32_t *ents = (uint32_t *)(smem + SM_ENT);
   uint16_t *rp = (uint16_t *)(smem + SM_RP);
 
-  // ---- stage constant tables into LDS
-  FEC_PHASE(0);
+  // ---- constant tables into LDS, once: the workgroup then loops over FEC blocks
   for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
   for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
   for (int i = tid; i <= d.q; i += FEC_THREADS) rp[i] = d.ldpc_rowptr[i];
+  if (MODE != FEC_BITS_TO_BITS) {
+    for (int i = tid; i < 256; i += FEC_THREADS) crc8[i] = d.crc8_tab[i];
+    for (int i = tid; i < 2048; i += FEC_THREADS) crcsh[i] = d.crc8_shift[i];
+  }
+  __syncthreads();
 
+  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
+  const int64_t B = io.first_block + bi;
+  FEC_PHASE(0);
+  do {   // one FEC block; `break` ends it early (block-API modes)
   if (MODE == FEC_BITS_TO_BITS) {
     // pack nbch unpacked info bits
-    const uint8_t *src = io.in + (int64_t)blockIdx.x * d.nbch;
+    const uint8_t *src = io.in + (int64_t)bi * d.nbch;
     for (int k = tid; k < NB; k += FEC_THREADS) {
       uint32_t v = 0;
       for (int e = 0; e < 8; e++) v |= (uint32_t)(src[8 * k + e] & 1) << (7 - e);
@@ -143,8 +155,6 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     }
     __syncthreads();
   } else {
-    for (int i = tid; i < 256; i += FEC_THREADS) crc8[i] = d.crc8_tab[i];
-    for (int i = tid; i < 2048; i += FEC_THREADS) crcsh[i] = d.crc8_shift[i];
     // ---- block geometry (closed form in the absolute block index B; reference keeps
     //      count / crc / fec_block as running state, bbheader:661-734)
     const int pay_full = (d.kbch - 80) >> 3;
@@ -160,20 +170,21 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     int count0;   // TS packet position of the next input byte at block start
     if (d.hem) count0 = J0 == 0 ? 0 : (int)((payload_pos(J0 - 1, 1) + 1) % 188);
     else count0 = (int)(pos0 % 188);
-    __syncthreads();
     FEC_PHASE(1);
     // ---- CRC-8 of each packet whose sync slot falls in this block (NM only):
     //      8 lanes per packet, 24-byte chunks combined with zero-extension tables
+    // NM: stage the raw stream bytes [pos0 - 188, pos0 + npay) once (independent dword loads;
+    // raw byte i = stream byte rs + i lives at LDS byte SM_RAW + delta + i); the CRC-8 chains and
+    // the payload words then read LDS
+    const int64_t rs = pos0 - 188;
+    int delta = 0, first_slot = 0;
+    const uint32_t *raww = (const uint32_t *)(smem + SM_RAW);
     if (!d.hem) {
-      // stage the raw stream bytes [pos0 - 188, pos0 + npay) once (independent loads); the CRC
-      // chains and the payload copy then read LDS
-      // (dword loads; raw[i] = stream byte rs + i lives at rawb[i + delta])
-      const int64_t rs = pos0 - 188;
       const int64_t rel = rs - io.ts_base;                 // >= -188
       const int64_t w0 = (rel >= 0 ? rel : rel - 3) / 4;   // floor
-      const int delta = (int)(rel - 4 * w0);
+      delta = (int)(rel - 4 * w0);
       const int nw = (delta + npay + 188 + 3) >> 2;
-      uint32_t *raww = (uint32_t *)(smem + SM_RAW);
+      uint32_t *rawst = (uint32_t *)(smem + SM_RAW);
       const bool aligned = (((uintptr_t)io.in) & 3) == 0;
       for (int i = tid; i < nw; i += FEC_THREADS) {
         const int64_t b = 4 * (w0 + i);
@@ -184,13 +195,15 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
           for (int e = 0; e < 4; e++)
             if (b + e >= 0 && b + e < io.ts_len) v |= (uint32_t)io.in[b + e] << (8 * e);
         }
-        raww[i] = v;
+        rawst[i] = v;
       }
       const uint8_t *raw = smem + SM_RAW + delta;
       __syncthreads();
-      const int first_slot = (188 - count0) % 188;
+      FEC_PHASE(2);
+      first_slot = (188 - count0) % 188;
       const int nslots = first_slot < npay ? (npay - 1 - first_slot) / 188 + 1 : 0;
-      // up to 36 sync slots per block (5/6 normal): 32 packets per pass
+      // CRC-8 of each packet whose sync slot falls in this block: 8 lanes per packet, 24-byte
+      // chunks combined with zero-extension tables; up to 36 slots per block (5/6 normal), 32 per pass
       for (int m0 = 0; m0 < nslots; m0 += FEC_THREADS / 8) {
         const int m = m0 + (tid >> 3), k = tid & 7;
         uint8_t part = 0;
@@ -215,51 +228,68 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
         if (k == 0 && m < nslots) syncv[m] = active ? (uint8_t)v : 0;
       }
       __syncthreads();
-      for (int j = tid; j < npay; j += FEC_THREADS) {
-        int r = (int)((count0 + j) % 188);
-        frame[10 + j] = r == 0 ? syncv[(j - first_slot) / 188] : raw[188 + j];
-      }
-    } else {
-      for (int j = tid; j < npay; j += FEC_THREADS) frame[10 + j] = io.in[payload_pos(J0 + j, 1) - io.ts_base];
+      FEC_PHASE(3);
     }
-    if (tid == 0) {
-      // BBHEADER (bbheader:272-325): MATYPE-1 = TS, SIS, CCM, ISSYI 0, NPD 0, RO 0; ISI 0
-      uint8_t h[10];
-      h[0] = 0xF0;
-      h[1] = 0x00;
-      int upl = d.hem ? 0 : 188 * 8, dfl = d.kbch - 80 - padding, sync = d.hem ? 0 : 0x47;
-      int syncd = count0 == 0 ? 0 : (188 - count0) * 8;
-      h[2] = (uint8_t)(upl >> 8); h[3] = (uint8_t)upl;
-      h[4] = (uint8_t)(dfl >> 8); h[5] = (uint8_t)dfl;
-      h[6] = (uint8_t)sync;
-      h[7] = (uint8_t)(syncd >> 8); h[8] = (uint8_t)syncd;
-      // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270)
-      uint32_t crc = 0;
-      for (int n = 0; n < 72; n++) {
-        uint32_t b = ((h[n >> 3] >> (7 - (n & 7))) & 1) ^ (crc & 1);
-        crc >>= 1;
-        if (b) crc ^= 0xAB;
+    // BBHEADER (bbheader:272-325), uniform across the workgroup: MATYPE-1 = TS, SIS, CCM, ISSYI 0,
+    // NPD 0, RO 0; ISI 0; bytes 0..7 big-endian in hw, byte 8 = SYNCD low, byte 9 = CRC-8
+    const uint32_t upl = d.hem ? 0u : 188u * 8u, dfl = (uint32_t)(d.kbch - 80 - padding);
+    const uint32_t syncb = d.hem ? 0u : 0x47u, syncd = count0 == 0 ? 0u : (uint32_t)(188 - count0) * 8u;
+    const uint64_t hw = (0xF0ull << 56) | ((uint64_t)upl << 32) | ((uint64_t)dfl << 16) | ((uint64_t)syncb << 8) |
+                        (uint64_t)(syncd >> 8);
+    uint32_t hcrc = 0;   // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270)
+    for (int n = 0; n < 72; n++) {
+      const uint32_t bit = n < 64 ? (uint32_t)(hw >> (63 - n)) & 1u : ((syncd & 0xFFu) >> (71 - n)) & 1u;
+      const uint32_t b = bit ^ (hcrc & 1u);
+      hcrc >>= 1;
+      if (b) hcrc ^= 0xABu;
+    }
+    if (d.hem) hcrc ^= 0x80u;
+    const uint32_t hcrc_rev = __builtin_bitreverse32(hcrc) >> 24;   // register LSB written first
+    auto slow_byte = [&](int pidx) -> uint32_t {   // BBFRAME byte pidx outside the bulk payload path
+      if (pidx < 8) return (uint32_t)(hw >> (56 - 8 * pidx)) & 0xFFu;
+      if (pidx == 8) return syncd & 0xFFu;
+      if (pidx == 9) return hcrc_rev;
+      const int j = pidx - 10;
+      if (j < npay) {
+        if (d.hem) return io.in[payload_pos(J0 + j, 1) - io.ts_base];
+        const int r = (count0 + j) % 188;
+        return r == 0 ? (uint32_t)syncv[(j - first_slot) / 188] : (uint32_t)smem[SM_RAW + delta + 188 + j];
       }
-      if (d.hem) crc ^= 0x80;
-      uint32_t rev = 0;   // bits written LSB of the register first
-      for (int n = 0; n < 8; n++) rev |= ((crc >> n) & 1) << (7 - n);
-      h[9] = (uint8_t)rev;
-      for (int i = 0; i < 10; i++) frame[i] = h[i];
-      if (padding) {
-        // in-band type B (bbheader:327-355): 01, 65 zero bits, TS rate (27 bits), 10 zeros
-        uint8_t ib[13] = {0x40, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int n = 0; n < 27; n++)
-          if ((d.ts_rate >> (26 - n)) & 1) {
-            int bit = 67 + n;
-            ib[bit >> 3] |= 1 << (7 - (bit & 7));
+      const int k = j - npay;   // in-band type B (bbheader:327-355): 01, 65 zero bits, TS rate (27 bits), 10 zeros
+      if (!padding || k >= 13) return 0u;
+      uint32_t v = k == 0 ? 0x40u : 0u;
+      for (int e = 0; e < 8; e++) {
+        const int bit = 8 * k + e;
+        if (bit >= 67 && bit < 94 && ((d.ts_rate >> (26 - (bit - 67))) & 1)) v |= 1u << (7 - e);
+      }
+      return v;
+    };
+    // BBFRAME words = header | payload (each sync slot carries the CRC-8 of the previous packet,
+    // bbheader:701-719) | in-band field, BB-scrambled (:694-696, :724-726)
+    {
+      uint32_t *framew = (uint32_t *)frame;
+      const uint32_t *prbsw = (const uint32_t *)d.prbs;
+      for (int w = tid; w < (L + 3) >> 2; w += FEC_THREADS) {
+        const int p0 = 4 * w, j0 = p0 - 10;
+        uint32_t v;
+        if (!d.hem && j0 >= 0 && j0 + 4 <= npay) {
+          const int q = delta + 188 + j0;
+          v = __builtin_amdgcn_alignbyte(raww[(q >> 2) + 1], raww[q >> 2], (uint32_t)(q & 3));
+          const int r0 = (count0 + j0) % 188, e = r0 == 0 ? 0 : 188 - r0;
+          if (e < 4) {
+            const uint32_t sb = syncv[(j0 + e - first_slot) / 188];
+            v = (v & ~(0xFFu << (8 * e))) | (sb << (8 * e));
           }
-        for (int i = 0; i < 13; i++) frame[10 + npay + i] = ib[i];
+        } else {
+          v = 0;
+          for (int e = 0; e < 4; e++) v |= slow_byte(p0 + e) << (8 * e);
+        }
+        framew[w] = v ^ prbsw[w];
       }
     }
     __syncthreads();
-    FEC_PHASE(2);
-    for (int i = tid; i < L; i += FEC_THREADS) frame[i] ^= d.prbs[i];   // BB scrambling
-    __syncthreads();
+    FEC_PHASE(4);
+    FEC_PHASE(5);
 
     // ---- BCH: lane t divides its chunk; Horner across lanes then waves
     {
@@ -269,11 +299,14 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
       const int lo = L - (128 - t) * C, hi = lane < 32 ? L - (127 - t) * C : 0;
       const int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
       // per-lane rows of M1 (v -> v x^(8C)) and M2 (v -> v x^(8*32*C)), loaded up front
+      // (reloaded per block, L1/L2 hits: kept out of the loop-carried register set)
+      const uint64_t *m1p = d.bch_m1, *m2p = d.bch_m2;
+      asm volatile("" : "+s"(m1p), "+s"(m2p));
       uint64_t m1[3][3], m2[3][3];
       for (int s = 0; s < 3; s++)
         for (int k = 0; k < 3; k++) {
-          m1[s][k] = d.bch_m1[(lane + 64 * s) * 3 + k];
-          m2[s][k] = d.bch_m2[(lane + 64 * s) * 3 + k];
+          m1[s][k] = m1p[(lane + 64 * s) * 3 + k];
+          m2[s][k] = m2p[(lane + 64 * s) * 3 + k];
         }
       uint64_t r0 = 0, r1 = 0, r2 = 0;
 #pragma unroll 4
@@ -317,19 +350,19 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
         for (int k = lane; k < P / 8; k += 64) frame[L + k] = get_byte192(acc, P - 8 - 8 * k);
       }
       __syncthreads();
-      FEC_PHASE(3);
+      FEC_PHASE(6);
     }
     if (MODE == FEC_TS_TO_BITS) {
-      uint8_t *dst = io.out + (int64_t)blockIdx.x * d.nbch;
+      uint8_t *dst = io.out + (int64_t)bi * d.nbch;
       for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
-      return;
+      break;
     }
   }
 
-  // ---- LDPC.  Doubled info groups: D[g][k] = big-endian word k of d_g || d_g || d_g[0..47]
+  // ---- LDPC.  Extended info groups: D[g][k] = big-endian word k of d_g || d_g[0..56)
   const int ngroups = d.nbch / 360;
-  for (int it = tid; it < ngroups * 24; it += FEC_THREADS) {
-    int g = it / 24, k = it - g * 24;
+  for (int it = tid; it < ngroups * FEC_DW; it += FEC_THREADS) {
+    int g = it / FEC_DW, k = it - g * FEC_DW;
     const uint8_t *gb = frame + 45 * g;
     int b = 4 * k;
     uint32_t w = ((uint32_t)gb[b % 45] << 24) | ((uint32_t)gb[(b + 1) % 45] << 16) |
@@ -337,7 +370,7 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     D[it] = w;
   }
   __syncthreads();
-  FEC_PHASE(4);
+  FEC_PHASE(7);
   // row a, word w of p[a][c] = XOR over entries (g, b) of d_g[(c - b) mod 360]
   const int q = d.q;
   for (int it = tid; it < q * 12; it += FEC_THREADS) {
@@ -346,8 +379,9 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     for (int e = rp[a]; e < rp[a + 1]; e++) {
       uint32_t ent = ents[e];
       int g = ent >> 16, b = ent & 0xFFFF;
-      int o = 32 * w + 360 - b;
-      const uint32_t *dg = D + g * 24 + (o >> 5);
+      int o = 32 * w - b;            // window start (c - b) mod 360 for c = 32 w
+      o += o < 0 ? 360 : 0;
+      const uint32_t *dg = D + g * FEC_DW + (o >> 5);
       uint64_t win = ((uint64_t)dg[0] << 32) | dg[1];
       acc ^= (uint32_t)(win >> (32 - (o & 31)));
     }
@@ -355,7 +389,7 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     rowA[it] = acc;
   }
   __syncthreads();
-  FEC_PHASE(5);
+  FEC_PHASE(8);
   // inclusive prefix XOR over rows a, in place: wave w scans word columns 3w..3w+2, 64 rows
   // per wave-level shuffle scan plus the carry of the previous 64
   uint32_t *cur = rowA;
@@ -392,21 +426,21 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
   __syncthreads();
   for (int it = tid; it < q * 12; it += FEC_THREADS) cur[it] ^= Wv[it % 12];
   __syncthreads();
-  FEC_PHASE(6);
+  FEC_PHASE(9);
   // parity bit of row a (interleaved position 360 a + c) / natural index a + q c
   auto pbit = [&](int a, int c) -> uint32_t { return (cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1; };
 
   if (MODE == FEC_BITS_TO_BITS) {
-    uint8_t *dst = io.out + (int64_t)blockIdx.x * d.nldpc;
+    uint8_t *dst = io.out + (int64_t)bi * d.nldpc;
     for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
     const int pbits = d.nldpc - d.nbch;
     for (int j = tid; j < pbits; j += FEC_THREADS) dst[d.nbch + j] = (uint8_t)pbit(j % q, j / q);
-    return;
+    break;
   }
-  // FEC_TS_TO_TEMPU: assemble the interleaver input bytes in LDS (over D), store as words
-  uint8_t *stage = (uint8_t *)D;
+  // FEC_TS_TO_TEMPU: the interleaver input bytes are assembled in LDS after the info bytes
+  // (frame[NB..cwb): parity), then stored as words
+  uint8_t *stage = frame;
   const int cwb = d.nldpc >> 3, pb = cwb - NB;
-  for (int i = tid; i < NB; i += FEC_THREADS) stage[i] = frame[i];
   if (d.parity_il) {
     for (int i = tid; i < pb; i += FEC_THREADS) {
       int a = i / 45, k = i - 45 * a;
@@ -423,22 +457,39 @@ __global__ __launch_bounds__(FEC_THREADS) void fec_kernel(FecDev d, FecIO io) {
     }
   }
   __syncthreads();
-  uint32_t *dstw = (uint32_t *)(io.out + (int64_t)blockIdx.x * io.cw_stride);
+  uint32_t *dstw = (uint32_t *)(io.out + (int64_t)bi * io.cw_stride);
   const uint32_t *srcw = (const uint32_t *)stage;
   for (int i = tid; i < cwb / 4 + (cwb & 3 ? 1 : 0); i += FEC_THREADS) dstw[i] = srcw[i];
 #if FEC_VARIANT & 1
   __syncthreads();
-  FEC_PHASE(7);
+  FEC_PHASE(10);
   if (tid == 0) {
     dstw[0] = (uint32_t)g_fec_ts[0];
-    for (int i = 1; i < 8; i++) dstw[i] = (uint32_t)(g_fec_ts[i] - g_fec_ts[0]);
+    for (int i = 1; i < 11; i++) dstw[i] = (uint32_t)(g_fec_ts[i] - g_fec_ts[0]);
   }
 #endif
+  } while (0);
+  __syncthreads();   // frame / phase regions are reused by the next block
+  }
 }
+
+// resident FEC workgroups for a persistent launch: FEC_WG_PER_CU per CU of the current device
+static int fec_grid(int nblocks) {
+  static int ncu[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!ncu[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    ncu[dev] = n;
+  }
+  return nblocks < ncu[dev] * FEC_WG_PER_CU ? nblocks : ncu[dev] * FEC_WG_PER_CU;
+}
+
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
-  dim3 grid(io.nblocks), block(FEC_THREADS);
+  dim3 grid(fec_grid(io.nblocks)), block(FEC_THREADS);
   switch (mode) {
     case FEC_TS_TO_TEMPU: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, FEC_SMEM, s, d, io); break;
     case FEC_TS_TO_BITS: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_BITS>, grid, block, FEC_SMEM, s, d, io); break;
@@ -636,6 +687,12 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {
 }
 
 // ============================================================================ OFDM kernel
+#ifndef OFDM_SPLIT_V
+#define OFDM_SPLIT_V 32
+#endif
+#ifndef OFDM_SQ16
+#define OFDM_SQ16 8
+#endif
 // exp(+2 pi i k / 32): exact at multiples of pi/2
 __device__ constexpr float kCos32[32] = {
     1.0f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f, 0.70710678118654757f,
@@ -887,7 +944,7 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     const uint32_t rn = SPLIT ? (half ? src.dn - src.dn0 : src.dn0) : src.dn;
     const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
     const uint32_t lastq = nq - 1u;
-    constexpr int SQ = 8;                        // quads per thread per round
+    constexpr int SQ = V >= 32 ? 8 : OFDM_SQ16;  // quads per thread per round
     for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
       uint2 b[SQ], c[SQ];
 #pragma unroll
@@ -945,11 +1002,12 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   FftPlan<NSUB, V>::Tail::run(v, lds, tw, tws, tid);
 }
 
+
 template <int N>
 struct OfdmShape {
   static constexpr bool SPLIT = N > 16384;
   static constexpr int NSUB = SPLIT ? N / 2 : N;
-  static constexpr int V = SPLIT ? 32 : 16;                           // values per thread
+  static constexpr int V = SPLIT ? OFDM_SPLIT_V : 16;                 // values per thread
   static constexpr int NT = NSUB / V;
   static constexpr int FFT_LDS = (NSUB + NSUB / 16 + 64) * 8;       // padded buffer + 64 dummy slots
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table

@@ -21,8 +21,8 @@ for _ in range(3):
 torch.cuda.synchronize()
 nb = B * ch.info["fec_blocks_per_frame"]
 cw = ch.debug_codewords(nb)
-w = cw[:, :32].copy().view(np.uint32).astype(np.int64)
-names = ["stage+geom", "crc+payload", "bch", "ldpc D", "ldpc rows", "prefix", "output"]
+w = cw[:, :44].copy().view(np.uint32).astype(np.int64)
+names = ["geometry", "raw stage", "crc-8", "payload+hdr", "scramble", "bch", "ldpc D", "ldpc rows", "prefix", "output"]
 prev = np.zeros(nb, np.int64)
 print("FEC phase durations (us), median / p90 over %d blocks" % nb)
 for i, n in enumerate(names):
@@ -31,5 +31,5 @@ for i, n in enumerate(names):
     print("  %-12s %7.2f %7.2f" % (n, np.median(dur), np.percentile(dur, 90)))
     prev = cur
 t0 = (w[:, 0] - w[:, 0].min()) & 0xFFFFFFFF
-print("  total        %7.2f" % np.median(w[:, 7] * 0.01))
-print("span %.1f us, start spread %.1f us" % (((t0 + w[:, 7]).max()) * 0.01, t0.max() * 0.01))
+print("  total        %7.2f" % np.median(w[:, len(names)] * 0.01))
+print("span %.1f us, start spread %.1f us" % (((t0 + w[:, len(names)]).max()) * 0.01, t0.max() * 0.01))
