@@ -124,6 +124,9 @@ struct MapTables {
     dev.F = 1;
     memcpy(dev.twist, plan.twist, 16);
     memcpy(dev.mux, plan.mux, 16);
+    // column feeding bit b of the demuxed row word (b = W - 1 - mux[e]); 255 = none
+    memset(dev.colsel, 255, 16);
+    for (int e = 0; e < plan.W && plan.mode != 0; e++) dev.colsel[plan.W - 1 - plan.mux[e]] = (uint8_t)e;
     return 0;
   }
 };

@@ -44,6 +44,7 @@ struct MapDev {
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
   const int16_t *part;     // chain, 32K only: slot - TI position of (block r, TI-store index j), at r*cs + j
   uint8_t twist[16], mux[16];
+  uint8_t colsel[16];      // column e whose bit lands at position b of the row word (W-1-mux[e] = b), 255: none
 };
 struct MapIO {
   const uint8_t *in;   // packed tempu codewords (stride cw_stride) or unpacked natural bits

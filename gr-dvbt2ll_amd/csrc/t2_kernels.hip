@@ -540,48 +540,94 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   const int cs = d.cs, nl = d.nldpc;
   MAP_PHASE(0);
   for (int i = tid; i < 256; i += MAP_THREADS) lut[i] = d.lut[i];
-  // ---- interleaver input bits (tempu) into LDS
+  // ---- interleaver input bits (tempu) into LDS as big-endian words: bit i of the codeword is
+  //      bit 31 - (i & 31) of word i >> 5
+  uint32_t *cww = (uint32_t *)cw;
+  const int nlw = (nl + 31) >> 5;
   if (io.packed_in) {
     const uint32_t *src = (const uint32_t *)(io.in + (int64_t)blk * io.cw_stride);
-    uint32_t *dst = (uint32_t *)cw;
-    for (int i = tid; i < nl / 32; i += MAP_THREADS) dst[i] = src[i];
-    if ((nl & 31) && tid == 0) dst[nl / 32] = src[nl / 32];
+    for (int i = tid; i < nlw; i += MAP_THREADS) cww[i] = __builtin_bswap32(src[i]);
   } else {
     const uint8_t *src = io.in + (int64_t)blk * nl;
     const int nbch = d.nbch, q = d.q;
-    for (int k = tid; k < nl / 8; k += MAP_THREADS) {
+    for (int k = tid; k < nlw; k += MAP_THREADS) {
       uint32_t v = 0;
-      for (int e = 0; e < 8; e++) {
-        int i = 8 * k + e, sidx = i;
+      for (int e = 0; e < 32; e++) {
+        int i = 32 * k + e, sidx = i;
+        if (i >= nl) break;
         if (d.parity_il && i >= nbch) {        // tempu[nbch + 360 t + s] = in[nbch + q s + t]
           int r = i - nbch, t = r / 360, s = r - 360 * t;
           sidx = nbch + q * s + t;
         }
-        v |= (uint32_t)(src[sidx] & 1) << (7 - e);
+        v |= (uint32_t)(src[sidx] & 1) << (31 - e);
       }
-      cw[k] = (uint8_t)v;
+      cww[k] = v;
     }
   }
   __syncthreads();
   MAP_PHASE(1);
-  auto bit = [&](int i) -> uint32_t { return (cw[i >> 3] >> (7 - (i & 7))) & 1; };
-  // ---- cell indices: column-twist write / row read / demux (interleavermod:351-403 ...)
+  // ---- cell indices: column-twist write / row read / demux (interleavermod:351-403, 440-500,
+  //      529-598, 626-677).  One thread per 32 rows: each column's 32 bits are one (twisted,
+  //      wrapping) window of the codeword, the W windows are ordered by demuxed bit position and
+  //      transposed as a bit matrix, giving each row's demuxed word directly.
   if (d.mode == 0) {
-    for (int j = tid; j < cs; j += MAP_THREADS) idx[j] = (uint8_t)((bit(2 * j) << 1) | bit(2 * j + 1));
+    // QPSK: cell j = codeword bits 2j, 2j+1 (no bit interleaving, interleavermod:309-314)
+    uint32_t *idxw = (uint32_t *)idx;
+    for (int w = tid; w < (cs + 3) >> 2; w += MAP_THREADS) {
+      const uint32_t word = cww[w >> 2], sh = 24u - 8u * (uint32_t)(w & 3);
+      const uint32_t byte = (word >> sh) & 0xFFu;   // cells 4w..4w+3
+      idxw[w] = ((byte >> 6) & 3u) | (((byte >> 4) & 3u) << 8) | (((byte >> 2) & 3u) << 16) | ((byte & 3u) << 24);
+    }
   } else {
-    const int W = d.W, R = d.R, mod = d.mod;
-    for (int j = tid; j < R; j += MAP_THREADS) {
-      uint32_t pack = 0;
-      for (int e = 0; e < W; e++) {
-        int r = j - d.twist[e];
-        r += r < 0 ? R : 0;
-        pack |= bit(e * R + r) << (W - 1 - d.mux[e]);
+    const int R = d.R, mod = d.mod;
+    auto window = [&](int s) -> uint32_t {    // codeword bits [s, s + 32), MSB first
+      const uint64_t v = ((uint64_t)cww[s >> 5] << 32) | cww[(s >> 5) + 1];
+      return (uint32_t)((v << (s & 31)) >> 32);
+    };
+    // 8-bit transpose (Hacker's Delight transpose8): bit 8 i + j <-> bit 8 j + i
+    auto tr8 = [](uint64_t x) -> uint64_t {
+      uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+      x ^= t ^ (t << 7);
+      t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+      x ^= t ^ (t << 14);
+      t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+      x ^= t ^ (t << 28);
+      return x;
+    };
+    // one thread per 8 rows: byte b of x = column colsel[b]'s 8 bits (row k at bit 7 - k); after
+    // the transpose byte 7 - k holds row k's demuxed bits b
+    for (int g = tid; g < (R + 7) >> 3; g += MAP_THREADS) {
+      const int j0 = 8 * g;
+      uint64_t x[2] = {0, 0};
+#pragma unroll
+      for (int b = 0; b < 16; b++) {
+        const int e = d.colsel[b];
+        if (e == 255) continue;
+        int off = j0 - d.twist[e];
+        off += off < 0 ? R : 0;
+        uint32_t win = window(e * R + off);
+        if (off + 8 > R) {                       // the column wraps inside these 8 rows
+          const int n1 = R - off;
+          win = (win & ~(0xFFFFFFFFu >> n1)) | (window(e * R) >> n1);
+        }
+        x[b >> 3] |= (uint64_t)(win >> 24) << (8 * (b & 7));
       }
-      if (d.mode == 1) {
-        idx[2 * j] = (uint8_t)(pack >> mod);
-        idx[2 * j + 1] = (uint8_t)(pack & ((1u << mod) - 1));
-      } else {
-        idx[j] = (uint8_t)(pack & 0xFF);
+      const uint64_t lo = tr8(x[0]), hi = d.W > 8 ? tr8(x[1]) : 0ull;
+      uint32_t *idxw = (uint32_t *)idx;
+      if (d.mode == 1) {                         // two cells per row: pack >> mod, pack & (2^mod - 1)
+        const uint32_t lo_mask = (1u << mod) - 1u;
+#pragma unroll
+        for (int qd = 0; qd < 4; qd++) {
+          const int k0 = 2 * qd;
+          const uint32_t p0 = (uint32_t)((lo >> (8 * (7 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (7 - k0))) & 0xFFu) << 8);
+          const uint32_t p1 = (uint32_t)((lo >> (8 * (6 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (6 - k0))) & 0xFFu) << 8);
+          if (j0 + k0 < R)
+            idxw[4 * g + qd] = (p0 >> mod) | ((p0 & lo_mask) << 8) | ((p1 >> mod) << 16) | ((p1 & lo_mask) << 24);
+        }
+      } else {                                   // 256-QAM short: one cell per row (byte-reversed lo)
+        const uint64_t rv = __builtin_bswap64(lo);
+        if (j0 < R) idxw[2 * g] = (uint32_t)rv;
+        if (j0 + 4 < R) idxw[2 * g + 1] = (uint32_t)(rv >> 32);
       }
     }
   }
