@@ -683,8 +683,10 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   // (10 B) per TI row (32K: through the half partition); the constellation lookup (QAM +
   // rotated-constellation Q delay) is fused into the OFDM kernel's bin scatter
   const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
+  // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
+  const int16_t *pr = d.part ? d.part + (int64_t)r * cs : nullptr;   // block-major int16 table
   for (int j0 = tid; j0 < cs; j0 += MB * MAP_THREADS) {
-    int64_t dsl[MB];
+    uint32_t dsl[MB];
     int tt[MB];
 #pragma unroll
     for (int u = 0; u < MB; u++) {
@@ -698,11 +700,11 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
         tt[u] = j;
         o = j;
       }
-      dsl[u] = fbase + o + (d.part ? d.part[(int64_t)r * cs + j] : 0);   // block-major int16 table
+      dsl[u] = (uint32_t)fbase + (uint32_t)o + (uint32_t)(pr ? (int)pr[j] : 0);
     }
 #pragma unroll
     for (int u = 0; u < MB; u++) {
-      if (j0 + u * MAP_THREADS < cs) dst[dsl[u]] = stage[tt[u]];
+      if (j0 + u * MAP_THREADS < cs) st_off(dst, dsl[u] * 2u, stage[tt[u]]);
     }
   }
 #if MAP_VARIANT & 1
