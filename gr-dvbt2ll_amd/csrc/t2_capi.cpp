@@ -81,18 +81,17 @@ struct DeviceCtx {
 // ---------------------------------------------------------------- FEC tables on device
 struct FecTables {
   FecPlan plan;
-  DevBuf tab, m1, m2, rowptr, ent, prbs, crc8, crcsh;
+  DevBuf tab, m1, rowptr, ent, prbs, crc8, crcsh;
   FecDev dev{};
   int init(int framesize, int rate, int constellation, int mode, int inband, int fecblocks, int tsrate) {
     if (build_fec(framesize, rate, constellation, plan)) return DVBT2LL_EINVAL;
     int r;
-    if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) || (r = upload(m2, plan.bch_m2)) ||
+    if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) ||
         (r = upload(rowptr, plan.ldpc_rowptr)) || (r = upload(ent, plan.ldpc_ent)) ||
         (r = upload(prbs, plan.prbs_bytes)) || (r = upload(crc8, plan.crc8_tab)) || (r = upload(crcsh, plan.crc8_shift)))
       return r;
     dev.bch_tab = tab.as<uint64_t>();
     dev.bch_m1 = m1.as<uint64_t>();
-    dev.bch_m2 = m2.as<uint64_t>();
     dev.ldpc_rowptr = rowptr.as<uint16_t>();
     dev.ldpc_ent = ent.as<uint32_t>();
     dev.prbs = prbs.as<uint8_t>();

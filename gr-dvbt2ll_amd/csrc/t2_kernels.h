@@ -15,7 +15,6 @@ enum FecMode {
 struct FecDev {
   const uint64_t *bch_tab;      // 256 x 3
   const uint64_t *bch_m1;       // 192 x 3
-  const uint64_t *bch_m2;       // 192 x 3
   const uint16_t *ldpc_rowptr;  // q + 1
   const uint32_t *ldpc_ent;     // nent
   const uint8_t *prbs;          // kbch / 8

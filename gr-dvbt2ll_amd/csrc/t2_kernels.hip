@@ -75,32 +75,29 @@ __shared__ uint64_t g_fec_ts[16];
 #define FEC_PHASE(i) do { } while (0)
 #endif
 constexpr int FEC_THREADS = 256;
-constexpr int FEC_FRAME_BYTES = 8112;   // >= max nldpc/8 (8100): info bytes, then the output parity bytes
-constexpr int FEC_MAX_GROUPS = 150;     // nbch / 360 (5/6 normal)
-constexpr int FEC_MAX_Q = 90;
-constexpr int FEC_MAX_ENT = 656;
+constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
+constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 233280 / 360)
 constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g || d_g[0..56)
-constexpr int FEC_WG_PER_CU = 5;
+constexpr int FEC_WG_PER_CU = 6;
 // dynamic LDS carve (bytes): a persistent part (the workgroup loops over FEC blocks; tables are
-// staged once), then one region reused by phase:  BB/CRC phase: [raw TS bytes]   LDPC: [D | rows]
+// staged once), then one region reused by phase:
+//   BB/CRC phase: [raw TS bytes | CRC-8 table | CRC-8 zero-extension tables] (tables per block)
+//   LDPC: [D: ngroups x 13 words | rows: q x 12 words], ngroups + q = nldpc / 360 (<= 180)
 constexpr int SM_FRAME = 0;
-constexpr int SM_SYNC = SM_FRAME + FEC_FRAME_BYTES;          // 64
-constexpr int SM_WACC = SM_SYNC + 64;                        // 4*3*8 = 96
-constexpr int SM_W = SM_WACC + 96;                           // 16*4
-constexpr int SM_ENT = SM_W + 64;                            // 656*4
-constexpr int SM_RP = SM_ENT + FEC_MAX_ENT * 4;              // 96*2
-constexpr int SM_BTAB = (SM_RP + 96 * 2 + 15) & ~15;         // 256*3*8 = 6144
-constexpr int SM_CRC8 = SM_BTAB + 6144;                      // 256
-constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
-constexpr int SM_PHASE = SM_CRCSH + 2048;
+constexpr int SM_SYNC = SM_FRAME + FEC_FRAME_BYTES;          // 48 (<= 36 sync slots)
+constexpr int SM_W = SM_SYNC + 48;                           // 12*4
+constexpr int SM_ENT = SM_W + 48;                            // 648*4
+constexpr int SM_BTAB = SM_ENT + FEC_MAX_ENT * 4;            // 256*3*8 = 6144
+constexpr int SM_PHASE = SM_BTAB + 6144;
 constexpr int SM_RAW = SM_PHASE;                             // raw TS bytes of the block (NM)
 constexpr int FEC_RAW_BYTES = 188 + 6720 + 16;               // one packet before + max payload
-constexpr int SM_D = SM_PHASE;                               // 150*13*4 = 7800 (after BCH)
-constexpr int SM_ROWA = SM_D + FEC_MAX_GROUPS * FEC_DW * 4;  // 90*12*4 = 4320
-constexpr int FEC_SMEM = (SM_RAW + FEC_RAW_BYTES > SM_ROWA + FEC_MAX_Q * 12 * 4 ? SM_RAW + FEC_RAW_BYTES
-                                                                                : SM_ROWA + FEC_MAX_Q * 12 * 4);
-static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0 && SM_WACC % 8 == 0, "LDS carve alignment");
-static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "five FEC workgroups per CU");
+constexpr int SM_CRC8 = SM_RAW + ((FEC_RAW_BYTES + 15) & ~15);   // 256
+constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
+constexpr int SM_D = SM_PHASE;                               // rows follow D at word ngroups * 13
+constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
+constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_BYTES ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_BYTES);
+static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0, "LDS carve alignment");
+static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "six FEC workgroups per CU");
 
 // stream position of payload byte J (counted over the payload bytes of the whole stream)
 __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
@@ -110,6 +107,15 @@ __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
 __device__ __forceinline__ uint8_t get_byte192(const uint64_t w[3], int lowbit) {
   // 8 bits [lowbit, lowbit+8) of a 192-bit value; lowbit multiple of 8
   return (uint8_t)(w[lowbit >> 6] >> (lowbit & 63));
+}
+
+// word k of LDPC info group g laid out for 32-bit rotation windows: big-endian bytes
+// (4k .. 4k+3) mod 45 of the group's 45 frame bytes (d_g || d_g[0..56))
+__device__ __forceinline__ void ldpc_group_word(uint32_t *D, const uint8_t *frame, int g, int k) {
+  const uint8_t *gb = frame + 45 * g;
+  const int b = 4 * k;
+  D[g * FEC_DW + k] = ((uint32_t)gb[b % 45] << 24) | ((uint32_t)gb[(b + 1) % 45] << 16) |
+                      ((uint32_t)gb[(b + 2) % 45] << 8) | (uint32_t)gb[(b + 3) % 45];
 }
 
 template <int MODE>
@@ -124,21 +130,13 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   uint8_t *crcsh = smem + SM_CRCSH;
   uint8_t *syncv = smem + SM_SYNC;
   uint64_t *btab = (uint64_t *)(smem + SM_BTAB);
-  uint64_t *wacc = (uint64_t *)(smem + SM_WACC);
   uint32_t *D = (uint32_t *)(smem + SM_D);
-  uint32_t *rowA = (uint32_t *)(smem + SM_ROWA);
   uint32_t *Wv = (uint32_t *)(smem + SM_W);
   uint32_t *ents = (uint32_t *)(smem + SM_ENT);
-  uint16_t *rp = (uint16_t *)(smem + SM_RP);
 
   // ---- constant tables into LDS, once: the workgroup then loops over FEC blocks
   for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
   for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
-  for (int i = tid; i <= d.q; i += FEC_THREADS) rp[i] = d.ldpc_rowptr[i];
-  if (MODE != FEC_BITS_TO_BITS) {
-    for (int i = tid; i < 256; i += FEC_THREADS) crc8[i] = d.crc8_tab[i];
-    for (int i = tid; i < 2048; i += FEC_THREADS) crcsh[i] = d.crc8_shift[i];
-  }
   __syncthreads();
 
   for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
@@ -185,6 +183,8 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
       delta = (int)(rel - 4 * w0);
       const int nw = (delta + npay + 188 + 3) >> 2;
       uint32_t *rawst = (uint32_t *)(smem + SM_RAW);
+      for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)crc8)[i] = ((const uint32_t *)d.crc8_tab)[i];
+      for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)crcsh)[i] = ((const uint32_t *)d.crc8_shift)[i];
       const bool aligned = (((uintptr_t)io.in) & 3) == 0;
       for (int i = tid; i < nw; i += FEC_THREADS) {
         const int64_t b = 4 * (w0 + i);
@@ -291,23 +291,21 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     FEC_PHASE(4);
     FEC_PHASE(5);
 
-    // ---- BCH: lane t divides its chunk; Horner across lanes then waves
-    {
+    // ---- BCH on wave 0: lane t divides chunk t (64 chunks of C bytes, t2_plan: bch_chunk), then a
+    //      Horner pass over the lanes with the shift matrix M1 (v -> v x^(8C) mod g) as wave ballots.
+    //      Meanwhile (chain mode) waves 1..3 lay out the LDPC info groups that hold no BCH parity.
+    const int ngroups = d.nbch / 360;
+    if (wave == 0) {
       const int C = d.chunk;
-      // 128 chunks of C bytes: chunk t = 32 wave + lane on lanes 0..31 (t2_plan: bch_chunk)
-      const int t = 32 * wave + lane;
-      const int lo = L - (128 - t) * C, hi = lane < 32 ? L - (127 - t) * C : 0;
+      const int lo = L - (64 - lane) * C, hi = L - (63 - lane) * C;
       const int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
-      // per-lane rows of M1 (v -> v x^(8C)) and M2 (v -> v x^(8*32*C)), loaded up front
-      // (reloaded per block, L1/L2 hits: kept out of the loop-carried register set)
-      const uint64_t *m1p = d.bch_m1, *m2p = d.bch_m2;
-      asm volatile("" : "+s"(m1p), "+s"(m2p));
-      uint64_t m1[3][3], m2[3][3];
+      // per-lane rows of M1, loaded up front (reloaded per block, L1/L2 hits: kept out of the
+      // loop-carried register set)
+      const uint64_t *m1p = d.bch_m1;
+      asm volatile("" : "+s"(m1p));
+      uint64_t m1[3][3];
       for (int s = 0; s < 3; s++)
-        for (int k = 0; k < 3; k++) {
-          m1[s][k] = m1p[(lane + 64 * s) * 3 + k];
-          m2[s][k] = m2p[(lane + 64 * s) * 3 + k];
-        }
+        for (int k = 0; k < 3; k++) m1[s][k] = m1p[(lane + 64 * s) * 3 + k];
       uint64_t r0 = 0, r1 = 0, r2 = 0;
 #pragma unroll 4
       for (int i = max(lo, 0); i < hi; i++) {
@@ -325,7 +323,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
         r2 ^= btab[idx * 3 + 2];
       }
       uint64_t a0 = rd_lane_u64(r0, 0), a1 = rd_lane_u64(r1, 0), a2 = rd_lane_u64(r2, 0);
-      for (int l = 1; l < 32; l++) {
+      for (int l = 1; l < 64; l++) {
         uint64_t n0 = __ballot(__popcll((m1[0][0] & a0) ^ (m1[0][1] & a1) ^ (m1[0][2] & a2)) & 1);
         uint64_t n1 = __ballot(__popcll((m1[1][0] & a0) ^ (m1[1][1] & a1) ^ (m1[1][2] & a2)) & 1);
         uint64_t n2 = __ballot(__popcll((m1[2][0] & a0) ^ (m1[2][1] & a1) ^ (m1[2][2] & a2)) & 1);
@@ -333,25 +331,26 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
         a1 = n1 ^ rd_lane_u64(r1, l);
         a2 = n2 ^ rd_lane_u64(r2, l);
       }
-      if (lane == 0) { wacc[wave * 3 + 0] = a0; wacc[wave * 3 + 1] = a1; wacc[wave * 3 + 2] = a2; }
-      __syncthreads();
-      if (wave == 0) {
-        a0 = wacc[0]; a1 = wacc[1]; a2 = wacc[2];
-        for (int w = 1; w < 4; w++) {
-          uint64_t n0 = __ballot(__popcll((m2[0][0] & a0) ^ (m2[0][1] & a1) ^ (m2[0][2] & a2)) & 1);
-          uint64_t n1 = __ballot(__popcll((m2[1][0] & a0) ^ (m2[1][1] & a1) ^ (m2[1][2] & a2)) & 1);
-          uint64_t n2 = __ballot(__popcll((m2[2][0] & a0) ^ (m2[2][1] & a1) ^ (m2[2][2] & a2)) & 1);
-          a0 = n0 ^ wacc[w * 3 + 0];
-          a1 = n1 ^ wacc[w * 3 + 1];
-          a2 = n2 ^ wacc[w * 3 + 2];
-        }
-        // parity bits MSB (x^(P-1)) first, appended after the BBFRAME
-        uint64_t acc[3] = {a0, a1, a2};
-        for (int k = lane; k < P / 8; k += 64) frame[L + k] = get_byte192(acc, P - 8 - 8 * k);
+      // parity bits MSB (x^(P-1)) first, appended after the BBFRAME
+      uint64_t acc[3] = {a0, a1, a2};
+      for (int k = lane; k < P / 8; k += 64) frame[L + k] = get_byte192(acc, P - 8 - 8 * k);
+      if (MODE == FEC_TS_TO_TEMPU) {
+        // the last info group holds the BCH parity (P < 360): lay it out here, after the parity
+        // bytes (same wave; LDS accesses of one wave complete in order)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (lane < FEC_DW) ldpc_group_word(D, frame, ngroups - 1, lane);
       }
-      __syncthreads();
-      FEC_PHASE(6);
+    } else if (MODE == FEC_TS_TO_TEMPU) {
+      for (int it = tid - 64; it < (ngroups - 1) * FEC_DW; it += FEC_THREADS - 64) {
+        const int g = it / FEC_DW;
+        ldpc_group_word(D, frame, g, it - g * FEC_DW);
+      }
     }
+    __syncthreads();
+    FEC_PHASE(6);
+    FEC_PHASE(7);
     if (MODE == FEC_TS_TO_BITS) {
       uint8_t *dst = io.out + (int64_t)bi * d.nbch;
       for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
@@ -360,19 +359,20 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   }
 
   // ---- LDPC.  Extended info groups: D[g][k] = big-endian word k of d_g || d_g[0..56)
+  //      (chain mode: laid out above, overlapping the BCH)
   const int ngroups = d.nbch / 360;
-  for (int it = tid; it < ngroups * FEC_DW; it += FEC_THREADS) {
-    int g = it / FEC_DW, k = it - g * FEC_DW;
-    const uint8_t *gb = frame + 45 * g;
-    int b = 4 * k;
-    uint32_t w = ((uint32_t)gb[b % 45] << 24) | ((uint32_t)gb[(b + 1) % 45] << 16) |
-                 ((uint32_t)gb[(b + 2) % 45] << 8) | (uint32_t)gb[(b + 3) % 45];
-    D[it] = w;
+  if (MODE == FEC_BITS_TO_BITS) {
+    for (int it = tid; it < ngroups * FEC_DW; it += FEC_THREADS) {
+      const int g = it / FEC_DW;
+      ldpc_group_word(D, frame, g, it - g * FEC_DW);
+    }
+    __syncthreads();
+    FEC_PHASE(7);
   }
-  __syncthreads();
-  FEC_PHASE(7);
   // row a, word w of p[a][c] = XOR over entries (g, b) of d_g[(c - b) mod 360]
   const int q = d.q;
+  uint32_t *rowA = D + ngroups * FEC_DW;
+  const uint16_t *rp = d.ldpc_rowptr;
   for (int it = tid; it < q * 12; it += FEC_THREADS) {
     int a = it / 12, w = it - a * 12;
     uint32_t acc = 0;
@@ -437,29 +437,37 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     for (int j = tid; j < pbits; j += FEC_THREADS) dst[d.nbch + j] = (uint8_t)pbit(j % q, j / q);
     break;
   }
-  // FEC_TS_TO_TEMPU: the interleaver input bytes are assembled in LDS after the info bytes
-  // (frame[NB..cwb): parity), then stored as words
-  uint8_t *stage = frame;
-  const int cwb = d.nldpc >> 3, pb = cwb - NB;
-  if (d.parity_il) {
-    for (int i = tid; i < pb; i += FEC_THREADS) {
-      int a = i / 45, k = i - 45 * a;
-      stage[NB + i] = (uint8_t)(cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3)));
+  // FEC_TS_TO_TEMPU: interleaver input words = info bytes (frame) | parity bytes (rows; parity
+  // interleaved: byte m = byte m % 45 of row m / 45)
+  const int cwb = d.nldpc >> 3;
+  auto parity_byte = [&](int m) -> uint32_t {
+    if (d.parity_il) {
+      const int a = m / 45, k = m - 45 * a;
+      return (cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu;
     }
-  } else {
-    for (int i = tid; i < pb; i += FEC_THREADS) {
-      uint32_t v = 0;
-      for (int e = 0; e < 8; e++) {
-        int j = 8 * i + e;
-        v |= pbit(j % q, j / q) << (7 - e);
-      }
-      stage[NB + i] = (uint8_t)v;
+    uint32_t v = 0;
+    for (int e = 0; e < 8; e++) {
+      const int j = 8 * m + e;
+      v |= pbit(j % q, j / q) << (7 - e);
     }
-  }
-  __syncthreads();
+    return v;
+  };
   uint32_t *dstw = (uint32_t *)(io.out + (int64_t)bi * io.cw_stride);
-  const uint32_t *srcw = (const uint32_t *)stage;
-  for (int i = tid; i < cwb / 4 + (cwb & 3 ? 1 : 0); i += FEC_THREADS) dstw[i] = srcw[i];
+  const uint32_t *framew = (const uint32_t *)frame;
+  for (int i = tid; i < (cwb + 3) >> 2; i += FEC_THREADS) {
+    uint32_t v;
+    if (4 * i + 4 <= NB) {
+      v = framew[i];
+    } else {
+      v = 0;
+      for (int e = 0; e < 4; e++) {
+        const int bidx = 4 * i + e;
+        const uint32_t by = bidx < NB ? (uint32_t)frame[bidx] : bidx < cwb ? parity_byte(bidx - NB) : 0u;
+        v |= by << (8 * e);
+      }
+    }
+    dstw[i] = v;
+  }
 #if FEC_VARIANT & 1
   __syncthreads();
   FEC_PHASE(10);
@@ -489,6 +497,10 @@ static int fec_grid(int nblocks) {
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
+  // the LDS carve is sized for the standard codes: refuse anything larger
+  if (d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 52 * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
+      d.P > 192 || d.chunk * 64 < d.kbch / 8)
+    return hipErrorInvalidValue;
   dim3 grid(fec_grid(io.nblocks)), block(FEC_THREADS);
   switch (mode) {
     case FEC_TS_TO_TEMPU: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, FEC_SMEM, s, d, io); break;

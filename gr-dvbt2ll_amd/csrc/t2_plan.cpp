@@ -159,10 +159,9 @@ int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
     for (int k = 0; k < 3; k++) fp.bch_tab[d * 3 + k] = v.w[k];
   }
   const int L = fp.kbch / 8;
-  // 128 chunks: lanes 0..31 of each of the 4 waves of the FEC kernel (BCH_CHUNKS)
-  fp.bch_chunk = (L + 127) / 128;
+  // 64 chunks: the 64 lanes of the FEC kernel's BCH wave
+  fp.bch_chunk = (L + 63) / 64;
   fp.bch_m1 = shift_matrix(g, P, 8L * fp.bch_chunk);
-  fp.bch_m2 = shift_matrix(g, P, 8L * fp.bch_chunk * 32);
   // LDPC: info group gidx (360 bits) with address x lands in parity row a = x mod q with
   // cyclic offset b = x div q (columns c = (b + n) mod 360, since pbits = 360 q)
   const t2_ldpc_code_t *c = find_code(normal, rate);

@@ -28,10 +28,9 @@ struct FecPlan {
   int normal = 0, rate = 0;
   int kbch = 0, nbch = 0, nparity = 0, nldpc = 0, q = 0, pbits = 0;
   bool parity_interleave = true;      // tempu carries parity in [a][c] (interleaved) order
-  int bch_chunk = 0;                  // message bytes per lane chunk (256 lanes)
+  int bch_chunk = 0;                  // message bytes per lane chunk (64 lanes)
   std::vector<uint64_t> bch_tab;      // 256 x 3 words: d(x) * x^P mod g(x)
   std::vector<uint64_t> bch_m1;       // 192 rows x 3 words: v -> v * x^(8*chunk) mod g
-  std::vector<uint64_t> bch_m2;       // 192 rows x 3 words: v -> v * x^(8*chunk*64) mod g
   std::vector<uint16_t> ldpc_rowptr;  // q + 1
   std::vector<uint32_t> ldpc_ent;     // (group << 16) | rotation, grouped by parity row
   std::vector<uint8_t> prbs_bytes;    // BB scrambler, kbch/8 bytes
