@@ -753,6 +753,9 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {
 #ifndef OFDM_SQ16
 #define OFDM_SQ16 8
 #endif
+#ifndef OFDM_PS32
+#define OFDM_PS32 5   // LDS pad shift of the 32K half-transforms (experiment switch: 4)
+#endif
 // exp(+2 pi i k / 32): exact at multiples of pi/2
 __device__ constexpr float kCos32[32] = {
     1.0f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f, 0.70710678118654757f,
@@ -814,11 +817,13 @@ struct Dft {
 // Pass with radix R over units j (Ns = product of earlier radices, Stockham autosort):
 //   in  : A[j + r*NSUB/R]                         (r < R)
 //   out : B[(j/Ns)*Ns*R + j%Ns + r*Ns] after twiddles w^((j%Ns)*r*NSUB/(Ns*R)) and DFT_R
-// Data live in LDS between passes as float2 with one pad slot per 16 (conflict-free for the
-// stride-R writes of the first pass and the unit-stride reads).  The first pass reads the
-// gathered inputs from registers, the last writes its outputs to registers:
-// thread t ends with n = t + NT*m, m = u + (16/R_last)*r.
-__device__ __forceinline__ uint32_t lds_pad(uint32_t a) { return a + (a >> 4); }
+// Data live in LDS between passes as float2 with one pad slot per 2^PS (PS = 4 for the radix-16
+// plans, 5 for the radix-32 32K halves: then the stride-33 first-pass writes, 16 lanes per
+// ds_write_b64 group, and the unit-stride reads, 32 lanes per ds_read_b64 group, are
+// bank-conflict free).  The first pass reads the gathered inputs from registers, the last writes
+// its outputs to registers: thread t ends with n = t + NT*m, m = u + (16/R_last)*r.
+template <int PS>
+__device__ __forceinline__ uint32_t lds_pad(uint32_t a) { return a + (a >> PS); }
 
 // w^i (w = exp(2 pi i / N)) from the two-level LDS table tw = [lo: w^l, l < 128][hi: w^(128 h)]
 __device__ __forceinline__ float2 tw_at(const float2 *tw, uint32_t i) {
@@ -852,13 +857,14 @@ __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32
   }
 }
 
-template <int NSUB, int NT, int R, int NS>
+template <int NSUB, int NT, int R, int NS, int PS>
 struct StockhamPass {
   static constexpr int V = NSUB / NT;       // values per thread
   static constexpr int U = V / R;           // units per thread
+  static constexpr int PAD = 1 << PS;
   // every LDS address below is lds_pad(thread base) + a compile-time offset (immediate field)
-  static_assert((NS == 1 && R % 16 == 0) || NS % 16 == 0, "pad offsets need NS == 1 (16 | R) or 16 | NS");
-  static_assert((NSUB / R) % 16 == 0, "pad offsets need 16 | NSUB / R");
+  static_assert((NS == 1 && R % PAD == 0) || NS % PAD == 0, "pad offsets need NS == 1 (PAD | R) or PAD | NS");
+  static_assert((NSUB / R) % PAD == 0, "pad offsets need PAD | NSUB / R");
   // twiddles + DFT on the thread's U units (v laid out [u][r])
   __device__ __forceinline__ static void compute(float2 *v, const float2 *tw, uint32_t tws, int tid) {
 #pragma unroll
@@ -875,54 +881,56 @@ struct StockhamPass {
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t j = (uint32_t)(tid + NT * u);
-      float2 *b = lds + lds_pad((j / NS) * (NS * R) + (j % NS));
+      float2 *b = lds + lds_pad<PS>((j / NS) * (NS * R) + (j % NS));
 #pragma unroll
-      for (int r = 0; r < R; r++) b[r * NS + ((r * NS) >> 4)] = v[u * R + r];
+      for (int r = 0; r < R; r++) b[r * NS + ((r * NS) >> PS)] = v[u * R + r];
     }
   }
   __device__ __forceinline__ static void load_lds(float2 *v, const float2 *lds, int tid) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const float2 *b = lds + lds_pad((uint32_t)(tid + NT * u));
+      const float2 *b = lds + lds_pad<PS>((uint32_t)(tid + NT * u));
 #pragma unroll
-      for (int r = 0; r < R; r++) v[u * R + r] = b[r * (NSUB / R) * 17 / 16];
+      for (int r = 0; r < R; r++) v[u * R + r] = b[r * (NSUB / R) + ((r * (NSUB / R)) >> PS)];
     }
   }
 };
 
 // remaining passes after the first, radices R2.. ; NS = product of radices already applied
-template <int NSUB, int NT, int NS, int... Rs>
+template <int NSUB, int NT, int PS, int NS, int... Rs>
 struct StockhamTail;
-template <int NSUB, int NT, int NS>
-struct StockhamTail<NSUB, NT, NS> {
-  static constexpr int RLAST = 16;   // unused
+template <int NSUB, int NT, int PS, int NS>
+struct StockhamTail<NSUB, NT, PS, NS> {
   __device__ __forceinline__ static void run(float2 *, float2 *, const float2 *, uint32_t, int) {}
 };
-template <int NSUB, int NT, int NS, int R, int... Rs>
-struct StockhamTail<NSUB, NT, NS, R, Rs...> {
+template <int NSUB, int NT, int PS, int NS, int R, int... Rs>
+struct StockhamTail<NSUB, NT, PS, NS, R, Rs...> {
   __device__ __forceinline__ static void run(float2 *v, float2 *lds, const float2 *tw, uint32_t tws, int tid) {
-    using P = StockhamPass<NSUB, NT, R, NS>;
+    using P = StockhamPass<NSUB, NT, R, NS, PS>;
     P::load_lds(v, lds, tid);
     __syncthreads();
     P::compute(v, tw, tws, tid);
     if (sizeof...(Rs) > 0) {
       P::store_lds(v, lds, tid);
       __syncthreads();
-      StockhamTail<NSUB, NT, NS * R, Rs...>::run(v, lds, tw, tws, tid);
+      StockhamTail<NSUB, NT, PS, NS * R, Rs...>::run(v, lds, tw, tws, tid);
     }
   }
 };
 
 // FFT plans: first pass radix V (values per thread) from LDS or registers, then the tail.
-// RL = radix of the last pass; thread t ends with n = t + NT*(u + (V/RL)*r).
+// RL = radix of the last pass; thread t ends with n = t + NT*(u + (V/RL)*r); PS = LDS pad shift.
 template <int NSUB, int V> struct FftPlan;
-template <> struct FftPlan<1024, 16> { static constexpr int RL = 4; using Tail = StockhamTail<1024, 64, 16, 16, 4>; };
-template <> struct FftPlan<2048, 16> { static constexpr int RL = 8; using Tail = StockhamTail<2048, 128, 16, 16, 8>; };
-template <> struct FftPlan<4096, 16> { static constexpr int RL = 16; using Tail = StockhamTail<4096, 256, 16, 16, 16>; };
-template <> struct FftPlan<8192, 16> { static constexpr int RL = 2; using Tail = StockhamTail<8192, 512, 16, 16, 16, 2>; };
-template <> struct FftPlan<16384, 16> { static constexpr int RL = 4; using Tail = StockhamTail<16384, 1024, 16, 16, 16, 4>; };
-// 32K halves: 512 threads x 32 values, radices 32 x 32 x 16 (three LDS passes)
-template <> struct FftPlan<16384, 32> { static constexpr int RL = 16; using Tail = StockhamTail<16384, 512, 32, 32, 16>; };
+template <> struct FftPlan<1024, 16> { static constexpr int RL = 4, PS = 4; using Tail = StockhamTail<1024, 64, 4, 16, 16, 4>; };
+template <> struct FftPlan<2048, 16> { static constexpr int RL = 8, PS = 4; using Tail = StockhamTail<2048, 128, 4, 16, 16, 8>; };
+template <> struct FftPlan<4096, 16> { static constexpr int RL = 16, PS = 4; using Tail = StockhamTail<4096, 256, 4, 16, 16, 16>; };
+template <> struct FftPlan<8192, 16> { static constexpr int RL = 2, PS = 4; using Tail = StockhamTail<8192, 512, 4, 16, 16, 16, 2>; };
+template <> struct FftPlan<16384, 16> { static constexpr int RL = 4, PS = 4; using Tail = StockhamTail<16384, 1024, 4, 16, 16, 16, 4>; };
+// 32K halves: 512 threads x 32 values, radices 32 x 32 x 16 (three LDS passes), one pad per 32
+template <> struct FftPlan<16384, 32> {
+  static constexpr int RL = 16, PS = OFDM_PS32;
+  using Tail = StockhamTail<16384, 512, OFDM_PS32, 32, 32, 16>;
+};
 
 // experiment switch (product builds: 0): bit 3 = phase timestamps (s_memrealtime, 100 MHz) of
 // each workgroup written over the first samples of its symbol's guard interval (wrong output;
@@ -962,6 +970,7 @@ template <int NSUB, bool SPLIT, int V>
 __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource &src, const float *isinc,
                                          const float2 *tw, uint32_t tws, int tid, int half) {
   constexpr int NT = NSUB / V, N = SPLIT ? 2 * NSUB : NSUB;
+  constexpr int PS = FftPlan<NSUB, V>::PS;
   // first pass (R = V, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
   const int32_t *m = src.map + (SPLIT ? half * NSUB : 0);
   if (src.inv) {
@@ -969,12 +978,12 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     // the data cells from the symbol's slot run (disjoint bins: one phase, no barrier between)
     {
       float4 *z = (float4 *)lds;
-      constexpr int NZ = (NSUB + NSUB / 16) / 2;
+      constexpr int NZ = (NSUB + (NSUB >> PS)) / 2;
       for (int i = tid; i < NZ; i += NT) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
     OFDM_PHASE(1 + 4 * half);
-    const uint32_t dummy = (uint32_t)(NSUB + NSUB / 16) + (uint32_t)(tid & 63);
+    const uint32_t dummy = (uint32_t)(NSUB + (NSUB >> PS)) + (uint32_t)(tid & 63);
     {
       const int4 g = src.agrp[half];
       // direct entries: quads of (bin, value); padding bins (0xFFFF) go to the dummy slot
@@ -984,15 +993,15 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
         const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
         const float4 v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
         const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
-        lds[k0 < (uint32_t)NSUB ? lds_pad(k0) : dummy] = make_float2(v01.x, v01.y);
-        lds[k1 < (uint32_t)NSUB ? lds_pad(k1) : dummy] = make_float2(v01.z, v01.w);
-        lds[k2 < (uint32_t)NSUB ? lds_pad(k2) : dummy] = make_float2(v23.x, v23.y);
-        lds[k3 < (uint32_t)NSUB ? lds_pad(k3) : dummy] = make_float2(v23.z, v23.w);
+        lds[k0 < (uint32_t)NSUB ? lds_pad<PS>(k0) : dummy] = make_float2(v01.x, v01.y);
+        lds[k1 < (uint32_t)NSUB ? lds_pad<PS>(k1) : dummy] = make_float2(v01.z, v01.w);
+        lds[k2 < (uint32_t)NSUB ? lds_pad<PS>(k2) : dummy] = make_float2(v23.x, v23.y);
+        lds[k3 < (uint32_t)NSUB ? lds_pad<PS>(k3) : dummy] = make_float2(v23.z, v23.w);
       }
       // indirect entries (per-frame L1-post cells): through the frame's aux variant
       for (uint32_t i = (uint32_t)tid; i < (uint32_t)g.w; i += NT) {
         const uint32_t e = src.aind[(uint32_t)g.z + i];
-        lds[lds_pad(e & 0x7FFFu)] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
+        lds[lds_pad<PS>(e & 0x7FFFu)] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
       }
     }
     // data cells: the symbol's slots streamed as aligned quads (8-byte loads of 4 index pairs
@@ -1023,13 +1032,13 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
           const uint32_t pr = cw >> (16 * (e & 1));
           const bool in_run = s + (uint32_t)e - r0 < rn;
           const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-          lds[in_run && bin < (uint32_t)NSUB ? lds_pad(bin) : dummy] = v;
+          lds[in_run && bin < (uint32_t)NSUB ? lds_pad<PS>(bin) : dummy] = v;
         }
       }
     }
     __syncthreads();
     OFDM_PHASE(2 + 4 * half);
-    StockhamPass<NSUB, NT, V, 1>::load_lds(v, lds, tid);
+    StockhamPass<NSUB, NT, V, 1, PS>::load_lds(v, lds, tid);
     __syncthreads();
   } else {
 #pragma unroll
@@ -1057,7 +1066,7 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   }
   __builtin_amdgcn_sched_barrier(0);
   Dft<V>::run(v);
-  StockhamPass<NSUB, NT, V, 1>::store_lds(v, lds, tid);
+  StockhamPass<NSUB, NT, V, 1, PS>::store_lds(v, lds, tid);
   __syncthreads();
   FftPlan<NSUB, V>::Tail::run(v, lds, tw, tws, tid);
 }
@@ -1069,7 +1078,8 @@ struct OfdmShape {
   static constexpr int NSUB = SPLIT ? N / 2 : N;
   static constexpr int V = SPLIT ? OFDM_SPLIT_V : 16;                 // values per thread
   static constexpr int NT = NSUB / V;
-  static constexpr int FFT_LDS = (NSUB + NSUB / 16 + 64) * 8;       // padded buffer + 64 dummy slots
+  static constexpr int PS = FftPlan<NSUB, V>::PS;
+  static constexpr int FFT_LDS = (NSUB + (NSUB >> PS) + 64) * 8;    // padded buffer + 64 dummy slots
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
   static constexpr int QAM_OFF = FFT_LDS + (TW_ENTRIES + 32) * 8;    // + w^(NT m), m < 32 (combine)
   static constexpr int LDS_BYTES = QAM_OFF + 256 * 8;                // + constellation re[256], im[256]
