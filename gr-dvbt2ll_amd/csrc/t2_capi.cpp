@@ -414,6 +414,8 @@ struct OfdmTables {
     dev.p1 = p1.as<float2>();
     dev.N = pp.N; dev.G = pp.G; dev.Nsym = pp.Nsym; dev.aux_len = aux_len; dev.t2frames = t2frames;
     dev.norm = pp.normalization;
+    dev.gain = 1.f;
+    dev.fmt = DVBT2LL_IQ_CF32;
     return 0;
   }
 };
@@ -706,13 +708,20 @@ extern "C" int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t 
                                       int64_t first_frame, int nframes, void *iq) {
   if (!h || !ts || !iq || nframes < 1 || nframes > h->max_frames) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
-  size_t iq_bytes = (size_t)nframes * h->iq_per_frame * 8;
+  size_t iq_bytes = (size_t)nframes * h->iq_per_frame * (h->ofdm.dev.fmt == DVBT2LL_IQ_SC16 ? 4 : 8);
   if (h->ts_tmp.ensure((size_t)ts_len + 16) || h->iq_tmp.ensure(iq_bytes)) return DVBT2LL_ENOMEM;
   HIP_TRY(hipMemcpyAsync(h->ts_tmp.p, ts, (size_t)ts_len, hipMemcpyHostToDevice, h->ctx.stream));
   int r = dvbt2ll_chain_run_device(h, h->ts_tmp.p, ts_base, ts_len, first_frame, nframes, h->iq_tmp.p, nullptr);
   if (r) return r;
   HIP_TRY(hipMemcpyAsync(iq, h->iq_tmp.p, iq_bytes, hipMemcpyDeviceToHost, h->ctx.stream));
   HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_set_output(dvbt2ll_chain *h, float gain, int format) {
+  if (!h || !(gain == gain) || (format != DVBT2LL_IQ_CF32 && format != DVBT2LL_IQ_SC16)) return DVBT2LL_EINVAL;
+  h->ofdm.dev.gain = gain;
+  h->ofdm.dev.fmt = format;
   return DVBT2LL_OK;
 }
 

@@ -77,6 +77,8 @@ struct OfdmDev {
   const int4 *agrp;
   int N, G, Nsym, aux_len, t2frames;
   float norm;
+  float gain;               // output gain after the normalisation (1 = pilotgen's own output)
+  int fmt;                  // IQ format: 0 complex64, 1 int16 I/Q (sc16, full scale 32767)
 };
 struct OfdmIO {
   const float2 *data;       // gather mode: aux variants at aux_off, frame f cells at cell_off + f*cell_stride

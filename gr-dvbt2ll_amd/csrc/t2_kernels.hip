@@ -1085,7 +1085,29 @@ struct OfdmShape {
   static constexpr int LDS_BYTES = QAM_OFF + 256 * 8;                // + constellation re[256], im[256]
 };
 
-template <int N>
+// IQ sample writer: the normalised sample times the output gain (the flowgraph's
+// blocks_multiply_const_xx after pilotgen, apps/vv009-4kshort.grc:335-385; 1 = the block's own
+// output), stored as complex64 (FMT 0) or as saturated round-to-nearest-even int16 I/Q at
+// full scale 32767 (FMT 1, the SDR sink's sc16 wire format)
+template <int FMT>
+struct IqOut {
+  char *base;   // sample 0 of this symbol (or of the P1 symbol)
+  float gain;
+  __device__ __forceinline__ void put(uint32_t n, float2 a) const {
+    a.x *= gain;
+    a.y *= gain;
+    if (FMT == 0) {
+      st_nt((float2 *)base, n * 8u, a);
+    } else {
+      const float i = fminf(fmaxf(rintf(a.x * 32767.f), -32768.f), 32767.f);
+      const float q = fminf(fmaxf(rintf(a.y * 32767.f), -32768.f), 32767.f);
+      const uint32_t w = ((uint32_t)(int)i & 0xFFFFu) | ((uint32_t)(int)q << 16);
+      __builtin_nontemporal_store(w, (uint32_t *)(base + n * 4u));
+    }
+  }
+};
+
+template <int N, int FMT>
 __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmIO io) {
   using Sh = OfdmShape<N>;
   constexpr int NSUB = Sh::NSUB, NT = Sh::NT, V = Sh::V, RL = FftPlan<NSUB, V>::RL, UL = V / RL;
@@ -1141,12 +1163,13 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
     }
     return;
   }
+  constexpr int SB = FMT == 0 ? 8 : 4;             // bytes per IQ sample
   if (j == 0) {                                   // P1 symbol (precomputed), pilotgen:2802-2810
-    float2 *p = io.out + (int64_t)f * io.out_stride;
-    for (int i = tid; i < 2048; i += NT) p[i] = d.p1[i];
+    const IqOut<FMT> p{(char *)io.out + (int64_t)f * io.out_stride * SB, d.gain};
+    for (int i = tid; i < 2048; i += NT) p.put((uint32_t)i, d.p1[i]);
   }
   const int G = d.G;
-  float2 *o = io.out + (int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + G);
+  const IqOut<FMT> o{(char *)io.out + ((int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + G)) * SB, d.gain};
   const float nrm = d.norm;
   float2 v[V];
   OFDM_PHASE(0);
@@ -1175,11 +1198,11 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
         float2 t = cmulf(v[i], cmulf(wt, wcomb[uu + UL * r]));
         float2 a = cadd(e[i], t), b = csub(e[i], t);
         a.x *= nrm; a.y *= nrm; b.x *= nrm; b.y *= nrm;
-        st_nt(o, ((uint32_t)G + n) * 8u, a);
+        o.put((uint32_t)G + n, a);
         const uint32_t n2 = n + (uint32_t)NSUB;
-        st_nt(o, ((uint32_t)G + n2) * 8u, b);
-        if (n2 >= (uint32_t)(N - G)) st_nt(o, (n2 - (uint32_t)(N - G)) * 8u, b);
-        if (n >= (uint32_t)(N - G)) st_nt(o, (n - (uint32_t)(N - G)) * 8u, a);
+        o.put((uint32_t)G + n2, b);
+        if (n2 >= (uint32_t)(N - G)) o.put(n2 - (uint32_t)(N - G), b);
+        if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
         if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
   } else {
@@ -1190,15 +1213,15 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
         const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
         float2 a = v[uu * RL + r];
         a.x *= nrm; a.y *= nrm;
-        st_nt(o, ((uint32_t)G + n) * 8u, a);
-        if (n >= (uint32_t)(N - G)) st_nt(o, (n - (uint32_t)(N - G)) * 8u, a);
+        o.put((uint32_t)G + n, a);
+        if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
       }
   }
 #if OFDM_VARIANT & 8
   __syncthreads();
   OFDM_PHASE(8);
   if (tid == 0) {
-    uint32_t *w = (uint32_t *)o;
+    uint32_t *w = (uint32_t *)o.base;
     w[0] = (uint32_t)(g_phase_ts[0] & 0xFFFFFFFFu);
     for (int i = 1; i < 9; i++) w[i] = (uint32_t)(g_phase_ts[i] - g_phase_ts[0]);
     w[9] = __smid();
@@ -1206,17 +1229,22 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
 #endif
 }
 
-template <int N>
-static hipError_t launch_ofdm_t(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
+template <int N, int FMT>
+static hipError_t launch_ofdm_f(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
   using Sh = OfdmShape<N>;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void *)ofdm_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void *)ofdm_kernel<N, FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               Sh::LDS_BYTES);
     attr_set = true;
   }
-  hipLaunchKernelGGL((ofdm_kernel<N>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
+  hipLaunchKernelGGL((ofdm_kernel<N, FMT>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
   return hipGetLastError();
+}
+template <int N>
+static hipError_t launch_ofdm_t(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
+  if (d.fmt == 1 && !io.carriers_only) return launch_ofdm_f<N, 1>(d, io, s);
+  return d.fmt == 0 || io.carriers_only ? launch_ofdm_f<N, 0>(d, io, s) : hipErrorInvalidValue;
 }
 
 hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {

@@ -12,6 +12,9 @@ import numpy as np
 from ._lib import lib, check, _ChainParams, _ChainInfo, _FmParams
 from .configs import ts_for_frames
 
+IQ_CF32 = 0   # DVBT2LL_IQ_CF32
+IQ_SC16 = 1   # DVBT2LL_IQ_SC16
+
 
 class Chain:
     def __init__(self, cfg, max_frames=1, device=0):
@@ -26,6 +29,17 @@ class Chain:
         info = _ChainInfo()
         check(lib().dvbt2ll_chain_get_info(self._h, ctypes.byref(info)), "chain info")
         self.info = {f: getattr(info, f) for f, _ in _ChainInfo._fields_}
+        self.iq_format = IQ_CF32
+
+    def set_output(self, gain=1.0, fmt=IQ_CF32):
+        """output gain (the flowgraph's multiply_const after pilotgen) and IQ format: IQ_CF32
+        (complex64, pilotgen's own output) or IQ_SC16 (int16 I/Q pairs, full scale 32767)"""
+        check(lib().dvbt2ll_chain_set_output(self._h, float(gain), int(fmt)), "chain output")
+        self.iq_format = int(fmt)
+
+    @property
+    def iq_bytes_per_sample(self):
+        return 4 if self.iq_format == IQ_SC16 else 8
 
     @property
     def iq_per_frame(self):
@@ -41,7 +55,10 @@ class Chain:
         if ts is None:
             ts, ts_base = ts_for_frames(self.cfg, first_frame, nframes, seed)
         ts = np.ascontiguousarray(ts, np.uint8)
-        iq = np.zeros(nframes * self.iq_per_frame, np.complex64)
+        if self.iq_format == IQ_SC16:   # interleaved int16 I, Q
+            iq = np.zeros((nframes * self.iq_per_frame, 2), np.int16)
+        else:
+            iq = np.zeros(nframes * self.iq_per_frame, np.complex64)
         check(lib().dvbt2ll_chain_run_host(self._h, ts.ctypes.data_as(ctypes.c_void_p), int(ts_base), len(ts),
                                            int(first_frame), int(nframes), iq.ctypes.data_as(ctypes.c_void_p)),
               "chain run")

@@ -161,13 +161,23 @@ int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info);
 /* ts_dev: device pointer to TS bytes whose first byte is absolute stream offset ts_base
  * (a multiple of 188, at least one packet before the first byte the frames consume so
  * the CRC-8 of the preceding packet can be formed); ts_len bytes valid.  iq_dev receives
- * nframes * iq_samples_per_frame complex64.  stream: hipStream_t (NULL = the handle's
+ * nframes * iq_samples_per_frame samples (complex64, or int16 I/Q pairs after
+ * dvbt2ll_chain_set_output(.., DVBT2LL_IQ_SC16)).  stream: hipStream_t (NULL = the handle's
  * own stream).  Asynchronous on that stream. */
 int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_base, int64_t ts_len,
                              int64_t first_frame, int nframes, void *iq_dev, void *stream);
 /* host buffers, synchronous */
 int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                            int64_t first_frame, int nframes, void *iq);
+/* IQ output of the chain (default: gain 1, DVBT2LL_IQ_CF32 = pilotgenp1insert_cc's own complex64
+ * output).  gain multiplies every normalised sample, as the blocks_multiply_const_xx that follows
+ * pilotgen in apps/vv009-4kshort.grc:335-385 (const 0.2) does.  DVBT2LL_IQ_SC16 stores each sample
+ * as interleaved int16 I, Q = saturate(round-half-even(x * 32767)), the sc16 wire format of the
+ * flowgraph's SDR sink (apps/vv009-4kshort.grc:802-1623): 4 bytes per sample instead of 8.
+ * Applies to later run calls. */
+#define DVBT2LL_IQ_CF32 0
+#define DVBT2LL_IQ_SC16 1
+int dvbt2ll_chain_set_output(dvbt2ll_chain *h, float gain, int format);
 /* per-stage kernel timing with HIP events on the launch stream: enable, then read the
  * accumulated milliseconds and launch counts of stages {0: fec, 1: map, 2: ofdm}. */
 int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable);

@@ -93,3 +93,38 @@ def test_chain_frames_independent(gpu, name):
     for k in (1, 2):
         one = ch.run(k, 1)
         np.testing.assert_array_equal(one.view(np.uint32), batch[k * per:(k + 1) * per].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg3"])
+def test_chain_output_gain_and_sc16(gpu, name):
+    """SURVEY 8(f) rank 1, the step after the path in apps/vv009-4kshort.grc: multiply_const (0.2)
+    and the SDR sink's sc16 wire format, fused into the IQ store.  gain: bit-exactly the float
+    product of pilotgen's output and the constant (two float multiplies, as the two blocks do);
+    sc16: saturate(round-half-even(x * 32767)) of that product, bit-exact.  (The sink's
+    conversion lives in the SDR driver, absent from the reference: parity unpinned there, the
+    rounding rule is this library's documented contract.)"""
+    cfg = CONFIGS[name]
+    ch = dvbt2ll.Chain(cfg, max_frames=2)
+    base = ch.run(0, 2)
+    ch.set_output(0.2, dvbt2ll.IQ_CF32)
+    scaled = ch.run(0, 2)
+    want = (base.view(np.float32) * np.float32(0.2)).astype(np.float32)
+    np.testing.assert_array_equal(scaled.view(np.float32), want)
+    ch.set_output(0.2, dvbt2ll.IQ_SC16)
+    sc = ch.run(0, 2)
+    assert sc.dtype == np.int16 and sc.shape == (2 * ch.iq_per_frame, 2)
+    ref = np.clip(np.rint(want.astype(np.float32) * np.float32(32767)), -32768, 32767).astype(np.int16)
+    np.testing.assert_array_equal(sc.reshape(-1), ref)
+    # saturation: a gain large enough to clip
+    ch.set_output(40.0, dvbt2ll.IQ_SC16)
+    big = ch.run(0, 1).reshape(-1)
+    refb = np.clip(np.rint((base[:ch.iq_per_frame].view(np.float32) * np.float32(40.0)) * np.float32(32767)),
+                   -32768, 32767).astype(np.int16)
+    np.testing.assert_array_equal(big, refb)
+    assert (np.abs(big.astype(np.int32)) == 32767).any() or (big == -32768).any()
+
+
+def test_chain_set_output_rejects_bad_format(gpu):
+    ch = dvbt2ll.Chain(CONFIGS["cfg1"], max_frames=1)
+    with pytest.raises(dvbt2ll.DVBT2Error):
+        ch.set_output(1.0, 7)
