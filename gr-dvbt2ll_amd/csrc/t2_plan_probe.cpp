@@ -92,4 +92,33 @@ int t2probe_chain(const int *p20, const int *pg3, int *info, int32_t *cmap, uint
   }
   return 0;
 }
+
+// the fused chain's compact aux lists (build_aux_lists) over the per-variant aux table the chain
+// uploads (frame aux cells with the 12 pilot values in every variant, as t2_capi.cpp composes
+// it).  Call with null outputs first: sizes = [dbin entries, ind entries, groups, aux_len,
+// t2frames]; auxv (aux_len * t2frames complex) is returned for the checker.
+int t2probe_aux_lists(const int *p20, const int *pg3, int *sizes, uint16_t *dbin, float *dval, uint32_t *ind,
+                      int32_t *grp, float *auxv_out) {
+  FmParams f{p20[0], p20[1], p20[2], p20[3], p20[4], p20[5], p20[6], p20[7], p20[8], p20[9],
+             p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
+  PgParams g{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
+             f.preamble, pg3[0], pg3[1], pg3[2], fft_points(f.fftsize)};
+  FramePlan fp;
+  PilotPlan pp;
+  ChainLayout cl;
+  if (build_frame(f, fp) || build_pilot(g, pp) || build_chain_layout(fp, pp, cl)) return -1;
+  std::vector<cf32> auxv = fp.aux;
+  for (int v = 0; v < fp.t2frames; v++)
+    for (int i = 0; i < 12; i++) auxv[(size_t)v * fp.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
+  AuxLists al;
+  if (build_aux_lists(cl, pp.N, pp.Nsym, auxv, fp.aux_len, fp.t2frames, al)) return -2;
+  sizes[0] = (int)al.dbin.size(); sizes[1] = (int)al.ind.size(); sizes[2] = (int)al.grp.size() / 4;
+  sizes[3] = fp.aux_len; sizes[4] = fp.t2frames;
+  if (dbin) memcpy(dbin, al.dbin.data(), al.dbin.size() * 2);
+  if (dval) memcpy(dval, al.dval.data(), al.dval.size() * 8);
+  if (ind) memcpy(ind, al.ind.data(), al.ind.size() * 4);
+  if (grp) memcpy(grp, al.grp.data(), al.grp.size() * 4);
+  if (auxv_out) memcpy(auxv_out, auxv.data(), (size_t)fp.aux_len * fp.t2frames * 8);
+  return 0;
+}
 }

@@ -133,6 +133,42 @@ def test_chain_cell_layout_matches_oracle(name, over):
         np.testing.assert_array_equal(bins.view(np.uint32), want[j].view(np.uint32), err_msg="symbol %d" % j)
 
 
+@pytest.mark.parametrize("name,over", GRID + [("cfg%d" % i, None) for i in range(1, 6)],
+                         ids=[g[0] for g in GRID] + ["cfg%d" % i for i in range(1, 6)])
+def test_chain_aux_lists_match_cmap(name, over):
+    """the OFDM kernel's non-data bins (t2_kernels.hip sub_ifft, scatter mode): zero fill, then
+    the direct (bin, value) quads and the indirect entries through aux variant v.  For every
+    t2_frame_num variant, every symbol and half, they rebuild exactly the non-data bins the
+    per-bin code row (cmap < 0) gives, and each listed bin is written once."""
+    cfg = CONFIGS[name] if over is None else grid_cfg(over)
+    lay = PP.chain_layout(cfg)
+    al = PP.aux_lists(cfg)
+    N, split = lay["N"], lay["split"]
+    nsub = N // 2 if split else N
+    grp, auxv = al["grp"], al["auxv"]
+    assert grp.shape[0] == 2 * lay["Nsym"] and (grp[:, 0] % 4 == 0).all() and (grp[:, 1] % 4 == 0).all()
+    for v in range(auxv.shape[0]):
+        for j in range(lay["Nsym"]):
+            for h in range(2 if split else 1):
+                code = lay["cmap_stored"][j][h * nsub:(h + 1) * nsub]
+                want = np.where(code < 0, auxv[v][np.clip(-code - 1, 0, None)], 0).astype(np.complex64)
+                got = np.zeros(nsub, np.complex64)
+                hits = np.zeros(nsub, np.int32)
+                d0, dn, i0, ni = grp[2 * j + h]
+                b = al["dbin"][d0:d0 + dn]
+                real = b != 0xFFFF
+                assert (al["dval"][d0:d0 + dn][~real] == 0).all()
+                got[b[real]] = al["dval"][d0:d0 + dn][real]
+                np.add.at(hits, b[real], 1)
+                e = al["ind"][i0:i0 + ni]
+                got[e & 0x7FFF] = auxv[v][(e >> 15) - 1]
+                np.add.at(hits, e & 0x7FFF, 1)
+                assert hits.max(initial=0) <= 1
+                assert (code[hits > 0] < 0).all()
+                np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64),
+                                              err_msg="variant %d symbol %d half %d" % (v, j, h))
+
+
 @pytest.mark.parametrize("name,over", GRID, ids=[g[0] for g in GRID])
 def test_pilot_map_matches_oracle(name, over):
     cfg = grid_cfg(over)
