@@ -547,7 +547,6 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if (!p || !out || p->max_frames < 1) return DVBT2LL_EINVAL;
   *out = nullptr;
   const dvbt2ll_framemapperfint_params &f = p->fm;
-  if (f.inband) return DVBT2LL_EINVAL;   // in-band type B signalling: block API only
   std::unique_ptr<dvbt2ll_chain> h(new (std::nothrow) dvbt2ll_chain());
   if (!h) return DVBT2LL_ENOMEM;
   h->p = *p;
@@ -559,7 +558,8 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if (h->pilot.active != h->frame.M) return DVBT2LL_EINVAL;
   int r = h->ctx.init(device);
   if (r) return r;
-  if ((r = h->fec.init(f.framesize, f.rate, f.constellation, f.inputmode, 0, f.fecblocks, 0))) return r;
+  if ((r = h->fec.init(f.framesize, f.rate, f.constellation, f.inputmode, f.inband, f.fecblocks, p->tsrate)))
+    return r;
   if ((r = h->map.init(f.framesize, f.rate, f.constellation, f.rotation, h->fec.plan))) return r;
   if ((r = upload(h->perm, h->frame.ci_perm)) || (r = upload(h->shift, h->frame.ci_shift))) return r;
   h->map.dev.ci_perm = h->perm.as<int16_t>();
@@ -618,7 +618,9 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   h->cw_stride = ((h->fec.plan.nldpc / 8) + 255) / 256 * 256;
   h->iq_per_frame = (int64_t)pp.Nsym * (pp.N + pp.G) + 2048;
   h->pay = (h->fec.plan.kbch - 80) / 8;
-  h->ts_per_frame = (int64_t)h->frame.F * h->pay;
+  // payload bytes per frame: in-band type B takes 13 bytes of the first BBFRAME of each frame
+  // (bbheader:327-355, fec_block == 0)
+  h->ts_per_frame = (int64_t)h->frame.F * h->pay - (f.inband ? 13 : 0);
   int64_t nblk = (int64_t)h->frame.F * h->max_frames;
   // the OFDM kernel addresses index pairs and aux cells with 32-bit byte offsets
   if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32))

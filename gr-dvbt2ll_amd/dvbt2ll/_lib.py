@@ -42,7 +42,7 @@ class _PgParams(ctypes.Structure):
 
 class _ChainParams(ctypes.Structure):
     _fields_ = [("fm", _FmParams), ("misogroup", ctypes.c_int), ("equalization", ctypes.c_int),
-                ("bandwidth", ctypes.c_int), ("max_frames", ctypes.c_int)]
+                ("bandwidth", ctypes.c_int), ("max_frames", ctypes.c_int), ("tsrate", ctypes.c_int)]
 
 
 class _ChainInfo(ctypes.Structure):

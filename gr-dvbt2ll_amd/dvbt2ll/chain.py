@@ -20,7 +20,8 @@ class Chain:
     def __init__(self, cfg, max_frames=1, device=0):
         self.cfg = cfg
         fm = _FmParams(*[int(v) for v in cfg.fm_args()])
-        p = _ChainParams(fm, int(cfg.misogroup), int(cfg.equalization), int(cfg.bandwidth), int(max_frames))
+        p = _ChainParams(fm, int(cfg.misogroup), int(cfg.equalization), int(cfg.bandwidth), int(max_frames),
+                         int(cfg.tsrate))
         h = ctypes.c_void_p()
         self._h = None
         check(lib().dvbt2ll_chain_create(ctypes.byref(p), int(device), ctypes.byref(h)), "chain create")

@@ -115,15 +115,21 @@ def payload_bytes_per_block(cfg):
     return (KBCH[(cfg.framesize, cfg.rate)] - 80) // 8
 
 
+def payload_pos(J, hem):
+    """stream position of payload byte J (HEM drops every packet's sync byte)"""
+    return 188 * (J // 187) + 1 + J % 187 if hem else J
+
+
 def ts_for_frames(cfg, first_frame, nframes, seed=1):
-    """TS bytes needed to encode T2 frames [first_frame, first_frame+nframes) in
-    INPUTMODE_NORMAL without in-band signalling.  Returns (buffer, base_offset) where
-    base_offset is the absolute stream offset of buffer[0]; the buffer starts one packet
-    before the first packet touched so the CRC-8 of the preceding packet is available."""
-    assert cfg.inputmode == E.INPUTMODE_NORMAL and cfg.inband == E.INBAND_OFF
-    per_frame = cfg.fecblocks * payload_bytes_per_block(cfg)
-    start = first_frame * per_frame
-    end = (first_frame + nframes) * per_frame
+    """TS bytes needed to encode T2 frames [first_frame, first_frame+nframes).  Returns
+    (buffer, base_offset) where base_offset is the absolute stream offset of buffer[0]; the
+    buffer starts one packet before the first packet touched so the CRC-8 of the preceding
+    packet is available (NM).  Payload per frame: F BBFRAME payloads, less the 13 in-band type
+    B bytes of the frame's first BBFRAME when in-band signalling is on (bbheader:327-355)."""
+    hem = cfg.inputmode != E.INPUTMODE_NORMAL
+    per_frame = cfg.fecblocks * payload_bytes_per_block(cfg) - (13 if cfg.inband != E.INBAND_OFF else 0)
+    start = payload_pos(first_frame * per_frame, hem)
+    end = payload_pos((first_frame + nframes) * per_frame, hem) + 1
     p0 = max(0, start // 188 - 1)
     p1 = (end + 187) // 188
     return ts_packets(p0, p1 - p0, seed), p0 * 188

@@ -147,6 +147,7 @@ typedef struct {
   dvbt2ll_framemapperfint_params fm;   /* framesize ... inband */
   int misogroup, equalization, bandwidth;
   int max_frames;                      /* largest nframes per run call */
+  int tsrate;                          /* bbheaderbch tsrate: the in-band type B TS rate field */
 } dvbt2ll_chain_params;
 typedef struct {
   int fec_blocks_per_frame;   /* F */

@@ -66,6 +66,12 @@ GRID = [
                         rate=E.C5_6)),
     ("8k_t2gi_pp4_tr_ext", dict(fftsize=E.FFTSIZE_8K_T2GI, pilotpattern=E.PILOT_PP4, paprmode=E.PAPR_BOTH,
                                 carriermode=E.CARRIERS_EXTENDED, guardinterval=E.GI_19_256, numdatasyms=4)),
+    # SURVEY 8(f) rank 2 through the fused chain: high-efficiency mode, in-band type B signalling
+    ("4k_hem", dict(inputmode=E.INPUTMODE_HIEFF)),
+    ("4k_inband_v131", dict(inband=E.INBAND_ON, version=E.VERSION_131, tsrate=12345678)),
+    ("32k_hem_inband", dict(fftsize=E.FFTSIZE_32K, pilotpattern=E.PILOT_PP4, carriermode=E.CARRIERS_EXTENDED,
+                            guardinterval=E.GI_1_16, numdatasyms=3, framesize=E.FECFRAME_NORMAL, rate=E.C3_5,
+                            inputmode=E.INPUTMODE_HIEFF, inband=E.INBAND_ON, version=E.VERSION_131)),
 ]
 
 
