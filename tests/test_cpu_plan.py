@@ -66,6 +66,11 @@ GRID = [
                         rate=E.C5_6)),
     ("8k_t2gi_pp4_tr_ext", dict(fftsize=E.FFTSIZE_8K_T2GI, pilotpattern=E.PILOT_PP4, paprmode=E.PAPR_BOTH,
                                 carriermode=E.CARRIERS_EXTENDED, guardinterval=E.GI_19_256, numdatasyms=4)),
+    # P1 preamble variants the reference accepts (pilotgen:54-56, 295, 898): T2-Lite SISO / MISO
+    ("8k_t2lite_siso", dict(fftsize=E.FFTSIZE_8K, preamble=E.PREAMBLE_T2_LITE_SISO, pilotpattern=E.PILOT_PP4,
+                            guardinterval=E.GI_1_16, numdatasyms=4)),
+    ("4k_t2lite_miso_tx2", dict(preamble=E.PREAMBLE_T2_LITE_MISO, misogroup=E.MISO_TX2, pilotpattern=E.PILOT_PP3,
+                                guardinterval=E.GI_1_8)),
     # SURVEY 8(f) rank 2 through the fused chain: high-efficiency mode, in-band type B signalling
     ("4k_hem", dict(inputmode=E.INPUTMODE_HIEFF)),
     ("4k_inband_v131", dict(inband=E.INBAND_ON, version=E.VERSION_131, tsrate=12345678)),
