@@ -511,7 +511,10 @@ hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s)
 }
 
 // ============================================================================ map kernel
-constexpr int MAP_THREADS = 512;
+#ifndef MAP_THREADS_EXP
+#define MAP_THREADS_EXP 256
+#endif
+constexpr int MAP_THREADS = MAP_THREADS_EXP;
 constexpr int MAP_LDS_MAX = 160 * 1024 - 256;   // leaves room for static LDS of experiment builds
 // LDS: [LUT 2 KB][cell indices, cs bytes][codeword bytes | cell-interleaved index pairs (2 cs)]
 // (<= 99 KB for QPSK normal, 26 KB for 256-QAM normal)
