@@ -104,6 +104,18 @@ __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
   return hem ? 188 * (J / 187) + 1 + (J % 187) : J;
 }
 
+// parity of (row . a) over GF(2) for a 192-bit matrix row m and the uniform 192-bit vector a:
+// the six 32-bit AND products folded with v_bitop3 ((x & y) ^ z, truth table 0x6A), one popcount
+__device__ __forceinline__ uint32_t row_parity(const uint64_t m[3], uint64_t a0, uint64_t a1, uint64_t a2) {
+  uint32_t acc = (uint32_t)m[0] & (uint32_t)a0;
+  acc = __builtin_amdgcn_bitop3_b32((uint32_t)(m[0] >> 32), (uint32_t)(a0 >> 32), acc, 0x6A);
+  acc = __builtin_amdgcn_bitop3_b32((uint32_t)m[1], (uint32_t)a1, acc, 0x6A);
+  acc = __builtin_amdgcn_bitop3_b32((uint32_t)(m[1] >> 32), (uint32_t)(a1 >> 32), acc, 0x6A);
+  acc = __builtin_amdgcn_bitop3_b32((uint32_t)m[2], (uint32_t)a2, acc, 0x6A);
+  acc = __builtin_amdgcn_bitop3_b32((uint32_t)(m[2] >> 32), (uint32_t)(a2 >> 32), acc, 0x6A);
+  return __builtin_popcount(acc) & 1u;
+}
+
 __device__ __forceinline__ uint8_t get_byte192(const uint64_t w[3], int lowbit) {
   // 8 bits [lowbit, lowbit+8) of a 192-bit value; lowbit multiple of 8
   return (uint8_t)(w[lowbit >> 6] >> (lowbit & 63));
@@ -324,9 +336,9 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
       }
       uint64_t a0 = rd_lane_u64(r0, 0), a1 = rd_lane_u64(r1, 0), a2 = rd_lane_u64(r2, 0);
       for (int l = 1; l < 64; l++) {
-        uint64_t n0 = __ballot(__popcll((m1[0][0] & a0) ^ (m1[0][1] & a1) ^ (m1[0][2] & a2)) & 1);
-        uint64_t n1 = __ballot(__popcll((m1[1][0] & a0) ^ (m1[1][1] & a1) ^ (m1[1][2] & a2)) & 1);
-        uint64_t n2 = __ballot(__popcll((m1[2][0] & a0) ^ (m1[2][1] & a1) ^ (m1[2][2] & a2)) & 1);
+        const uint64_t n0 = __ballot(row_parity(m1[0], a0, a1, a2));
+        const uint64_t n1 = __ballot(row_parity(m1[1], a0, a1, a2));
+        const uint64_t n2 = __ballot(row_parity(m1[2], a0, a1, a2));
         a0 = n0 ^ rd_lane_u64(r0, l);
         a1 = n1 ^ rd_lane_u64(r1, l);
         a2 = n2 ^ rd_lane_u64(r2, l);
