@@ -130,6 +130,49 @@ __device__ __forceinline__ void ldpc_group_word(uint32_t *D, const uint8_t *fram
                       ((uint32_t)gb[(b + 2) % 45] << 8) | (uint32_t)gb[(b + 3) % 45];
 }
 
+// BCH parity of the BBFRAME frame[0..L) on one wave, written MSB (x^(P-1)) first to frame[L..):
+// lane t divides chunk t (64 chunks of C bytes, t2_plan: bch_chunk) by the byte table, then one
+// Horner pass over the lanes with the shift matrix M1 (v -> v x^(8C) mod g) as wave ballots.
+// P is a template parameter so the register geometry (top byte, masks) is compile-time.
+template <int P>
+__device__ __forceinline__ void bch_wave(uint8_t *frame, const uint64_t *btab, const uint64_t *m1g, int L, int C,
+                                         int lane) {
+  const int lo = L - (64 - lane) * C, hi = L - (63 - lane) * C;
+  constexpr int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
+  constexpr uint64_t k1 = P >= 128 ? ~0ull : (1ull << (P - 64)) - 1;
+  constexpr uint64_t k2 = P >= 192 ? ~0ull : P <= 128 ? 0ull : (1ull << (P - 128)) - 1;
+  // per-lane rows of M1, loaded up front (reloaded per block, L1/L2 hits: kept out of the
+  // loop-carried register set)
+  const uint64_t *m1p = m1g;
+  asm volatile("" : "+s"(m1p));
+  uint64_t m1[3][3];
+  for (int s = 0; s < 3; s++)
+    for (int k = 0; k < 3; k++) m1[s][k] = m1p[(lane + 64 * s) * 3 + k];
+  uint64_t r0 = 0, r1 = 0, r2 = 0;
+#pragma unroll 4
+  for (int i = max(lo, 0); i < hi; i++) {
+    const uint32_t top = (uint32_t)(((tw == 0 ? r0 : tw == 1 ? r1 : r2) >> tsft) & 0xFF);
+    const uint32_t idx = top ^ frame[i];
+    r2 = ((r2 << 8) | (r1 >> 56)) & k2;
+    r1 = ((r1 << 8) | (r0 >> 56)) & k1;
+    r0 <<= 8;
+    r0 ^= btab[idx * 3 + 0];
+    r1 ^= btab[idx * 3 + 1];
+    r2 ^= btab[idx * 3 + 2];
+  }
+  uint64_t a0 = rd_lane_u64(r0, 0), a1 = rd_lane_u64(r1, 0), a2 = rd_lane_u64(r2, 0);
+  for (int l = 1; l < 64; l++) {
+    const uint64_t n0 = __ballot(row_parity(m1[0], a0, a1, a2));
+    const uint64_t n1 = __ballot(row_parity(m1[1], a0, a1, a2));
+    const uint64_t n2 = __ballot(row_parity(m1[2], a0, a1, a2));
+    a0 = n0 ^ rd_lane_u64(r0, l);
+    a1 = n1 ^ rd_lane_u64(r1, l);
+    a2 = n2 ^ rd_lane_u64(r2, l);
+  }
+  const uint64_t acc[3] = {a0, a1, a2};
+  if (lane < P / 8) frame[L + lane] = get_byte192(acc, P - 8 - 8 * lane);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -308,44 +351,12 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     //      Meanwhile (chain mode) waves 1..3 lay out the LDPC info groups that hold no BCH parity.
     const int ngroups = d.nbch / 360;
     if (wave == 0) {
-      const int C = d.chunk;
-      const int lo = L - (64 - lane) * C, hi = L - (63 - lane) * C;
-      const int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
-      // per-lane rows of M1, loaded up front (reloaded per block, L1/L2 hits: kept out of the
-      // loop-carried register set)
-      const uint64_t *m1p = d.bch_m1;
-      asm volatile("" : "+s"(m1p));
-      uint64_t m1[3][3];
-      for (int s = 0; s < 3; s++)
-        for (int k = 0; k < 3; k++) m1[s][k] = m1p[(lane + 64 * s) * 3 + k];
-      uint64_t r0 = 0, r1 = 0, r2 = 0;
-#pragma unroll 4
-      for (int i = max(lo, 0); i < hi; i++) {
-        uint32_t top = (uint32_t)(((tw == 0 ? r0 : tw == 1 ? r1 : r2) >> tsft) & 0xFF);
-        uint32_t idx = top ^ frame[i];
-        r2 = (r2 << 8) | (r1 >> 56);
-        r1 = (r1 << 8) | (r0 >> 56);
-        r0 <<= 8;
-        if (P < 192) {
-          if (P <= 128) { r2 = 0; if (P < 128) r1 &= (1ull << (P - 64)) - 1; }
-          else r2 &= (1ull << (P - 128)) - 1;
-        }
-        r0 ^= btab[idx * 3 + 0];
-        r1 ^= btab[idx * 3 + 1];
-        r2 ^= btab[idx * 3 + 2];
+      switch (P) {   // compile-time register geometry per BCH parity length (t = 12, 10, 8; short 12)
+        case 192: bch_wave<192>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
+        case 168: bch_wave<168>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
+        case 160: bch_wave<160>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
+        default: bch_wave<128>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
       }
-      uint64_t a0 = rd_lane_u64(r0, 0), a1 = rd_lane_u64(r1, 0), a2 = rd_lane_u64(r2, 0);
-      for (int l = 1; l < 64; l++) {
-        const uint64_t n0 = __ballot(row_parity(m1[0], a0, a1, a2));
-        const uint64_t n1 = __ballot(row_parity(m1[1], a0, a1, a2));
-        const uint64_t n2 = __ballot(row_parity(m1[2], a0, a1, a2));
-        a0 = n0 ^ rd_lane_u64(r0, l);
-        a1 = n1 ^ rd_lane_u64(r1, l);
-        a2 = n2 ^ rd_lane_u64(r2, l);
-      }
-      // parity bits MSB (x^(P-1)) first, appended after the BBFRAME
-      uint64_t acc[3] = {a0, a1, a2};
-      for (int k = lane; k < P / 8; k += 64) frame[L + k] = get_byte192(acc, P - 8 - 8 * k);
       if (MODE == FEC_TS_TO_TEMPU) {
         // the last info group holds the BCH parity (P < 360): lay it out here, after the parity
         // bytes (same wave; LDS accesses of one wave complete in order)
@@ -511,7 +522,7 @@ hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s)
   if (io.nblocks <= 0) return hipSuccess;
   // the LDS carve is sized for the standard codes: refuse anything larger
   if (d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 52 * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
-      d.P > 192 || d.chunk * 64 < d.kbch / 8)
+      (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.chunk * 64 < d.kbch / 8)
     return hipErrorInvalidValue;
   dim3 grid(fec_grid(io.nblocks)), block(FEC_THREADS);
   switch (mode) {
