@@ -21,8 +21,22 @@ namespace t2 {
 // ============================================================================ helpers
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+#ifndef CMUL_PACKED
+#define CMUL_PACKED 1
+#endif
+typedef float f2v __attribute__((ext_vector_type(2)));
+// complex product as two packed-FP32 ops: t = (ax bx, ax by); (ay (-by) + t.x, ay bx + t.y)
+// (operand swizzles and the negation ride on op_sel / neg_lo instead of extra moves)
 __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
+#if CMUL_PACKED
+  const f2v av = {a.x, a.y}, bv = {b.x, b.y};
+  f2v t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(av), "v"(bv));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(av), "v"(bv), "v"(t));
+  return make_float2(r.x, r.y);
+#else
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+#endif
 }
 
 // uniform (SGPR) base + 32-bit unsigned byte offset: lets the compiler use the global
@@ -534,6 +548,9 @@ hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s)
 }
 
 // ============================================================================ map kernel
+#ifndef MAP_MB
+#define MAP_MB 8   // cells per thread per batched load round (CI and TI loops)
+#endif
 #ifndef MAP_THREADS_EXP
 #define MAP_THREADS_EXP 256
 #endif
@@ -697,7 +714,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
   // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
   // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
-  constexpr int MB = 8;
+  constexpr int MB = MAP_MB;
   for (int j0 = tid; j0 < cs; j0 += MB * MAP_THREADS) {
     int t[MB];
 #pragma unroll
