@@ -572,7 +572,11 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   // OFDM side: aux bins from cmap, data cells streamed per symbol and scattered through inv
   ChainLayout layout;
   if (build_chain_layout(h->frame, h->pilot, layout)) return DVBT2LL_EINVAL;
-  std::vector<uint16_t> inv_pad(layout.inv);
+  // stored bins -> padded LDS slots within their half (the kernel writes them as they are)
+  const int nsub_h = ofdm_split(h->pilot.N) ? h->pilot.N / 2 : h->pilot.N;
+  std::vector<uint16_t> inv_pad(layout.inv.size());
+  for (size_t s = 0; s < layout.inv.size(); s++)
+    inv_pad[s] = (uint16_t)ofdm_padded_bin(h->pilot.N, layout.inv[s] % nsub_h);
   inv_pad.resize(((layout.inv.size() + 7) & ~(size_t)7) + 8, 0);   // the kernel reads aligned quads
   if ((r = upload(h->inv, inv_pad)) || (r = upload(h->sym_d0, layout.sym_d0)) ||
       (r = upload(h->sym_n, layout.sym_n)) || (r = upload(h->sym_n0, layout.sym_n0)))
@@ -599,6 +603,9 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if ((r = h->ofdm.init(pp, layout.cmap, h->frame.aux_len, h->frame.t2frames))) return r;
   AuxLists al;
   if (build_aux_lists(layout, pp.N, pp.Nsym, auxv, h->frame.aux_len, h->frame.t2frames, al)) return DVBT2LL_EINVAL;
+  for (auto &b : al.dbin)
+    if (b != 0xFFFF) b = (uint16_t)ofdm_padded_bin(pp.N, b);
+  for (auto &e : al.ind) e = ofdm_padded_bin(pp.N, e & 0x7FFFu) | (e & ~0x7FFFu);
   al.ind.push_back(0);   // never empty (device pointer)
   al.dbin.resize(al.dbin.size() + 4, 0xFFFF);
   al.dval.resize(al.dval.size() + 4, cf32{0.f, 0.f});

@@ -59,11 +59,18 @@ struct MapIO {
 };
 
 // ---------------------------------------------------------------- OFDM symbols
+// LDS layout of a sub-transform: bin k of the half lives at float2 slot k + (k >> pad shift)
+// (one pad slot per 2^shift; the chain's bin tables are stored already padded)
+constexpr int OFDM_PAD_SHIFT_32K = 5;
+__host__ __device__ inline int ofdm_pad_shift(int N) { return N > 16384 ? OFDM_PAD_SHIFT_32K : 4; }
+__host__ __device__ inline uint32_t ofdm_padded_bin(int N, uint32_t k) {   // k: bin within its half
+  return k + (k >> ofdm_pad_shift(N));
+}
 struct OfdmDev {
   const int32_t *bin_map;   // Nsym x N (stored row order): >= 0 cell index, < 0 aux entry
   // chain (scatter) mode: symbol j's cells are the slots [sym_d0[j], +sym_n[j]), slot s goes to
   // stored bin inv[s]; null -> gather mode (bin_map >= 0 codes are read per bin)
-  const uint16_t *inv;
+  const uint16_t *inv;       // padded bin within the symbol's half (ofdm_padded_bin)
   const int32_t *sym_d0, *sym_n, *sym_n0;   // sym_n0: slots of the even-bin half (split)
   const float2 *twiddle;    // 128 + N/128: two-level table (PilotPlan::twiddle)
   const float *isinc;       // N or null
@@ -71,9 +78,9 @@ struct OfdmDev {
   const float2 *qam;        // scatter mode: 256-entry constellation; cell = (qam[lo].x, qam[hi].y)
   // scatter mode: non-data bins as compact lists per (symbol, half) group 2 j + h (t2_plan.h
   // AuxLists): agrp[g] = {direct offset, direct count, indirect offset, indirect count}
-  const uint16_t *abin;     // direct bins, quads (0xFFFF = padding)
+  const uint16_t *abin;     // direct padded bins, quads (0xFFFF = padding)
   const float2 *aval;       // direct values
-  const uint32_t *aind;     // indirect: bin | code << 15, value at aux abase + code
+  const uint32_t *aind;     // indirect: padded bin | code << 15, value at aux abase + code
   const int4 *agrp;
   int N, G, Nsym, aux_len, t2frames;
   float norm;

@@ -796,9 +796,7 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {
 #ifndef OFDM_SQ16
 #define OFDM_SQ16 8
 #endif
-#ifndef OFDM_PS32
-#define OFDM_PS32 5   // LDS pad shift of the 32K half-transforms (experiment switch: 4)
-#endif
+#define OFDM_PS32 OFDM_PAD_SHIFT_32K   // LDS pad shift of the 32K half-transforms (t2_kernels.h)
 // exp(+2 pi i k / 32): exact at multiples of pi/2
 __device__ constexpr float kCos32[32] = {
     1.0f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f, 0.70710678118654757f,
@@ -1036,22 +1034,21 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
         const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
         const float4 v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
         const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
-        lds[k0 < (uint32_t)NSUB ? lds_pad<PS>(k0) : dummy] = make_float2(v01.x, v01.y);
-        lds[k1 < (uint32_t)NSUB ? lds_pad<PS>(k1) : dummy] = make_float2(v01.z, v01.w);
-        lds[k2 < (uint32_t)NSUB ? lds_pad<PS>(k2) : dummy] = make_float2(v23.x, v23.y);
-        lds[k3 < (uint32_t)NSUB ? lds_pad<PS>(k3) : dummy] = make_float2(v23.z, v23.w);
+        lds[k0 != 0xFFFFu ? k0 : dummy] = make_float2(v01.x, v01.y);   // bins stored padded
+        lds[k1 != 0xFFFFu ? k1 : dummy] = make_float2(v01.z, v01.w);
+        lds[k2 != 0xFFFFu ? k2 : dummy] = make_float2(v23.x, v23.y);
+        lds[k3 != 0xFFFFu ? k3 : dummy] = make_float2(v23.z, v23.w);
       }
       // indirect entries (per-frame L1-post cells): through the frame's aux variant
       for (uint32_t i = (uint32_t)tid; i < (uint32_t)g.w; i += NT) {
         const uint32_t e = src.aind[(uint32_t)g.z + i];
-        lds[lds_pad<PS>(e & 0x7FFFu)] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
+        lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
       }
     }
     // data cells: the symbol's slots streamed as aligned quads (8-byte loads of 4 index pairs
     // and 4 stored bins), looked up in the constellation and written to their bins; slots
     // outside the run (quad edges) go to a per-lane dummy slot past the buffer (branch-free)
     // (split: the run is partitioned, so half h streams only its own slots)
-    const uint32_t lo = SPLIT ? (uint32_t)half * NSUB : 0u;
     const uint32_t r0 = src.d0 + (SPLIT && half ? src.dn0 : 0u);
     const uint32_t rn = SPLIT ? (half ? src.dn - src.dn0 : src.dn0) : src.dn;
     const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
@@ -1071,11 +1068,11 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
 #pragma unroll
         for (int e = 0; e < 4; e++) {
           const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
-          const uint32_t bin = ((bw >> (16 * (e & 1))) & 0xFFFFu) - lo;
+          const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the half
           const uint32_t pr = cw >> (16 * (e & 1));
           const bool in_run = s + (uint32_t)e - r0 < rn;
           const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-          lds[in_run && bin < (uint32_t)NSUB ? lds_pad<PS>(bin) : dummy] = v;
+          lds[in_run ? bin : dummy] = v;
         }
       }
     }
