@@ -38,6 +38,32 @@ __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 #endif
 }
+// a + i b and a - i b as one packed add each (b's halves swapped and one negated by op_sel /
+// neg_lo / neg_hi); a * s for a real s as one packed multiply
+__device__ __forceinline__ float2 cadd_i(float2 a, float2 b) {
+#if CMUL_PACKED
+  const f2v av = {a.x, a.y}, bv = {b.x, b.y};
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(av), "v"(bv));
+  return make_float2(r.x, r.y);
+#else
+  return make_float2(a.x - b.y, a.y + b.x);
+#endif
+}
+__device__ __forceinline__ float2 csub_i(float2 a, float2 b) {
+#if CMUL_PACKED
+  const f2v av = {a.x, a.y}, bv = {b.x, b.y};
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(av), "v"(bv));
+  return make_float2(r.x, r.y);
+#else
+  return make_float2(a.x + b.y, a.y - b.x);
+#endif
+}
+__device__ __forceinline__ float2 cscale(float2 a, float sc) {
+  const f2v r = f2v{a.x, a.y} * f2v{sc, sc};
+  return make_float2(r.x, r.y);
+}
 
 // uniform (SGPR) base + 32-bit unsigned byte offset: lets the compiler use the global
 // saddr form (one VGPR per address instead of a 64-bit VGPR pair per element)
@@ -841,8 +867,12 @@ struct Dft {
 #pragma unroll
         for (int k = 0; k < len / 2; k++) {
           float2 a = x[i + k], b = x[i + k + len / 2], t;
+          if (4 * k == len && k != 0) {                                             // * i
+            x[i + k] = cadd_i(a, b);
+            x[i + k + len / 2] = csub_i(a, b);
+            continue;
+          }
           if (k == 0) t = b;
-          else if (4 * k == len) t = make_float2(-b.y, b.x);                        // * i
           else t = cmulf(b, make_float2(kCos32[k * (32 / len)], kSin32[k * (32 / len)]));
           x[i + k] = cadd(a, t);
           x[i + k + len / 2] = csub(a, t);
@@ -1134,8 +1164,7 @@ struct IqOut {
   char *base;   // sample 0 of this symbol (or of the P1 symbol)
   float gain;
   __device__ __forceinline__ void put(uint32_t n, float2 a) const {
-    a.x *= gain;
-    a.y *= gain;
+    a = cscale(a, gain);
     if (FMT == 0) {
       st_nt((float2 *)base, n * 8u, a);
     } else {
@@ -1237,7 +1266,8 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
         const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
         float2 t = cmulf(v[i], cmulf(wt, wcomb[uu + UL * r]));
         float2 a = cadd(e[i], t), b = csub(e[i], t);
-        a.x *= nrm; a.y *= nrm; b.x *= nrm; b.y *= nrm;
+        a = cscale(a, nrm);
+        b = cscale(b, nrm);
         o.put((uint32_t)G + n, a);
         const uint32_t n2 = n + (uint32_t)NSUB;
         o.put((uint32_t)G + n2, b);
@@ -1252,7 +1282,7 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
       for (int r = 0; r < RL; r++) {
         const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
         float2 a = v[uu * RL + r];
-        a.x *= nrm; a.y *= nrm;
+        a = cscale(a, nrm);
         o.put((uint32_t)G + n, a);
         if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
       }
