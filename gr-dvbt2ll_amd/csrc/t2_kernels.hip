@@ -331,14 +331,18 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     const uint32_t syncb = d.hem ? 0u : 0x47u, syncd = count0 == 0 ? 0u : (uint32_t)(188 - count0) * 8u;
     const uint64_t hw = (0xF0ull << 56) | ((uint64_t)upl << 32) | ((uint64_t)dfl << 16) | ((uint64_t)syncb << 8) |
                         (uint64_t)(syncd >> 8);
-    uint32_t hcrc = 0;   // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270)
-    for (int n = 0; n < 72; n++) {
-      const uint32_t bit = n < 64 ? (uint32_t)(hw >> (63 - n)) & 1u : ((syncd & 0xFFu) >> (71 - n)) & 1u;
-      const uint32_t b = bit ^ (hcrc & 1u);
-      hcrc >>= 1;
-      if (b) hcrc ^= 0xABu;
+    // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270); only
+    // wave 0 writes the header word (bytes 8..11), so only it runs the (scalar) bit loop
+    uint32_t hcrc = 0;
+    if (__builtin_amdgcn_readfirstlane(wave) == 0) {
+      for (int n = 0; n < 72; n++) {
+        const uint32_t bit = n < 64 ? (uint32_t)(hw >> (63 - n)) & 1u : ((syncd & 0xFFu) >> (71 - n)) & 1u;
+        const uint32_t b = bit ^ (hcrc & 1u);
+        hcrc >>= 1;
+        if (b) hcrc ^= 0xABu;
+      }
+      if (d.hem) hcrc ^= 0x80u;
     }
-    if (d.hem) hcrc ^= 0x80u;
     const uint32_t hcrc_rev = __builtin_bitreverse32(hcrc) >> 24;   // register LSB written first
     auto slow_byte = [&](int pidx) -> uint32_t {   // BBFRAME byte pidx outside the bulk payload path
       if (pidx < 8) return (uint32_t)(hw >> (56 - 8 * pidx)) & 0xFFu;
