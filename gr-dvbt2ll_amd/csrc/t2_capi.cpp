@@ -81,14 +81,15 @@ struct DeviceCtx {
 // ---------------------------------------------------------------- FEC tables on device
 struct FecTables {
   FecPlan plan;
-  DevBuf tab, m1, rowptr, ent, prbs, crc8, crcsh;
+  DevBuf hcrc, tab, m1, rowptr, ent, prbs, crc8, crcsh;
   FecDev dev{};
   int init(int framesize, int rate, int constellation, int mode, int inband, int fecblocks, int tsrate) {
     if (build_fec(framesize, rate, constellation, plan)) return DVBT2LL_EINVAL;
     int r;
     if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) ||
         (r = upload(rowptr, plan.ldpc_rowptr)) || (r = upload(ent, plan.ldpc_ent)) ||
-        (r = upload(prbs, plan.prbs_bytes)) || (r = upload(crc8, plan.crc8_tab)) || (r = upload(crcsh, plan.crc8_shift)))
+        (r = upload(prbs, plan.prbs_bytes)) || (r = upload(crc8, plan.crc8_tab)) || (r = upload(crcsh, plan.crc8_shift)) ||
+        (r = upload(hcrc, plan.hcrc_bits)))
       return r;
     dev.bch_tab = tab.as<uint64_t>();
     dev.bch_m1 = m1.as<uint64_t>();
@@ -97,6 +98,7 @@ struct FecTables {
     dev.prbs = prbs.as<uint8_t>();
     dev.crc8_tab = crc8.as<uint8_t>();
     dev.crc8_shift = crcsh.as<uint8_t>();
+    dev.hcrc_bits = hcrc.as<uint8_t>();
     dev.kbch = plan.kbch; dev.nbch = plan.nbch; dev.P = plan.nparity; dev.nldpc = plan.nldpc;
     dev.q = plan.q; dev.nent = (int)plan.ldpc_ent.size(); dev.chunk = plan.bch_chunk;
     dev.parity_il = plan.parity_interleave ? 1 : 0;

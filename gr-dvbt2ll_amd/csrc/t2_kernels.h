@@ -20,6 +20,7 @@ struct FecDev {
   const uint8_t *prbs;          // kbch / 8
   const uint8_t *crc8_tab;      // 256
   const uint8_t *crc8_shift;    // 8 x 256
+  const uint8_t *hcrc_bits;     // 72: BBHEADER CRC-8 contribution of each header bit
   int kbch, nbch, P, nldpc, q, nent, chunk, parity_il;
   int hem, inband, fec_blocks, ts_rate;
 };

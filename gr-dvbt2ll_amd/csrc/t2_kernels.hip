@@ -126,7 +126,8 @@ constexpr int FEC_WG_PER_CU = 6;
 constexpr int SM_FRAME = 0;
 constexpr int SM_SYNC = SM_FRAME + FEC_FRAME_BYTES;          // 48 (<= 36 sync slots)
 constexpr int SM_W = SM_SYNC + 48;                           // 12*4
-constexpr int SM_ENT = SM_W + 48;                            // 648*4
+constexpr int SM_HCRC = SM_W + 48;                           // 72 (+8)
+constexpr int SM_ENT = SM_HCRC + 80;                         // 648*4
 constexpr int SM_BTAB = SM_ENT + FEC_MAX_ENT * 4;            // 256*3*8 = 6144
 constexpr int SM_PHASE = SM_BTAB + 6144;
 constexpr int SM_RAW = SM_PHASE;                             // raw TS bytes of the block (NM)
@@ -223,6 +224,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   uint8_t *frame = smem + SM_FRAME;
   uint8_t *crc8 = smem + SM_CRC8;
   uint8_t *crcsh = smem + SM_CRCSH;
+  uint8_t *hcrc8 = smem + SM_HCRC;
   uint8_t *syncv = smem + SM_SYNC;
   uint64_t *btab = (uint64_t *)(smem + SM_BTAB);
   uint32_t *D = (uint32_t *)(smem + SM_D);
@@ -232,6 +234,8 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   // ---- constant tables into LDS, once: the workgroup then loops over FEC blocks
   for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
   for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
+  if (MODE != FEC_BITS_TO_BITS)
+    for (int i = tid; i < 72; i += FEC_THREADS) hcrc8[i] = d.hcrc_bits[i];
   __syncthreads();
 
   for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
@@ -331,16 +335,20 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     const uint32_t syncb = d.hem ? 0u : 0x47u, syncd = count0 == 0 ? 0u : (uint32_t)(188 - count0) * 8u;
     const uint64_t hw = (0xF0ull << 56) | ((uint64_t)upl << 32) | ((uint64_t)dfl << 16) | ((uint64_t)syncb << 8) |
                         (uint64_t)(syncd >> 8);
-    // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270); only
-    // wave 0 writes the header word (bytes 8..11), so only it runs the (scalar) bit loop
+    // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270): XOR
+    // of the per-bit contributions (t2_plan hcrc_bits), lane n taking header bit n (and 64 + n),
+    // then an XOR reduction over the wave; only wave 0 writes the header word (bytes 8..11)
     uint32_t hcrc = 0;
     if (__builtin_amdgcn_readfirstlane(wave) == 0) {
-      for (int n = 0; n < 72; n++) {
-        const uint32_t bit = n < 64 ? (uint32_t)(hw >> (63 - n)) & 1u : ((syncd & 0xFFu) >> (71 - n)) & 1u;
-        const uint32_t b = bit ^ (hcrc & 1u);
-        hcrc >>= 1;
-        if (b) hcrc ^= 0xABu;
-      }
+      uint32_t v = ((hw >> (63 - lane)) & 1u) ? (uint32_t)hcrc8[lane] : 0u;
+      if (lane < 8 && (((syncd & 0xFFu) >> (7 - lane)) & 1u)) v ^= hcrc8[64 + lane];
+      v ^= __shfl_xor(v, 32);
+      v ^= __shfl_xor(v, 16);
+      v ^= __shfl_xor(v, 8);
+      v ^= __shfl_xor(v, 4);
+      v ^= __shfl_xor(v, 2);
+      v ^= __shfl_xor(v, 1);
+      hcrc = __builtin_amdgcn_readfirstlane(v);
       if (d.hem) hcrc ^= 0x80u;
     }
     const uint32_t hcrc_rev = __builtin_bitreverse32(hcrc) >> 24;   // register LSB written first

@@ -195,6 +195,19 @@ int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
     for (int k = 0; k < 8; k++) r = ((r & 0x80) ? (r << 1) ^ 0xD5u : r << 1) & 0xFFu;
     fp.crc8_tab[i] = (uint8_t)r;
   }
+  // BBHEADER CRC-8 (add_crc8_bits, bbheader:247-270): LSB-first register, polynomial 0xAB, the
+  // 72 header bits MSB first.  Linear with a zero start, so the CRC is the XOR of the
+  // contributions of the set bits (the kernel forms it with one lane per bit)
+  fp.hcrc_bits.assign(72, 0);
+  for (int n = 0; n < 72; n++) {
+    unsigned crc = 0;
+    for (int m = 0; m < 72; m++) {
+      const unsigned b = (m == n ? 1u : 0u) ^ (crc & 1u);
+      crc >>= 1;
+      if (b) crc ^= 0xABu;
+    }
+    fp.hcrc_bits[n] = (uint8_t)crc;
+  }
   fp.crc8_shift.assign(8 * 256, 0);
   for (int k = 0; k < 8; k++) {
     int after = 187 - std::min(24 * k + 24, 187);

@@ -36,6 +36,7 @@ struct FecPlan {
   std::vector<uint8_t> prbs_bytes;    // BB scrambler, kbch/8 bytes
   std::vector<uint8_t> crc8_tab;      // CRC-8 (0xD5) table, 256
   std::vector<uint8_t> crc8_shift;    // 8 x 256: crc after appending k zero bytes (packet CRC combine)
+  std::vector<uint8_t> hcrc_bits;     // 72: BBHEADER CRC-8 contribution of each header bit
 };
 int build_fec(int framesize, int rate, int constellation, FecPlan &fp);
 
