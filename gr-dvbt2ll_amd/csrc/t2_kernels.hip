@@ -1049,9 +1049,10 @@ struct BinSource {
 
 // One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split) by NT = NSUB/V
 // threads, ending with v[u*RL + r] = y[t + NT*(u + (V/RL)*r)].
-template <int NSUB, bool SPLIT, int V>
+// The first sub-transform (half 0) also stores the kernel's constant tables (`stage`) to LDS.
+template <int NSUB, bool SPLIT, int V, class Stage>
 __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource &src, const float *isinc,
-                                         const float2 *tw, uint32_t tws, int tid, int half) {
+                                         const float2 *tw, uint32_t tws, int tid, int half, const Stage &stage) {
   constexpr int NT = NSUB / V, N = SPLIT ? 2 * NSUB : NSUB;
   constexpr int PS = FftPlan<NSUB, V>::PS;
   // first pass (R = V, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
@@ -1064,6 +1065,7 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
       constexpr int NZ = (NSUB + (NSUB >> PS)) / 2;
       for (int i = tid; i < NZ; i += NT) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    if (half == 0) stage.store((unsigned char *)lds, true, tid);
     __syncthreads();
     OFDM_PHASE(1 + 4 * half);
     const uint32_t dummy = (uint32_t)(NSUB + (NSUB >> PS)) + (uint32_t)(tid & 63);
@@ -1123,6 +1125,7 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     StockhamPass<NSUB, NT, V, 1, PS>::load_lds(v, lds, tid);
     __syncthreads();
   } else {
+    if (half == 0) stage.store((unsigned char *)lds, false, tid);
 #pragma unroll
     for (int c0 = 0; c0 < V; c0 += 8) {
       uint32_t off[8];
@@ -1188,6 +1191,53 @@ struct IqOut {
   }
 };
 
+// the OFDM kernel's constant LDS tables (twiddles, split-combine twiddles, constellation),
+// held in registers between load() and store()
+template <int N>
+struct TableStage {
+  using Sh = OfdmShape<N>;
+  static constexpr int NT = Sh::NT, TWK = (Sh::TW_ENTRIES + NT - 1) / NT, QK = (256 + NT - 1) / NT;
+  float2 tw[TWK], q[QK], wc;
+  __device__ __forceinline__ void load(const OfdmDev &d, int tid) {
+#pragma unroll
+    for (int k = 0; k < TWK; k++) {
+      const int i = tid + k * NT;
+      if (i < Sh::TW_ENTRIES) tw[k] = d.twiddle[i];
+    }
+    if (Sh::SPLIT && tid < 32) {
+      const uint32_t e = (uint32_t)(NT * tid);
+      wc = cmulf(d.twiddle[128 + (e >> 7)], d.twiddle[e & 127]);
+    }
+    if (d.inv) {
+#pragma unroll
+      for (int k = 0; k < QK; k++) {
+        const int i = tid + k * NT;
+        if (i < 256) q[k] = d.qam[i];
+      }
+    }
+  }
+  __device__ __forceinline__ void store(unsigned char *smem, bool chain, int tid) const {
+    float2 *twl = (float2 *)(smem + Sh::FFT_LDS);
+#pragma unroll
+    for (int k = 0; k < TWK; k++) {
+      const int i = tid + k * NT;
+      if (i < Sh::TW_ENTRIES) twl[i] = tw[k];
+    }
+    if (Sh::SPLIT && tid < 32) twl[Sh::TW_ENTRIES + tid] = wc;
+    if (chain) {
+      float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + 256;
+#pragma unroll
+      for (int k = 0; k < QK; k++) {
+        const int i = tid + k * NT;
+        if (i < 256) {
+          qre[i] = q[k].x;
+          qim[i] = q[k].y;
+        }
+      }
+    }
+  }
+};
+
 template <int N, int FMT>
 __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmIO io) {
   using Sh = OfdmShape<N>;
@@ -1196,19 +1246,12 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   float2 *lds = (float2 *)smem;
   float2 *twl = (float2 *)(smem + Sh::FFT_LDS);
   const int tid = threadIdx.x;
-  for (int i = tid; i < Sh::TW_ENTRIES; i += NT) twl[i] = d.twiddle[i];   // visible after the first barrier
   float2 *wcomb = twl + Sh::TW_ENTRIES;            // split combine: w^(NT m), uniform across lanes
-  if (Sh::SPLIT && tid < 32) {
-    const uint32_t e = (uint32_t)(NT * tid);
-    wcomb[tid] = cmulf(d.twiddle[128 + (e >> 7)], d.twiddle[e & 127]);
-  }
   float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + 256;
-  if (d.inv)
-    for (int i = tid; i < 256; i += NT) {
-      const float2 c = d.qam[i];
-      qre[i] = c.x;
-      qim[i] = c.y;
-    }
+  // constant tables: loaded into registers here, stored to LDS by the first sub-transform
+  // after its zero fill (the loads' latency overlaps the fill; visible after its barrier)
+  TableStage<N> tabs;
+  tabs.load(d, tid);
   // one workgroup per (symbol, frame); XCD-major so each XCD walks a contiguous run of symbols
   // for all frames of the launch at once and reads each bin_map row from its own L2
   const int u = xcd_major(blockIdx.x, gridDim.x);
@@ -1254,7 +1297,7 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const float nrm = d.norm;
   float2 v[V];
   OFDM_PHASE(0);
-  sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid, 0);
+  sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid, 0, tabs);
   OFDM_PHASE(3);
   if (Sh::SPLIT) {
     // x[n] = E[n] + w^n O[n], x[n + NSUB] = E[n] - w^n O[n], w = exp(2 pi i / N): the even-bin
@@ -1267,7 +1310,7 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
     // arithmetic alive for reuse by the second
     int tid2 = tid;
     asm volatile("" : "+v"(tid2));
-    sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid2, 1);
+    sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid2, 1, tabs);
     OFDM_PHASE(7);
     const float2 wt = tw_at(twl, (uint32_t)tid);   // w^n = w^tid * w^(NT m)
 #pragma unroll
