@@ -10,9 +10,14 @@ Multi-GPU: frame-sharded, one process per GPU (torchrun); each rank encodes its 
 disjoint T2 frames with closed-form stream state, no data-path collective ("weak" scaling).
 Rank 0 prints one JSON line.  Synthetic data: splitmix64 TS packets (dvbt2ll.configs).
 
-Extra fields: roofline (dominant kernel, HIP-event timed on the launch stream inside the
-timed region; traffic from rocprofv3 PMC passes run as child processes BEFORE this process
-touches the GPU) and cpu_baseline (the oracle C restatement, single thread, bounded sample).
+Steps are pipelined: the chain handle holds --slots intermediate buffer sets and step s is
+issued on HIP stream s % slots (dvbt2ll_chain_set_slots), so consecutive steps overlap on the GPU.
+
+Extra fields: roofline (dominant kernel, HIP-event timed on the launch stream inside a serial
+timed pass of the same K steps on one stream -- per-kernel event durations mean nothing under
+cross-stream overlap; traffic from rocprofv3 PMC passes run as child processes BEFORE this
+process touches the GPU), serial_1_stream (that pass's rate) and cpu_baseline (the oracle C
+restatement, single thread, bounded sample).
 """
 import argparse
 import glob
@@ -43,6 +48,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sc16", action="store_true", help="skip the secondary sc16-output timing")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--slots", type=int, default=2,
+                    help="chain buffer slots = HIP streams the steps alternate over (1 = serial)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -160,73 +167,78 @@ def main():
         ts, base = ts_for_frames(cfg, first, B)
         ts_dev.append(torch.from_numpy(ts).cuda())
         ts_meta.append((first, base, len(ts)))
-    iq = torch.empty((B * per, 2), dtype=torch.float32, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
+    # pipelined steps: the handle holds `slots` intermediate buffer sets and step s is issued on
+    # stream s % slots into its own IQ buffer, so one step's kernels fill the CUs the previous
+    # step's kernel tails leave idle (dvbt2ll_chain_set_slots); every step still does all the work
+    S = max(1, args.slots)
+    chain.set_slots(S)
+    iq = [torch.empty((B * per, 2), dtype=torch.float32, device="cuda") for _ in range(S)]
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    torch.cuda.synchronize()
 
-    def step(s):
+    def step(s, serial=False):
         first, base, n = ts_meta[s % R]
-        chain.run_device(ts_dev[s % R].data_ptr(), base, n, first, B, iq.data_ptr(), stream)
+        st = streams[0] if serial else streams[s % S]
+        chain.run_device(ts_dev[s % R].data_ptr(), base, n, first, B, out[0][s % S].data_ptr(), st.cuda_stream)
 
+    out = [iq]
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
     if args.pmc_child:
         for s in range(args.steps):
-            step(s)
+            step(s, serial=True)
         torch.cuda.synchronize()
         return
-    chain.set_timing(True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        step(s)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    stage_ms, launches = chain.timing()
-    chain.set_timing(False)
-    elapsed = t1 - t0
+
+    def timed(serial=False, timing=False):
+        """K steps between barrier + synchronize on both sides; max over ranks"""
+        if timing:
+            chain.set_timing(True)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s in range(args.steps):
+            step(s, serial)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        e = time.perf_counter() - t0
+        st = None
+        if timing:
+            st = chain.timing()
+            chain.set_timing(False)
+        if dist:
+            t = torch.tensor([e], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e = float(t.item())
+        return e, st
+
+    # the headline: pipelined steps over S streams.  Per-kernel HIP-event durations are only
+    # meaningful without cross-stream overlap, so the roofline comes from a serial pass of the same
+    # K steps (all on one stream) right after it
+    if S > 1:
+        elapsed, _ = timed()
+        serial_elapsed, (stage_ms, launches) = timed(serial=True, timing=True)
+    else:
+        elapsed, (stage_ms, launches) = timed(timing=True)
+        serial_elapsed = elapsed
     # secondary line (not `value`): the same chain with the flowgraph's output step fused into the
     # IQ store (x0.2 gain, sc16 wire format: 4 B per sample instead of 8)
     sc16 = None
     if not args.no_sc16:
-        iq16 = torch.empty((B * per, 2), dtype=torch.int16, device="cuda")
+        torch.cuda.synchronize()
+        out[0] = [torch.empty((B * per, 2), dtype=torch.int16, device="cuda") for _ in range(S)]
         chain.set_output(0.2, dvbt2ll.IQ_SC16)
-
-        def step16(s):
-            first, base, n = ts_meta[s % R]
-            chain.run_device(ts_dev[s % R].data_ptr(), base, n, first, B, iq16.data_ptr(), stream)
-
-        step16(0)
-        chain.set_timing(True)
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
-        u0 = time.perf_counter()
-        for s in range(args.steps):
-            step16(s)
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        u1 = time.perf_counter()
-        ms16, n16 = chain.timing()
-        chain.set_timing(False)
+        for s in range(S):
+            step(s)
+        e16, _ = timed()
+        _, (ms16, n16) = timed(serial=True, timing=True)
         chain.set_output(1.0, dvbt2ll.IQ_CF32)
-        del iq16
-        e16 = u1 - u0
-        if dist:
-            t16 = torch.tensor([e16], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t16, op=dist.ReduceOp.MAX)
-            e16 = float(t16.item())
+        out[0] = iq
         sc16 = {"ms_per_step": e16 / args.steps * 1e3, "elapsed": e16,
                 "ofdm_avg_launch_ms": ms16[2] / max(1, n16[2])}
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     frames_total = B * args.steps * world
     samples_total = frames_total * per
     fec_total = frames_total * info["fec_blocks_per_frame"]
@@ -256,8 +268,13 @@ def main():
             "config": {"workload": "%s: TS->IQ full DVB-T2 chain, %d T2 frames per step per GPU "
                                    "(%d FEC blocks, %d IQ samples per frame)"
                                    % (cfg.name, B, info["fec_blocks_per_frame"], per),
-                       "frames_per_step_per_gpu": B, "parallelism": "frame-sharded x%d (replicas, no collective)" % world},
+                       "frames_per_step_per_gpu": B, "slots_streams_per_gpu": S,
+                       "parallelism": "frame-sharded x%d (replicas, no collective)" % world},
             "fec_blocks_per_sec": fec_total / elapsed,
+            "serial_1_stream": {"value": samples_total / serial_elapsed / 1e6,
+                                "ms_per_step": serial_elapsed / args.steps * 1e3,
+                                "note": "same K steps issued on one stream (no cross-step overlap); the "
+                                        "stage timings and roofline come from this pass"},
             "x_realtime": msps * 1e6 / RT_SPS,
             "stages": stages,
             "roofline": roof,

@@ -38,7 +38,12 @@ hipError_t &last_hip_error() {
 struct DevBuf {
   void *p = nullptr;
   size_t n = 0;
-  ~DevBuf() { if (p) (void)hipFree(p); }
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
   int ensure(size_t bytes) {
     if (bytes <= n) return 0;
     if (p) (void)hipFree(p);
@@ -503,8 +508,16 @@ struct dvbt2ll_chain {
   FramePlan frame;
   PilotPlan pilot;
   OfdmTables ofdm;
-  DevBuf cw, aux, pairs, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
+  DevBuf aux, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
   DevBuf abin, aval, aind, agrp;   // non-data bins as compact lists (t2_plan.h AuxLists)
+  // intermediate buffer slots (codewords, index pairs): run calls take them round-robin, so
+  // calls issued on different streams overlap; a slot reused on another stream first waits for
+  // its previous run (slot_done) -- see dvbt2ll_chain_set_slots
+  DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], pairs[DVBT2LL_CHAIN_MAX_SLOTS];
+  hipEvent_t slot_done[DVBT2LL_CHAIN_MAX_SLOTS] = {};
+  hipStream_t slot_stream[DVBT2LL_CHAIN_MAX_SLOTS] = {};
+  bool slot_used[DVBT2LL_CHAIN_MAX_SLOTS] = {};
+  int nslots = 1, next_slot = 0, last_slot = 0;
   int max_frames = 0;
   int64_t pair_stride = 0;   // pairs buffer: frame k's slots at k * pair_stride (multiple of 8)
   int64_t cw_stride = 0;
@@ -539,8 +552,16 @@ struct dvbt2ll_chain {
     evused = 0;
     return 0;
   }
+  int alloc_slot(int k) {
+    if (cw[k].ensure((size_t)frame.F * max_frames * cw_stride) || pairs[k].ensure((size_t)pair_stride * max_frames * 2))
+      return DVBT2LL_ENOMEM;
+    if (!slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
+    return 0;
+  }
   ~dvbt2ll_chain() {
     for (auto &e : evpool)
+      if (e) (void)hipEventDestroy(e);
+    for (auto &e : slot_done)
       if (e) (void)hipEventDestroy(e);
   }
 };
@@ -630,12 +651,10 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   // payload bytes per frame: in-band type B takes 13 bytes of the first BBFRAME of each frame
   // (bbheader:327-355, fec_block == 0)
   h->ts_per_frame = (int64_t)h->frame.F * h->pay - (f.inband ? 13 : 0);
-  int64_t nblk = (int64_t)h->frame.F * h->max_frames;
   // the OFDM kernel addresses index pairs and aux cells with 32-bit byte offsets
   if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32))
     return DVBT2LL_EINVAL;
-  if (h->cw.ensure((size_t)nblk * h->cw_stride) || h->pairs.ensure((size_t)h->pair_stride * h->max_frames * 2))
-    return DVBT2LL_ENOMEM;
+  if ((r = h->alloc_slot(0))) return r;
   if ((r = upload(h->aux, auxv))) return r;
   *out = h.release();
   return DVBT2LL_OK;
@@ -673,6 +692,9 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   int64_t lo = start >= 188 ? (start / 188) * 188 - 188 : 0;
   if (ts_base > lo || ts_base + ts_len < end) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
+  const int slot = h->next_slot;
+  if (h->slot_used[slot] && h->slot_stream[slot] != s) HIP_TRY(hipStreamWaitEvent(s, h->slot_done[slot], 0));
+  DevBuf &cw = h->cw[slot], &pairs = h->pairs[slot];
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   if (h->timing) {
     if (h->evused + 4 > 4096 && h->fold_timing()) return DVBT2LL_EDEVICE;
@@ -685,15 +707,15 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   fio.ts_base = ts_base;
   fio.ts_len = ts_len;
   fio.first_block = first_frame * F;
-  fio.out = h->cw.as<uint8_t>();
+  fio.out = cw.as<uint8_t>();
   fio.cw_stride = h->cw_stride;
   fio.nblocks = F * nframes;
   HIP_TRY(launch_fec(FEC_TS_TO_TEMPU, h->fec.dev, fio, s));
   if (h->timing) HIP_TRY(hipEventRecord(ev[1], s));
   MapIO mio{};
-  mio.in = h->cw.as<uint8_t>();
+  mio.in = cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
-  mio.out_pairs = h->pairs.as<uint16_t>();
+  mio.out_pairs = pairs.as<uint16_t>();
   mio.frame_stride = h->pair_stride;
   mio.nblocks = F * nframes;
   mio.packed_in = 1;
@@ -705,13 +727,37 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   oio.aux_off = 0;
   oio.cell_off = 0;
   oio.cell_stride = (uint32_t)h->pair_stride;
-  oio.pairs = h->pairs.as<uint16_t>();
+  oio.pairs = pairs.as<uint16_t>();
   oio.out = (float2 *)iq_dev;
   oio.out_stride = h->iq_per_frame;
   oio.first_frame = first_frame;
   oio.nframes = nframes;
   HIP_TRY(launch_ofdm(h->ofdm.dev, oio, s));
   if (h->timing) HIP_TRY(hipEventRecord(ev[3], s));
+  HIP_TRY(hipEventRecord(h->slot_done[slot], s));
+  h->slot_used[slot] = true;
+  h->slot_stream[slot] = s;
+  h->last_slot = slot;
+  h->next_slot = (slot + 1) % h->nslots;
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots) {
+  if (!h || nslots < 1 || nslots > DVBT2LL_CHAIN_MAX_SLOTS) return DVBT2LL_EINVAL;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  HIP_TRY(hipDeviceSynchronize());   // no run in flight while slots change
+  for (int k = 0; k < nslots; k++) {
+    int r = h->alloc_slot(k);
+    if (r) return r;
+  }
+  for (int k = nslots; k < DVBT2LL_CHAIN_MAX_SLOTS; k++) {
+    h->cw[k].release();
+    h->pairs[k].release();
+    h->slot_used[k] = false;
+  }
+  h->nslots = nslots;
+  h->next_slot = 0;
+  if (h->last_slot >= nslots) h->last_slot = 0;
   return DVBT2LL_OK;
 }
 
@@ -753,23 +799,24 @@ extern "C" int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *l
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes) {
-  if (!h || !out || bytes < 0 || (size_t)bytes > h->cw.n) return DVBT2LL_EINVAL;
+  if (!h || !out || bytes < 0 || (size_t)bytes > h->cw[h->last_slot].n) return DVBT2LL_EINVAL;
+  const DevBuf &cw = h->cw[h->last_slot];
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, h->cw.p, (size_t)bytes, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out, cw.p, (size_t)bytes, hipMemcpyDeviceToHost));
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_debug_cell_pairs(dvbt2ll_chain *h, void *out, int64_t cells) {
-  if (!h || !out || cells < 0 || (size_t)cells * 2 > h->pairs.n) return DVBT2LL_EINVAL;
+  if (!h || !out || cells < 0 || (size_t)cells * 2 > h->pairs[h->last_slot].n) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(out, h->pairs.p, (size_t)cells * 2, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(out, h->pairs[h->last_slot].p, (size_t)cells * 2, hipMemcpyDeviceToHost));
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells) {
   // frame 0's data cells: index pairs expanded through the constellation exactly as the OFDM
   // kernel does, (lut[lo].re, lut[hi].im)
-  if (!h || !out || cells < 0 || (size_t)cells * 2 > h->pairs.n) return DVBT2LL_EINVAL;
+  if (!h || !out || cells < 0 || (size_t)cells * 2 > h->pairs[h->last_slot].n) return DVBT2LL_EINVAL;
   std::vector<uint16_t> pr((size_t)cells);
   int r = dvbt2ll_chain_debug_cell_pairs(h, pr.data(), cells);
   if (r) return r;

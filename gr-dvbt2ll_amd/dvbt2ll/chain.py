@@ -31,12 +31,19 @@ class Chain:
         check(lib().dvbt2ll_chain_get_info(self._h, ctypes.byref(info)), "chain info")
         self.info = {f: getattr(info, f) for f, _ in _ChainInfo._fields_}
         self.iq_format = IQ_CF32
+        self.nslots = 1
 
     def set_output(self, gain=1.0, fmt=IQ_CF32):
         """output gain (the flowgraph's multiply_const after pilotgen) and IQ format: IQ_CF32
         (complex64, pilotgen's own output) or IQ_SC16 (int16 I/Q pairs, full scale 32767)"""
         check(lib().dvbt2ll_chain_set_output(self._h, float(gain), int(fmt)), "chain output")
         self.iq_format = int(fmt)
+
+    def set_slots(self, nslots):
+        """intermediate buffer slots taken round-robin by run calls: with nslots > 1, calls
+        issued on different streams overlap on the GPU (dvbt2ll_chain_set_slots)"""
+        check(lib().dvbt2ll_chain_set_slots(self._h, int(nslots)), "chain slots")
+        self.nslots = int(nslots)
 
     @property
     def iq_bytes_per_sample(self):

@@ -167,6 +167,15 @@ int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info);
  * own stream).  Asynchronous on that stream. */
 int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_base, int64_t ts_len,
                              int64_t first_frame, int nframes, void *iq_dev, void *stream);
+/* intermediate buffer slots (packed codewords + cell index pairs, ~310 MB per slot for 64 cfg3
+ * frames): run calls take the slots round-robin, so calls issued on different streams run
+ * concurrently on the GPU (one call's kernels fill the CUs the other call's kernel tails leave
+ * idle).  A slot reused on a different stream than its previous run first waits for that run
+ * (hipStreamWaitEvent), so any call order is safe.  1 <= nslots <= DVBT2LL_CHAIN_MAX_SLOTS;
+ * synchronises the device.  Default 1.  Not part of the reference (GNU Radio runs one
+ * general_work per block at a time): the pipelined form of the same calls. */
+#define DVBT2LL_CHAIN_MAX_SLOTS 4
+int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots);
 /* host buffers, synchronous */
 int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                            int64_t first_frame, int nframes, void *iq);

@@ -10,12 +10,12 @@ rc=$?
 tail -25 gpurun_out/tests_$TAG.log
 echo "STEP tests EXIT $rc"
 [ $rc = 0 ] || exit $rc
-timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-pmc --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
+timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-pmc --no-cpu-baseline $BENCH_ARGS > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 rc=$?
 echo "STEP bench EXIT $rc"
 [ $rc = 0 ] || { tail -5 gpurun_out/bench_$TAG.err; exit $rc; }
 python - <<EOF
 import json; d = json.load(open("gpurun_out/bench_$TAG.json"))
-print("value %.0f Msps  ms/step %.3f" % (d["value"], d["ms_per_step"]))
+print("value %.0f Msps  ms/step %.3f  serial %.0f  sc16 %.0f" % (d["value"], d["ms_per_step"], d["serial_1_stream"]["value"], d.get("iq_sc16_x0.2", {}).get("value", 0)))
 for k, v in d["stages"].items(): print("  %-5s %.4f ms  %.0f GB/s" % (k, v["avg_launch_ms"], v["achieved_GBs"]))
 EOF
