@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sc16", action="store_true", help="skip the secondary sc16-output timing")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--shard", choices=("frames", "streams"), default="frames",
+                    help="frames: one TS stream, disjoint frame ranges per rank; streams: an independent "
+                         "TS stream per rank (seed = rank + 1), SURVEY 8(e)'s two modes")
     ap.add_argument("--slots", type=int, default=2,
                     help="chain buffer slots = HIP streams the steps alternate over (1 = serial)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -104,15 +107,16 @@ def pmc_passes(args):
     return {"fetch_bytes": fetch, "write_bytes": write, "total": fetch + write}, None
 
 
-def cpu_baseline(cfg, seconds):
-    """Oracle C restatement (single thread) over a bounded sample of the same workload."""
+def _oracle_stream(cfg, seconds, max_frames, seed=1):
+    """one oracle replica: the five blocks over consecutive T2 frames of one TS stream until the
+    time or frame bound; returns (frames, IQ samples, seconds)"""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib as O
     from dvbt2ll.configs import ts_for_frames
     F = cfg.fecblocks
     bb = O.BB(*cfg.bb_args()); ld = O.LDPC(cfg.framesize, cfg.rate); im = O.IM(*cfg.im_args())
     fm = O.FM(*cfg.fm_args()); pg = O.PG(*cfg.pg_args())
-    ts, _ = ts_for_frames(cfg, 0, 64)
+    ts, _ = ts_for_frames(cfg, 0, max_frames, seed)
     off, frames, samples = 0, 0, 0
     t0 = time.perf_counter()
     while True:
@@ -123,8 +127,30 @@ def cpu_baseline(cfg, seconds):
         frames += 1
         samples += len(iq)
         dt = time.perf_counter() - t0
-        if dt >= seconds or frames >= 64:
-            break
+        if dt >= seconds or frames >= max_frames:
+            return frames, samples, dt
+
+
+def cpu_host_replicas(cfg, seconds, threads):
+    """SURVEY 8(d) whole-host figure: `threads` independent oracle stream replicas (one per host
+    thread; the oracle's C calls release the GIL), aggregate IQ rate over a common window"""
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        res = list(ex.map(lambda k: _oracle_stream(cfg, seconds, 64, seed=k + 1), range(threads)))
+        dt = time.perf_counter() - t0
+    frames = sum(r[0] for r in res)
+    rate = sum(r[1] / r[2] for r in res)     # concurrent replicas, each timed over its own frames
+    return {"value": rate / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": "%d independent %s streams, %d T2 frames in total through the oracle C restatement "
+                      "(one replica per thread, each timed over its own frames), %.1f s wall" % (threads, cfg.name, frames, dt),
+            "fec_blocks_per_sec": sum(r[0] / r[2] for r in res) * cfg.fecblocks}
+
+
+def cpu_baseline(cfg, seconds):
+    """Oracle C restatement (single thread) over a bounded sample of the same workload."""
+    frames, samples, dt = _oracle_stream(cfg, seconds, 64)
+    F = cfg.fecblocks
     return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
             "sample": "%d %s T2 frames (%d FEC blocks) through the oracle C restatement of all five "
                       "blocks, one thread, own radix-2 float IFFT (FFTW unavailable), %.1f s"
@@ -161,10 +187,13 @@ def main():
     from dvbt2ll.distributed import frame_range
     R = 2
     rank_first, _ = frame_range(world * R * B, rank, world)
+    seed = 1
+    if args.shard == "streams":
+        rank_first, seed = 0, rank + 1
     ts_dev, ts_meta = [], []
     for r in range(R):
         first = rank_first + r * B
-        ts, base = ts_for_frames(cfg, first, B)
+        ts, base = ts_for_frames(cfg, first, B, seed)
         ts_dev.append(torch.from_numpy(ts).cuda())
         ts_meta.append((first, base, len(ts)))
     # pipelined steps: the handle holds `slots` intermediate buffer sets and step s is issued on
@@ -269,7 +298,8 @@ def main():
                                    "(%d FEC blocks, %d IQ samples per frame)"
                                    % (cfg.name, B, info["fec_blocks_per_frame"], per),
                        "frames_per_step_per_gpu": B, "slots_streams_per_gpu": S,
-                       "parallelism": "frame-sharded x%d (replicas, no collective)" % world},
+                       "parallelism": "%s x%d (no data-path collective)"
+                                      % ("frame-sharded" if args.shard == "frames" else "independent streams", world)},
             "fec_blocks_per_sec": fec_total / elapsed,
             "serial_1_stream": {"value": samples_total / serial_elapsed / 1e6,
                                 "ms_per_step": serial_elapsed / args.steps * 1e3,
@@ -287,6 +317,9 @@ def main():
                         "multiply_const and SDR wire format fused into the IQ store); not `value`"}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+            # the box's CPU share is 16 threads (os.cpu_count() reports the whole machine)
+            threads = min(16, os.cpu_count() or 1)
+            out["cpu_baseline"]["whole_host"] = cpu_host_replicas(cfg, args.cpu_seconds / 2, threads)
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
