@@ -315,7 +315,7 @@ def main():
                 "ms_per_step": sc16["ms_per_step"], "ofdm_avg_launch_ms": sc16["ofdm_avg_launch_ms"],
                 "note": "secondary: same chain, output gain 0.2 + int16 I/Q store (the flowgraph's "
                         "multiply_const and SDR wire format fused into the IQ store); not `value`"}
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only (host cores are shared)
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
             # the box's CPU share is 16 threads (os.cpu_count() reports the whole machine)
             threads = min(16, os.cpu_count() or 1)
