@@ -114,6 +114,9 @@ __shared__ uint64_t g_fec_ts[16];
 #else
 #define FEC_PHASE(i) do { } while (0)
 #endif
+#ifndef FEC_BCH_PRIO
+#define FEC_BCH_PRIO 1   // wave priority (s_setprio) of the BCH wave while it runs (0: off)
+#endif
 constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
 constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 233280 / 360)
@@ -403,6 +406,9 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     //      Meanwhile (chain mode) waves 1..3 lay out the LDPC info groups that hold no BCH parity.
     const int ngroups = d.nbch / 360;
     if (wave == 0) {
+#if FEC_BCH_PRIO
+      __builtin_amdgcn_s_setprio(FEC_BCH_PRIO);   // the BCH wave is the block's critical path
+#endif
       switch (P) {   // compile-time register geometry per BCH parity length (t = 12, 10, 8; short 12)
         case 192: bch_wave<192>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
         case 168: bch_wave<168>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
@@ -417,6 +423,9 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane < FEC_DW) ldpc_group_word(D, frame, ngroups - 1, lane);
       }
+#if FEC_BCH_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     } else if (MODE == FEC_TS_TO_TEMPU) {
       for (int it = tid - 64; it < (ngroups - 1) * FEC_DW; it += FEC_THREADS - 64) {
         const int g = it / FEC_DW;
