@@ -500,6 +500,21 @@ extern "C" int dvbt2ll_pilotgenp1insert_debug_carriers(dvbt2ll_pilotgenp1insert 
 extern "C" void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h) { delete h; }
 
 // ============================================================================ chain
+// one instantiated hipGraph of the chain's three kernels (fec -> map -> ofdm), per (nframes,
+// IQ format): captured once from the ordinary launch path, then every call rewrites the three
+// kernel nodes' arguments (hipGraphExecKernelNodeSetParams) and launches the graph
+struct ChainGraph {
+  int nframes = 0, fmt = -1;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipGraphNode_t node[3] = {};
+  hipKernelNodeParams base[3] = {};
+  ~ChainGraph() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+  }
+};
+
 struct dvbt2ll_chain {
   DeviceCtx ctx;
   dvbt2ll_chain_params p{};
@@ -518,6 +533,10 @@ struct dvbt2ll_chain {
   hipStream_t slot_stream[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   bool slot_used[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   int nslots = 1, next_slot = 0, last_slot = 0;
+  // hipGraph mode (dvbt2ll_chain_set_graph)
+  bool use_graph = false;
+  hipStream_t cap_stream = nullptr;
+  std::vector<std::unique_ptr<ChainGraph>> graphs;
   int max_frames = 0;
   int64_t pair_stride = 0;   // pairs buffer: frame k's slots at k * pair_stride (multiple of 8)
   int64_t cw_stride = 0;
@@ -552,6 +571,83 @@ struct dvbt2ll_chain {
     evused = 0;
     return 0;
   }
+  // capture the three launches once per (nframes, format) on a private stream, then per call
+  // rewrite the kernel nodes' arguments and launch the instantiated graph on s
+  int graph_launch(const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, hipStream_t s) {
+    ChainGraph *g = nullptr;
+    for (auto &c : graphs)
+      if (c->nframes == nframes && c->fmt == ofdm.dev.fmt) g = c.get();
+    if (!g) {
+      if (!cap_stream) HIP_TRY(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
+      std::unique_ptr<ChainGraph> c(new (std::nothrow) ChainGraph());
+      if (!c) return DVBT2LL_ENOMEM;
+      c->nframes = nframes;
+      c->fmt = ofdm.dev.fmt;
+      HIP_TRY(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
+      hipError_t e1 = launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, cap_stream);
+      hipError_t e2 = e1 == hipSuccess ? launch_map(map.dev, mio, cap_stream) : e1;
+      hipError_t e3 = e2 == hipSuccess ? launch_ofdm(ofdm.dev, oio, cap_stream) : e2;
+      hipError_t ec = hipStreamEndCapture(cap_stream, &c->graph);
+      HIP_TRY(e3);
+      HIP_TRY(ec);
+      // the kernel nodes in dependency order: a linear chain of exactly three
+      size_t n = 0;
+      HIP_TRY(hipGraphGetNodes(c->graph, nullptr, &n));
+      std::vector<hipGraphNode_t> nodes(n);
+      HIP_TRY(hipGraphGetNodes(c->graph, nodes.data(), &n));
+      std::vector<hipGraphNode_t> kn;
+      for (auto nd : nodes) {
+        hipGraphNodeType t;
+        HIP_TRY(hipGraphNodeGetType(nd, &t));
+        if (t == hipGraphNodeTypeKernel) kn.push_back(nd);
+      }
+      if (kn.size() != 3) return DVBT2LL_EDEVICE;
+      auto ndeps = [&](hipGraphNode_t nd, size_t &k) -> int {
+        HIP_TRY(hipGraphNodeGetDependencies(nd, nullptr, &k));
+        return 0;
+      };
+      // order: the root (no dependencies), then the node depending on it, then the last
+      hipGraphNode_t prev = nullptr;
+      for (int k = 0; k < 3; k++) {
+        for (auto nd : kn) {
+          size_t nd_n = 0;
+          if (ndeps(nd, nd_n)) return DVBT2LL_EDEVICE;
+          bool ok = false;
+          if (k == 0) {
+            ok = nd_n == 0;
+          } else if (nd_n == 1) {
+            hipGraphNode_t dep = nullptr;
+            size_t one = 1;
+            HIP_TRY(hipGraphNodeGetDependencies(nd, &dep, &one));
+            ok = dep == prev;
+          }
+          if (ok) { c->node[k] = nd; break; }
+        }
+        if (!c->node[k]) return DVBT2LL_EDEVICE;
+        prev = c->node[k];
+        HIP_TRY(hipGraphKernelNodeGetParams(c->node[k], &c->base[k]));
+      }
+      HIP_TRY(hipGraphInstantiate(&c->exec, c->graph, nullptr, nullptr, 0));
+      g = c.get();
+      graphs.push_back(std::move(c));
+    }
+    FecDev fd = fec.dev;
+    MapDev md = map.dev;
+    OfdmDev od = ofdm.dev;
+    FecIO fi = fio;
+    MapIO mi = mio;
+    OfdmIO oi = oio;
+    void *a0[2] = {&fd, &fi}, *a1[2] = {&md, &mi}, *a2[2] = {&od, &oi};
+    void **args[3] = {a0, a1, a2};
+    for (int k = 0; k < 3; k++) {
+      hipKernelNodeParams p = g->base[k];
+      p.kernelParams = args[k];
+      p.extra = nullptr;
+      HIP_TRY(hipGraphExecKernelNodeSetParams(g->exec, g->node[k], &p));
+    }
+    HIP_TRY(hipGraphLaunch(g->exec, s));
+    return 0;
+  }
   int alloc_slot(int k) {
     if (cw[k].ensure((size_t)frame.F * max_frames * cw_stride) || pairs[k].ensure((size_t)pair_stride * max_frames * 2))
       return DVBT2LL_ENOMEM;
@@ -559,6 +655,8 @@ struct dvbt2ll_chain {
     return 0;
   }
   ~dvbt2ll_chain() {
+    graphs.clear();
+    if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (auto &e : evpool)
       if (e) (void)hipEventDestroy(e);
     for (auto &e : slot_done)
@@ -696,13 +794,15 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   if (h->slot_used[slot] && h->slot_stream[slot] != s) HIP_TRY(hipStreamWaitEvent(s, h->slot_done[slot], 0));
   DevBuf &cw = h->cw[slot], &pairs = h->pairs[slot];
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  if (h->timing) {
+  if (h->timing && !h->use_graph) {   // per-stage events only on the direct launch path
     if (h->evused + 4 > 4096 && h->fold_timing()) return DVBT2LL_EDEVICE;
     for (auto &e : ev)
       if (!(e = h->next_event())) return DVBT2LL_EDEVICE;
     HIP_TRY(hipEventRecord(ev[0], s));
   }
   FecIO fio{};
+  MapIO mio{};
+  OfdmIO oio{};
   fio.in = (const uint8_t *)ts_dev;
   fio.ts_base = ts_base;
   fio.ts_len = ts_len;
@@ -710,9 +810,6 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   fio.out = cw.as<uint8_t>();
   fio.cw_stride = h->cw_stride;
   fio.nblocks = F * nframes;
-  HIP_TRY(launch_fec(FEC_TS_TO_TEMPU, h->fec.dev, fio, s));
-  if (h->timing) HIP_TRY(hipEventRecord(ev[1], s));
-  MapIO mio{};
   mio.in = cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
   mio.out_pairs = pairs.as<uint16_t>();
@@ -720,9 +817,6 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   mio.nblocks = F * nframes;
   mio.packed_in = 1;
   mio.apply_ci = 1;
-  HIP_TRY(launch_map(h->map.dev, mio, s));
-  if (h->timing) HIP_TRY(hipEventRecord(ev[2], s));
-  OfdmIO oio{};
   oio.data = h->aux.as<float2>();
   oio.aux_off = 0;
   oio.cell_off = 0;
@@ -732,13 +826,28 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   oio.out_stride = h->iq_per_frame;
   oio.first_frame = first_frame;
   oio.nframes = nframes;
-  HIP_TRY(launch_ofdm(h->ofdm.dev, oio, s));
-  if (h->timing) HIP_TRY(hipEventRecord(ev[3], s));
+  if (h->use_graph) {
+    int r = h->graph_launch(fio, mio, oio, nframes, s);
+    if (r) return r;
+  } else {
+    HIP_TRY(launch_fec(FEC_TS_TO_TEMPU, h->fec.dev, fio, s));
+    if (h->timing) HIP_TRY(hipEventRecord(ev[1], s));
+    HIP_TRY(launch_map(h->map.dev, mio, s));
+    if (h->timing) HIP_TRY(hipEventRecord(ev[2], s));
+    HIP_TRY(launch_ofdm(h->ofdm.dev, oio, s));
+    if (h->timing) HIP_TRY(hipEventRecord(ev[3], s));
+  }
   HIP_TRY(hipEventRecord(h->slot_done[slot], s));
   h->slot_used[slot] = true;
   h->slot_stream[slot] = s;
   h->last_slot = slot;
   h->next_slot = (slot + 1) % h->nslots;
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_set_graph(dvbt2ll_chain *h, int enable) {
+  if (!h) return DVBT2LL_EINVAL;
+  h->use_graph = enable != 0;
   return DVBT2LL_OK;
 }
 

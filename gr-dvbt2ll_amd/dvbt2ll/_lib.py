@@ -64,7 +64,7 @@ for _b in BLOCKS:
                 ("create", "output_multiple", "forecast", "general_work", "destroy")]
 EXPORTS += ["dvbt2ll_framemapperfint_stream_items", "dvbt2ll_pilotgenp1insert_active_items",
             "dvbt2ll_pilotgenp1insert_debug_carriers"]
-EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_host", "set_output", "set_slots", "set_timing",
+EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_host", "set_output", "set_slots", "set_graph", "set_timing",
                                            "get_timing", "debug_codewords", "debug_cell_pairs", "debug_cells",
                                            "synchronize",
                                            "destroy")]
@@ -98,6 +98,7 @@ def lib():
     L.dvbt2ll_chain_run_host.argtypes = [vp, vp, i64, i64, i64, ci, vp]
     L.dvbt2ll_chain_set_output.argtypes = [vp, ctypes.c_float, ci]
     L.dvbt2ll_chain_set_slots.argtypes = [vp, ci]
+    L.dvbt2ll_chain_set_graph.argtypes = [vp, ci]
     L.dvbt2ll_chain_set_timing.argtypes = [vp, ci]
     L.dvbt2ll_chain_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), ci]
     L.dvbt2ll_chain_debug_codewords.argtypes = [vp, vp, i64]

@@ -45,6 +45,10 @@ class Chain:
         check(lib().dvbt2ll_chain_set_slots(self._h, int(nslots)), "chain slots")
         self.nslots = int(nslots)
 
+    def set_graph(self, enable=True):
+        """launch the three kernels as one hipGraph per call (dvbt2ll_chain_set_graph)"""
+        check(lib().dvbt2ll_chain_set_graph(self._h, int(bool(enable))), "chain graph")
+
     @property
     def iq_bytes_per_sample(self):
         return 4 if self.iq_format == IQ_SC16 else 8

@@ -176,6 +176,13 @@ int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_ba
  * general_work per block at a time): the pipelined form of the same calls. */
 #define DVBT2LL_CHAIN_MAX_SLOTS 4
 int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots);
+/* hipGraph launch mode: run_device issues the three kernels as one instantiated hipGraph,
+ * captured on first use for each (nframes, IQ format) and re-armed per call by rewriting the
+ * kernel nodes' arguments (hipGraphExecKernelNodeSetParams), then one hipGraphLaunch.  For
+ * small per-call batches (one T2 frame per call, as GNU Radio's scheduler calls a block);
+ * output identical to the direct launches.  Per-stage timing events are skipped in this mode.
+ * Default off. */
+int dvbt2ll_chain_set_graph(dvbt2ll_chain *h, int enable);
 /* host buffers, synchronous */
 int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                            int64_t first_frame, int nframes, void *iq);

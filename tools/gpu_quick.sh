@@ -18,4 +18,5 @@ python - <<EOF
 import json; d = json.load(open("gpurun_out/bench_$TAG.json"))
 print("value %.0f Msps  ms/step %.3f  serial %.0f  sc16 %.0f" % (d["value"], d["ms_per_step"], d["serial_1_stream"]["value"], d.get("iq_sc16_x0.2", {}).get("value", 0)))
 for k, v in d["stages"].items(): print("  %-5s %.4f ms  %.0f GB/s" % (k, v["avg_launch_ms"], v["achieved_GBs"]))
+print("latency", d["latency_1_frame"])
 EOF
