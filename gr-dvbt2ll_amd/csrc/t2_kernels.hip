@@ -148,6 +148,22 @@ __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
   return hem ? 188 * (J / 187) + 1 + (J % 187) : J;
 }
 
+// inclusive prefix XOR over the 64 lanes of a wave with DPP moves (VALU latency, no LDS
+// crossbar): row_shr 1, 2, 4, 8 within each 16-lane row, then row_bcast:15 into rows 1 and 3 and
+// row_bcast:31 into rows 2 and 3 (GFX9-family DPP)
+#ifndef FEC_DPP_SCAN
+#define FEC_DPP_SCAN 1
+#endif
+__device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return v;
+}
+
 // parity of (row . a) over GF(2) for a 192-bit matrix row m and the uniform 192-bit vector a:
 // the six 32-bit AND products folded with v_bitop3 ((x & y) ^ z, truth table 0x6A), one popcount
 __device__ __forceinline__ uint32_t row_parity(const uint64_t m[3], uint64_t a0, uint64_t a1, uint64_t a2) {
@@ -482,14 +498,18 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     for (int a0 = 0; a0 < q; a0 += 64) {
       const int a = a0 + lane;
       uint32_t v = a < q ? cur[a * 12 + col] : 0u;
+#if FEC_DPP_SCAN
+      v = wave_prefix_xor(v);
+#else
 #pragma unroll
       for (int dd = 1; dd < 64; dd <<= 1) {
         uint32_t t = __shfl_up(v, dd);
         if (lane >= dd) v ^= t;
       }
+#endif
       v ^= carry;
       if (a < q) cur[a * 12 + col] = v;
-      carry = __shfl(v, 63);
+      carry = rd_lane_u32(v, 63);
     }
   }
   __syncthreads();
