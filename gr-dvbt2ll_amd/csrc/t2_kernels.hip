@@ -339,10 +339,11 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
             if (i < n) c = crc8[by[i] ^ c];
           part = crcsh[k * 256 + c];
         }
+        // XOR of the 8 lanes' parts into lane k == 0: DPP quad_perm [1,0,3,2], [2,3,0,1], row_shl:4
         uint32_t v = part;
-        v ^= __shfl_xor(v, 1);
-        v ^= __shfl_xor(v, 2);
-        v ^= __shfl_xor(v, 4);
+        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);
+        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);
+        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, true);
         if (k == 0 && m < nslots) syncv[m] = active ? (uint8_t)v : 0;
       }
       __syncthreads();
@@ -361,13 +362,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     if (__builtin_amdgcn_readfirstlane(wave) == 0) {
       uint32_t v = ((hw >> (63 - lane)) & 1u) ? (uint32_t)hcrc8[lane] : 0u;
       if (lane < 8 && (((syncd & 0xFFu) >> (7 - lane)) & 1u)) v ^= hcrc8[64 + lane];
-      v ^= __shfl_xor(v, 32);
-      v ^= __shfl_xor(v, 16);
-      v ^= __shfl_xor(v, 8);
-      v ^= __shfl_xor(v, 4);
-      v ^= __shfl_xor(v, 2);
-      v ^= __shfl_xor(v, 1);
-      hcrc = __builtin_amdgcn_readfirstlane(v);
+      hcrc = rd_lane_u32(wave_prefix_xor(v), 63);   // XOR over the wave
       if (d.hem) hcrc ^= 0x80u;
     }
     const uint32_t hcrc_rev = __builtin_bitreverse32(hcrc) >> 24;   // register LSB written first
