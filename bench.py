@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sc16", action="store_true", help="skip the secondary sc16-output timing")
+    ap.add_argument("--no-latency", action="store_true", help="skip the one-frame latency calls")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--shard", choices=("frames", "streams"), default="frames",
                     help="frames: one TS stream, disjoint frame ranges per rank; streams: an independent "
@@ -156,6 +157,39 @@ def cpu_baseline(cfg, seconds):
                       "blocks, one thread, own radix-2 float IFFT (FFTW unavailable), %.1f s"
                       % (frames, cfg.name, frames * F, dt),
             "fec_blocks_per_sec": frames * F / dt}
+
+
+def one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per):
+    """per-frame latency (the reference's stated aim, README:21-29): one T2 frame per call, TS
+    resident in HBM, from the call to the frame's IQ complete in HBM; median / p90 of 20 calls,
+    direct launches and hipGraph mode"""
+    import torch
+    lat = []
+    first, base, n = ts_meta[0]
+    for k in range(25):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        chain.run_device(ts_dev[0].data_ptr(), base, n, first, 1, iq[0].data_ptr(), streams[0].cuda_stream)
+        streams[0].synchronize()
+        lat.append((time.perf_counter() - t0) * 1e3)
+    lat = sorted(lat[5:])
+    latency = {"median_ms": lat[len(lat) // 2], "p90_ms": lat[int(len(lat) * 0.9)],
+               "frame_airtime_ms": per / RT_SPS * 1e3,
+               "note": "one T2 frame per run_device call (TS resident, IQ to HBM, host-synchronised); "
+                       "not `value`"}
+    chain.set_graph(True)          # the same calls as one hipGraph launch each
+    lat = []
+    for k in range(25):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        chain.run_device(ts_dev[0].data_ptr(), base, n, first, 1, iq[0].data_ptr(), streams[0].cuda_stream)
+        streams[0].synchronize()
+        lat.append((time.perf_counter() - t0) * 1e3)
+    chain.set_graph(False)
+    lat = sorted(lat[5:])
+    latency["graph_median_ms"] = lat[len(lat) // 2]
+    latency["graph_p90_ms"] = lat[int(len(lat) * 0.9)]
+    return latency
 
 
 def main():
@@ -268,33 +302,9 @@ def main():
         out[0] = iq
         sc16 = {"ms_per_step": e16 / args.steps * 1e3, "elapsed": e16,
                 "ofdm_avg_launch_ms": ms16[2] / max(1, n16[2])}
-    # per-frame latency (the reference's stated aim, README:21-29): one T2 frame per call, TS
-    # resident in HBM, from the call to the frame's IQ complete in HBM; median / p90 of 20 calls
-    lat = []
-    first, base, n = ts_meta[0]
-    for k in range(25):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        chain.run_device(ts_dev[0].data_ptr(), base, n, first, 1, iq[0].data_ptr(), streams[0].cuda_stream)
-        streams[0].synchronize()
-        lat.append((time.perf_counter() - t0) * 1e3)
-    lat = sorted(lat[5:])
-    latency = {"median_ms": lat[len(lat) // 2], "p90_ms": lat[int(len(lat) * 0.9)],
-               "frame_airtime_ms": per / RT_SPS * 1e3,
-               "note": "one T2 frame per run_device call (TS resident, IQ to HBM, host-synchronised); "
-                       "not `value`"}
-    chain.set_graph(True)          # the same calls as one hipGraph launch each
-    lat = []
-    for k in range(25):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        chain.run_device(ts_dev[0].data_ptr(), base, n, first, 1, iq[0].data_ptr(), streams[0].cuda_stream)
-        streams[0].synchronize()
-        lat.append((time.perf_counter() - t0) * 1e3)
-    chain.set_graph(False)
-    lat = sorted(lat[5:])
-    latency["graph_median_ms"] = lat[len(lat) // 2]
-    latency["graph_p90_ms"] = lat[int(len(lat) * 0.9)]
+    latency = None
+    if not args.no_latency:
+        latency = one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per)
     frames_total = B * args.steps * world
     samples_total = frames_total * per
     fec_total = frames_total * info["fec_blocks_per_frame"]
@@ -353,7 +363,8 @@ def main():
                 "ms_per_step": sc16["ms_per_step"], "ofdm_avg_launch_ms": sc16["ofdm_avg_launch_ms"],
                 "note": "secondary: same chain, output gain 0.2 + int16 I/Q store (the flowgraph's "
                         "multiply_const and SDR wire format fused into the IQ store); not `value`"}
-        out["latency_1_frame"] = latency
+        if latency:
+            out["latency_1_frame"] = latency
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only (host cores are shared)
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
             # the box's CPU share is 16 threads (os.cpu_count() reports the whole machine)

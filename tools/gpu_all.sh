@@ -18,7 +18,7 @@ step smoke 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s
 tail -2 gpurun_out/smoke_$TAG.log
 step bench 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 cat gpurun_out/bench_$TAG.json
-step trace 300 rocprofv3 --kernel-trace --stats -T -f csv -d gpurun_out/prof/trace_$TAG -o bench -- python3 bench.py --steps 10 --warmup 2 --no-pmc --no-cpu-baseline --no-sc16 --slots 1 > gpurun_out/prof/trace_$TAG.json 2> gpurun_out/prof/trace_$TAG.err
+step trace 300 rocprofv3 --kernel-trace --stats -T -f csv -d gpurun_out/prof/trace_$TAG -o bench -- python3 bench.py --steps 10 --warmup 2 --no-pmc --no-cpu-baseline --no-sc16 --no-latency --slots 1 > gpurun_out/prof/trace_$TAG.json 2> gpurun_out/prof/trace_$TAG.err
 if [ "${PMC:-1}" = 1 ]; then
 for set in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE"; do
   t=$(echo $set | tr ' ' '_' | cut -c1-40)
