@@ -524,7 +524,7 @@ struct dvbt2ll_chain {
   PilotPlan pilot;
   OfdmTables ofdm;
   DevBuf aux, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
-  DevBuf abin, aval, aind, agrp;   // non-data bins as compact lists (t2_plan.h AuxLists)
+  DevBuf abin, aval, aind, agrp, azr;   // non-data bins as compact lists (t2_plan.h AuxLists)
   // intermediate buffer slots (codewords, index pairs): run calls take them round-robin, so
   // calls issued on different streams overlap; a slot reused on another stream first waits for
   // its previous run (slot_done) -- see dvbt2ll_chain_set_slots
@@ -727,16 +727,23 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   for (auto &b : al.dbin)
     if (b != 0xFFFF) b = (uint16_t)ofdm_padded_bin(pp.N, b);
   for (auto &e : al.ind) e = ofdm_padded_bin(pp.N, e & 0x7FFFu) | (e & ~0x7FFFu);
+  std::vector<int32_t> zr(al.zrun.size());   // zero runs as padded slot ranges
+  for (size_t g = 0; g + 1 < al.zrun.size(); g += 2) {
+    const int z0 = al.zrun[g], z1 = al.zrun[g + 1];
+    zr[g] = z1 > z0 ? (int32_t)ofdm_padded_bin(pp.N, (uint32_t)z0) : 0;
+    zr[g + 1] = z1 > z0 ? (int32_t)ofdm_padded_bin(pp.N, (uint32_t)(z1 - 1)) + 1 : 0;
+  }
   al.ind.push_back(0);   // never empty (device pointer)
   al.dbin.resize(al.dbin.size() + 4, 0xFFFF);
   al.dval.resize(al.dval.size() + 4, cf32{0.f, 0.f});
   if ((r = upload(h->abin, al.dbin)) || (r = upload(h->aval, al.dval)) || (r = upload(h->aind, al.ind)) ||
-      (r = upload(h->agrp, al.grp)))
+      (r = upload(h->agrp, al.grp)) || (r = upload(h->azr, zr)))
     return r;
   h->ofdm.dev.abin = h->abin.as<uint16_t>();
   h->ofdm.dev.aval = h->aval.as<float2>();
   h->ofdm.dev.aind = h->aind.as<uint32_t>();
   h->ofdm.dev.agrp = h->agrp.as<int4>();
+  h->ofdm.dev.azr = h->azr.as<int2>();
   h->ofdm.dev.inv = h->inv.as<uint16_t>();
   h->ofdm.dev.sym_d0 = h->sym_d0.as<int32_t>();
   h->ofdm.dev.sym_n = h->sym_n.as<int32_t>();

@@ -83,6 +83,7 @@ struct OfdmDev {
   const float2 *aval;       // direct values
   const uint32_t *aind;     // indirect: padded bin | code << 15, value at aux abase + code
   const int4 *agrp;
+  const int2 *azr;          // per group: padded LDS slot range [x, y) zeroed as a run (AuxLists::zrun)
   int N, G, Nsym, aux_len, t2frames;
   float norm;
   float gain;               // output gain after the normalisation (1 = pilotgen's own output)

@@ -1069,6 +1069,7 @@ struct BinSource {
   const float2 *aval;
   const uint32_t *aind;
   const int4 *agrp;            // this symbol's two groups (halves)
+  const int2 *azr;             // this symbol's two zero runs (padded LDS slot ranges)
 };
 
 // One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split) by NT = NSUB/V
@@ -1082,12 +1083,13 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   // first pass (R = V, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
   const int32_t *m = src.map + (SPLIT ? half * NSUB : 0);
   if (src.inv) {
-    // zero every bin (and pad slot), then write the non-data bins from the compact aux lists and
-    // the data cells from the symbol's slot run (disjoint bins: one phase, no barrier between)
+    // zero the half's run of band-edge null bins (the planner's zero run; isolated zero bins
+    // are direct entries), write the non-data bins from the compact aux lists and the data cells
+    // from the symbol's slot run: every bin written exactly once, all targets disjoint, so the
+    // three writers share one phase (the barrier below publishes the constant tables)
     {
-      float4 *z = (float4 *)lds;
-      constexpr int NZ = (NSUB + (NSUB >> PS)) / 2;
-      for (int i = tid; i < NZ; i += NT) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int2 zr = src.azr[half];
+      for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
     }
     if (half == 0) stage.store((unsigned char *)lds, true, tid);
     __syncthreads();
@@ -1287,12 +1289,14 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
   const int32_t *map = d.bin_map + (int64_t)j * N;
   const uint32_t tws = Sh::SPLIT ? 2u : 1u;       // sub-transform twiddle = table index * tws
-  BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u, d.abin, d.aval, d.aind, nullptr};
+  BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u, d.abin, d.aval, d.aind, nullptr,
+                nullptr};
   if (d.inv) {
     src.d0 = (uint32_t)d.sym_d0[j];
     src.dn = (uint32_t)d.sym_n[j];
     src.dn0 = (uint32_t)d.sym_n0[j];
     src.agrp = d.agrp + 2 * j;
+    src.azr = d.azr + 2 * j;
   }
 
   if (io.carriers_only) {                          // test hook (gather mode): bins in natural order

@@ -1037,6 +1037,7 @@ int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf
   if ((int64_t)aux_len * t2frames > (int64_t)auxv.size() || nsub > 32768) return -1;
   al.dbin.clear(); al.dval.clear(); al.ind.clear();
   al.grp.assign((size_t)4 * ngrp, 0);
+  al.zrun.assign((size_t)2 * ngrp, 0);
   auto same_in_all = [&](int a) {
     for (int v = 1; v < t2frames; v++) {
       const cf32 x = auxv[a], y = auxv[(size_t)v * aux_len + a];
@@ -1050,16 +1051,40 @@ int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf
     al.grp[4 * g + 2] = (int32_t)al.ind.size();
     if (h && !split) continue;
     const int32_t *row = &cl.cmap[(size_t)j * N + (size_t)h * nsub];
+    // zero bins: AUX_ZERO, or an aux cell that is +0 in every variant
+    auto is_zero = [&](int k) {
+      const int32_t c = row[k];
+      if (c >= 0) return false;
+      if (c == -AUX_ZERO - 1) return true;
+      const int a = -c - 1;
+      if (a >= aux_len || !same_in_all(a)) return false;
+      uint64_t bits;
+      std::memcpy(&bits, &auxv[a], sizeof(bits));
+      return bits == 0;
+    };
+    int z0 = 0, z1 = 0;
+    for (int k = 0; k < nsub;) {   // longest run of zero bins
+      if (!is_zero(k)) { k++; continue; }
+      int e = k;
+      while (e < nsub && is_zero(e)) e++;
+      if (e - k > z1 - z0) { z0 = k; z1 = e; }
+      k = e;
+    }
+    al.zrun[2 * g + 0] = z0;
+    al.zrun[2 * g + 1] = z1;
     for (int k = 0; k < nsub; k++) {
       const int32_t c = row[k];
-      if (c >= 0 || c == -AUX_ZERO - 1) continue;
+      if (c >= 0) continue;
+      if (k >= z0 && k < z1) continue;   // zeroed as a range by the kernel
+      if (is_zero(k)) {                  // an isolated zero bin: direct entry of value 0
+        al.dbin.push_back((uint16_t)k);
+        al.dval.push_back(cf32{0.f, 0.f});
+        continue;
+      }
       const int a = -c - 1;
       if (a >= aux_len) return -1;
       if (same_in_all(a)) {
         const cf32 v = auxv[a];
-        uint64_t bits;
-        std::memcpy(&bits, &v, sizeof(bits));
-        if (bits == 0) continue;   // +0: covered by the zero fill
         al.dbin.push_back((uint16_t)k);
         al.dval.push_back(v);
       } else {

@@ -129,6 +129,9 @@ struct AuxLists {
   std::vector<cf32> dval;
   std::vector<uint32_t> ind;
   std::vector<int32_t> grp;   // 4 per group: direct offset, direct count, indirect offset, count
+  // 2 per group: the longest run [z0, z1) of zero bins (band-edge nulls), zeroed by the kernel
+  // as a range; every other zero bin is a direct entry with value 0
+  std::vector<int32_t> zrun;
 };
 int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf32> &auxv, int aux_len,
                     int t2frames, AuxLists &al);

@@ -98,7 +98,7 @@ int t2probe_chain(const int *p20, const int *pg3, int *info, int32_t *cmap, uint
 // it).  Call with null outputs first: sizes = [dbin entries, ind entries, groups, aux_len,
 // t2frames]; auxv (aux_len * t2frames complex) is returned for the checker.
 int t2probe_aux_lists(const int *p20, const int *pg3, int *sizes, uint16_t *dbin, float *dval, uint32_t *ind,
-                      int32_t *grp, float *auxv_out) {
+                      int32_t *grp, float *auxv_out, int32_t *zrun) {
   FmParams f{p20[0], p20[1], p20[2], p20[3], p20[4], p20[5], p20[6], p20[7], p20[8], p20[9],
              p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
   PgParams g{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
@@ -119,6 +119,7 @@ int t2probe_aux_lists(const int *p20, const int *pg3, int *sizes, uint16_t *dbin
   if (ind) memcpy(ind, al.ind.data(), al.ind.size() * 4);
   if (grp) memcpy(grp, al.grp.data(), al.grp.size() * 4);
   if (auxv_out) memcpy(auxv_out, auxv.data(), (size_t)fp.aux_len * fp.t2frames * 8);
+  if (zrun) memcpy(zrun, al.zrun.data(), al.zrun.size() * 4);
   return 0;
 }
 }

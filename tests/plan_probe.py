@@ -27,7 +27,7 @@ def lib():
         L.t2probe_map.argtypes = [ctypes.c_int] * 4 + [vp, vp]
         L.t2probe_fec.argtypes = [ctypes.c_int] * 3 + [vp, vp, vp]
         L.t2probe_chain.argtypes = [vp] * 9
-        L.t2probe_aux_lists.argtypes = [vp] * 8
+        L.t2probe_aux_lists.argtypes = [vp] * 9
         _L = L
     return _L
 
@@ -129,20 +129,23 @@ def chain_layout(cfg):
 def aux_lists(cfg):
     """the fused chain's compact non-data bin lists (t2_plan.h AuxLists) and the per-variant aux
     table they index: dbin, dval (direct (bin, value) entries, quads), ind (bin | code << 15),
-    grp (groups 2 j + h: direct offset, count, indirect offset, count), auxv [t2frames, aux_len]"""
+    grp (groups 2 j + h: direct offset, count, indirect offset, count), auxv [t2frames, aux_len],
+    zrun (groups: the [z0, z1) run of zero bins the kernel zeroes as a range)"""
     p = np.array(cfg.fm_args(), np.int32)
     g = np.array([cfg.misogroup, cfg.equalization, cfg.bandwidth], np.int32)
     sz = np.zeros(5, np.int32)
-    assert lib().t2probe_aux_lists(_p(p), _p(g), _p(sz), None, None, None, None, None) == 0
+    assert lib().t2probe_aux_lists(_p(p), _p(g), _p(sz), None, None, None, None, None, None) == 0
     nd, ni, ng, aux_len, t2f = (int(x) for x in sz)
     dbin = np.zeros(nd, np.uint16)
     dval = np.zeros(nd, np.complex64)
     ind = np.zeros(max(ni, 1), np.uint32)
     grp = np.zeros(4 * ng, np.int32)
     auxv = np.zeros(aux_len * t2f, np.complex64)
-    assert lib().t2probe_aux_lists(_p(p), _p(g), _p(sz), _p(dbin), _p(dval), _p(ind), _p(grp), _p(auxv)) == 0
+    zrun = np.zeros(2 * ng, np.int32)
+    assert lib().t2probe_aux_lists(_p(p), _p(g), _p(sz), _p(dbin), _p(dval), _p(ind), _p(grp), _p(auxv),
+                                   _p(zrun)) == 0
     return dict(dbin=dbin.astype(np.int64), dval=dval, ind=ind[:ni].astype(np.int64), grp=grp.reshape(ng, 4),
-                auxv=auxv.reshape(t2f, aux_len))
+                auxv=auxv.reshape(t2f, aux_len), zrun=zrun.reshape(ng, 2))
 
 
 def stored_to_natural(row, N, split):

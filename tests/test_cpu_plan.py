@@ -147,10 +147,11 @@ def test_chain_cell_layout_matches_oracle(name, over):
 @pytest.mark.parametrize("name,over", GRID + [("cfg%d" % i, None) for i in range(1, 6)],
                          ids=[g[0] for g in GRID] + ["cfg%d" % i for i in range(1, 6)])
 def test_chain_aux_lists_match_cmap(name, over):
-    """the OFDM kernel's non-data bins (t2_kernels.hip sub_ifft, scatter mode): zero fill, then
-    the direct (bin, value) quads and the indirect entries through aux variant v.  For every
-    t2_frame_num variant, every symbol and half, they rebuild exactly the non-data bins the
-    per-bin code row (cmap < 0) gives, and each listed bin is written once."""
+    """the OFDM kernel's non-data bins (t2_kernels.hip sub_ifft, scatter mode): the zero run
+    [z0, z1), the direct (bin, value) quads and the indirect entries through aux variant v.  For
+    every t2_frame_num variant, every symbol and half, they rebuild exactly the non-data bins the
+    per-bin code row (cmap < 0) gives, every such bin is written exactly once, and no data bin
+    (cmap >= 0) is touched."""
     cfg = CONFIGS[name] if over is None else grid_cfg(over)
     lay = PP.chain_layout(cfg)
     al = PP.aux_lists(cfg)
@@ -163,8 +164,12 @@ def test_chain_aux_lists_match_cmap(name, over):
             for h in range(2 if split else 1):
                 code = lay["cmap_stored"][j][h * nsub:(h + 1) * nsub]
                 want = np.where(code < 0, auxv[v][np.clip(-code - 1, 0, None)], 0).astype(np.complex64)
-                got = np.zeros(nsub, np.complex64)
+                got = np.full(nsub, np.nan, np.complex64)
                 hits = np.zeros(nsub, np.int32)
+                z0, z1 = al["zrun"][2 * j + h]
+                assert 0 <= z0 <= z1 <= nsub
+                got[z0:z1] = 0
+                hits[z0:z1] += 1
                 d0, dn, i0, ni = grp[2 * j + h]
                 b = al["dbin"][d0:d0 + dn]
                 real = b != 0xFFFF
@@ -176,7 +181,9 @@ def test_chain_aux_lists_match_cmap(name, over):
                 np.add.at(hits, e & 0x7FFF, 1)
                 assert hits.max(initial=0) <= 1
                 assert (code[hits > 0] < 0).all()
-                np.testing.assert_array_equal(got.view(np.uint64), want.view(np.uint64),
+                assert (hits[code < 0] == 1).all(), "variant %d symbol %d half %d" % (v, j, h)
+                aux = code < 0
+                np.testing.assert_array_equal(got[aux].view(np.uint64), want[aux].view(np.uint64),
                                               err_msg="variant %d symbol %d half %d" % (v, j, h))
 
 
