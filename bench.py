@@ -59,7 +59,9 @@ def parse():
 
 
 def algorithmic_bytes(cfg, info):
-    """SURVEY.md section 8(d) per-frame algorithmic bytes of each stage."""
+    """SURVEY.md section 8(d) per-frame algorithmic bytes of each stage (the standalone-pass HBM
+    traffic of an unfused S1..S4 pipeline; the fused kernels report against these as a second,
+    separately named figure)."""
     from dvbt2ll.configs import KBCH
     F = info["fec_blocks_per_frame"]
     nldpc = 64800 if cfg.framesize == 1 else 16200
@@ -73,39 +75,81 @@ def algorithmic_bytes(cfg, info):
     return {"fec": s1, "map": s2, "ofdm": s3 + s4}
 
 
+def minimal_bytes(cfg, info, iq_bytes=8):
+    """per-frame bytes each kernel of the fused chain must move through HBM at least:
+    fec reads the TS payload and writes packed codewords; map reads the codewords and writes one
+    2-byte constellation index pair per cell; ofdm reads the pairs and writes the IQ samples (its
+    per-symbol tables are shared by every frame of a launch and are not counted)"""
+    from dvbt2ll.configs import KBCH
+    F = info["fec_blocks_per_frame"]
+    nldpc = 64800 if cfg.framesize == 1 else 16200
+    kbch = KBCH[(cfg.framesize, cfg.rate)]
+    cs, S, IQ = info["cell_size"], info["stream_items"], info["iq_samples_per_frame"]
+    return {"fec": F * ((kbch - 80) // 8 + nldpc // 8), "map": F * (nldpc // 8 + 2 * cs),
+            "ofdm": 2 * S + iq_bytes * IQ}
+
+
+KERNELS = ("fec", "map", "ofdm")
+# rocprofv3 FETCH_SIZE / WRITE_SIZE (KiB) -> bytes.  gfx950 tallies 128-B read requests at 64 B
+# (MI355X_MICROARCH.md, HBM): x2 on the read side, calibrated per access width by tools/fetch_calib
+# (profiles/r2_fetch_calib.json); the kernels' dominant widths: fec 4 B (TS words), map 4 B
+# (codeword words), ofdm 8 B (slot bins, index pairs)
+LOAD_WIDTH = {"fec": 4, "map": 4, "ofdm": 8}
+STORE_WIDTH = {"fec": 4, "map": 2, "ofdm": 8}
+
+
+def _calibration():
+    f = ROOT / "profiles" / "r2_fetch_calib.json"
+    try:
+        return json.loads(f.read_text())
+    except Exception:  # noqa: BLE001
+        return {}
+
+
 def pmc_passes(args):
-    """rocprofv3 FETCH_SIZE / WRITE_SIZE of the ofdm kernel, one counter set per pass, run as child
-    processes before this process initialises the GPU.  Returns per-launch corrected bytes or None."""
+    """rocprofv3 passes (one counter set each, run as child processes before this process initialises
+    the GPU): FETCH_SIZE, WRITE_SIZE and the SQ instruction counts of the three kernels.  Returns
+    ({kernel: {counter: mean per launch}}, note)."""
     import shutil
+    import csv
     rp = shutil.which("rocprofv3")
     if rp is None:
         return None, "rocprofv3 not found"
-    res = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    res = {k: {} for k in KERNELS}
+    for ctrs in (["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"]):
         d = tempfile.mkdtemp(prefix="t2pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [rp, "--pmc", ctr, "--kernel-include-regex", "ofdm_kernel", "-T", "-f", "csv", "-d", d, "-o", "pmc",
-               "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--config", args.config,
+        cmd = [rp, "--pmc", *ctrs, "--kernel-include-regex", "(fec|map|ofdm)_kernel", "-T", "-f", "csv", "-d", d,
+               "-o", "pmc", "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--config", args.config,
                "--frames", str(args.frames), "--steps", "2", "--warmup", "1"]
         try:
             subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         except Exception as e:  # noqa: BLE001
-            return None, "rocprofv3 %s pass failed: %s" % (ctr, e)
-        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-        vals = []
-        for fn in files:
-            import csv
+            return None, "rocprofv3 %s pass failed: %s" % (ctrs, e)
+        vals = {}
+        for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(fn) as fh:
                 for row in csv.DictReader(fh):
-                    if row.get("Counter_Name") == ctr and "ofdm_kernel" in row.get("Kernel_Name", ""):
-                        vals.append(float(row["Counter_Value"]))
-        if not vals:
-            return None, "no %s rows" % ctr
-        res[ctr] = sum(vals) / len(vals)
-    # FETCH_SIZE / WRITE_SIZE are in KiB; gfx950 FETCH_SIZE reads half of the streamed bytes
-    # (MI355X_MICROARCH.md, HBM section) -> x2 on the read side
-    fetch = res["FETCH_SIZE"] * 1024 * 2
-    write = res["WRITE_SIZE"] * 1024
-    return {"fetch_bytes": fetch, "write_bytes": write, "total": fetch + write}, None
+                    for k in KERNELS:
+                        if row.get("Counter_Name") in ctrs and (k + "_kernel") in row.get("Kernel_Name", ""):
+                            vals.setdefault((k, row["Counter_Name"]), []).append(float(row["Counter_Value"]))
+        for (k, c), v in vals.items():
+            res[k][c] = sum(v) / len(v)
+        shutil.rmtree(d, ignore_errors=True)
+    cal = _calibration()
+    for k in KERNELS:
+        r = res[k]
+        if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
+            fr = cal.get("FETCH_SIZE rd %dB" % LOAD_WIDTH[k], 0.5)
+            wr = cal.get("WRITE_SIZE wr %dB" % STORE_WIDTH[k], 1.0)
+            r["fetch_bytes"] = r["FETCH_SIZE"] * 1024 / fr
+            r["write_bytes"] = r["WRITE_SIZE"] * 1024 / wr
+            r["hbm_bytes"] = r["fetch_bytes"] + r["write_bytes"]
+            r["calibration"] = {"fetch_counter_per_byte": fr, "write_counter_per_byte": wr,
+                                "source": "profiles/r2_fetch_calib.json" if cal else "MI355X_MICROARCH.md default"}
+    return res, None
+
+
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave-instructions/s: 256 CUs x 4 SIMDs, one wave64 VALU op per 2 cycles
 
 
 def _oracle_stream(cfg, seconds, max_frames, seed=1):
@@ -148,15 +192,86 @@ def cpu_host_replicas(cfg, seconds, threads):
             "fec_blocks_per_sec": sum(r[0] / r[2] for r in res) * cfg.fecblocks}
 
 
-def cpu_baseline(cfg, seconds):
-    """Oracle C restatement (single thread) over a bounded sample of the same workload."""
-    frames, samples, dt = _oracle_stream(cfg, seconds, 64)
+def cpu_stage_times(cfg, seconds, max_frames=64, seed=1):
+    """per-frame time of each reference block restated in the oracle (bbheaderbch, ldpc,
+    interleavermod, framemapperfint, pilotgenp1insert), one thread, over consecutive frames of one
+    stream until the time bound; plus the FFTW-class variant of the pilotgen stage: its carrier
+    fill (oracle) + numpy's single-precision pocketfft IFFT, scale and guard interval instead of
+    the oracle's radix-2 IFFT (FFTW is absent)"""
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    from dvbt2ll.configs import ts_for_frames
     F = cfg.fecblocks
-    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": 1, "kind": "port",
-            "sample": "%d %s T2 frames (%d FEC blocks) through the oracle C restatement of all five "
-                      "blocks, one thread, own radix-2 float IFFT (FFTW unavailable), %.1f s"
-                      % (frames, cfg.name, frames * F, dt),
-            "fec_blocks_per_sec": frames * F / dt}
+    bb = O.BB(*cfg.bb_args()); ld = O.LDPC(cfg.framesize, cfg.rate); im = O.IM(*cfg.im_args())
+    fm = O.FM(*cfg.fm_args()); pg = O.PG(*cfg.pg_args())
+    N, G, nrm = pg.vlength, pg.guard, np.float32(pg.normalization)
+    ts, _ = ts_for_frames(cfg, 0, max_frames, seed)
+    tot = dict.fromkeys(("bbheaderbch", "ldpc", "interleavermod", "framemapperfint", "pilotgenp1insert",
+                         "pilotgen_fill", "pocketfft_ifft_gi"), 0.0)
+    off, frames, samples = 0, 0, 0
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        bits, cons = bb.work(ts[off:], F)
+        t1 = time.perf_counter()
+        cw = ld.work(bits, F)
+        t2 = time.perf_counter()
+        cells = im.work(cw, F)
+        t3 = time.perf_counter()
+        mapped = fm.work(cells)
+        t4 = time.perf_counter()
+        iq = pg.work(mapped)
+        t5 = time.perf_counter()
+        car = pg.carriers(mapped)
+        t6 = time.perf_counter()
+        x = np.fft.ifft(np.fft.ifftshift(car, axes=1), axis=1) * np.float32(N) * nrm
+        out = np.concatenate([x[:, N - G:], x], axis=1)
+        t7 = time.perf_counter()
+        assert out.dtype == np.complex64
+        off += cons
+        for k, dt in zip(tot, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5, t7 - t6)):
+            tot[k] += dt
+        frames += 1
+        samples += len(iq)
+        if time.perf_counter() - t_start >= seconds or frames >= max_frames:
+            break
+    per = {k: v / frames for k, v in tot.items()}
+    return per, frames, samples // frames
+
+
+def cpu_config_figures(cfg, seconds):
+    """SURVEY 8(d)'s CPU figures for one config: single-thread sequential chain (sum of the block
+    times), GR-style pipelined (one thread per block, throughput = 1 / slowest block), each with the
+    oracle's radix-2 IFFT and with the FFTW-class pocketfft IFFT; Msamples/s, FEC blocks/s, x RT"""
+    per, frames, iq = cpu_stage_times(cfg, seconds)
+    blocks = ("bbheaderbch", "ldpc", "interleavermod", "framemapperfint", "pilotgenp1insert")
+    fast = dict(per)
+    fast["pilotgenp1insert"] = per["pilotgen_fill"] + per["pocketfft_ifft_gi"]
+
+    def fig(times, pipelined):
+        t = max(times[b] for b in blocks) if pipelined else sum(times[b] for b in blocks)
+        return {"msps": iq / t / 1e6, "fec_blocks_per_sec": cfg.fecblocks / t, "x_realtime": iq / t / RT_SPS}
+    return {"frames": frames, "stage_ms_per_frame": {k: v * 1e3 for k, v in per.items()},
+            "sequential_radix2": fig(per, False), "sequential_pocketfft": fig(fast, False),
+            "gr_pipelined_5_threads_radix2": fig(per, True), "gr_pipelined_5_threads_pocketfft": fig(fast, True)}
+
+
+def cpu_baseline(cfg, seconds, all_configs=True):
+    """Oracle C restatement (single thread) over a bounded sample of the same workload; per-config
+    figures for every BASELINE config beside it."""
+    from dvbt2ll.configs import CONFIGS
+    main = cpu_config_figures(cfg, seconds)
+    seq = main["sequential_radix2"]
+    out = {"value": seq["msps"], "unit": "Msamples/s", "cores": 1, "kind": "port",
+           "sample": "%d %s T2 frames (%d FEC blocks) through the oracle C restatement of all five "
+                     "blocks, one thread, own radix-2 float IFFT (FFTW unavailable)"
+                     % (main["frames"], cfg.name, main["frames"] * cfg.fecblocks),
+           "fec_blocks_per_sec": seq["fec_blocks_per_sec"], "x_realtime": seq["x_realtime"],
+           "figures": main}
+    if all_configs:
+        out["per_config"] = {n: cpu_config_figures(c, 2.0) for n, c in CONFIGS.items() if c is not cfg}
+    return out
 
 
 def one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per):
@@ -305,39 +420,71 @@ def main():
     latency = None
     if not args.no_latency:
         latency = one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per)
+    gathered = None
+    if dist and args.shard == "frames":
+        # secondary (not `value`): each step followed by the ordered IQ gather to rank 0, the
+        # chain's one exchange step (point-to-point sends to the root over RCCL / xGMI)
+        from dvbt2ll.distributed import gather_frames
+        kg = min(args.steps, 5)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for s_ in range(kg):
+            step(s_, serial=True)
+            torch.cuda.current_stream().wait_stream(streams[0])
+            gather_frames(iq[s_ % S], world * B, per)
+        torch.cuda.synchronize()
+        dist.barrier()
+        eg = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(eg, op=dist.ReduceOp.MAX)
+        eg = float(eg.item())
+        gathered = {"value": world * B * kg * per / eg / 1e6, "unit": "Msamples/s", "steps": kg,
+                    "ms_per_step": eg / kg * 1e3, "bytes_to_root_per_step": (world - 1) * B * per * 8,
+                    "note": "secondary: every step's complex64 IQ gathered in frame order on rank 0 "
+                            "(dvbt2ll.distributed.gather_frames, grouped send/recv); not `value`"}
     frames_total = B * args.steps * world
     samples_total = frames_total * per
     fec_total = frames_total * info["fec_blocks_per_frame"]
     msps = samples_total / elapsed / 1e6
     if rank == 0:
         ab = algorithmic_bytes(cfg, info)
-        stages = {}
-        for k, name in enumerate(("fec", "map", "ofdm")):
+        mb = minimal_bytes(cfg, info)
+        stages, rooflines = {}, {}
+        for k, name in enumerate(KERNELS):
             avg_ms = stage_ms[k] / max(1, launches[k])
-            bytes_launch = ab[name] * B
-            stages[name] = {"avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": bytes_launch,
-                            "achieved_GBs": bytes_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else None}
-        dom = max(stages, key=lambda n: stages[n]["avg_launch_ms"])
-        st = stages[dom]
-        roof = {"kernel": dom + "_kernel", "bound": "hbm", "achieved": st["achieved_GBs"], "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": st["achieved_GBs"] / HBM_PEAK_GBS if st["achieved_GBs"] else None,
-                "traffic": (traffic["total"] if (traffic and dom == "ofdm") else None),
-                "traffic_note": pmc_note if traffic is None else
-                "rocprofv3 PMC passes (FETCH_SIZE x1024 x2 gfx950 read correction + WRITE_SIZE x1024), "
-                "ofdm_kernel per launch",
-                "algorithmic_bytes_per_launch": st["algorithmic_bytes_per_launch"],
-                "avg_launch_ms": st["avg_launch_ms"]}
-        if roof["traffic"]:
-            # what HBM actually carried: the fused kernel never writes or re-reads the cells as
-            # complex64 (SURVEY 8(d)'s S3 + S4 stage figures), so its measured traffic is far below
-            # the algorithmic bytes and `achieved` can approach or pass the HBM peak
-            tgbs = roof["traffic"] / (st["avg_launch_ms"] * 1e-3) / 1e9
-            roof["traffic_GBs"] = tgbs
-            roof["traffic_frac"] = tgbs / HBM_PEAK_GBS
-            roof["note"] = ("achieved = SURVEY 8(d) stage bytes of the unfused S3+S4 pipeline / kernel time, i.e. "
-                            "the fused kernel's speed as a fraction of an ideal unfused pipeline at HBM peak; "
-                            "traffic_frac = measured HBM bytes / time / peak (the kernel is LDS/VALU-latency "
-                            "bound at one 138 KB workgroup per CU, not HBM-bound)")
+            t = avg_ms * 1e-3
+            stages[name] = {"avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": ab[name] * B,
+                            "achieved_GBs": ab[name] * B / t / 1e9 if t > 0 else None}
+            e = {"kernel": name + "_kernel", "bound": "hbm", "avg_launch_ms": avg_ms, "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "min_bytes_per_launch": mb[name] * B,
+                 "achieved": mb[name] * B / t / 1e9 if t > 0 else None,
+                 "stage_bytes_per_launch": ab[name] * B,
+                 "stage_bytes_frac": ab[name] * B / t / 1e9 / HBM_PEAK_GBS if t > 0 else None}
+            e["frac"] = e["achieved"] / HBM_PEAK_GBS if e["achieved"] else None
+            pm = (traffic or {}).get(name, {})
+            e["traffic"] = pm.get("hbm_bytes")
+            if e["traffic"] and t > 0:
+                e["traffic_GBs"] = e["traffic"] / t / 1e9
+                e["traffic_frac"] = e["traffic_GBs"] / HBM_PEAK_GBS
+                e["traffic_over_min"] = e["traffic"] / (mb[name] * B)
+                e["calibration"] = pm.get("calibration")
+            if name == "fec":
+                nb = info["fec_blocks_per_frame"] * B
+                e["fec_blocks_per_s"] = nb / t if t > 0 else None
+                e["note"] = ("integer BCH/LDPC codec: latency/issue-bound, not HBM-bound (SURVEY 8(d)); "
+                             "frac is its minimal HBM bytes / time / peak")
+                if "SQ_INSTS_VALU" in pm and t > 0:
+                    e["valu_wave_instr_per_block"] = pm["SQ_INSTS_VALU"] / nb
+                    e["salu_wave_instr_per_block"] = pm.get("SQ_INSTS_SALU", 0) / nb
+                    e["valu_issue_frac"] = pm["SQ_INSTS_VALU"] / t / VALU_ISSUE_PEAK
+            rooflines[name] = e
+        dom = max(KERNELS, key=lambda n: stages[n]["avg_launch_ms"])
+        roof = dict(rooflines[dom])
+        roof["note"] = ("frac = the kernel's minimal HBM bytes (DESIGN.md 5) / its HIP-event launch time / 8 TB/s; "
+                        "traffic = calibrated rocprofv3 FETCH_SIZE + WRITE_SIZE per launch; stage_bytes_frac = "
+                        "SURVEY 8(d)'s unfused stage bytes over the same time (not an HBM utilisation)")
+        if traffic is None:
+            roof["traffic_note"] = pmc_note
         out = {
             "metric": METRIC, "value": msps, "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -356,6 +503,7 @@ def main():
             "x_realtime": msps * 1e6 / RT_SPS,
             "stages": stages,
             "roofline": roof,
+            "rooflines": rooflines,
         }
         if sc16:
             out["iq_sc16_x0.2"] = {
@@ -365,6 +513,8 @@ def main():
                         "multiply_const and SDR wire format fused into the IQ store); not `value`"}
         if latency:
             out["latency_1_frame"] = latency
+        if gathered:
+            out["gather_to_rank0"] = gathered
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only (host cores are shared)
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
             # the box's CPU share is 16 threads (os.cpu_count() reports the whole machine)

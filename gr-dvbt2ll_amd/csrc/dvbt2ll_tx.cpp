@@ -34,12 +34,13 @@ const Preset kPresets[] = {
     {"cfg3", 1, 1, 3, 1, 195, 3, 1, 5, 1, 3, 3, 2, 59},
     {"cfg4", 1, 0, 1, 0, 24, 3, 0, 1, 0, 3, 6, 2, 59},
     {"cfg5", 1, 5, 3, 0, 197, 3, 0, 5, 4, 3, 6, 2, 59},
+    {"cfg1q", 0, 0, 0, 1, 2, 3, 0, 2, 0, 3, 6, 2, 3},   // BASELINE config 1 as worded: QPSK 1/2
 };
 
 void usage(FILE *f) {
   std::fprintf(f,
                "usage: dvbt2ll_tx --in TS_FILE --out IQ_FILE [options]\n"
-               "  --preset cfg1..cfg5     parameter preset (default cfg1, the shipped flowgraph)\n"
+               "  --preset cfg1..cfg5|cfg1q parameter preset (default cfg1, the shipped flowgraph)\n"
                "  --set NAME=VALUE        override one chain parameter (framemapperfint_cc names:\n"
                "                          framesize rate constellation rotation fecblocks tiblocks\n"
                "                          carriermode fftsize guardinterval l1constellation\n"

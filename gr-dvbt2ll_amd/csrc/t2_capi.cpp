@@ -167,6 +167,8 @@ struct dvbt2ll_bbheaderbch {
   std::vector<uint8_t> history;  // last <= 376 consumed TS bytes (previous packet for CRC-8)
   DevBuf din, dout;
   std::vector<uint8_t> hbuf;
+  DevBuf sync_err;               // device counter: TS sync bytes != 0x47 consumed so far
+  uint32_t sync_err_host = 0;
 };
 
 extern "C" int dvbt2ll_bbheaderbch_create(const dvbt2ll_bbheaderbch_params *p, int device, dvbt2ll_bbheaderbch **out) {
@@ -179,6 +181,8 @@ extern "C" int dvbt2ll_bbheaderbch_create(const dvbt2ll_bbheaderbch_params *p, i
   int r = h->ctx.init(device);
   if (r) return r;
   if ((r = h->fec.init(p->framesize, p->rate, 3, p->mode, p->inband, p->fecblocks, p->tsrate))) return r;
+  if (h->sync_err.ensure(4)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemset(h->sync_err.p, 0, 4));
   *out = h.release();
   return DVBT2LL_OK;
 }
@@ -232,8 +236,10 @@ extern "C" int dvbt2ll_bbheaderbch_general_work(dvbt2ll_bbheaderbch *h, int nout
   io.first_block = h->blocks_done;
   io.out = h->dout.as<uint8_t>();
   io.nblocks = nb;
+  io.sync_err = h->sync_err.as<uint32_t>();
   HIP_TRY(launch_fec(FEC_TS_TO_BITS, d, io, h->ctx.stream));
   HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)nb * d.nbch, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipMemcpyAsync(&h->sync_err_host, h->sync_err.p, 4, hipMemcpyDeviceToHost, h->ctx.stream));
   HIP_TRY(hipStreamSynchronize(h->ctx.stream));
   h->blocks_done += nb;
   h->consumed_total += need;
@@ -241,6 +247,9 @@ extern "C" int dvbt2ll_bbheaderbch_general_work(dvbt2ll_bbheaderbch *h, int nout
   h->history.assign(h->hbuf.end() - keep, h->hbuf.end());
   if (consumed) *consumed = (int)need;
   return nb * d.nbch;
+}
+extern "C" int64_t dvbt2ll_bbheaderbch_sync_errors(const dvbt2ll_bbheaderbch *h) {
+  return h ? (int64_t)h->sync_err_host : 0;
 }
 extern "C" void dvbt2ll_bbheaderbch_destroy(dvbt2ll_bbheaderbch *h) { delete h; }
 
@@ -504,7 +513,7 @@ extern "C" void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h) { 
 // IQ format): captured once from the ordinary launch path, then every call rewrites the three
 // kernel nodes' arguments (hipGraphExecKernelNodeSetParams) and launches the graph
 struct ChainGraph {
-  int nframes = 0, fmt = -1;
+  int nframes = 0, fmt = -1, slot = -1;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   hipGraphNode_t node[3] = {};
@@ -525,6 +534,7 @@ struct dvbt2ll_chain {
   OfdmTables ofdm;
   DevBuf aux, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
   DevBuf abin, aval, aind, agrp, azr;   // non-data bins as compact lists (t2_plan.h AuxLists)
+  DevBuf sync_err;                      // TS sync bytes != 0x47 consumed by run calls (bbheader:675, 703)
   // intermediate buffer slots (codewords, index pairs): run calls take them round-robin, so
   // calls issued on different streams overlap; a slot reused on another stream first waits for
   // its previous run (slot_done) -- see dvbt2ll_chain_set_slots
@@ -558,31 +568,45 @@ struct dvbt2ll_chain {
     }
     return evpool[evused++];
   }
+  // every run's end event is waited on (runs may sit on several streams, so the last recorded
+  // event does not imply the earlier ones); the pool is emptied even when a query fails
   int fold_timing() {
     if (!evused) return 0;
-    HIP_TRY(hipEventSynchronize(evpool[evused - 1]));
-    for (size_t b = 0; b + 3 < evused; b += 4)
-      for (int k = 0; k < 3; k++) {
+    int st = 0;
+    for (size_t b = 0; b + 3 < evused && !st; b += 4) {
+      hipError_t e = hipEventSynchronize(evpool[b + 3]);
+      for (int k = 0; k < 3 && e == hipSuccess; k++) {
         float t = 0;
-        HIP_TRY(hipEventElapsedTime(&t, evpool[b + k], evpool[b + k + 1]));
-        ms[k] += t;
-        launches[k] += 1;
+        e = hipEventElapsedTime(&t, evpool[b + k], evpool[b + k + 1]);
+        if (e == hipSuccess) {
+          ms[k] += t;
+          launches[k] += 1;
+        }
       }
+      if (e != hipSuccess) {
+        last_hip_error() = e;
+        st = DVBT2LL_EDEVICE;
+      }
+    }
     evused = 0;
-    return 0;
+    return st;
   }
-  // capture the three launches once per (nframes, format) on a private stream, then per call
-  // rewrite the kernel nodes' arguments and launch the instantiated graph on s
-  int graph_launch(const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, hipStream_t s) {
+  // capture the three launches once per (nframes, format, slot) on a private stream, then per
+  // call rewrite the kernel nodes' arguments and launch the instantiated graph on s.  An exec is
+  // only re-armed after its previous launch has completed (host wait on the slot's completion
+  // event, recorded after every run on the slot), so no in-flight launch ever sees arguments
+  // rewritten under it; with several slots the calls still overlap on the device
+  int graph_launch(const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, int slot, hipStream_t s) {
     ChainGraph *g = nullptr;
     for (auto &c : graphs)
-      if (c->nframes == nframes && c->fmt == ofdm.dev.fmt) g = c.get();
+      if (c->nframes == nframes && c->fmt == ofdm.dev.fmt && c->slot == slot) g = c.get();
     if (!g) {
       if (!cap_stream) HIP_TRY(hipStreamCreateWithFlags(&cap_stream, hipStreamNonBlocking));
       std::unique_ptr<ChainGraph> c(new (std::nothrow) ChainGraph());
       if (!c) return DVBT2LL_ENOMEM;
       c->nframes = nframes;
       c->fmt = ofdm.dev.fmt;
+      c->slot = slot;
       HIP_TRY(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
       hipError_t e1 = launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, cap_stream);
       hipError_t e2 = e1 == hipSuccess ? launch_map(map.dev, mio, cap_stream) : e1;
@@ -631,6 +655,7 @@ struct dvbt2ll_chain {
       g = c.get();
       graphs.push_back(std::move(c));
     }
+    if (slot_used[slot]) HIP_TRY(hipEventSynchronize(slot_done[slot]));
     FecDev fd = fec.dev;
     MapDev md = map.dev;
     OfdmDev od = ofdm.dev;
@@ -761,6 +786,8 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
     return DVBT2LL_EINVAL;
   if ((r = h->alloc_slot(0))) return r;
   if ((r = upload(h->aux, auxv))) return r;
+  if (h->sync_err.ensure(4)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemset(h->sync_err.p, 0, 4));
   *out = h.release();
   return DVBT2LL_OK;
 }
@@ -783,7 +810,8 @@ extern "C" int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info
 
 extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_base, int64_t ts_len,
                                         int64_t first_frame, int nframes, void *iq_dev, void *stream) {
-  if (!h || !ts_dev || !iq_dev || nframes < 1 || nframes > h->max_frames || first_frame < 0 || ts_base < 0)
+  if (!h || !ts_dev || !iq_dev || nframes < 1 || nframes > h->max_frames || first_frame < 0 || ts_base < 0 ||
+      ts_base % 188 != 0)
     return DVBT2LL_EINVAL;
   hipStream_t s = stream ? (hipStream_t)stream : h->ctx.stream;
   const int F = h->frame.F;
@@ -817,6 +845,7 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   fio.out = cw.as<uint8_t>();
   fio.cw_stride = h->cw_stride;
   fio.nblocks = F * nframes;
+  fio.sync_err = h->sync_err.as<uint32_t>();
   mio.in = cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
   mio.out_pairs = pairs.as<uint16_t>();
@@ -834,7 +863,7 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   oio.first_frame = first_frame;
   oio.nframes = nframes;
   if (h->use_graph) {
-    int r = h->graph_launch(fio, mio, oio, nframes, s);
+    int r = h->graph_launch(fio, mio, oio, nframes, slot, s);
     if (r) return r;
   } else {
     HIP_TRY(launch_fec(FEC_TS_TO_TEMPU, h->fec.dev, fio, s));
@@ -939,6 +968,15 @@ extern "C" int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t ce
   cf32 *o = (cf32 *)out;
   const cf32 *lut = h->map.plan.lut;
   for (int64_t i = 0; i < cells; i++) o[i] = cf32{lut[pr[i] & 0xFF].re, lut[pr[i] >> 8].im};
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_chain_sync_errors(dvbt2ll_chain *h, int64_t *count) {
+  if (!h || !count) return DVBT2LL_EINVAL;
+  uint32_t v = 0;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(&v, h->sync_err.p, 4, hipMemcpyDeviceToHost));
+  *count = (int64_t)v;
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_synchronize(dvbt2ll_chain *h) {

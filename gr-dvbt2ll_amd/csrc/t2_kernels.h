@@ -33,6 +33,7 @@ struct FecIO {
   uint8_t *out;            // packed codewords (stride cw_stride) or unpacked bits
   int64_t cw_stride;
   int nblocks;
+  uint32_t *sync_err;      // ts modes, optional: += TS sync bytes != 0x47 consumed (bbheader:675, 703)
 };
 
 // ---------------------------------------------------------------- bit interleave + QAM + CI

@@ -16,6 +16,11 @@
 // No MFMA: these are bitwise / permutation / complex-FFT paths.
 #include "t2_kernels.h"
 
+#include <atomic>
+#include <mutex>
+#include <set>
+#include <utility>
+
 namespace t2 {
 
 // ============================================================================ helpers
@@ -100,6 +105,21 @@ __device__ __forceinline__ uint32_t rd_lane_u32(uint32_t v, int l) { return __bu
 __device__ __forceinline__ uint64_t rd_lane_u64(uint64_t v, int l) {
   uint32_t lo = rd_lane_u32((uint32_t)v, l), hi = rd_lane_u32((uint32_t)(v >> 32), l);
   return ((uint64_t)hi << 32) | lo;
+}
+
+// Raise a kernel's dynamic-LDS limit once per (kernel, device): thread-safe, and repeated for
+// every device a process launches on (the attribute belongs to the current device's function).
+static hipError_t lds_limit(const void *fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<const void *, int>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count({fn, dev})) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.insert({fn, dev});
+  return e;
 }
 
 // ============================================================================ FEC kernel
@@ -344,10 +364,21 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
         v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);
         v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);
         v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, true);
-        if (k == 0 && m < nslots) syncv[m] = active ? (uint8_t)v : 0;
+        if (k == 0 && m < nslots) {
+          syncv[m] = active ? (uint8_t)v : 0;
+          // the reference warns on every consumed sync byte that is not 0x47 (bbheader:703-705)
+          if (io.sync_err && raw[p - rs] != 0x47) atomicAdd(io.sync_err, 1u);
+        }
       }
       __syncthreads();
       FEC_PHASE(3);
+    }
+    if (d.hem && io.sync_err) {
+      // HEM drops each packet's sync byte; the one of packet p is consumed just before payload
+      // byte 187 p (bbheader:673-680, warning at :675-677)
+      const int64_t p0 = (J0 + 186) / 187;
+      for (int64_t pk = p0 + tid; 187 * pk < J0 + npay; pk += FEC_THREADS)
+        if (io.in[188 * pk - io.ts_base] != 0x47) atomicAdd(io.sync_err, 1u);
     }
     // BBHEADER (bbheader:272-325), uniform across the workgroup: MATYPE-1 = TS, SIS, CCM, ISSYI 0,
     // NPD 0, RO 0; ISI 0; bytes 0..7 big-endian in hw, byte 8 = SYNCD low, byte 9 = CRC-8
@@ -582,15 +613,15 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
 
 // resident FEC workgroups for a persistent launch: FEC_WG_PER_CU per CU of the current device
 static int fec_grid(int nblocks) {
-  static int ncu[64] = {0};
+  static std::atomic<int> ncu[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (!ncu[dev]) {
-    int n = 0;
+  int n = ncu[dev].load(std::memory_order_relaxed);
+  if (!n) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    ncu[dev] = n;
+    ncu[dev].store(n, std::memory_order_relaxed);
   }
-  return nblocks < ncu[dev] * FEC_WG_PER_CU ? nblocks : ncu[dev] * FEC_WG_PER_CU;
+  return nblocks < n * FEC_WG_PER_CU ? nblocks : n * FEC_WG_PER_CU;
 }
 
 
@@ -842,11 +873,8 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
   int smem = map_smem(d.cs, d.nldpc / 8 + 4, io.apply_ci);
   if (smem > MAP_LDS_MAX) return hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void *)map_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, MAP_LDS_MAX);
-    attr_set = true;
-  }
+  hipError_t e = lds_limit((const void *)map_kernel, MAP_LDS_MAX);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(map_kernel, dim3(io.nblocks), dim3(MAP_THREADS), smem, s, d, io);
   return hipGetLastError();
 }
@@ -1385,12 +1413,8 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
 template <int N, int FMT>
 static hipError_t launch_ofdm_f(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
   using Sh = OfdmShape<N>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void *)ofdm_kernel<N, FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              Sh::LDS_BYTES);
-    attr_set = true;
-  }
+  hipError_t e = lds_limit((const void *)ofdm_kernel<N, FMT>, Sh::LDS_BYTES);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((ofdm_kernel<N, FMT>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
   return hipGetLastError();
 }

@@ -461,7 +461,9 @@ int build_frame(const FmParams &p, FramePlan &fp) {
   int normal = p.framesize == 1;
   fp.cs = cell_size_of(normal, p.constellation);
   if (!fp.cs || p.fecblocks < 1 || p.t2frames < 1 || p.t2frames > 255 || p.numdatasyms < 1) return -1;
-  if (p.tiblocks < 0 || (p.tiblocks > p.fecblocks)) return -1;
+  // tiblocks > fecblocks is accepted like the reference (framemapper:1114-1119): the surplus TI
+  // blocks are "small" ones of floor(fecblocks / tiblocks) = 0 FEC blocks, which carry no cells
+  if (p.tiblocks < 0 || p.tiblocks > 255) return -1;
   int N = fft_points(p.fftsize);
   Counts c;
   if (!active_counts(p.fftsize, p.carriermode, p.pilotpattern, p.paprmode, p.guardinterval, p.preamble, c))
@@ -1102,4 +1104,15 @@ int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf
   return 0;
 }
 
+}  // namespace t2
+
+namespace t2 {
+// N_P2, C_P2, C_DATA, N_FC, C_FC of a configuration (the framemapper's cell-count tables), for the
+// CPU tests that cross-check them against the pilot maps symbol by symbol
+int frame_cell_counts(int fftsize, int carriermode, int pp, int papr, int gi, int preamble, int out[5]) {
+  Counts c;
+  if (!active_counts(fftsize, carriermode, pp, papr, gi, preamble, c)) return -1;
+  out[0] = c.n_p2; out[1] = c.c_p2; out[2] = c.c_data; out[3] = c.n_fc; out[4] = c.c_fc;
+  return 0;
+}
 }  // namespace t2

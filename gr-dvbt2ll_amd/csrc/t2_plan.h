@@ -138,4 +138,7 @@ int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf
 // time-interleaver output index (frame data order) of cell-interleaved cell t of FEC block r
 int64_t ti_dest(const FramePlan &fp, int r, int t);
 
+// framemapper cell counts {N_P2, C_P2, C_DATA, N_FC, C_FC} (framemapper:290-356, 425-915); -1 if invalid
+int frame_cell_counts(int fftsize, int carriermode, int pp, int papr, int gi, int preamble, int out[5]);
+
 }  // namespace t2

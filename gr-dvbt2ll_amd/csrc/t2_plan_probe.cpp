@@ -45,6 +45,10 @@ int t2probe_pilot(const int *p12, int *info, int32_t *bin_map, float *pilot_valu
   return 0;
 }
 
+int t2probe_counts(int fftsize, int carriermode, int pp, int papr, int gi, int preamble, int *out5) {
+  return frame_cell_counts(fftsize, carriermode, pp, papr, gi, preamble, out5);
+}
+
 // info: [mode, mod, W, R, cs]; lut 256 complex
 int t2probe_map(int framesize, int rate, int constellation, int rotation, int *info, float *lut) {
   MapPlan mp;

@@ -63,10 +63,10 @@ for _b in BLOCKS:
     EXPORTS += ["dvbt2ll_%s_%s" % (_b, f) for f in
                 ("create", "output_multiple", "forecast", "general_work", "destroy")]
 EXPORTS += ["dvbt2ll_framemapperfint_stream_items", "dvbt2ll_pilotgenp1insert_active_items",
-            "dvbt2ll_pilotgenp1insert_debug_carriers"]
+            "dvbt2ll_pilotgenp1insert_debug_carriers", "dvbt2ll_bbheaderbch_sync_errors"]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_host", "set_output", "set_slots", "set_graph", "set_timing",
                                            "get_timing", "debug_codewords", "debug_cell_pairs", "debug_cells",
-                                           "synchronize",
+                                           "synchronize", "sync_errors",
                                            "destroy")]
 
 
@@ -105,6 +105,9 @@ def lib():
     L.dvbt2ll_chain_debug_cell_pairs.argtypes = [vp, vp, i64]
     L.dvbt2ll_chain_debug_cells.argtypes = [vp, vp, i64]
     L.dvbt2ll_chain_synchronize.argtypes = [vp]
+    L.dvbt2ll_chain_sync_errors.argtypes = [vp, ctypes.POINTER(i64)]
+    L.dvbt2ll_bbheaderbch_sync_errors.argtypes = [vp]
+    L.dvbt2ll_bbheaderbch_sync_errors.restype = i64
     L.dvbt2ll_chain_destroy.argtypes = [vp]
     L.dvbt2ll_chain_destroy.restype = None
     _lib = L

@@ -67,6 +67,10 @@ class bbheaderbch_bb(_Block):
     (include/dvbt2ll/bbheaderbch_bb.h:49): TS bytes -> BBFRAME + BCH, one bit per byte."""
     _name, _params = "bbheaderbch", _BbParams
 
+    def sync_errors(self):
+        """TS sync bytes != 0x47 consumed so far (reference: a GR_LOG_WARN each, :675, :703)"""
+        return lib().dvbt2ll_bbheaderbch_sync_errors(self._h)
+
 
 class ldpc_bb(_Block):
     """gr-dtv dvb_ldpc_bb(DVBT2, framesize, rate, MOD_OTHER) replacement used between

@@ -101,6 +101,13 @@ class Chain:
         check(lib().dvbt2ll_chain_debug_cells(self._h, out.ctypes.data_as(ctypes.c_void_p), ncells), "cells")
         return out
 
+    def sync_errors(self):
+        """TS sync bytes != 0x47 consumed so far (the reference's "Transport Stream sync error!"
+        warnings, bbheaderbch_bb_impl.cc:675, 703); synchronises the device"""
+        n = ctypes.c_int64(0)
+        check(lib().dvbt2ll_chain_sync_errors(self._h, ctypes.byref(n)), "sync errors")
+        return n.value
+
     def synchronize(self):
         check(lib().dvbt2ll_chain_synchronize(self._h), "sync")
 

@@ -81,6 +81,11 @@ CONFIGS = {
                      24, 3, E.CARRIERS_NORMAL, E.FFTSIZE_8K, E.GI_1_32, E.L1_MOD_64QAM, E.PILOT_PP7, 2, 59),
     "cfg5": T2Config("cfg5-32k-256qam-5/6-pp7", E.FECFRAME_NORMAL, E.C5_6, E.MOD_256QAM, E.ROTATION_OFF,
                      197, 3, E.CARRIERS_NORMAL, E.FFTSIZE_32K, E.GI_1_128, E.L1_MOD_64QAM, E.PILOT_PP7, 2, 59),
+    # BASELINE.json config 1 as worded ("4K FFT, short FECFRAME, QPSK 1/2"): the GRC flowgraph's
+    # other parameters, 2 FEC blocks (the frame's capacity, SURVEY 6: fecblocks <= 2); tiblocks 3
+    # as in the GRC, i.e. one empty small TI block (framemapper:1114-1119)
+    "cfg1q": T2Config("cfg1q-4k-short-qpsk-1/2", E.FECFRAME_SHORT, E.C1_2, E.MOD_QPSK, E.ROTATION_ON,
+                      2, 3, E.CARRIERS_NORMAL, E.FFTSIZE_4K, E.GI_1_32, E.L1_MOD_64QAM, E.PILOT_PP7, 2, 3),
 }
 
 KBCH = {(1, 0): 32208, (1, 1): 38688, (1, 2): 43040, (1, 3): 48408, (1, 4): 51648, (1, 5): 53840,

@@ -22,21 +22,34 @@ def frame_range(total_frames, rank, world, first_frame=0):
 
 
 def gather_frames(local, total_frames, per_frame, group=None, dst=0):
-    """ordered gather of per-rank frame shards (local: [count * per_frame, ...] tensor) to rank dst.
-    Returns the [total_frames * per_frame, ...] tensor on dst, None elsewhere.  Ragged shards are
-    padded to the largest shard for the all_gather."""
+    """ordered gather of per-rank frame shards (local: [count * per_frame, ...] tensor) to rank dst,
+    the chain's one exchange step: RCCL has no gather primitive, so every other rank
+    sends its shard point-to-point (one grouped batch of isend / irecv, ncclGroupStart/End under the
+    nccl backend) straight into its place in dst's output.  dst receives world - 1 shards, the
+    other ranks receive nothing.  Returns the [total_frames * per_frame, ...] tensor on dst, None
+    elsewhere; empty shards (more ranks than frames) send nothing."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     counts = [frame_range(total_frames, r, world)[1] for r in range(world)]
+    firsts = [frame_range(total_frames, r, world)[0] for r in range(world)]
     assert local.shape[0] == counts[rank] * per_frame, "shard size mismatch"
-    cap = max(counts) * per_frame
-    pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
-    bufs = [torch.empty_like(pad) for _ in range(world)]
-    dist.all_gather(bufs, pad, group=group)
+
+    def peer(r):
+        return dist.get_global_rank(group, r) if group is not None else r
+
     if rank != dst:
+        if counts[rank]:
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), peer(dst), group)]):
+                req.wait()
         return None
-    return torch.cat([b[: c * per_frame] for b, c in zip(bufs, counts)], 0)
+    out = torch.empty((total_frames * per_frame,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    out[firsts[rank] * per_frame:(firsts[rank] + counts[rank]) * per_frame] = local
+    ops = [dist.P2POp(dist.irecv, out[firsts[r] * per_frame:(firsts[r] + counts[r]) * per_frame], peer(r), group)
+           for r in range(world) if r != dst and counts[r]]
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    return out
 
 
 def encode_sharded(chain, first_frame, total_frames, group=None, gather=True, seed=1):

@@ -57,6 +57,9 @@ int dvbt2ll_bbheaderbch_output_multiple(const dvbt2ll_bbheaderbch *h);          
 int dvbt2ll_bbheaderbch_forecast(const dvbt2ll_bbheaderbch *h, int noutput_items, int *ninput_items_required);
 int dvbt2ll_bbheaderbch_general_work(dvbt2ll_bbheaderbch *h, int noutput_items, int ninput_items,
                                      const void *in, void *out, int *consumed);
+/* TS sync bytes != 0x47 consumed so far (the reference logs "Transport Stream sync error!" for each,
+ * lib/bbheaderbch_bb_impl.cc:675-677, 703-705; the output is unaffected in both input modes) */
+int64_t dvbt2ll_bbheaderbch_sync_errors(const dvbt2ll_bbheaderbch *h);
 void dvbt2ll_bbheaderbch_destroy(dvbt2ll_bbheaderbch *h);
 
 /* ---------------------------------------------------------------------------
@@ -160,7 +163,7 @@ typedef struct {
 int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, dvbt2ll_chain **out);
 int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info);
 /* ts_dev: device pointer to TS bytes whose first byte is absolute stream offset ts_base
- * (a multiple of 188, at least one packet before the first byte the frames consume so
+ * (a multiple of 188, else DVBT2LL_EINVAL; at least one packet before the first byte the frames consume so
  * the CRC-8 of the preceding packet can be formed); ts_len bytes valid.  iq_dev receives
  * nframes * iq_samples_per_frame samples (complex64, or int16 I/Q pairs after
  * dvbt2ll_chain_set_output(.., DVBT2LL_IQ_SC16)).  stream: hipStream_t (NULL = the handle's
@@ -180,7 +183,8 @@ int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots);
  * captured on first use for each (nframes, IQ format) and re-armed per call by rewriting the
  * kernel nodes' arguments (hipGraphExecKernelNodeSetParams), then one hipGraphLaunch.  For
  * small per-call batches (one T2 frame per call, as GNU Radio's scheduler calls a block);
- * output identical to the direct launches.  Per-stage timing events are skipped in this mode.
+ * output identical to the direct launches.  One instantiated graph per buffer slot; re-arming it
+ * first waits (host side) for the slot's previous run to complete.  Per-stage timing events are skipped in this mode.
  * Default off. */
 int dvbt2ll_chain_set_graph(dvbt2ll_chain *h, int enable);
 /* host buffers, synchronous */
@@ -206,6 +210,9 @@ int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, in
 int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes);
 int dvbt2ll_chain_debug_cell_pairs(dvbt2ll_chain *h, void *out, int64_t cells);
 int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells);
+/* TS sync bytes != 0x47 consumed by all run calls so far (bbheaderbch_bb_impl.cc:675, 703);
+ * synchronises the device */
+int dvbt2ll_chain_sync_errors(dvbt2ll_chain *h, int64_t *count);
 int dvbt2ll_chain_synchronize(dvbt2ll_chain *h);
 void dvbt2ll_chain_destroy(dvbt2ll_chain *h);
 

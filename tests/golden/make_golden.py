@@ -18,7 +18,7 @@ sys.path[:0] = [str(HERE.parent), str(HERE.parents[1] / "gr-dvbt2ll_amd")]
 from dvbt2ll.configs import CONFIGS, ts_for_frames  # noqa: E402
 import oracle_lib as O  # noqa: E402
 
-CASES = {"cfg1": (2, True), "cfg4": (1, False)}   # name: (frames, keep carriers)
+CASES = {"cfg1": (2, True), "cfg1q": (2, True), "cfg4": (1, False)}   # name: (frames, keep carriers)
 
 
 def stages(cfg, nframes):

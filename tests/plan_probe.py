@@ -27,6 +27,7 @@ def lib():
         L.t2probe_map.argtypes = [ctypes.c_int] * 4 + [vp, vp]
         L.t2probe_fec.argtypes = [ctypes.c_int] * 3 + [vp, vp, vp]
         L.t2probe_chain.argtypes = [vp] * 9
+        L.t2probe_counts.argtypes = [ctypes.c_int] * 6 + [vp]
         L.t2probe_aux_lists.argtypes = [vp] * 9
         _L = L
     return _L
@@ -71,6 +72,14 @@ def pilot_plan(pg_args):
     assert lib().t2probe_pilot(_p(p), _p(info), _p(bm), _p(pv), _p(p1), _p(isinc), _p(norm)) == 0
     return dict(Nsym=Nsym, N=N, active=int(info[2]), G=int(info[3]), C_PS=int(info[4]), eq=int(info[5]),
                 bin_map=bm.reshape(Nsym, N), pilot_values=pv, p1=p1, isinc=isinc, norm=float(norm[0]))
+
+
+def cell_counts(fftsize, carriermode, pp, papr, gi, preamble):
+    """framemapper cell-count table entry {N_P2, C_P2, C_DATA, N_FC, C_FC} or None"""
+    out = np.zeros(5, np.int32)
+    if lib().t2probe_counts(fftsize, carriermode, pp, papr, gi, preamble, _p(out)):
+        return None
+    return dict(zip(["N_P2", "C_P2", "C_DATA", "N_FC", "C_FC"], (int(x) for x in out)))
 
 
 def map_plan(framesize, rate, constellation, rotation):

@@ -55,6 +55,8 @@ def _worker(rank, world, port, total, q):
         per = ref.shape[1]
         local = torch.from_numpy(ref.reshape(-1).view(np.float32).reshape(-1, 2).copy())
         got = D.gather_frames(local, total, per)
+        if rank != 0:
+            assert got is None           # only the root receives (point-to-point, not all_gather)
         if rank == 0:
             want = _oracle_frames(cfg, total).reshape(-1).view(np.float32).reshape(-1, 2)
             q.put(bool(np.array_equal(got.numpy(), want)))
@@ -62,14 +64,15 @@ def _worker(rank, world, port, total, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("total", [4, 5])
-def test_gloo_two_rank_ordered_gather(total):
+@pytest.mark.parametrize("total,world", [(4, 2), (5, 2), (2, 3)])
+def test_gloo_ordered_gather(total, world):
+    """world_size 2 (even and ragged shards) and 3 with one empty shard"""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, total, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

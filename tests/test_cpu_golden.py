@@ -10,7 +10,7 @@ from dvbt2ll.configs import CONFIGS, ts_for_frames
 GOLD = Path(__file__).resolve().parent / "golden"
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg4"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg4"])
 def test_oracle_reproduces_golden(name):
     import sys
     sys.path.insert(0, str(GOLD))

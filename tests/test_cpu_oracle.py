@@ -81,7 +81,7 @@ def test_ts_generator_structure_and_slicing():
     np.testing.assert_array_equal(full[base:], buf)
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_oracle_cell_counts_consistent(name):
     """framemapper mapped_items == pilotgen active_items: C_P2/C_DATA/N_FC tables agree with the
     pilot maps, and the interleaver cell counts match"""
@@ -98,3 +98,100 @@ def test_bbheader_hem_and_inband_run():
     ts = ts_packets(0, 200)
     out, cons = bb.work(ts, 4)
     assert len(out) == 4 * bb.nbch and cons > 0
+
+
+# ---------------------------------------------------------------- independent cross-checks of the
+# extracted tables (the oracle and the product share tools/extract_tables.py's header, so an
+# extraction error would be common-mode; these tie it to data extracted from elsewhere)
+
+def _pilot_combos():
+    """every (FFT size, pilot pattern, carrier mode, PAPR, preamble) the framemapper's cell-count
+    table accepts, with one guard interval per distinct frame-closing (N_FC) behaviour"""
+    import plan_probe as PP
+    seen = {}
+    for fft in (0, 1, 2, 3, 4, 5, 6, 7, 11):
+        for pp in range(8):
+            for car in (0, 1):
+                for papr in range(4):
+                    for gi in range(7):
+                        for pre in (0, 1, 3, 4):
+                            c = PP.cell_counts(fft, car, pp, papr, gi, pre)
+                            if c and c["C_DATA"] > 0:
+                                seen.setdefault((fft, pp, car, papr, pre, c["N_FC"] > 0), (gi, c))
+    return sorted(seen.items())
+
+
+@pytest.mark.parametrize("fft", [0, 1, 2, 3, 4, 5, 6, 7, 11])
+def test_pilot_maps_match_cell_count_tables(fft):
+    """For every accepted combination: the data carriers per symbol of the oracle's pilot maps
+    (pilotgen:1285-2782, from the pilot-position tables :2909-3505) and of the product planner's
+    maps equal C_P2 for the P2 symbols, C_DATA for data symbols and N_FC for the frame-closing
+    symbol -- the framemapper's own tables (framemapper:290-356, 425-915), extracted separately.
+    The data cells fill the carriers in input order."""
+    import plan_probe as PP
+    from dvbt2ll.configs import FFT_POINTS
+    nds = 3
+    for (f, pp, car, papr, pre, _), (gi, c) in _pilot_combos():
+        if f != fft:
+            continue
+        args = (car, f, pp, gi, nds, papr, 0, pre, 0, 0, 3, FFT_POINTS[f])
+        want = [c["C_P2"]] * c["N_P2"] + [c["C_DATA"]] * (nds - (1 if c["N_FC"] else 0)) + \
+               ([c["N_FC"]] if c["N_FC"] else [])
+        plan = PP.pilot_plan(args)
+        got = list((plan["bin_map"] >= 0).sum(axis=1))
+        assert got == want, (args, got, want)
+        pg = O.PG(*args)
+        active = pg.active_items
+        assert active == sum(want)
+        cells = (np.arange(active, dtype=np.float32) + 1.0) + 1j * np.float32(4321.0)
+        car_ = pg.carriers(cells.astype(np.complex64))
+        mark = car_.imag == np.float32(4321.0)
+        assert list(mark.sum(axis=1)) == want, (args, list(mark.sum(axis=1)), want)
+        np.testing.assert_array_equal(car_.real[mark], np.arange(active, dtype=np.float32) + 1.0)
+
+
+# LDPC edge counts from the DVB-S2/T2 degree distributions (EN 302 307 table 7a, EN 302 755 table
+# A.1): normal frames have q * 360 parity bits and info-bit degrees {high, 3}
+LDPC_EDGES = {(1, 0): 12960 * 8 + 19440 * 3, (1, 1): 12960 * 12 + 25920 * 3, (1, 2): 4320 * 13 + 38880 * 3,
+              (1, 3): 5400 * 12 + 43200 * 3, (1, 4): 6480 * 11 + 45360 * 3, (1, 5): 5400 * 13 + 48600 * 3,
+              (0, 4): 12600 * 3}
+
+
+@pytest.mark.parametrize("framesize,rate", [(1, r) for r in range(6)] + [(0, r) for r in range(8)])
+def test_ldpc_table_structure(framesize, rate):
+    """the extracted LDPC tables have the standard's shape: k/360 rows (one per info group), every
+    row of one of two degrees with the low degree 3, entries < nldpc - k, and the known edge
+    counts (e.g. 3/5 normal 233,280; 4/5 short 37,800)"""
+    import plan_probe as PP
+    f = PP.fec_plan(framesize, rate)
+    nldpc = 64800 if framesize else 16200
+    k = f["nbch"]
+    q = f["q"]
+    assert q * 360 == nldpc - k
+    ent = f["ent"]
+    groups = ent >> 16
+    deg = np.bincount(groups, minlength=k // 360)
+    assert len(deg) == k // 360
+    degs = set(deg.tolist())
+    assert 3 in degs and len(degs - {3}) <= 1, degs
+    assert (ent & 0xFFFF).max() < 360
+    edges = int(deg.sum()) * 360
+    if (framesize, rate) in LDPC_EDGES:
+        assert edges == LDPC_EDGES[(framesize, rate)]
+
+
+def test_extracted_tables_match_reference():
+    """tools/extract_tables.py re-run on the reference tree reproduces the committed generated
+    header byte for byte (build container only: the reference does not travel)"""
+    import subprocess
+    import sys
+    from pathlib import Path
+    ref = Path("/root/reference")
+    if not (ref / "lib").is_dir():
+        pytest.skip("reference tree not present")
+    root = Path(__file__).resolve().parents[1]
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        out = Path(d) / "t.h"
+        subprocess.run([sys.executable, str(root / "tools" / "extract_tables.py"), str(ref), str(out)], check=True)
+        assert out.read_bytes() == (root / "gr-dvbt2ll_amd" / "csrc" / "gen" / "dvbt2_std_tables.h").read_bytes()

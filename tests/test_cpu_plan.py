@@ -37,6 +37,7 @@ def _apply(gmap, src, aux):
 
 
 BASE = CONFIGS["cfg1"]
+BENCH_CFGS = ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"]
 GRID = [
     # (name, overrides)
     ("4k_grc", {}),
@@ -101,8 +102,8 @@ def test_framemapper_map_matches_oracle(name, over):
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
-@pytest.mark.parametrize("name,over", GRID + [("cfg%d" % i, None) for i in range(1, 6)],
-                         ids=[g[0] for g in GRID] + ["cfg%d" % i for i in range(1, 6)])
+@pytest.mark.parametrize("name,over", GRID + [(n, None) for n in BENCH_CFGS],
+                         ids=[g[0] for g in GRID] + BENCH_CFGS)
 def test_chain_cell_layout_matches_oracle(name, over):
     """the fused chain's indexing, as the kernels apply it: the map kernel stores QAM cell (r, j)
     at ti_dest(r, (perm[j] + shift[r]) mod cs); the OFDM kernel fills aux bins from cmap < 0 and
@@ -144,8 +145,8 @@ def test_chain_cell_layout_matches_oracle(name, over):
         np.testing.assert_array_equal(bins.view(np.uint32), want[j].view(np.uint32), err_msg="symbol %d" % j)
 
 
-@pytest.mark.parametrize("name,over", GRID + [("cfg%d" % i, None) for i in range(1, 6)],
-                         ids=[g[0] for g in GRID] + ["cfg%d" % i for i in range(1, 6)])
+@pytest.mark.parametrize("name,over", GRID + [(n, None) for n in BENCH_CFGS],
+                         ids=[g[0] for g in GRID] + BENCH_CFGS)
 def test_chain_aux_lists_match_cmap(name, over):
     """the OFDM kernel's non-data bins (t2_kernels.hip sub_ifft, scatter mode): the zero run
     [z0, z1), the direct (bin, value) quads and the indirect entries through aux variant v.  For
@@ -210,7 +211,7 @@ def test_pilot_map_matches_oracle(name, over):
     assert np.abs(plan["p1"] - pg.p1()).max() < 2e-6
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_benchmark_configs_plan(name):
     cfg = CONFIGS[name]
     fplan = PP.frame_plan(cfg.fm_args())

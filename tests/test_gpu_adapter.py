@@ -1,0 +1,68 @@
+"""GPU: the header-only GNU Radio adapters (include/dvbt2ll/*_impl_hip.h) compiled into a
+GR-style scheduler (tests/adapter/gr_flowgraph.cpp, against the stand-in GR headers in
+tests/gr_stub): make() -> set_output_multiple -> forecast -> general_work with random multiples of
+the output multiple and random-size TS chunks -> consume_each, over several T2 frames.  The IQ it
+writes equals the oracle chain (IQ bounds of SURVEY 8(c)) and, bit for bit, the fused chain."""
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import dvbt2ll
+from dvbt2ll.configs import CONFIGS, ts_for_frames
+import iq_check
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+DRIVER = Path(__file__).resolve().parent / "adapter" / "gr_flowgraph"
+
+
+def params(cfg):
+    return [str(int(v)) for v in cfg.fm_args()] + [str(int(v)) for v in
+                                                   (cfg.misogroup, cfg.equalization, cfg.bandwidth, cfg.tsrate)]
+
+
+def run_driver(tmp_path, cfg, nframes, ts, seed):
+    (tmp_path / "in.ts").write_bytes(ts.tobytes())
+    r = subprocess.run([str(DRIVER), str(tmp_path / "in.ts"), str(tmp_path / "iq.bin"), str(nframes), str(seed)]
+                       + params(cfg), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    return np.fromfile(tmp_path / "iq.bin", np.complex64), r
+
+
+@pytest.mark.parametrize("name,nframes,seed", [("cfg1", 4, 1), ("cfg1q", 3, 2), ("cfg4", 3, 3), ("cfg1", 3, 4)])
+def test_gr_adapter_flowgraph(gpu, tmp_path, name, nframes, seed):
+    cfg = CONFIGS[name]
+    ts, base = ts_for_frames(cfg, 0, nframes + 1)
+    assert base == 0
+    iq, r = run_driver(tmp_path, cfg, nframes, ts, seed)
+    assert "warnings=0" in r.stdout.splitlines()[0]
+    ch = dvbt2ll.Chain(cfg, max_frames=nframes)
+    want = ch.run(0, nframes)
+    np.testing.assert_array_equal(iq.view(np.uint32), want.view(np.uint32))
+    # and the oracle chain, frame by frame
+    F = cfg.fecblocks
+    bb = O.BB(*cfg.bb_args()); ld = O.LDPC(cfg.framesize, cfg.rate); im = O.IM(*cfg.im_args())
+    fm = O.FM(*cfg.fm_args()); pg = O.PG(*cfg.pg_args())
+    per, off = ch.iq_per_frame, 0
+    for k in range(nframes):
+        bits, cons = bb.work(ts[off:], F)
+        off += cons
+        car = pg.carriers(fm.work(im.work(ld.work(bits, F), F)))
+        iq_check.check_frame(iq[k * per:(k + 1) * per], car, pg.vlength, pg.guard, pg.normalization, pg.p1(),
+                             "adapter %s frame %d" % (name, k))
+
+
+def test_gr_adapter_sync_warnings(gpu, tmp_path):
+    """the bbheaderbch adapter logs one "Transport Stream sync error!" per corrupted sync byte,
+    as the reference does (bbheaderbch_bb_impl.cc:703-705), and the IQ is unchanged"""
+    cfg = CONFIGS["cfg1"]
+    ts, _ = ts_for_frames(cfg, 0, 3)
+    clean, _ = run_driver(tmp_path, cfg, 2, ts, 5)
+    bad = ts.copy()
+    bad[[188 * 5, 188 * 40]] = 0
+    dirty, r = run_driver(tmp_path, cfg, 2, bad, 5)
+    assert "bbheaderbch_bb" in r.stdout and "warnings=2" in r.stdout.splitlines()[0], r.stdout
+    assert r.stderr.count("Transport Stream sync error!") == 2
+    np.testing.assert_array_equal(dirty.view(np.uint32), clean.view(np.uint32))

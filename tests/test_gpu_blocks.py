@@ -10,11 +10,9 @@ import dvbt2ll
 from dvbt2ll import enums as E
 from dvbt2ll.configs import CONFIGS, ts_for_frames, ts_packets
 import oracle_lib as O
+import iq_check
 
 pytestmark = pytest.mark.gpu
-
-IQ_RTOL = 2e-6   # IFFT tolerance: max |GPU - float64 IFFT| / rms(float64 IFFT)
-
 
 def _ts(cfg, nframes=1):
     ts, base = ts_for_frames(cfg, 0, nframes)
@@ -22,7 +20,7 @@ def _ts(cfg, nframes=1):
     return ts
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_bbheaderbch_bit_exact(gpu, name):
     cfg = CONFIGS[name]
     ts = _ts(cfg)
@@ -55,7 +53,7 @@ def test_bbheaderbch_split_calls(gpu, name):
         off += cons
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_ldpc_bit_exact(gpu, name):
     cfg = CONFIGS[name]
     bb = O.BB(*cfg.bb_args())
@@ -67,7 +65,7 @@ def test_ldpc_bit_exact(gpu, name):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_interleavermod_bit_exact(gpu, name):
     cfg = CONFIGS[name]
     bb = O.BB(*cfg.bb_args())
@@ -115,15 +113,7 @@ def test_pilotgen_carriers_bit_exact_and_iq(gpu, name):
     np.testing.assert_array_equal(got_car.view(np.uint32), want_car.view(np.uint32))
     iq = np.zeros(pg.output_items, np.complex64)
     assert blk.general_work([mapped], [iq]) == pg.output_items
-    N, G = pg.vlength, pg.guard
-    ref_p1 = pg.p1()
-    assert np.abs(iq[:2048] - ref_p1).max() <= 1e-5
-    for j in range(pg.num_symbols):
-        x = np.fft.ifft(np.fft.fftshift(want_car[j].astype(np.complex128))) * N * pg.normalization
-        ref = np.concatenate([x[N - G:], x])
-        y = iq[2048 + j * (N + G): 2048 + (j + 1) * (N + G)]
-        rms = np.sqrt(np.mean(np.abs(ref) ** 2))
-        assert np.abs(y - ref).max() <= IQ_RTOL * rms * 10, (j, np.abs(y - ref).max() / rms)
+    iq_check.check_frame(iq, want_car, pg.vlength, pg.guard, pg.normalization, pg.p1(), "pilotgen " + name)
 
 
 ALL_CODES = [(1, r) for r in range(6)] + [(0, r) for r in range(8)]

@@ -5,6 +5,7 @@ import pytest
 import dvbt2ll
 from dvbt2ll.configs import CONFIGS, ts_for_frames
 import oracle_lib as O
+import iq_check
 
 pytestmark = pytest.mark.gpu
 
@@ -25,7 +26,7 @@ def oracle_chain(cfg, nframes):
     return out, pg
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_chain_cells_match_oracle(gpu, name):
     """stage check inside the fused chain: the cells buffer (FEC + bit interleave + QAM + cell
     and time interleaving = the frame data region in transmission order) equals the oracle's"""
@@ -54,21 +55,14 @@ def _check_chain(cfg, nframes):
     ref, pg = oracle_chain(cfg, nframes)
     ch = dvbt2ll.Chain(cfg, max_frames=nframes)
     iq = ch.run(0, nframes)
-    N, G = pg.vlength, pg.guard
     per = ch.iq_per_frame
+    p1 = pg.p1()
     for k in range(nframes):
-        car = ref[k][0]
-        f = iq[k * per:(k + 1) * per]
-        for j in range(pg.num_symbols):
-            x = np.fft.ifft(np.fft.fftshift(car[j].astype(np.complex128))) * N * pg.normalization
-            want = np.concatenate([x[N - G:], x])
-            y = f[2048 + j * (N + G): 2048 + (j + 1) * (N + G)]
-            rms = np.sqrt(np.mean(np.abs(want) ** 2))
-            assert np.abs(y - want).max() <= 2e-5 * rms, (k, j, np.abs(y - want).max() / rms)
-        assert np.abs(f[:2048] - pg.p1()).max() <= 1e-5
+        iq_check.check_frame(iq[k * per:(k + 1) * per], ref[k][0], pg.vlength, pg.guard, pg.normalization, p1,
+                             "%s frame %d" % (cfg.name, k))
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg3", "cfg4", "cfg5"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_chain_iq_matches_oracle(gpu, name):
     _check_chain(CONFIGS[name], 3 if name == "cfg1" else (2 if name == "cfg3" else 1))
 

@@ -88,3 +88,87 @@ def test_chain_rejects_oversized_fecblocks(gpu):
     big = dataclasses.replace(cfg, fecblocks=cfg.fecblocks * 4)
     with pytest.raises(dvbt2ll.DVBT2Error):
         dvbt2ll.Chain(big, max_frames=1)
+
+
+@pytest.mark.parametrize("mode", [dvbt2ll.INPUTMODE_NORMAL, dvbt2ll.INPUTMODE_HIEFF], ids=["nm", "hem"])
+def test_sync_errors_counted_output_unchanged(gpu, mode):
+    """a TS sync byte != 0x47 is what the reference warns about ("Transport Stream sync error!",
+    bbheaderbch_bb_impl.cc:675-677, 703-705) without changing its output (NM: the slot carries the
+    CRC-8; HEM: the byte is dropped).  Block and chain count exactly the corrupted sync bytes the
+    encoded frames consume, and produce the same output as for the clean stream."""
+    import oracle_lib as O
+    cfg = CONFIGS["cfg1"].with_(inputmode=mode)
+    ts, base = ts_for_frames(cfg, 0, 2)
+    assert base == 0
+    bad = ts.copy()
+    corrupt = [3, 10, 17]               # packets whose sync byte the first frame consumes
+    bad[[188 * p for p in corrupt]] = 0x46
+    F = cfg.fecblocks
+    want, cons = O.BB(*cfg.bb_args()).work(ts, F)
+    assert cons > 188 * 18
+    blk = dvbt2ll.bbheaderbch_bb(*cfg.bb_args())
+    got = np.zeros_like(want)
+    blk.general_work([bad], [got])
+    np.testing.assert_array_equal(got, want)
+    assert blk.sync_errors() == len(corrupt)
+    ch = dvbt2ll.Chain(cfg, max_frames=1)
+    clean = ch.run(0, 1)
+    assert ch.sync_errors() == 0
+    dirty = ch.run(0, 1, ts=bad, ts_base=0)
+    np.testing.assert_array_equal(dirty.view(np.uint32), clean.view(np.uint32))
+    assert ch.sync_errors() == len(corrupt)
+
+
+def test_chain_rejects_unaligned_ts_base(gpu):
+    cfg = CONFIGS["cfg1"]
+    ch = dvbt2ll.Chain(cfg, max_frames=1)
+    ts, base = ts_for_frames(cfg, 2, 1)
+    with pytest.raises(dvbt2ll.DVBT2Error):
+        ch.run(2, 1, ts=ts[1:], ts_base=base + 1)
+
+
+def test_graph_mode_async_calls_on_two_streams(gpu):
+    """hipGraph mode re-armed by back-to-back asynchronous calls on two streams with two slots (no
+    host synchronisation between calls): every call's IQ equals the direct launches' bit-exactly"""
+    import torch
+    cfg = CONFIGS["cfg1"]
+    B, ncalls = 1, 8
+    ref = dvbt2ll.Chain(cfg, max_frames=B)
+    ch = dvbt2ll.Chain(cfg, max_frames=B)
+    ch.set_slots(2)
+    ch.set_graph(True)
+    per = ch.iq_per_frame
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    ts_all, base_all = ts_for_frames(cfg, 0, B * ncalls)
+    ts_dev = torch.from_numpy(ts_all).cuda()
+    outs = [torch.empty((B * per, 2), dtype=torch.float32, device="cuda") for _ in range(ncalls)]
+    torch.cuda.synchronize()
+    for c in range(ncalls):
+        ch.run_device(ts_dev.data_ptr(), base_all, len(ts_all), c * B, B, outs[c].data_ptr(),
+                      streams[c % 2].cuda_stream)
+    torch.cuda.synchronize()
+    for c in range(ncalls):
+        want = ref.run(c * B, B)
+        got = outs[c].cpu().numpy().view(np.complex64).reshape(-1)
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg="call %d" % c)
+
+
+def test_timing_with_two_streams(gpu):
+    """stage timing enabled while calls alternate over two streams and two slots: every call's
+    three stages are counted once and the fold succeeds (each run's end event is waited on)"""
+    import torch
+    cfg = CONFIGS["cfg1"]
+    ch = dvbt2ll.Chain(cfg, max_frames=2)
+    ch.set_slots(2)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    ts_all, base_all = ts_for_frames(cfg, 0, 2)
+    ts_dev = torch.from_numpy(ts_all).cuda()
+    outs = [torch.empty((2 * ch.iq_per_frame, 2), dtype=torch.float32, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    ch.set_timing(True)
+    for c in range(10):
+        ch.run_device(ts_dev.data_ptr(), base_all, len(ts_all), 0, 2, outs[c % 2].data_ptr(),
+                      streams[c % 2].cuda_stream)
+    ms, n = ch.timing()
+    assert n == [10, 10, 10] and all(t > 0 for t in ms)
+    ch.set_timing(False)

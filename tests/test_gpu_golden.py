@@ -20,7 +20,7 @@ def _eq(got, g, key):
         assert hashlib.sha256(np.ascontiguousarray(got).tobytes()).digest() == g[key + "_sha256"].tobytes(), key
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg4"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg4"])
 def test_blocks_reproduce_golden(gpu, name):
     cfg = CONFIGS[name]
     g = np.load(GOLD / ("%s.npz" % name))
