@@ -23,9 +23,30 @@ def width_of(name):
     return m.group(1), WIDTH.get(m.group(2), m.group(2))
 
 
+ORDER = [("rd", 2), ("rd", 4), ("rd", 8), ("rd", 16), ("wr", 2), ("wr", 4), ("wr", 8), ("wr", 16)]
+
+
+def from_db(d, rows):
+    """rocpd (sqlite) output: kernel names are truncated (-T), so the launch order of
+    tools/fetch_calib.hip (rd 2/4/8/16 B, wr 2/4/8/16 B, twice) identifies each dispatch"""
+    import sqlite3
+    for fn in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
+        c = sqlite3.connect(fn)
+        k = 0
+        for name, ctr, val in c.execute("select kernel_name, counter_name, value from counters_collection "
+                                        "order by dispatch_id"):
+            if not (name.startswith("rd_kernel") or name.startswith("wr_kernel")):
+                continue
+            kind, w = ORDER[k % len(ORDER)]
+            assert name.startswith(kind), (name, kind)
+            rows[(ctr, kind, w)].append(float(val))
+            k += 1
+
+
 def main(dirs):
     rows = defaultdict(list)
     for d in dirs:
+        from_db(d, rows)
         for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(fn) as fh:
                 for r in csv.DictReader(fh):
