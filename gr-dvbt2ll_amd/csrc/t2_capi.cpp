@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -86,18 +87,21 @@ struct DeviceCtx {
 // ---------------------------------------------------------------- FEC tables on device
 struct FecTables {
   FecPlan plan;
-  DevBuf hcrc, tab, m1, rowptr, ent, prbs, crc8, crcsh;
+  DevBuf hcrc, tab, m1, m64, rowptr, ent, prbs, crc8, crcsh;
   FecDev dev{};
   int init(int framesize, int rate, int constellation, int mode, int inband, int fecblocks, int tsrate) {
-    if (build_fec(framesize, rate, constellation, plan)) return DVBT2LL_EINVAL;
+    // tuning knob for kernel experiments (tools/): waves sharing the BCH division, default 1
+    const char *bw = std::getenv("DVBT2LL_FEC_BCH_WAVES");
+    if (build_fec(framesize, rate, constellation, plan, bw ? std::atoi(bw) : 1)) return DVBT2LL_EINVAL;
     int r;
-    if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) ||
+    if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) || (r = upload(m64, plan.bch_m64)) ||
         (r = upload(rowptr, plan.ldpc_rowptr)) || (r = upload(ent, plan.ldpc_ent)) ||
         (r = upload(prbs, plan.prbs_bytes)) || (r = upload(crc8, plan.crc8_tab)) || (r = upload(crcsh, plan.crc8_shift)) ||
         (r = upload(hcrc, plan.hcrc_bits)))
       return r;
     dev.bch_tab = tab.as<uint64_t>();
     dev.bch_m1 = m1.as<uint64_t>();
+    dev.bch_m64 = m64.as<uint64_t>();
     dev.ldpc_rowptr = rowptr.as<uint16_t>();
     dev.ldpc_ent = ent.as<uint32_t>();
     dev.prbs = prbs.as<uint8_t>();
@@ -106,6 +110,7 @@ struct FecTables {
     dev.hcrc_bits = hcrc.as<uint8_t>();
     dev.kbch = plan.kbch; dev.nbch = plan.nbch; dev.P = plan.nparity; dev.nldpc = plan.nldpc;
     dev.q = plan.q; dev.nent = (int)plan.ldpc_ent.size(); dev.chunk = plan.bch_chunk;
+    dev.bch_waves = plan.bch_waves;
     dev.parity_il = plan.parity_interleave ? 1 : 0;
     dev.hem = mode ? 1 : 0;
     dev.inband = inband ? 1 : 0;

@@ -14,7 +14,8 @@ enum FecMode {
 
 struct FecDev {
   const uint64_t *bch_tab;      // 256 x 3
-  const uint64_t *bch_m1;       // 192 x 3
+  const uint64_t *bch_m1;       // 192 x 3: x^(8 chunk) mod g (one wave's Horner step)
+  const uint64_t *bch_m64;      // 192 x 3: x^(8 * 64 chunk) mod g (combine of the four waves)
   const uint16_t *ldpc_rowptr;  // q + 1
   const uint32_t *ldpc_ent;     // nent
   const uint8_t *prbs;          // kbch / 8
@@ -22,6 +23,7 @@ struct FecDev {
   const uint8_t *crc8_shift;    // 8 x 256
   const uint8_t *hcrc_bits;     // 72: BBHEADER CRC-8 contribution of each header bit
   int kbch, nbch, P, nldpc, q, nent, chunk, parity_il;
+  int bch_waves;                // waves sharing the BCH division (t2_plan FecPlan::bch_waves)
   int hem, inband, fec_blocks, ts_rate;
 };
 

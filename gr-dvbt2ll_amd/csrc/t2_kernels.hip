@@ -161,6 +161,7 @@ constexpr int SM_D = SM_PHASE;                               // rows follow D at
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
 constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_BYTES ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_BYTES);
 static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0, "LDS carve alignment");
+static_assert(SM_SYNC % 8 == 0 && SM_HCRC - SM_SYNC >= 4 * 3 * 8, "BCH wave remainders in SM_SYNC + SM_W");
 static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "six FEC workgroups per CU");
 
 // stream position of payload byte J (counted over the payload bytes of the whole stream)
@@ -210,29 +211,48 @@ __device__ __forceinline__ void ldpc_group_word(uint32_t *D, const uint8_t *fram
                       ((uint32_t)gb[(b + 2) % 45] << 8) | (uint32_t)gb[(b + 3) % 45];
 }
 
-// BCH parity of the BBFRAME frame[0..L) on one wave, written MSB (x^(P-1)) first to frame[L..):
-// lane t divides chunk t (64 chunks of C bytes, t2_plan: bch_chunk) by the byte table, then one
-// Horner pass over the lanes with the shift matrix M1 (v -> v x^(8C) mod g) as wave ballots.
+// new = M . a over GF(2) for the uniform 192-bit vector a, as three wave ballots: lane l holds rows
+// l, l + 64, l + 128 of M (m[s] = row l + 64 s)
+__device__ __forceinline__ void gf2_matvec(const uint64_t m[3][3], uint64_t &a0, uint64_t &a1, uint64_t &a2) {
+  const uint64_t n0 = __ballot(row_parity(m[0], a0, a1, a2));
+  const uint64_t n1 = __ballot(row_parity(m[1], a0, a1, a2));
+  const uint64_t n2 = __ballot(row_parity(m[2], a0, a1, a2));
+  a0 = n0;
+  a1 = n1;
+  a2 = n2;
+}
+
+__device__ __forceinline__ void load_rows(uint64_t m[3][3], const uint64_t *g, int lane) {
+  asm volatile("" : "+s"(g));   // keep the row loads out of the loop-carried register set
+  for (int s = 0; s < 3; s++)
+    for (int k = 0; k < 3; k++) m[s][k] = g[(lane + 64 * s) * 3 + k];
+}
+
+// One wave's share of the BCH parity of the BBFRAME frame[0..L): lane t = 64 w + lane divides chunk
+// t of the NC = 64 bch_waves chunks of C bytes (t2_plan: bch_chunk; the chunks end at L, leading
+// ones may be empty) by the byte table, then a Horner pass over the wave's 64 lanes with M1 (v -> v x^(8C)
+// mod g) as wave ballots.  Returns the wave's remainder sum_l r_l x^(8C (63 - l)) (uniform).
 // P is a template parameter so the register geometry (top byte, masks) is compile-time.
 template <int P>
-__device__ __forceinline__ void bch_wave(uint8_t *frame, const uint64_t *btab, const uint64_t *m1g, int L, int C,
-                                         int lane) {
-  const int lo = L - (64 - lane) * C, hi = L - (63 - lane) * C;
+__device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64_t *btab, const uint64_t *m1g,
+                                              int L, int C, int NC, int t, int lane, uint64_t a[3]) {
+  const int lo = L - (NC - t) * C, hi = L - (NC - 1 - t) * C;
   constexpr int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
   constexpr uint64_t k1 = P >= 128 ? ~0ull : (1ull << (P - 64)) - 1;
   constexpr uint64_t k2 = P >= 192 ? ~0ull : P <= 128 ? 0ull : (1ull << (P - 128)) - 1;
-  // per-lane rows of M1, loaded up front (reloaded per block, L1/L2 hits: kept out of the
-  // loop-carried register set)
-  const uint64_t *m1p = m1g;
-  asm volatile("" : "+s"(m1p));
   uint64_t m1[3][3];
-  for (int s = 0; s < 3; s++)
-    for (int k = 0; k < 3; k++) m1[s][k] = m1p[(lane + 64 * s) * 3 + k];
+  load_rows(m1, m1g, lane);
   uint64_t r0 = 0, r1 = 0, r2 = 0;
-#pragma unroll 4
-  for (int i = max(lo, 0); i < hi; i++) {
+  // byte-table division; the next message byte is read before the table lookup's wait (LDS
+  // returns in order, so it costs no extra round trip)
+  int i = max(lo, 0);
+  uint32_t nxt = i < hi ? frame[i] : 0u;
+#pragma unroll 2
+  for (; i < hi; i++) {
+    const uint32_t cur = nxt;
+    if (i + 1 < hi) nxt = frame[i + 1];
     const uint32_t top = (uint32_t)(((tw == 0 ? r0 : tw == 1 ? r1 : r2) >> tsft) & 0xFF);
-    const uint32_t idx = top ^ frame[i];
+    const uint32_t idx = top ^ cur;
     r2 = ((r2 << 8) | (r1 >> 56)) & k2;
     r1 = ((r1 << 8) | (r0 >> 56)) & k1;
     r0 <<= 8;
@@ -242,12 +262,29 @@ __device__ __forceinline__ void bch_wave(uint8_t *frame, const uint64_t *btab, c
   }
   uint64_t a0 = rd_lane_u64(r0, 0), a1 = rd_lane_u64(r1, 0), a2 = rd_lane_u64(r2, 0);
   for (int l = 1; l < 64; l++) {
-    const uint64_t n0 = __ballot(row_parity(m1[0], a0, a1, a2));
-    const uint64_t n1 = __ballot(row_parity(m1[1], a0, a1, a2));
-    const uint64_t n2 = __ballot(row_parity(m1[2], a0, a1, a2));
-    a0 = n0 ^ rd_lane_u64(r0, l);
-    a1 = n1 ^ rd_lane_u64(r1, l);
-    a2 = n2 ^ rd_lane_u64(r2, l);
+    gf2_matvec(m1, a0, a1, a2);
+    a0 ^= rd_lane_u64(r0, l);
+    a1 ^= rd_lane_u64(r1, l);
+    a2 ^= rd_lane_u64(r2, l);
+  }
+  a[0] = a0;
+  a[1] = a1;
+  a[2] = a2;
+}
+
+// the nw wave remainders R_w (LDS, 3 words each) -> (..(R0 M64 + R1) M64 + ..) M64 + R_(nw-1),
+// written MSB (x^(P-1)) first as the BCH parity bytes frame[L..L + P/8) (bbheader:504-531)
+template <int P>
+__device__ __forceinline__ void bch_combine(uint8_t *frame, const uint64_t *wres, const uint64_t *m64g, int L,
+                                            int nw, int lane) {
+  uint64_t m[3][3];
+  if (nw > 1) load_rows(m, m64g, lane);
+  uint64_t a0 = wres[0], a1 = wres[1], a2 = wres[2];
+  for (int w = 1; w < nw; w++) {
+    gf2_matvec(m, a0, a1, a2);
+    a0 ^= wres[3 * w];
+    a1 ^= wres[3 * w + 1];
+    a2 ^= wres[3 * w + 2];
   }
   const uint64_t acc[3] = {a0, a1, a2};
   if (lane < P / 8) frame[L + lane] = get_byte192(acc, P - 8 - 8 * lane);
@@ -269,6 +306,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   uint32_t *D = (uint32_t *)(smem + SM_D);
   uint32_t *Wv = (uint32_t *)(smem + SM_W);
   uint32_t *ents = (uint32_t *)(smem + SM_ENT);
+  uint64_t *wres = (uint64_t *)(smem + SM_SYNC);   // BCH wave remainders (SM_SYNC + SM_W, free then)
 
   // ---- constant tables into LDS, once: the workgroup then loops over FEC blocks
   for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
@@ -443,19 +481,35 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     FEC_PHASE(4);
     FEC_PHASE(5);
 
-    // ---- BCH on wave 0: lane t divides chunk t (64 chunks of C bytes, t2_plan: bch_chunk), then a
-    //      Horner pass over the lanes with the shift matrix M1 (v -> v x^(8C) mod g) as wave ballots.
-    //      Meanwhile (chain mode) waves 1..3 lay out the LDPC info groups that hold no BCH parity.
+    // ---- BCH: waves 0 .. bch_waves - 1 divide 64 chunks each and Horner-combine them
+    //      (bch_wave_part); wave 0 then combines the wave remainders and writes the parity.  The
+    //      other waves meanwhile (chain mode) lay out the LDPC info groups that hold no BCH parity.
     const int ngroups = d.nbch / 360;
-    if (wave == 0) {
+    const int nbw = d.bch_waves, nchunks = 64 * nbw;
 #if FEC_BCH_PRIO
-      __builtin_amdgcn_s_setprio(FEC_BCH_PRIO);   // the BCH wave is the block's critical path
+    if (wave < nbw) __builtin_amdgcn_s_setprio(FEC_BCH_PRIO);   // the BCH is the block's critical path
 #endif
+    if (wave < nbw) {
+      uint64_t a[3];
       switch (P) {   // compile-time register geometry per BCH parity length (t = 12, 10, 8; short 12)
-        case 192: bch_wave<192>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
-        case 168: bch_wave<168>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
-        case 160: bch_wave<160>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
-        default: bch_wave<128>(frame, btab, d.bch_m1, L, d.chunk, lane); break;
+        case 192: bch_wave_part<192>(frame, btab, d.bch_m1, L, d.chunk, nchunks, tid, lane, a); break;
+        case 168: bch_wave_part<168>(frame, btab, d.bch_m1, L, d.chunk, nchunks, tid, lane, a); break;
+        case 160: bch_wave_part<160>(frame, btab, d.bch_m1, L, d.chunk, nchunks, tid, lane, a); break;
+        default: bch_wave_part<128>(frame, btab, d.bch_m1, L, d.chunk, nchunks, tid, lane, a); break;
+      }
+      if (lane < 3) wres[3 * wave + lane] = lane == 0 ? a[0] : lane == 1 ? a[1] : a[2];
+    }
+    if (nbw > 1) __syncthreads();     // uniform: every wave remainder is in LDS
+    if (wave == 0) {
+      // same wave as the remainder writes when nbw == 1: its LDS accesses complete in order
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      switch (P) {
+        case 192: bch_combine<192>(frame, wres, d.bch_m64, L, nbw, lane); break;
+        case 168: bch_combine<168>(frame, wres, d.bch_m64, L, nbw, lane); break;
+        case 160: bch_combine<160>(frame, wres, d.bch_m64, L, nbw, lane); break;
+        default: bch_combine<128>(frame, wres, d.bch_m64, L, nbw, lane); break;
       }
       if (MODE == FEC_TS_TO_TEMPU) {
         // the last info group holds the BCH parity (P < 360): lay it out here, after the parity
@@ -465,15 +519,16 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane < FEC_DW) ldpc_group_word(D, frame, ngroups - 1, lane);
       }
-#if FEC_BCH_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
     } else if (MODE == FEC_TS_TO_TEMPU) {
+      // waves 1..3 (after their BCH share, if any) lay out the info groups without parity
       for (int it = tid - 64; it < (ngroups - 1) * FEC_DW; it += FEC_THREADS - 64) {
         const int g = it / FEC_DW;
         ldpc_group_word(D, frame, g, it - g * FEC_DW);
       }
     }
+#if FEC_BCH_PRIO
+    if (wave < nbw) __builtin_amdgcn_s_setprio(0);
+#endif
     __syncthreads();
     FEC_PHASE(6);
     FEC_PHASE(7);
@@ -629,7 +684,8 @@ hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s)
   if (io.nblocks <= 0) return hipSuccess;
   // the LDS carve is sized for the standard codes: refuse anything larger
   if (d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 52 * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
-      (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.chunk * 64 < d.kbch / 8)
+      (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.bch_waves < 1 || d.bch_waves > 4 ||
+      d.chunk * 64 * d.bch_waves < d.kbch / 8)
     return hipErrorInvalidValue;
   dim3 grid(fec_grid(io.nblocks)), block(FEC_THREADS);
   switch (mode) {

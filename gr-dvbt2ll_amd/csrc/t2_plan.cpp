@@ -138,7 +138,7 @@ static bool fec_numbers(int normal, int rate, int *kbch, int *nbch, int *q, int 
   return true;
 }
 
-int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
+int build_fec(int framesize, int rate, int constellation, FecPlan &fp, int bch_waves) {
   int normal = framesize == 1;
   if (framesize != 0 && framesize != 1) return -1;
   if (!fec_numbers(normal, rate, &fp.kbch, &fp.nbch, &fp.q, &fp.nparity)) return -1;
@@ -159,9 +159,13 @@ int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
     for (int k = 0; k < 3; k++) fp.bch_tab[d * 3 + k] = v.w[k];
   }
   const int L = fp.kbch / 8;
-  // 64 chunks: the 64 lanes of the FEC kernel's BCH wave
-  fp.bch_chunk = (L + 63) / 64;
+  // 64 chunks per BCH wave: each wave combines its 64 chunk remainders with M1 = x^(8 chunk), wave
+  // 0 the wave results with M64
+  if (bch_waves < 1 || bch_waves > 4) return -1;
+  fp.bch_waves = bch_waves;
+  fp.bch_chunk = (L + 64 * bch_waves - 1) / (64 * bch_waves);
   fp.bch_m1 = shift_matrix(g, P, 8L * fp.bch_chunk);
+  fp.bch_m64 = shift_matrix(g, P, 8L * 64 * fp.bch_chunk);
   // LDPC: info group gidx (360 bits) with address x lands in parity row a = x mod q with
   // cyclic offset b = x div q (columns c = (b + n) mod 360, since pbits = 360 q)
   const t2_ldpc_code_t *c = find_code(normal, rate);

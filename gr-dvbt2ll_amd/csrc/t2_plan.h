@@ -28,9 +28,11 @@ struct FecPlan {
   int normal = 0, rate = 0;
   int kbch = 0, nbch = 0, nparity = 0, nldpc = 0, q = 0, pbits = 0;
   bool parity_interleave = true;      // tempu carries parity in [a][c] (interleaved) order
-  int bch_chunk = 0;                  // message bytes per lane chunk (64 lanes)
+  int bch_waves = 1;                  // waves sharing the BCH division (64 chunks each)
+  int bch_chunk = 0;                  // message bytes per lane chunk (64 * bch_waves lanes)
   std::vector<uint64_t> bch_tab;      // 256 x 3 words: d(x) * x^P mod g(x)
   std::vector<uint64_t> bch_m1;       // 192 rows x 3 words: v -> v * x^(8*chunk) mod g
+  std::vector<uint64_t> bch_m64;      // 192 rows x 3 words: v -> v * x^(8*64*chunk) mod g
   std::vector<uint16_t> ldpc_rowptr;  // q + 1
   std::vector<uint32_t> ldpc_ent;     // (group << 16) | rotation, grouped by parity row
   std::vector<uint8_t> prbs_bytes;    // BB scrambler, kbch/8 bytes
@@ -38,7 +40,9 @@ struct FecPlan {
   std::vector<uint8_t> crc8_shift;    // 8 x 256: crc after appending k zero bytes (packet CRC combine)
   std::vector<uint8_t> hcrc_bits;     // 72: BBHEADER CRC-8 contribution of each header bit
 };
-int build_fec(int framesize, int rate, int constellation, FecPlan &fp);
+// bch_waves: waves of the FEC kernel that share the BCH division (64 chunks each; 1 = the fewest
+// instructions, more = a shorter per-block critical path for more Horner work)
+int build_fec(int framesize, int rate, int constellation, FecPlan &fp, int bch_waves = 1);
 
 // ----------------------------------------------------------------------------- bit interleave + map
 enum MapMode { MAP_PAIRS = 0, MAP_TWIST2 = 1, MAP_TWIST1 = 2 };
