@@ -420,17 +420,17 @@ static PgParams to_pg(const dvbt2ll_pilotgenp1insert_params &p) {
 }
 
 struct OfdmTables {
-  DevBuf map, tw, isinc, p1;
+  DevBuf map, tw, tw1k, isinc, p1;
   OfdmDev dev{};
-  // stored_map: per-symbol rows in the kernel's read order (ofdm_stored_rows: [even | odd]
-  // bins when N > 16K, where the kernel runs two N/2 transforms)
+  // stored_map: per-symbol rows in the kernel's read order (ofdm_stored_rows: natural order)
   int init(const PilotPlan &pp, const std::vector<int32_t> &stored_map, int aux_len, int t2frames) {
     int r;
     if ((r = upload(map, stored_map))) return r;
-    if ((r = upload(tw, pp.twiddle)) || (r = upload(p1, pp.p1))) return r;
+    if ((r = upload(tw, pp.twiddle)) || (r = upload(tw1k, pp.twiddle1k)) || (r = upload(p1, pp.p1))) return r;
     if (pp.eq && (r = upload(isinc, pp.isinc))) return r;
     dev.bin_map = map.as<int32_t>();
     dev.twiddle = tw.as<float2>();
+    dev.twiddle1k = tw1k.as<float2>();
     dev.isinc = pp.eq ? isinc.as<float>() : nullptr;
     dev.p1 = p1.as<float2>();
     dev.N = pp.N; dev.G = pp.G; dev.Nsym = pp.Nsym; dev.aux_len = aux_len; dev.t2frames = t2frames;

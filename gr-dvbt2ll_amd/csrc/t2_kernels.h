@@ -71,12 +71,13 @@ __host__ __device__ inline uint32_t ofdm_padded_bin(int N, uint32_t k) {   // k:
   return k + (k >> ofdm_pad_shift(N));
 }
 struct OfdmDev {
-  const int32_t *bin_map;   // Nsym x N (stored row order): >= 0 cell index, < 0 aux entry
+  const int32_t *bin_map;   // Nsym x N (natural FFT-input order): >= 0 cell index, < 0 aux entry
   // chain (scatter) mode: symbol j's cells are the slots [sym_d0[j], +sym_n[j]), slot s goes to
   // stored bin inv[s]; null -> gather mode (bin_map >= 0 codes are read per bin)
   const uint16_t *inv;       // padded bin within the symbol's half (ofdm_padded_bin)
-  const int32_t *sym_d0, *sym_n, *sym_n0;   // sym_n0: slots of the even-bin half (split)
+  const int32_t *sym_d0, *sym_n, *sym_n0;   // sym_n0: slots of the bins < N/2 (32K: two halves)
   const float2 *twiddle;    // 128 + N/128: two-level table (PilotPlan::twiddle)
+  const float2 *twiddle1k;  // 1024: w_1024^m (PilotPlan::twiddle1k; 32K kernel)
   const float *isinc;       // N or null
   const float2 *p1;         // 2048
   const float2 *qam;        // scatter mode: 256-entry constellation; cell = (qam[lo].x, qam[hi].y)

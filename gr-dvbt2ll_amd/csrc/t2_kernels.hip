@@ -935,14 +935,10 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ============================================================================ OFDM kernel
-#ifndef OFDM_SPLIT_V
-#define OFDM_SPLIT_V 32
-#endif
+// ============================================================================ OFDM kernels
 #ifndef OFDM_SQ16
-#define OFDM_SQ16 8
+#define OFDM_SQ16 8   // data-slot quads per thread per scatter round (N <= 16K)
 #endif
-#define OFDM_PS32 OFDM_PAD_SHIFT_32K   // LDS pad shift of the 32K half-transforms (t2_kernels.h)
 // exp(+2 pi i k / 32): exact at multiples of pi/2
 __device__ constexpr float kCos32[32] = {
     1.0f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f, 0.70710678118654757f,
@@ -1109,7 +1105,7 @@ struct StockhamTail<NSUB, NT, PS, NS, R, Rs...> {
   }
 };
 
-// FFT plans: first pass radix V (values per thread) from LDS or registers, then the tail.
+// FFT plans (N <= 16K): first pass radix V = 16 from LDS or registers, then the tail.
 // RL = radix of the last pass; thread t ends with n = t + NT*(u + (V/RL)*r); PS = LDS pad shift.
 template <int NSUB, int V> struct FftPlan;
 template <> struct FftPlan<1024, 16> { static constexpr int RL = 4, PS = 4; using Tail = StockhamTail<1024, 64, 4, 16, 16, 4>; };
@@ -1117,11 +1113,6 @@ template <> struct FftPlan<2048, 16> { static constexpr int RL = 8, PS = 4; usin
 template <> struct FftPlan<4096, 16> { static constexpr int RL = 16, PS = 4; using Tail = StockhamTail<4096, 256, 4, 16, 16, 16>; };
 template <> struct FftPlan<8192, 16> { static constexpr int RL = 2, PS = 4; using Tail = StockhamTail<8192, 512, 4, 16, 16, 16, 2>; };
 template <> struct FftPlan<16384, 16> { static constexpr int RL = 4, PS = 4; using Tail = StockhamTail<16384, 1024, 4, 16, 16, 16, 4>; };
-// 32K halves: 512 threads x 32 values, radices 32 x 32 x 16 (three LDS passes), one pad per 32
-template <> struct FftPlan<16384, 32> {
-  static constexpr int RL = 16, PS = OFDM_PS32;
-  using Tail = StockhamTail<16384, 512, OFDM_PS32, 32, 32, 16>;
-};
 
 // experiment switch (product builds: 0): bit 3 = phase timestamps (s_memrealtime, 100 MHz) of
 // each workgroup written over the first samples of its symbol's guard interval (wrong output;
@@ -1136,13 +1127,13 @@ __shared__ uint64_t g_phase_ts[16];
 #define OFDM_PHASE(i) do { } while (0)
 #endif
 
-// Where a sub-transform's inputs come from.  Gather (pilotgen block: cells in carrier order,
-// so per-bin loads are near unit-stride): bin k reads map[k].  Scatter (fused chain: cells in
-// TI output order, randomly placed by the frequency interleaver): aux bins (map < 0) are filled
-// from the aux table, then the symbol's contiguous run of data slots is streamed with unit-stride
-// loads and each cell is written to LDS at its bin inv[slot].
+// Where a transform's inputs come from.  Gather (pilotgen block: cells in carrier order, so per-bin
+// loads are near unit-stride): bin k reads map[k].  Scatter (fused chain: cells in TI output order,
+// randomly placed by the frequency interleaver): aux bins (map < 0) are filled from the aux
+// table, then the symbol's contiguous run of data slots is streamed with unit-stride loads and
+// each cell is written to LDS at its bin inv[slot].
 struct BinSource {
-  const int32_t *map;          // this symbol's stored row
+  const int32_t *map;          // this symbol's row (natural FFT-input order)
   const float2 *data;          // uniform base; cells at cbase + code (gather), aux at abase - code
   uint32_t cbase, abase;
   const uint16_t *inv;         // scatter mode: stored bin of each data slot (null: gather mode)
@@ -1152,96 +1143,91 @@ struct BinSource {
   const uint16_t *abin;        // scatter mode: aux lists (OfdmDev)
   const float2 *aval;
   const uint32_t *aind;
-  const int4 *agrp;            // this symbol's two groups (halves)
-  const int2 *azr;             // this symbol's two zero runs (padded LDS slot ranges)
+  const int4 *agrp;            // this symbol's groups (halves)
+  const int2 *azr;             // this symbol's zero runs (padded LDS slot ranges)
 };
 
-// One NSUB-point sub-transform of bins sub + 2*k' (SPLIT) or k' (no split) by NT = NSUB/V
-// threads, ending with v[u*RL + r] = y[t + NT*(u + (V/RL)*r)].
-// The first sub-transform (half 0) also stores the kernel's constant tables (`stage`) to LDS.
-template <int NSUB, bool SPLIT, int V, class Stage>
+// Scatter-mode fill of one group (a whole symbol, or one half of a split 32K symbol) into LDS,
+// every bin written exactly once (t2_plan build_aux_lists / build_chain_layout):
+//   the direct aux quads (pilots, L1-pre, dummy cells: bin + value), the indirect entries (the
+//   frame's L1-post cells through its aux variant) and the data slots, streamed as aligned quads
+//   of (uint16 bin, uint16 index pair) and looked up in the constellation (QAM + rotated-Q
+//   delay).  Slots outside the run (quad edges) and padding bins go to a per-lane dummy slot.
+// The zero run is written separately by the caller.
+template <int NT, int SQ>
+__device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src, int g, uint32_t r0, uint32_t rn,
+                                              uint32_t dummy, int tid) {
+  const int4 gr = src.agrp[g];
+  for (uint32_t q = (uint32_t)tid; q < (uint32_t)gr.y >> 2; q += NT) {
+    const uint32_t e0 = (uint32_t)gr.x + 4u * q;
+    const uint2 b = ld_off((const uint2 *)src.abin, e0 * 2u);
+    const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
+    const float4 v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
+    const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
+    lds[k0 != 0xFFFFu ? k0 : dummy] = make_float2(v01.x, v01.y);   // bins stored padded
+    lds[k1 != 0xFFFFu ? k1 : dummy] = make_float2(v01.z, v01.w);
+    lds[k2 != 0xFFFFu ? k2 : dummy] = make_float2(v23.x, v23.y);
+    lds[k3 != 0xFFFFu ? k3 : dummy] = make_float2(v23.z, v23.w);
+  }
+  for (uint32_t i = (uint32_t)tid; i < (uint32_t)gr.w; i += NT) {
+    const uint32_t e = src.aind[(uint32_t)gr.z + i];
+    lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
+  }
+  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
+  const uint32_t lastq = nq - 1u;
+  for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
+    uint2 b[SQ], c[SQ];
+#pragma unroll
+    for (int u = 0; u < SQ; u++) {
+      const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
+      b[u] = ld_off((const uint2 *)src.inv, s * 2u);
+      c[u] = ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u);
+    }
+#pragma unroll
+    for (int u = 0; u < SQ; u++) {
+      const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
+        const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the group
+        const uint32_t pr = cw >> (16 * (e & 1));
+        const bool in_run = s + (uint32_t)e - r0 < rn;
+        const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+        lds[in_run ? bin : dummy] = v;
+      }
+    }
+  }
+}
+
+// One NSUB-point transform (N <= 16K) by NT = NSUB/V threads, ending with
+// v[u*RL + r] = y[t + NT*(u + (V/RL)*r)].  Also stores the kernel's constant tables (`stage`) to LDS.
+template <int NSUB, int V, class Stage>
 __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource &src, const float *isinc,
-                                         const float2 *tw, uint32_t tws, int tid, int half, const Stage &stage) {
-  constexpr int NT = NSUB / V, N = SPLIT ? 2 * NSUB : NSUB;
+                                         const float2 *tw, int tid, const Stage &stage) {
+  constexpr int NT = NSUB / V, N = NSUB;
   constexpr int PS = FftPlan<NSUB, V>::PS;
-  // first pass (R = V, Ns = 1) inputs A[tid + r*NT]; map rows are [even | odd] when SPLIT
-  const int32_t *m = src.map + (SPLIT ? half * NSUB : 0);
   if (src.inv) {
-    // zero the half's run of band-edge null bins (the planner's zero run; isolated zero bins
-    // are direct entries), write the non-data bins from the compact aux lists and the data cells
-    // from the symbol's slot run: every bin written exactly once, all targets disjoint, so the
-    // three writers share one phase (the barrier below publishes the constant tables)
     {
-      const int2 zr = src.azr[half];
+      const int2 zr = src.azr[0];
       for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
     }
-    if (half == 0) stage.store((unsigned char *)lds, true, tid);
+    stage.store((unsigned char *)lds, true, tid);
     __syncthreads();
-    OFDM_PHASE(1 + 4 * half);
+    OFDM_PHASE(1);
     const uint32_t dummy = (uint32_t)(NSUB + (NSUB >> PS)) + (uint32_t)(tid & 63);
-    {
-      const int4 g = src.agrp[half];
-      // direct entries: quads of (bin, value); padding bins (0xFFFF) go to the dummy slot
-      for (uint32_t q = (uint32_t)tid; q < (uint32_t)g.y >> 2; q += NT) {
-        const uint32_t e0 = (uint32_t)g.x + 4u * q;
-        const uint2 b = ld_off((const uint2 *)src.abin, e0 * 2u);
-        const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
-        const float4 v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
-        const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
-        lds[k0 != 0xFFFFu ? k0 : dummy] = make_float2(v01.x, v01.y);   // bins stored padded
-        lds[k1 != 0xFFFFu ? k1 : dummy] = make_float2(v01.z, v01.w);
-        lds[k2 != 0xFFFFu ? k2 : dummy] = make_float2(v23.x, v23.y);
-        lds[k3 != 0xFFFFu ? k3 : dummy] = make_float2(v23.z, v23.w);
-      }
-      // indirect entries (per-frame L1-post cells): through the frame's aux variant
-      for (uint32_t i = (uint32_t)tid; i < (uint32_t)g.w; i += NT) {
-        const uint32_t e = src.aind[(uint32_t)g.z + i];
-        lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
-      }
-    }
-    // data cells: the symbol's slots streamed as aligned quads (8-byte loads of 4 index pairs
-    // and 4 stored bins), looked up in the constellation and written to their bins; slots
-    // outside the run (quad edges) go to a per-lane dummy slot past the buffer (branch-free)
-    // (split: the run is partitioned, so half h streams only its own slots)
-    const uint32_t r0 = src.d0 + (SPLIT && half ? src.dn0 : 0u);
-    const uint32_t rn = SPLIT ? (half ? src.dn - src.dn0 : src.dn0) : src.dn;
-    const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
-    const uint32_t lastq = nq - 1u;
-    constexpr int SQ = V >= 32 ? 8 : OFDM_SQ16;  // quads per thread per round
-    for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
-      uint2 b[SQ], c[SQ];
-#pragma unroll
-      for (int u = 0; u < SQ; u++) {
-        const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
-        b[u] = ld_off((const uint2 *)src.inv, s * 2u);
-        c[u] = ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u);
-      }
-#pragma unroll
-      for (int u = 0; u < SQ; u++) {
-        const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
-          const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the half
-          const uint32_t pr = cw >> (16 * (e & 1));
-          const bool in_run = s + (uint32_t)e - r0 < rn;
-          const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-          lds[in_run ? bin : dummy] = v;
-        }
-      }
-    }
+    scatter_group<NT, OFDM_SQ16>(lds, src, 0, src.d0, src.dn, dummy, tid);
     __syncthreads();
-    OFDM_PHASE(2 + 4 * half);
+    OFDM_PHASE(2);
     StockhamPass<NSUB, NT, V, 1, PS>::load_lds(v, lds, tid);
     __syncthreads();
   } else {
-    if (half == 0) stage.store((unsigned char *)lds, false, tid);
+    stage.store((unsigned char *)lds, false, tid);
 #pragma unroll
     for (int c0 = 0; c0 < V; c0 += 8) {
       uint32_t off[8];
 #pragma unroll
       for (int u = 0; u < 8; u++) {
-        int code = ld_off(m, (uint32_t)(tid + NT * (c0 + u)) * 4u);
+        int code = ld_off(src.map, (uint32_t)(tid + NT * (c0 + u)) * 4u);
         off[u] = (code >= 0 ? src.cbase + (uint32_t)code : src.abase - (uint32_t)code) * 8u;
       }
 #pragma unroll
@@ -1252,9 +1238,8 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   if (isinc) {
 #pragma unroll
     for (int r = 0; r < V; r++) {
-      uint32_t k = (uint32_t)(tid + NT * r);
-      if (SPLIT) k = 2 * k + half;
-      float sc = isinc[(k + N / 2) & (N - 1)];
+      const uint32_t k = (uint32_t)(tid + NT * r);
+      const float sc = isinc[(k + N / 2) & (N - 1)];
       v[r].x *= sc;
       v[r].y *= sc;
     }
@@ -1263,20 +1248,17 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   Dft<V>::run(v);
   StockhamPass<NSUB, NT, V, 1, PS>::store_lds(v, lds, tid);
   __syncthreads();
-  FftPlan<NSUB, V>::Tail::run(v, lds, tw, tws, tid);
+  FftPlan<NSUB, V>::Tail::run(v, lds, tw, 1u, tid);
 }
-
 
 template <int N>
 struct OfdmShape {
-  static constexpr bool SPLIT = N > 16384;
-  static constexpr int NSUB = SPLIT ? N / 2 : N;
-  static constexpr int V = SPLIT ? OFDM_SPLIT_V : 16;                 // values per thread
-  static constexpr int NT = NSUB / V;
-  static constexpr int PS = FftPlan<NSUB, V>::PS;
-  static constexpr int FFT_LDS = (NSUB + (NSUB >> PS) + 64) * 8;    // padded buffer + 64 dummy slots
+  static constexpr int V = 16;                                        // values per thread
+  static constexpr int NT = N / V;
+  static constexpr int PS = FftPlan<N, V>::PS;
+  static constexpr int FFT_LDS = (N + (N >> PS) + 64) * 8;           // padded buffer + 64 dummy slots
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
-  static constexpr int QAM_OFF = FFT_LDS + (TW_ENTRIES + 32) * 8;    // + w^(NT m), m < 32 (combine)
+  static constexpr int QAM_OFF = FFT_LDS + TW_ENTRIES * 8;
   static constexpr int LDS_BYTES = QAM_OFF + 256 * 8;                // + constellation re[256], im[256]
 };
 
@@ -1301,22 +1283,18 @@ struct IqOut {
   }
 };
 
-// the OFDM kernel's constant LDS tables (twiddles, split-combine twiddles, constellation),
-// held in registers between load() and store()
+// the OFDM kernel's constant LDS tables (twiddles, constellation), held in registers between
+// load() and store()
 template <int N>
 struct TableStage {
   using Sh = OfdmShape<N>;
   static constexpr int NT = Sh::NT, TWK = (Sh::TW_ENTRIES + NT - 1) / NT, QK = (256 + NT - 1) / NT;
-  float2 tw[TWK], q[QK], wc;
+  float2 tw[TWK], q[QK];
   __device__ __forceinline__ void load(const OfdmDev &d, int tid) {
 #pragma unroll
     for (int k = 0; k < TWK; k++) {
       const int i = tid + k * NT;
       if (i < Sh::TW_ENTRIES) tw[k] = d.twiddle[i];
-    }
-    if (Sh::SPLIT && tid < 32) {
-      const uint32_t e = (uint32_t)(NT * tid);
-      wc = cmulf(d.twiddle[128 + (e >> 7)], d.twiddle[e & 127]);
     }
     if (d.inv) {
 #pragma unroll
@@ -1333,7 +1311,6 @@ struct TableStage {
       const int i = tid + k * NT;
       if (i < Sh::TW_ENTRIES) twl[i] = tw[k];
     }
-    if (Sh::SPLIT && tid < 32) twl[Sh::TW_ENTRIES + tid] = wc;
     if (chain) {
       float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + 256;
 #pragma unroll
@@ -1348,18 +1325,18 @@ struct TableStage {
   }
 };
 
+// OFDM symbols of N <= 16K points: one workgroup of N / 16 threads per (symbol, frame), the
+// symbol's bins in LDS, radix-16 Stockham passes, normalisation, GI copy, IQ store
 template <int N, int FMT>
 __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmIO io) {
   using Sh = OfdmShape<N>;
-  constexpr int NSUB = Sh::NSUB, NT = Sh::NT, V = Sh::V, RL = FftPlan<NSUB, V>::RL, UL = V / RL;
+  constexpr int NT = Sh::NT, V = Sh::V, RL = FftPlan<N, V>::RL, UL = V / RL;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2 *lds = (float2 *)smem;
   float2 *twl = (float2 *)(smem + Sh::FFT_LDS);
   const int tid = threadIdx.x;
-  float2 *wcomb = twl + Sh::TW_ENTRIES;            // split combine: w^(NT m), uniform across lanes
   float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + 256;
-  // constant tables: loaded into registers here, stored to LDS by the first sub-transform
-  // after its zero fill (the loads' latency overlaps the fill; visible after its barrier)
+  // constant tables: loaded into registers here, stored to LDS after the zero fill
   TableStage<N> tabs;
   tabs.load(d, tid);
   // one workgroup per (symbol, frame); XCD-major so each XCD walks a contiguous run of symbols
@@ -1372,7 +1349,6 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const uint32_t cbase = io.cell_off + (uint32_t)f * io.cell_stride;
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
   const int32_t *map = d.bin_map + (int64_t)j * N;
-  const uint32_t tws = Sh::SPLIT ? 2u : 1u;       // sub-transform twiddle = table index * tws
   BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u, d.abin, d.aval, d.aind, nullptr,
                 nullptr};
   if (d.inv) {
@@ -1382,16 +1358,14 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
     src.agrp = d.agrp + 2 * j;
     src.azr = d.azr + 2 * j;
   }
-
   if (io.carriers_only) {                          // test hook (gather mode): bins in natural order
     if (d.inv) return;
     float2 *o = io.out + (int64_t)f * io.out_stride + (int64_t)j * N;
     for (int k = tid; k < N; k += NT) {
-      const int sub = Sh::SPLIT ? (k & 1) : 0, kk = Sh::SPLIT ? (k >> 1) : k;
-      int code = map[sub * NSUB + kk];
+      const int code = map[k];
       float2 v = data[code >= 0 ? cbase + (uint32_t)code : abase - (uint32_t)code];
       if (d.isinc) {
-        float sc = d.isinc[(k + N / 2) & (N - 1)];
+        const float sc = d.isinc[(k + N / 2) & (N - 1)];
         v.x *= sc;
         v.y *= sc;
       }
@@ -1409,51 +1383,18 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const float nrm = d.norm;
   float2 v[V];
   OFDM_PHASE(0);
-  sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid, 0, tabs);
+  sub_ifft<N, V>(v, lds, src, d.isinc, twl, tid, tabs);
   OFDM_PHASE(3);
-  if (Sh::SPLIT) {
-    // x[n] = E[n] + w^n O[n], x[n + NSUB] = E[n] - w^n O[n], w = exp(2 pi i / N): the even-bin
-    // transform E stays in registers (32 values per thread) while the odd-bin one runs
-    float2 e[V];
 #pragma unroll
-    for (int i = 0; i < V; i++) e[i] = v[i];
-    OFDM_PHASE(4);
-    // launder tid: stops the compiler from keeping the first transform's index/twiddle
-    // arithmetic alive for reuse by the second
-    int tid2 = tid;
-    asm volatile("" : "+v"(tid2));
-    sub_ifft<NSUB, Sh::SPLIT, V>(v, lds, src, d.isinc, twl, tws, tid2, 1, tabs);
-    OFDM_PHASE(7);
-    const float2 wt = tw_at(twl, (uint32_t)tid);   // w^n = w^tid * w^(NT m)
+  for (int uu = 0; uu < UL; uu++)
 #pragma unroll
-    for (int uu = 0; uu < UL; uu++)
-#pragma unroll
-      for (int r = 0; r < RL; r++) {
-        const int i = uu * RL + r;
-        const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
-        float2 t = cmulf(v[i], cmulf(wt, wcomb[uu + UL * r]));
-        float2 a = cadd(e[i], t), b = csub(e[i], t);
-        a = cscale(a, nrm);
-        b = cscale(b, nrm);
-        o.put((uint32_t)G + n, a);
-        const uint32_t n2 = n + (uint32_t)NSUB;
-        o.put((uint32_t)G + n2, b);
-        if (n2 >= (uint32_t)(N - G)) o.put(n2 - (uint32_t)(N - G), b);
-        if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
-        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-      }
-  } else {
-#pragma unroll
-    for (int uu = 0; uu < UL; uu++)
-#pragma unroll
-      for (int r = 0; r < RL; r++) {
-        const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
-        float2 a = v[uu * RL + r];
-        a = cscale(a, nrm);
-        o.put((uint32_t)G + n, a);
-        if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
-      }
-  }
+    for (int r = 0; r < RL; r++) {
+      const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
+      float2 a = v[uu * RL + r];
+      a = cscale(a, nrm);
+      o.put((uint32_t)G + n, a);
+      if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
+    }
 #if OFDM_VARIANT & 8
   __syncthreads();
   OFDM_PHASE(8);
@@ -1466,12 +1407,247 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
 #endif
 }
 
+// ---------------------------------------------------------------- 32K symbols
+// One workgroup of 1024 threads per (symbol, frame); the whole 32768-point symbol stays in VGPRs
+// (32 complex values per thread) through three radix-32 stages of a 32 x 32 x 32 decomposition.
+// With m = m0 + 32 m1 + 1024 m2 (input bin) and n = n2 + 32 n1 + 1024 n0 (output sample),
+//   stage A: DFT over m2, then * w^((m0 + 32 m1) n2)      thread (a, b) = (m0, m1)
+//   stage B: DFT over m1, then * w_1024^(m0 n1)           thread (a, b) = (m0, n2)
+//   stage C: DFT over m0 -> x[n2 + 32 n1 + 1024 n0]       thread (a, b) = (n1, n2)
+// (w = exp(2 pi i / 32768); thread t <-> a = t[4..7] | t[8] << 4, b = t[0..3] | t[9] << 4).
+// Each exchange keeps one coordinate of the thread (a across the first, b across the second), so
+// it splits into two closed halves -- the threads with t[8] (resp. t[9]) = 0, then 1 -- and each
+// half round trips through LDS alone: 16384 points, 128 KB, in an LDS of 160 KB.  The chain's bins
+// arrive the same way: its data slots and aux lists are partitioned per symbol into bins < 16384
+// and >= 16384 (t2_plan build_chain_layout / build_aux_lists, natural FFT-input order), which are
+// m2 < 16 and m2 >= 16; the pilotgen block's gather mode loads each thread's 32 bins straight
+// from global memory.  Thread (a, b) ends with samples b + 32 a + 1024 r: each IQ store is four
+// runs of 16 consecutive samples per wave.
+// Twiddles: a thread's 31 factors w^(e r) are products of at most three table values w^(e k),
+// k in {1, 2, 3, 4, 8, 12, 16} (w_1024^m exact for stage B; the two-level w^i = hi[i >> 7] lo[i & 127]
+// for stage A), so each is within a few ulp.
+constexpr int O32_NT = 1024, O32_H = 16384, O32_PS = OFDM_PAD_SHIFT_32K;
+constexpr int O32_DATA = (O32_H + (O32_H >> O32_PS) + 64) * 8;   // padded half + 64 dummy slots
+constexpr int O32_TW1K = O32_DATA;                                // w_1024^m, m < 1024
+constexpr int O32_TW2 = O32_TW1K + 1024 * 8;                      // two-level table, 128 + 256
+constexpr int O32_QAM = O32_TW2 + 384 * 8;                        // constellation re[256], im[256]
+constexpr int O32_LDS = O32_QAM + 256 * 8;
+static_assert(O32_LDS <= 160 * 1024, "32K OFDM LDS");
+
+// bins within a half as the scatter stores them (one pad slot per 32, t2_kernels.h)
+__device__ __forceinline__ uint32_t o32_bin(uint32_t k) { return k + (k >> O32_PS); }
+// exchange slots: one pad per 512 (stride-512 lane patterns spread over the banks)
+__device__ __forceinline__ uint32_t o32_x(uint32_t e) { return e + (e >> 9); }
+
+// v[r] *= w^(e r) for r = 1..31 from the seven table values w^(e k) (k = 1, 2, 3, 4, 8, 12, 16):
+// r = 16 t + 4 h + l -> top^t hi[h] lo[l]
+template <class Lookup>
+__device__ __forceinline__ void o32_twiddle(float2 *v, const Lookup &tw) {
+  float2 lo[4], hi[4];
+  lo[1] = tw(1); lo[2] = tw(2); lo[3] = tw(3);
+  hi[1] = tw(4); hi[2] = tw(8); hi[3] = tw(12);
+  const float2 top = tw(16);
+#pragma unroll
+  for (int r = 1; r < 32; r++) {
+    const int t = r >> 4, h = (r >> 2) & 3, l = r & 3;
+    float2 w = h == 0 ? lo[l] : (l == 0 ? hi[h] : cmulf(hi[h], lo[l]));
+    if (t) w = (h == 0 && l == 0) ? top : cmulf(top, w);
+    v[r] = cmulf(v[r], w);
+  }
+}
+
+// one exchange, as two closed halves: the threads whose bit SPLIT is h write their 32 values and
+// read their 32 new ones, h = 0 then 1.  Slots: exchange 1 (SPLIT 8) writes (m0 = a, m1 = b,
+// n2 = r) and reads (m0 = a, m1 = r, n2 = b) at (m1 & 15) + 16 (m0 & 15) + 256 (m1 >> 4) + 512 n2;
+// exchange 2 (SPLIT 9) writes (n2 = b, m0 = a, n1 = r) and reads (n2 = b, m0 = r, n1 = a) at
+// (n2 & 15) + 16 (n1 & 15) + 256 (n1 >> 4) + 512 m0
+template <int SPLIT>
+__device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t tid, uint32_t a, uint32_t b) {
+#pragma unroll
+  for (uint32_t h = 0; h < 2; h++) {
+    __syncthreads();
+    const bool mine = ((tid >> SPLIT) & 1u) == h;
+    if (mine) {
+#pragma unroll
+      for (uint32_t r = 0; r < 32; r++) {
+        const uint32_t e = SPLIT == 8 ? (b & 15u) + 16u * (a & 15u) + 256u * (b >> 4) + 512u * r
+                                      : (b & 15u) + 16u * (r & 15u) + 256u * (r >> 4) + 512u * a;
+        lds[o32_x(e)] = v[r];
+      }
+    }
+    __syncthreads();
+    if (mine) {
+#pragma unroll
+      for (uint32_t r = 0; r < 32; r++) {
+        const uint32_t e = SPLIT == 8 ? (r & 15u) + 16u * (a & 15u) + 256u * (r >> 4) + 512u * b
+                                      : (b & 15u) + 16u * (a & 15u) + 256u * (a >> 4) + 512u * r;
+        v[r] = lds[o32_x(e)];
+      }
+    }
+  }
+}
+
+// stages A, B, C with the two exchanges: v[r] = bin kin + 1024 r on entry (kin = a + 32 b), sample
+// b + 32 a + 1024 r on exit.  Every thread is past its last LDS access of the symbol on return.
+__device__ __forceinline__ void o32_fft(float2 *v, float2 *lds, const float2 *tw1k, const float2 *tw2, uint32_t tid,
+                                        uint32_t ta, uint32_t tb) {
+  const uint32_t kin = ta + 32u * tb;
+  // stage A: DFT over m2, twiddle w^((m0 + 32 m1) n2) = w^(kin r)
+  __builtin_amdgcn_sched_barrier(0);
+  Dft<32>::run(v);
+  o32_twiddle(v, [&](int k) {
+    const uint32_t i = kin * (uint32_t)k;   // < 16384
+    return cmulf(tw2[128 + (i >> 7)], tw2[i & 127u]);
+  });
+  OFDM_PHASE(3);
+  o32_exchange<8>(v, lds, tid, ta, tb);
+  OFDM_PHASE(4);
+  // stage B: DFT over m1, twiddle w_1024^(m0 n1) = w_1024^(a r)
+  __builtin_amdgcn_sched_barrier(0);
+  Dft<32>::run(v);
+  o32_twiddle(v, [&](int k) { return tw1k[(ta * (uint32_t)k) & 1023u]; });
+  OFDM_PHASE(5);
+  o32_exchange<9>(v, lds, tid, ta, tb);
+  OFDM_PHASE(6);
+  // stage C: DFT over m0 -> x[b + 32 a + 1024 r]
+  __builtin_amdgcn_sched_barrier(0);
+  Dft<32>::run(v);
+  OFDM_PHASE(7);
+}
+
+// normalisation, guard interval and IQ store of samples b + 32 a + 1024 r, r in [R0, R1)
+template <int FMT, int R0, int R1>
+__device__ __forceinline__ void o32_store(const float2 *v, const IqOut<FMT> &o, uint32_t nout, float nrm, int G) {
+  constexpr uint32_t N = 32768;
+#pragma unroll
+  for (uint32_t r = R0; r < R1; r++) {
+    const uint32_t n = nout + 1024u * r;
+    const float2 a = cscale(v[r], nrm);
+    o.put((uint32_t)G + n, a);
+    if (n >= N - (uint32_t)G) o.put(n - (N - (uint32_t)G), a);
+  }
+}
+
+// 32K symbols, one workgroup per (symbol, frame): scatter mode (the fused chain), gather mode (the
+// pilotgen block: cells already in carrier order) and the carriers-only test hook
+template <int FMT>
+__global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
+  constexpr int N = 32768, NT = O32_NT;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float2 *lds = (float2 *)smem;
+  float2 *tw1k = (float2 *)(smem + O32_TW1K), *tw2 = (float2 *)(smem + O32_TW2);
+  const int tid = threadIdx.x;
+  const uint32_t ta = (((uint32_t)tid >> 4) & 15u) | ((((uint32_t)tid >> 8) & 1u) << 4);
+  const uint32_t tb = ((uint32_t)tid & 15u) | ((((uint32_t)tid >> 9) & 1u) << 4);
+  const uint32_t kin = ta + 32u * tb;             // stage-A input bins kin + 1024 r
+  const int u = xcd_major(blockIdx.x, gridDim.x);
+  const int j = u / io.nframes;                   // symbol
+  const int f = u - j * io.nframes;               // frame within launch
+  const int64_t frame = io.first_frame + f;
+  const float2 *data = io.data;
+  const uint32_t cbase = io.cell_off + (uint32_t)f * io.cell_stride;
+  const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
+  const int32_t *map = d.bin_map + (int64_t)j * N;
+  if (io.carriers_only) {                          // test hook: bins in natural order
+    float2 *o = io.out + (int64_t)f * io.out_stride + (int64_t)j * N;
+    for (int k = tid; k < N; k += NT) {
+      const int code = map[k];
+      float2 v = data[code >= 0 ? cbase + (uint32_t)code : abase - (uint32_t)code];
+      if (d.isinc) {
+        const float sc = d.isinc[(k + N / 2) & (N - 1)];
+        v.x *= sc;
+        v.y *= sc;
+      }
+      o[(k + N / 2) & (N - 1)] = v;
+    }
+    return;
+  }
+  constexpr int SB = FMT == 0 ? 8 : 4;
+  if (j == 0) {                                   // P1 symbol (precomputed), pilotgen:2802-2810
+    const IqOut<FMT> p{(char *)io.out + (int64_t)f * io.out_stride * SB, d.gain};
+    for (int i = tid; i < 2048; i += NT) p.put((uint32_t)i, d.p1[i]);
+  }
+  OFDM_PHASE(0);
+  tw1k[tid] = d.twiddle1k[tid];
+  if (tid < 384) tw2[tid] = d.twiddle[tid];
+  float2 v[32];
+  if (d.inv) {
+    // scatter mode, one half of the bins (m2 < 16, then m2 >= 16) at a time
+    float *qre = (float *)(smem + O32_QAM), *qim = qre + 256;
+    const float2 tq = tid < 256 ? d.qam[tid] : make_float2(0.f, 0.f);
+    BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, (uint32_t)d.sym_d0[j], (uint32_t)d.sym_n[j],
+                  (uint32_t)d.sym_n0[j], d.abin, d.aval, d.aind, d.agrp + 2 * j, d.azr + 2 * j};
+    const uint32_t dummy = (uint32_t)(O32_H + (O32_H >> O32_PS)) + (uint32_t)(tid & 63);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (h) __syncthreads();                     // half 0 read back before half 1 overwrites it
+      const int2 zr = src.azr[h];
+      for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
+      if (h == 0) {
+        if (tid < 256) {
+          qre[tid] = tq.x;
+          qim[tid] = tq.y;
+        }
+        __syncthreads();                          // constellation visible to the scatter
+      }
+      const uint32_t r0 = src.d0 + (h ? src.dn0 : 0u), rn = h ? src.dn - src.dn0 : src.dn0;
+      scatter_group<NT, 4>(lds, src, h, r0, rn, dummy, tid);
+      __syncthreads();
+      if (h == 0) OFDM_PHASE(1);
+#pragma unroll
+      for (uint32_t r = 0; r < 16; r++) v[16 * h + r] = lds[o32_bin(kin + 1024u * r)];
+    }
+  } else {
+#pragma unroll
+  for (int c0 = 0; c0 < 32; c0 += 8) {
+    uint32_t off[8];
+#pragma unroll
+    for (int uu = 0; uu < 8; uu++) {
+      const int code = ld_off(map, (kin + 1024u * (uint32_t)(c0 + uu)) * 4u);
+      off[uu] = (code >= 0 ? cbase + (uint32_t)code : abase - (uint32_t)code) * 8u;
+    }
+#pragma unroll
+    for (int uu = 0; uu < 8; uu++) v[c0 + uu] = ld_off(data, off[uu]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  }
+  if (d.isinc) {
+#pragma unroll
+    for (uint32_t r = 0; r < 32; r++) {
+      const float sc = d.isinc[(kin + 1024u * r + N / 2) & (N - 1)];
+      v[r].x *= sc;
+      v[r].y *= sc;
+    }
+  }
+  OFDM_PHASE(2);
+  o32_fft(v, lds, tw1k, tw2, (uint32_t)tid, ta, tb);   // its first barrier publishes the tables
+  const IqOut<FMT> o{(char *)io.out + ((int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + d.G)) * SB, d.gain};
+  o32_store<FMT, 0, 32>(v, o, tb + 32u * ta, d.norm, d.G);
+#if OFDM_VARIANT & 8
+  __syncthreads();
+  OFDM_PHASE(8);
+  if (tid == 0) {
+    uint32_t *ww = (uint32_t *)o.base;
+    ww[0] = (uint32_t)(g_phase_ts[0] & 0xFFFFFFFFu);
+    for (int i = 1; i < 9; i++) ww[i] = (uint32_t)(g_phase_ts[i] - g_phase_ts[0]);
+    ww[9] = __smid();
+  }
+#endif
+}
+
 template <int N, int FMT>
 static hipError_t launch_ofdm_f(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
-  using Sh = OfdmShape<N>;
-  hipError_t e = lds_limit((const void *)ofdm_kernel<N, FMT>, Sh::LDS_BYTES);
+  if (N == 32768) {
+    hipError_t e = lds_limit((const void *)ofdm32_kernel<FMT>, O32_LDS);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((ofdm32_kernel<FMT>), dim3(d.Nsym * io.nframes), dim3(O32_NT), O32_LDS, s, d, io);
+    return hipGetLastError();
+  }
+  constexpr int NN = N > 16384 ? 16384 : N;
+  using Sh = OfdmShape<NN>;
+  hipError_t e = lds_limit((const void *)ofdm_kernel<NN, FMT>, Sh::LDS_BYTES);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((ofdm_kernel<N, FMT>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
+  hipLaunchKernelGGL((ofdm_kernel<NN, FMT>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
   return hipGetLastError();
 }
 template <int N>

@@ -961,15 +961,20 @@ int build_pilot(const PgParams &p, PilotPlan &pp) {
     double a = 2.0 * M_PI * (double)(128 * h) / (double)N;
     pp.twiddle[128 + h] = cf32{(float)std::cos(a), (float)std::sin(a)};
   }
+  pp.twiddle1k.resize(1024);
+  for (int m = 0; m < 1024; m++) {
+    double a = 2.0 * M_PI * (double)m / 1024.0;
+    pp.twiddle1k[m] = cf32{(float)std::cos(a), (float)std::sin(a)};
+  }
   return 0;
 }
 
+// the OFDM kernels read every symbol row in natural FFT-input order (the 32K kernel's two halves
+// are bins < N/2 and >= N/2)
 std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t> &bin_map) {
-  if (!ofdm_split(N)) return bin_map;
-  std::vector<int32_t> m(bin_map.size());
-  for (int j = 0; j < Nsym; j++)
-    for (int k = 0; k < N; k++) m[(size_t)j * N + (k & 1) * (N / 2) + (k >> 1)] = bin_map[(size_t)j * N + k];
-  return m;
+  (void)N;
+  (void)Nsym;
+  return bin_map;
 }
 
 int64_t ti_dest(const FramePlan &fp, int r, int t) {

@@ -93,14 +93,15 @@ struct PilotPlan {
   std::vector<float> isinc;              // N (pre-shift bin order), only if eq
   std::vector<cf32> p1;                  // 2048
   std::vector<cf32> twiddle;             // 128 + N/128: [lo: w^l, l < 128][hi: w^(128 h)], w = exp(2 pi i / N)
+  std::vector<cf32> twiddle1k;           // 1024: exp(2 pi i m / 1024) (the 32K kernel's second pass)
 };
 int build_pilot(const PgParams &p, PilotPlan &pp);
 
 int fft_points(int fftsize);
 
 // ----------------------------------------------------------------------------- fused chain layout
-// The OFDM kernel transforms N > 16384 as two N/2 sub-transforms (even / odd bins), so its
-// per-symbol map rows are stored [even | odd]; otherwise in IFFT-input order k.
+// The OFDM kernels read the per-symbol map rows in IFFT-input order k; for N > 16384 the 32K
+// kernel fills its bins one half (k < N/2, then k >= N/2) at a time.
 inline bool ofdm_split(int N) { return N > 16384; }
 std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t> &bin_map);
 
@@ -109,9 +110,9 @@ std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t
 // symbol j's data cells are the contiguous slots [sym_d0[j], sym_d0[j] + sym_n[j]).  The OFDM
 // kernel streams that range with unit-stride loads and scatters each cell into its IFFT bin in
 // LDS (inv), after filling pilot / null / L1 / dummy bins from the aux table (cmap < 0).
-// When the OFDM kernel splits N = 32K into even / odd-bin halves, each symbol's run is further
-// partitioned [cells of even bins | cells of odd bins] (each part in TI output order), so a half
-// streams only its own cells; `part` maps the TI output index to that slot (empty: identity).
+// For N = 32K each symbol's run is further partitioned [cells of bins < N/2 | cells of bins >= N/2]
+// (each part in TI output order), so a half streams only its own cells; `part` maps the TI output
+// index to that slot (empty: identity).
 struct ChainLayout {
   std::vector<int32_t> cmap;     // Nsym x N, stored row order: >= 0 data slot, < 0 aux (-code - 1)
   std::vector<uint16_t> inv;     // S: data slot -> stored bin index within its symbol's row

@@ -115,10 +115,9 @@ def ti_dest(plan, r, t):
 
 
 def chain_layout(cfg):
-    """the fused chain's layout: cmap (Nsym x N, stored row order: [even | odd] bins when split;
-    data codes are frame data slots), inv (slot -> stored bin), each symbol's contiguous slot
-    range [d0, d0 + n) with its first n0 slots feeding the even half when split, and part
-    (TI output index -> slot)"""
+    """the fused chain's layout: cmap (Nsym x N, natural FFT-input order; data codes are frame data
+    slots), inv (slot -> bin), each symbol's contiguous slot range [d0, d0 + n) with its first n0
+    slots feeding the bins < N/2 when split (32K), and part (TI output index -> slot)"""
     p = np.array(cfg.fm_args(), np.int32)
     g = np.array([cfg.misogroup, cfg.equalization, cfg.bandwidth], np.int32)
     info = np.zeros(4, np.int32)
@@ -158,9 +157,6 @@ def aux_lists(cfg):
 
 
 def stored_to_natural(row, N, split):
-    if not split:
-        return row
-    nat = np.empty_like(row)
-    nat[0::2] = row[: N // 2]
-    nat[1::2] = row[N // 2:]
-    return nat
+    """the kernels' stored row order is the natural FFT-input order (32K: halves = bins < N/2 and
+    >= N/2, t2_plan ofdm_stored_rows)"""
+    return row

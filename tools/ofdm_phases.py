@@ -33,7 +33,8 @@ a = np.array(rows)
 t0 = a[:, 0]
 t0 = (t0 - t0.min()) & 0xFFFFFFFF
 d = a[:, 1:9]
-names = ["fill0", "scatter0", "fft0", "hold E", "fill1", "scatter1", "fft1", "combine"]
+names = (["fill0", "scatter0", "fft0", "hold E", "fill1", "scatter1", "fft1", "combine"] if N < 32768 else
+         ["scatter0", "scatter1+read", "stageA", "exch1", "stageB", "exch2", "stageC", "store"])
 prev = np.zeros(len(a), np.int64)
 print("phase durations (us), median / p90 over %d workgroups" % len(a))
 for i, n in enumerate(names):
