@@ -71,7 +71,10 @@ def algorithmic_bytes(cfg, info):
     s2 = F * (nldpc // 8 + 8 * cs)
     s3 = 8 * S + 8 * M
     s4 = 8 * M + 8 * IQ
-    # kernel stages: fec = S1 (+ LDPC), map = S2, ofdm = S3 + S4 (fused)
+    # kernel stages: fec = S1 (+ LDPC), map = S2, ofdm = S3 + S4 (fused); fec = S1 + S2 when the
+    # FEC and map kernels are one
+    if info.get("fused_fec_map"):
+        return {"fec": s1 + s2, "map": 0, "ofdm": s3 + s4}
     return {"fec": s1, "map": s2, "ofdm": s3 + s4}
 
 
@@ -85,6 +88,8 @@ def minimal_bytes(cfg, info, iq_bytes=8):
     nldpc = 64800 if cfg.framesize == 1 else 16200
     kbch = KBCH[(cfg.framesize, cfg.rate)]
     cs, S, IQ = info["cell_size"], info["stream_items"], info["iq_samples_per_frame"]
+    if info.get("fused_fec_map"):   # one kernel: TS in, index pairs out, codewords only in LDS
+        return {"fec": F * ((kbch - 80) // 8 + 2 * cs), "map": 0, "ofdm": 2 * S + iq_bytes * IQ}
     return {"fec": F * ((kbch - 80) // 8 + nldpc // 8), "map": F * (nldpc // 8 + 2 * cs),
             "ofdm": 2 * S + iq_bytes * IQ}
 
@@ -118,7 +123,7 @@ def pmc_passes(args):
     res = {k: {} for k in KERNELS}
     for ctrs in (["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"]):
         d = tempfile.mkdtemp(prefix="t2pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [rp, "--pmc", *ctrs, "--kernel-include-regex", "(fec|map|ofdm)_kernel", "-T", "-f", "csv", "-d", d,
+        cmd = [rp, "--pmc", *ctrs, "--kernel-include-regex", "(fec|map|ofdm|ofdm32)_kernel", "-T", "-f", "csv", "-d", d,
                "-o", "pmc", "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--config", args.config,
                "--frames", str(args.frames), "--steps", "2", "--warmup", "1"]
         try:
@@ -130,7 +135,9 @@ def pmc_passes(args):
             with open(fn) as fh:
                 for row in csv.DictReader(fh):
                     for k in KERNELS:
-                        if row.get("Counter_Name") in ctrs and (k + "_kernel") in row.get("Kernel_Name", ""):
+                        kn = row.get("Kernel_Name", "")
+                        if row.get("Counter_Name") in ctrs and (kn.startswith(k + "_kernel") or
+                                                                 (k == "ofdm" and kn.startswith("ofdm32_kernel"))):
                             vals.setdefault((k, row["Counter_Name"]), []).append(float(row["Counter_Value"]))
         for (k, c), v in vals.items():
             res[k][c] = sum(v) / len(v)
@@ -451,6 +458,8 @@ def main():
         mb = minimal_bytes(cfg, info)
         stages, rooflines = {}, {}
         for k, name in enumerate(KERNELS):
+            if name == "map" and info.get("fused_fec_map"):
+                continue                  # FEC and map run as one kernel ("fec")
             avg_ms = stage_ms[k] / max(1, launches[k])
             t = avg_ms * 1e-3
             stages[name] = {"avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": ab[name] * B,
@@ -478,7 +487,7 @@ def main():
                     e["salu_wave_instr_per_block"] = pm.get("SQ_INSTS_SALU", 0) / nb
                     e["valu_issue_frac"] = pm["SQ_INSTS_VALU"] / t / VALU_ISSUE_PEAK
             rooflines[name] = e
-        dom = max(KERNELS, key=lambda n: stages[n]["avg_launch_ms"])
+        dom = max(stages, key=lambda n: stages[n]["avg_launch_ms"])
         roof = dict(rooflines[dom])
         roof["note"] = ("frac = the kernel's minimal HBM bytes (DESIGN.md 5) / its HIP-event launch time / 8 TB/s; "
                         "traffic = calibrated rocprofv3 FETCH_SIZE + WRITE_SIZE per launch; stage_bytes_frac = "

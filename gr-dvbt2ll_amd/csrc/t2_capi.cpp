@@ -553,6 +553,9 @@ struct dvbt2ll_chain {
   hipStream_t cap_stream = nullptr;
   std::vector<std::unique_ptr<ChainGraph>> graphs;
   int max_frames = 0;
+  // fused: FEC and map in one kernel (fec_kernel FEC_TS_TO_PAIRS, the codeword never leaves LDS);
+  // an experiment switch, see dvbt2ll_chain_create
+  bool fused = false;
   int64_t pair_stride = 0;   // pairs buffer: frame k's slots at k * pair_stride (multiple of 8)
   int64_t cw_stride = 0;
   int64_t iq_per_frame = 0;
@@ -596,12 +599,25 @@ struct dvbt2ll_chain {
     evused = 0;
     return st;
   }
-  // capture the three launches once per (nframes, format, slot) on a private stream, then per
-  // call rewrite the kernel nodes' arguments and launch the instantiated graph on s.  An exec is
-  // only re-armed after its previous launch has completed (host wait on the slot's completion
-  // event, recorded after every run on the slot), so no in-flight launch ever sees arguments
-  // rewritten under it; with several slots the calls still overlap on the device
+  // the chain's kernels on stream s: fused FEC + map, or FEC then map; then OFDM.  ev (timing):
+  // recorded after the FEC (+ map) and after the map kernel
+  hipError_t launch_chain(const FecIO &fio, const MapIO &mio, const OfdmIO &oio, hipStream_t s, hipEvent_t ev1,
+                          hipEvent_t ev2) {
+    hipError_t e = fused ? launch_fec_map(fec.dev, fio, map.dev, mio.out_pairs, mio.frame_stride, s)
+                         : launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, s);
+    if (e == hipSuccess && ev1) e = hipEventRecord(ev1, s);
+    if (e == hipSuccess && !fused) e = launch_map(map.dev, mio, s);
+    if (e == hipSuccess && ev2) e = hipEventRecord(ev2, s);
+    if (e == hipSuccess) e = launch_ofdm(ofdm.dev, oio, s);
+    return e;
+  }
+  // capture the launches once per (nframes, format, slot) on a private stream, then per call
+  // rewrite the kernel nodes' arguments and launch the instantiated graph on s.  An exec is only
+  // re-armed after its previous launch has completed (host wait on the slot's completion event,
+  // recorded after every run on the slot), so no in-flight launch ever sees arguments rewritten
+  // under it; with several slots the calls still overlap on the device
   int graph_launch(const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, int slot, hipStream_t s) {
+    const int nk = fused ? 2 : 3;
     ChainGraph *g = nullptr;
     for (auto &c : graphs)
       if (c->nframes == nframes && c->fmt == ofdm.dev.fmt && c->slot == slot) g = c.get();
@@ -613,13 +629,11 @@ struct dvbt2ll_chain {
       c->fmt = ofdm.dev.fmt;
       c->slot = slot;
       HIP_TRY(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
-      hipError_t e1 = launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, cap_stream);
-      hipError_t e2 = e1 == hipSuccess ? launch_map(map.dev, mio, cap_stream) : e1;
-      hipError_t e3 = e2 == hipSuccess ? launch_ofdm(ofdm.dev, oio, cap_stream) : e2;
+      hipError_t e1 = launch_chain(fio, mio, oio, cap_stream, nullptr, nullptr);
       hipError_t ec = hipStreamEndCapture(cap_stream, &c->graph);
-      HIP_TRY(e3);
+      HIP_TRY(e1);
       HIP_TRY(ec);
-      // the kernel nodes in dependency order: a linear chain of exactly three
+      // the kernel nodes in dependency order: a linear chain of nk
       size_t n = 0;
       HIP_TRY(hipGraphGetNodes(c->graph, nullptr, &n));
       std::vector<hipGraphNode_t> nodes(n);
@@ -630,14 +644,14 @@ struct dvbt2ll_chain {
         HIP_TRY(hipGraphNodeGetType(nd, &t));
         if (t == hipGraphNodeTypeKernel) kn.push_back(nd);
       }
-      if (kn.size() != 3) return DVBT2LL_EDEVICE;
+      if ((int)kn.size() != nk) return DVBT2LL_EDEVICE;
       auto ndeps = [&](hipGraphNode_t nd, size_t &k) -> int {
         HIP_TRY(hipGraphNodeGetDependencies(nd, nullptr, &k));
         return 0;
       };
-      // order: the root (no dependencies), then the node depending on it, then the last
+      // order: the root (no dependencies), then the node depending on it, and so on
       hipGraphNode_t prev = nullptr;
-      for (int k = 0; k < 3; k++) {
+      for (int k = 0; k < nk; k++) {
         for (auto nd : kn) {
           size_t nd_n = 0;
           if (ndeps(nd, nd_n)) return DVBT2LL_EDEVICE;
@@ -662,14 +676,18 @@ struct dvbt2ll_chain {
     }
     if (slot_used[slot]) HIP_TRY(hipEventSynchronize(slot_done[slot]));
     FecDev fd = fec.dev;
-    MapDev md = map.dev;
+    MapDev md = map.dev, md0{};
     OfdmDev od = ofdm.dev;
     FecIO fi = fio;
     MapIO mi = mio;
     OfdmIO oi = oio;
-    void *a0[2] = {&fd, &fi}, *a1[2] = {&md, &mi}, *a2[2] = {&od, &oi};
+    uint16_t *op = fused ? mio.out_pairs : nullptr;
+    int64_t fs = fused ? mio.frame_stride : 0;
+    void *a0[5] = {&fd, &fi, fused ? (void *)&md : (void *)&md0, &op, &fs};
+    void *a1[2] = {&md, &mi}, *a2[2] = {&od, &oi};
     void **args[3] = {a0, a1, a2};
-    for (int k = 0; k < 3; k++) {
+    if (fused) args[1] = a2;
+    for (int k = 0; k < nk; k++) {
       hipKernelNodeParams p = g->base[k];
       p.kernelParams = args[k];
       p.extra = nullptr;
@@ -679,7 +697,8 @@ struct dvbt2ll_chain {
     return 0;
   }
   int alloc_slot(int k) {
-    if (cw[k].ensure((size_t)frame.F * max_frames * cw_stride) || pairs[k].ensure((size_t)pair_stride * max_frames * 2))
+    if ((!fused && cw[k].ensure((size_t)frame.F * max_frames * cw_stride)) ||
+        pairs[k].ensure((size_t)pair_stride * max_frames * 2))
       return DVBT2LL_ENOMEM;
     if (!slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
     return 0;
@@ -789,6 +808,15 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   // the OFDM kernel addresses index pairs and aux cells with 32-bit byte offsets
   if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32))
     return DVBT2LL_EINVAL;
+  {
+    // tuning knob for kernel experiments (tools/gpu_fused_ab.sh): DVBT2LL_CHAIN_FUSED=1 runs FEC and
+    // map as one kernel where its LDS allows 3+ workgroups per CU.  Off by default: measured slower
+    // (cfg3 0.707 ms against 0.343 + 0.269 ms per 64 frames; the map phases' table loads are not
+    // hidden at 4 workgroups per CU), kept parity-tested for the record
+    const char *fu = std::getenv("DVBT2LL_CHAIN_FUSED");
+    const int lds = fec_map_lds(h->frame.cs, h->fec.plan.nldpc);
+    h->fused = lds && (160 * 1024) / lds >= 3 && fu && std::atoi(fu);
+  }
   if ((r = h->alloc_slot(0))) return r;
   if ((r = upload(h->aux, auxv))) return r;
   if (h->sync_err.ensure(4)) return DVBT2LL_ENOMEM;
@@ -810,6 +838,7 @@ extern "C" int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info
   info->fft_size = h->pilot.N;
   info->guard_interval = h->pilot.G;
   info->cw_stride_bytes = h->cw_stride;
+  info->fused_fec_map = h->fused ? 1 : 0;
   return DVBT2LL_OK;
 }
 
@@ -847,7 +876,7 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   fio.ts_base = ts_base;
   fio.ts_len = ts_len;
   fio.first_block = first_frame * F;
-  fio.out = cw.as<uint8_t>();
+  fio.out = h->fused ? nullptr : cw.as<uint8_t>();
   fio.cw_stride = h->cw_stride;
   fio.nblocks = F * nframes;
   fio.sync_err = h->sync_err.as<uint32_t>();
@@ -871,11 +900,7 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
     int r = h->graph_launch(fio, mio, oio, nframes, slot, s);
     if (r) return r;
   } else {
-    HIP_TRY(launch_fec(FEC_TS_TO_TEMPU, h->fec.dev, fio, s));
-    if (h->timing) HIP_TRY(hipEventRecord(ev[1], s));
-    HIP_TRY(launch_map(h->map.dev, mio, s));
-    if (h->timing) HIP_TRY(hipEventRecord(ev[2], s));
-    HIP_TRY(launch_ofdm(h->ofdm.dev, oio, s));
+    HIP_TRY(h->launch_chain(fio, mio, oio, s, h->timing ? ev[1] : nullptr, h->timing ? ev[2] : nullptr));
     if (h->timing) HIP_TRY(hipEventRecord(ev[3], s));
   }
   HIP_TRY(hipEventRecord(h->slot_done[slot], s));
@@ -901,7 +926,7 @@ extern "C" int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots) {
     if (r) return r;
   }
   for (int k = nslots; k < DVBT2LL_CHAIN_MAX_SLOTS; k++) {
-    h->cw[k].release();
+    h->cw[k].release();   // (never allocated when fused)
     h->pairs[k].release();
     h->slot_used[k] = false;
   }
@@ -949,7 +974,8 @@ extern "C" int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *l
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes) {
-  if (!h || !out || bytes < 0 || (size_t)bytes > h->cw[h->last_slot].n) return DVBT2LL_EINVAL;
+  // the fused kernel keeps codewords in LDS: only the two-kernel path has them
+  if (!h || !out || bytes < 0 || h->fused || (size_t)bytes > h->cw[h->last_slot].n) return DVBT2LL_EINVAL;
   const DevBuf &cw = h->cw[h->last_slot];
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipDeviceSynchronize());

@@ -10,6 +10,8 @@ enum FecMode {
   FEC_TS_TO_TEMPU = 0,   // chain: TS bytes -> packed interleaver-input codeword
   FEC_TS_TO_BITS = 1,    // bbheaderbch block: TS bytes -> unpacked nbch bits
   FEC_BITS_TO_BITS = 2,  // ldpc block: unpacked nbch bits -> unpacked nldpc bits (natural)
+  FEC_TS_TO_PAIRS = 3,   // fused chain: TS bytes -> codeword in LDS -> bit interleave + demux + cell
+                         // and time interleave -> constellation index pairs (FEC and map kernels in one)
 };
 
 struct FecDev {
@@ -117,6 +119,11 @@ struct GatherIO {
 };
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s);
+// fused FEC + map (FEC_TS_TO_PAIRS): index pairs of launch block b into out_pairs + (b / F) * frame_stride
+hipError_t launch_fec_map(const FecDev &d, const FecIO &io, const MapDev &md, uint16_t *out_pairs,
+                          int64_t frame_stride, hipStream_t s);
+// LDS bytes of the fused kernel for a constellation's cell size / 0 when it would not fit
+int fec_map_lds(int cs, int nldpc);
 hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s);
 hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s);
 hipError_t launch_gather(const GatherIO &io, hipStream_t s);

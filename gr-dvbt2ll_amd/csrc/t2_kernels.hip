@@ -143,16 +143,19 @@ constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 2
 constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g || d_g[0..56)
 constexpr int FEC_WG_PER_CU = 6;
 // dynamic LDS carve (bytes): a persistent part (the workgroup loops over FEC blocks; tables are
-// staged once), then one region reused by phase:
-//   BB/CRC phase: [raw TS bytes | CRC-8 table | CRC-8 zero-extension tables] (tables per block)
-//   LDPC: [D: ngroups x 13 words | rows: q x 12 words], ngroups + q = nldpc / 360 (<= 180)
-constexpr int SM_FRAME = 0;
-constexpr int SM_SYNC = SM_FRAME + FEC_FRAME_BYTES;          // 48 (<= 36 sync slots)
+// staged once), then the per-block area, reused by phase:
+//   BB/CRC phase: [frame | raw TS bytes | CRC-8 table | CRC-8 zero-extension tables]
+//   LDPC: [frame | D: ngroups x 13 words | rows: q x 12 words], ngroups + q = nldpc / 360 (<= 180)
+//   fused map phase (FEC_TS_TO_PAIRS): [cell indices | index pairs] over the whole per-block area,
+//   the interleaver-input words (built from frame + rows) beyond it (fec_map_lds)
+constexpr int SM_BTAB = 0;                                   // 256*3*8 = 6144
+constexpr int SM_ENT = SM_BTAB + 6144;                       // 648*4
+constexpr int SM_HCRC = SM_ENT + FEC_MAX_ENT * 4;            // 72 (+8)
+constexpr int SM_SYNC = SM_HCRC + 80;                        // 48 (<= 36 sync slots)
 constexpr int SM_W = SM_SYNC + 48;                           // 12*4
-constexpr int SM_HCRC = SM_W + 48;                           // 72 (+8)
-constexpr int SM_ENT = SM_HCRC + 80;                         // 648*4
-constexpr int SM_BTAB = SM_ENT + FEC_MAX_ENT * 4;            // 256*3*8 = 6144
-constexpr int SM_PHASE = SM_BTAB + 6144;
+constexpr int SM_BLK = SM_W + 48;                            // per-block area
+constexpr int SM_FRAME = SM_BLK;
+constexpr int SM_PHASE = SM_FRAME + FEC_FRAME_BYTES;
 constexpr int SM_RAW = SM_PHASE;                             // raw TS bytes of the block (NM)
 constexpr int FEC_RAW_BYTES = 188 + 6720 + 16;               // one packet before + max payload
 constexpr int SM_CRC8 = SM_RAW + ((FEC_RAW_BYTES + 15) & ~15);   // 256
@@ -160,8 +163,8 @@ constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
 constexpr int SM_D = SM_PHASE;                               // rows follow D at word ngroups * 13
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
 constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_BYTES ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_BYTES);
-static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0, "LDS carve alignment");
-static_assert(SM_SYNC % 8 == 0 && SM_HCRC - SM_SYNC >= 4 * 3 * 8, "BCH wave remainders in SM_SYNC + SM_W");
+static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0 && SM_BLK % 16 == 0, "LDS carve alignment");
+static_assert(SM_SYNC % 8 == 0 && SM_BLK - SM_SYNC >= 4 * 3 * 8, "BCH wave remainders in SM_SYNC + SM_W");
 static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "six FEC workgroups per CU");
 
 // stream position of payload byte J (counted over the payload bytes of the whole stream)
@@ -290,8 +293,27 @@ __device__ __forceinline__ void bch_combine(uint8_t *frame, const uint64_t *wres
   if (lane < P / 8) frame[L + lane] = get_byte192(acc, P - 8 - 8 * lane);
 }
 
+// fused mode: the map phases' LDS (cell indices at SM_BLK, index pairs after them, the codeword
+// words beyond the FEC carve and the indices)
+__host__ __device__ inline int fec_map_idx_bytes(int cs) { return (cs + 15) & ~15; }
+__host__ __device__ inline int fec_map_cww_off(int cs) {
+  const int a = SM_BLK + fec_map_idx_bytes(cs), b = (FEC_SMEM + 15) & ~15;
+  return a > b ? a : b;
+}
+__host__ __device__ inline int fec_map_smem(int cs, int nldpc) {
+  const int cw = fec_map_cww_off(cs) + ((nldpc / 8 + 4 + 15) & ~15);
+  const int st = SM_BLK + fec_map_idx_bytes(cs) + ((2 * cs + 15) & ~15);
+  return cw > st ? cw : st;
+}
+
+template <int NT> __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, int tid);
+template <int NT>
+__device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
+                                uint16_t *stage, int blk, int tid);
+
 template <int MODE>
-__global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io) {
+__global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io, MapDev md,
+                                                                        uint16_t *out_pairs, int64_t frame_stride) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int L = d.kbch >> 3;           // BBFRAME bytes
@@ -315,7 +337,17 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     for (int i = tid; i < 72; i += FEC_THREADS) hcrc8[i] = d.hcrc_bits[i];
   __syncthreads();
 
-  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
+  // blocks of this workgroup: a stride over the launch, or (fused mode, grid a multiple of 8) a
+  // stride within the eighth of the launch that its XCD covers, so that the FEC blocks of a time-
+  // interleaver block, whose index pairs interleave in 10-byte runs, are stored through one L2
+  int bstart = blockIdx.x, bstep = gridDim.x, bend = io.nblocks;
+  if (MODE == FEC_TS_TO_PAIRS && (gridDim.x & 7) == 0) {
+    const int q = (io.nblocks + 7) >> 3, x = blockIdx.x & 7;
+    bstart = x * q + (blockIdx.x >> 3);
+    bstep = gridDim.x >> 3;
+    bend = min((x + 1) * q, io.nblocks);
+  }
+  for (int bi = bstart; bi < bend; bi += bstep) {
   const int64_t B = io.first_block + bi;
   FEC_PHASE(0);
   do {   // one FEC block; `break` ends it early (block-API modes)
@@ -511,7 +543,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
         case 160: bch_combine<160>(frame, wres, d.bch_m64, L, nbw, lane); break;
         default: bch_combine<128>(frame, wres, d.bch_m64, L, nbw, lane); break;
       }
-      if (MODE == FEC_TS_TO_TEMPU) {
+      if (MODE == FEC_TS_TO_TEMPU || MODE == FEC_TS_TO_PAIRS) {
         // the last info group holds the BCH parity (P < 360): lay it out here, after the parity
         // bytes (same wave; LDS accesses of one wave complete in order)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -519,7 +551,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane < FEC_DW) ldpc_group_word(D, frame, ngroups - 1, lane);
       }
-    } else if (MODE == FEC_TS_TO_TEMPU) {
+    } else if (MODE == FEC_TS_TO_TEMPU || MODE == FEC_TS_TO_PAIRS) {
       // waves 1..3 (after their BCH share, if any) lay out the info groups without parity
       for (int it = tid - 64; it < (ngroups - 1) * FEC_DW; it += FEC_THREADS - 64) {
         const int g = it / FEC_DW;
@@ -639,6 +671,30 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   };
   uint32_t *dstw = (uint32_t *)(io.out + (int64_t)bi * io.cw_stride);
   const uint32_t *framew = (const uint32_t *)frame;
+  if (MODE == FEC_TS_TO_PAIRS) {
+    // the codeword as the map phases read it (big-endian words, one word of slack), in LDS
+    const int cs = md.cs, ib = fec_map_idx_bytes(cs);
+    uint32_t *cww = (uint32_t *)(smem + fec_map_cww_off(cs));
+    for (int i = tid; i <= (cwb + 3) >> 2; i += FEC_THREADS) {
+      uint32_t v = 0;
+      if (4 * i + 4 <= NB) {
+        v = framew[i];
+      } else if (4 * i < cwb) {
+        for (int e = 0; e < 4; e++) {
+          const int bidx = 4 * i + e;
+          const uint32_t by = bidx < NB ? (uint32_t)frame[bidx] : bidx < cwb ? parity_byte(bidx - NB) : 0u;
+          v |= by << (8 * e);
+        }
+      }
+      cww[i] = __builtin_bswap32(v);
+    }
+    __syncthreads();
+    uint8_t *idx = smem + SM_BLK;
+    map_cells<FEC_THREADS>(md, cww, idx, tid);
+    __syncthreads();
+    map_store_pairs<FEC_THREADS>(md, out_pairs, frame_stride, idx, (uint16_t *)(smem + SM_BLK + ib), bi, tid);
+    break;
+  }
   for (int i = tid; i < (cwb + 3) >> 2; i += FEC_THREADS) {
     uint32_t v;
     if (4 * i + 4 <= NB) {
@@ -666,8 +722,8 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   }
 }
 
-// resident FEC workgroups for a persistent launch: FEC_WG_PER_CU per CU of the current device
-static int fec_grid(int nblocks) {
+// resident FEC workgroups for a persistent launch: per_cu per CU of the current device
+static int fec_grid(int nblocks, int per_cu) {
   static std::atomic<int> ncu[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
@@ -676,23 +732,51 @@ static int fec_grid(int nblocks) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
     ncu[dev].store(n, std::memory_order_relaxed);
   }
-  return nblocks < n * FEC_WG_PER_CU ? nblocks : n * FEC_WG_PER_CU;
+  return nblocks < n * per_cu ? nblocks : n * per_cu;
 }
 
+static bool fec_plan_fits(const FecDev &d) {
+  // the LDS carve is sized for the standard codes: refuse anything larger
+  return !(d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 52 * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
+           (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.bch_waves < 1 || d.bch_waves > 4 ||
+           d.chunk * 64 * d.bch_waves < d.kbch / 8);
+}
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
-  // the LDS carve is sized for the standard codes: refuse anything larger
-  if (d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 52 * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
-      (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.bch_waves < 1 || d.bch_waves > 4 ||
-      d.chunk * 64 * d.bch_waves < d.kbch / 8)
-    return hipErrorInvalidValue;
-  dim3 grid(fec_grid(io.nblocks)), block(FEC_THREADS);
+  if (!fec_plan_fits(d)) return hipErrorInvalidValue;
+  dim3 grid(fec_grid(io.nblocks, FEC_WG_PER_CU)), block(FEC_THREADS);
+  const MapDev md{};
   switch (mode) {
-    case FEC_TS_TO_TEMPU: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, FEC_SMEM, s, d, io); break;
-    case FEC_TS_TO_BITS: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_BITS>, grid, block, FEC_SMEM, s, d, io); break;
-    default: hipLaunchKernelGGL(fec_kernel<FEC_BITS_TO_BITS>, grid, block, FEC_SMEM, s, d, io); break;
+    case FEC_TS_TO_TEMPU:
+      hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, FEC_SMEM, s, d, io, md, nullptr, (int64_t)0);
+      break;
+    case FEC_TS_TO_BITS:
+      hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_BITS>, grid, block, FEC_SMEM, s, d, io, md, nullptr, (int64_t)0);
+      break;
+    default:
+      hipLaunchKernelGGL(fec_kernel<FEC_BITS_TO_BITS>, grid, block, FEC_SMEM, s, d, io, md, nullptr, (int64_t)0);
+      break;
   }
+  return hipGetLastError();
+}
+
+int fec_map_lds(int cs, int nldpc) {
+  const int b = fec_map_smem(cs, nldpc);
+  return b <= 160 * 1024 ? b : 0;
+}
+
+hipError_t launch_fec_map(const FecDev &d, const FecIO &io, const MapDev &md, uint16_t *out_pairs,
+                          int64_t frame_stride, hipStream_t s) {
+  if (io.nblocks <= 0) return hipSuccess;
+  const int lds = fec_map_lds(md.cs, d.nldpc);
+  if (!fec_plan_fits(d) || !lds || md.F < 1) return hipErrorInvalidValue;
+  hipError_t e = lds_limit((const void *)fec_kernel<FEC_TS_TO_PAIRS>, lds);
+  if (e != hipSuccess) return e;
+  int per_cu = (160 * 1024) / lds;
+  per_cu = per_cu < 1 ? 1 : per_cu > FEC_WG_PER_CU ? FEC_WG_PER_CU : per_cu;
+  dim3 grid(fec_grid(io.nblocks, per_cu)), block(FEC_THREADS);
+  hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_PAIRS>, grid, block, lds, s, d, io, md, out_pairs, frame_stride);
   return hipGetLastError();
 }
 
@@ -733,6 +817,148 @@ __shared__ uint64_t g_map_ts[8];
 #define MAP_PHASE(i) do { } while (0)
 #endif
 
+// column twist + demux of one FEC block: interleaver-input bits (big-endian words cww, one word of
+// slack past the end) -> cell indices idx (one byte per cell)
+template <int NT>
+__device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, int tid) {
+  const int cs = d.cs;
+  // ---- cell indices: column-twist write / row read / demux (interleavermod:351-403, 440-500,
+  //      529-598, 626-677).  One thread per 32 rows: each column's 32 bits are one (twisted,
+  //      wrapping) window of the codeword, the W windows are ordered by demuxed bit position and
+  //      transposed as a bit matrix, giving each row's demuxed word directly.
+  if (d.mode == 0) {
+    // QPSK: cell j = codeword bits 2j, 2j+1 (no bit interleaving, interleavermod:309-314)
+    uint32_t *idxw = (uint32_t *)idx;
+    for (int w = tid; w < (cs + 3) >> 2; w += NT) {
+      const uint32_t word = cww[w >> 2], sh = 24u - 8u * (uint32_t)(w & 3);
+      const uint32_t byte = (word >> sh) & 0xFFu;   // cells 4w..4w+3
+      idxw[w] = ((byte >> 6) & 3u) | (((byte >> 4) & 3u) << 8) | (((byte >> 2) & 3u) << 16) | ((byte & 3u) << 24);
+    }
+  } else {
+    const int R = d.R, mod = d.mod;
+    auto window = [&](int s) -> uint32_t {    // codeword bits [s, s + 32), MSB first
+      const uint64_t v = ((uint64_t)cww[s >> 5] << 32) | cww[(s >> 5) + 1];
+      return (uint32_t)((v << (s & 31)) >> 32);
+    };
+    // 8-bit transpose (Hacker's Delight transpose8): bit 8 i + j <-> bit 8 j + i
+    auto tr8 = [](uint64_t x) -> uint64_t {
+      uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+      x ^= t ^ (t << 7);
+      t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+      x ^= t ^ (t << 14);
+      t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+      x ^= t ^ (t << 28);
+      return x;
+    };
+    // one thread per 8 rows: byte b of x = column colsel[b]'s 8 bits (row k at bit 7 - k); after
+    // the transpose byte 7 - k holds row k's demuxed bits b
+    for (int g = tid; g < (R + 7) >> 3; g += NT) {
+      const int j0 = 8 * g;
+      uint64_t x[2] = {0, 0};
+#pragma unroll
+      for (int b = 0; b < 16; b++) {
+        const int e = d.colsel[b];
+        if (e == 255) continue;
+        int off = j0 - d.twist[e];
+        off += off < 0 ? R : 0;
+        uint32_t win = window(e * R + off);
+        if (off + 8 > R) {                       // the column wraps inside these 8 rows
+          const int n1 = R - off;
+          win = (win & ~(0xFFFFFFFFu >> n1)) | (window(e * R) >> n1);
+        }
+        x[b >> 3] |= (uint64_t)(win >> 24) << (8 * (b & 7));
+      }
+      const uint64_t lo = tr8(x[0]), hi = d.W > 8 ? tr8(x[1]) : 0ull;
+      uint32_t *idxw = (uint32_t *)idx;
+      if (d.mode == 1) {                         // two cells per row: pack >> mod, pack & (2^mod - 1)
+        const uint32_t lo_mask = (1u << mod) - 1u;
+#pragma unroll
+        for (int qd = 0; qd < 4; qd++) {
+          const int k0 = 2 * qd;
+          const uint32_t p0 = (uint32_t)((lo >> (8 * (7 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (7 - k0))) & 0xFFu) << 8);
+          const uint32_t p1 = (uint32_t)((lo >> (8 * (6 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (6 - k0))) & 0xFFu) << 8);
+          if (j0 + k0 < R)
+            idxw[4 * g + qd] = (p0 >> mod) | ((p0 & lo_mask) << 8) | ((p1 >> mod) << 16) | ((p1 & lo_mask) << 24);
+        }
+      } else {                                   // 256-QAM short: one cell per row (byte-reversed lo)
+        const uint64_t rv = __builtin_bswap64(lo);
+        if (j0 < R) idxw[2 * g] = (uint32_t)rv;
+        if (j0 + 4 < R) idxw[2 * g + 1] = (uint32_t)(rv >> 32);
+      }
+    }
+  }
+}
+
+// chain: cell interleaver (framemapper:1973-1998) of block blk's (index, previous index) pairs through
+// LDS (stage, 2 cs bytes), then the time-interleaver (framemapper:1999-2028) store into the frame
+// data region out_pairs + (blk / F) frame_stride
+template <int NT>
+__device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
+                                uint16_t *stage, int blk, int tid) {
+  const int cs = d.cs;
+  const int r = blk % d.F;
+  const int shift = d.ci_shift[r];
+  uint16_t *dst = out_pairs + (int64_t)(blk / d.F) * frame_stride;   // frame data region
+  int r0 = r, nb = 1;
+  if (d.ti_on) {
+    const int ns = d.ti_nsmall * d.ti_small;
+    if (r < ns) { r0 = r - r % d.ti_small; nb = d.ti_small; }
+    else { r0 = r - (r - ns) % d.ti_big; nb = d.ti_big; }
+  }
+  const int rows = cs / 5, cols = 5 * nb;
+  const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
+  // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
+  // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
+  constexpr int MB = MAP_MB;
+  for (int j0 = tid; j0 < cs; j0 += MB * NT) {
+    int t[MB];
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+      const int j = min(j0 + u * NT, cs - 1);
+      t[u] = d.ci_perm[j] + shift;
+    }
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+      const int j = j0 + u * NT;
+      if (j < cs) {
+        const int tt = t[u] >= cs ? t[u] - cs : t[u];
+        const uint32_t lo = idx[j], hi = d.rotation ? idx[j == 0 ? cs - 1 : j - 1] : lo;
+        stage[tt] = (uint16_t)(lo | (hi << 8));
+      }
+    }
+  }
+  __syncthreads();
+  MAP_PHASE(3);
+  // time-interleaver store of the index pairs: row-major over (row, e), 5 consecutive cells
+  // (10 B) per TI row (32K: through the half partition); the constellation lookup (QAM +
+  // rotated-constellation Q delay) is fused into the OFDM kernel's bin scatter
+  const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
+  // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
+  const int16_t *pr = d.part ? d.part + (int64_t)r * cs : nullptr;   // block-major int16 table
+  for (int j0 = tid; j0 < cs; j0 += MB * NT) {
+    uint32_t dsl[MB];
+    int tt[MB];
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+      const int j = min(j0 + u * NT, cs - 1);
+      int o;
+      if (d.ti_on) {
+        const int row = j / 5, e = j - 5 * row;
+        tt[u] = e * rows + row;
+        o = row * cols + e;
+      } else {
+        tt[u] = j;
+        o = j;
+      }
+      dsl[u] = (uint32_t)fbase + (uint32_t)o + (uint32_t)(pr ? (int)pr[j] : 0);
+    }
+#pragma unroll
+    for (int u = 0; u < MB; u++) {
+      if (j0 + u * NT < cs) st_off(dst, dsl[u] * 2u, stage[tt[u]]);
+    }
+  }
+}
+
 __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -770,71 +996,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   }
   __syncthreads();
   MAP_PHASE(1);
-  // ---- cell indices: column-twist write / row read / demux (interleavermod:351-403, 440-500,
-  //      529-598, 626-677).  One thread per 32 rows: each column's 32 bits are one (twisted,
-  //      wrapping) window of the codeword, the W windows are ordered by demuxed bit position and
-  //      transposed as a bit matrix, giving each row's demuxed word directly.
-  if (d.mode == 0) {
-    // QPSK: cell j = codeword bits 2j, 2j+1 (no bit interleaving, interleavermod:309-314)
-    uint32_t *idxw = (uint32_t *)idx;
-    for (int w = tid; w < (cs + 3) >> 2; w += MAP_THREADS) {
-      const uint32_t word = cww[w >> 2], sh = 24u - 8u * (uint32_t)(w & 3);
-      const uint32_t byte = (word >> sh) & 0xFFu;   // cells 4w..4w+3
-      idxw[w] = ((byte >> 6) & 3u) | (((byte >> 4) & 3u) << 8) | (((byte >> 2) & 3u) << 16) | ((byte & 3u) << 24);
-    }
-  } else {
-    const int R = d.R, mod = d.mod;
-    auto window = [&](int s) -> uint32_t {    // codeword bits [s, s + 32), MSB first
-      const uint64_t v = ((uint64_t)cww[s >> 5] << 32) | cww[(s >> 5) + 1];
-      return (uint32_t)((v << (s & 31)) >> 32);
-    };
-    // 8-bit transpose (Hacker's Delight transpose8): bit 8 i + j <-> bit 8 j + i
-    auto tr8 = [](uint64_t x) -> uint64_t {
-      uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
-      x ^= t ^ (t << 7);
-      t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
-      x ^= t ^ (t << 14);
-      t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
-      x ^= t ^ (t << 28);
-      return x;
-    };
-    // one thread per 8 rows: byte b of x = column colsel[b]'s 8 bits (row k at bit 7 - k); after
-    // the transpose byte 7 - k holds row k's demuxed bits b
-    for (int g = tid; g < (R + 7) >> 3; g += MAP_THREADS) {
-      const int j0 = 8 * g;
-      uint64_t x[2] = {0, 0};
-#pragma unroll
-      for (int b = 0; b < 16; b++) {
-        const int e = d.colsel[b];
-        if (e == 255) continue;
-        int off = j0 - d.twist[e];
-        off += off < 0 ? R : 0;
-        uint32_t win = window(e * R + off);
-        if (off + 8 > R) {                       // the column wraps inside these 8 rows
-          const int n1 = R - off;
-          win = (win & ~(0xFFFFFFFFu >> n1)) | (window(e * R) >> n1);
-        }
-        x[b >> 3] |= (uint64_t)(win >> 24) << (8 * (b & 7));
-      }
-      const uint64_t lo = tr8(x[0]), hi = d.W > 8 ? tr8(x[1]) : 0ull;
-      uint32_t *idxw = (uint32_t *)idx;
-      if (d.mode == 1) {                         // two cells per row: pack >> mod, pack & (2^mod - 1)
-        const uint32_t lo_mask = (1u << mod) - 1u;
-#pragma unroll
-        for (int qd = 0; qd < 4; qd++) {
-          const int k0 = 2 * qd;
-          const uint32_t p0 = (uint32_t)((lo >> (8 * (7 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (7 - k0))) & 0xFFu) << 8);
-          const uint32_t p1 = (uint32_t)((lo >> (8 * (6 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (6 - k0))) & 0xFFu) << 8);
-          if (j0 + k0 < R)
-            idxw[4 * g + qd] = (p0 >> mod) | ((p0 & lo_mask) << 8) | ((p1 >> mod) << 16) | ((p1 & lo_mask) << 24);
-        }
-      } else {                                   // 256-QAM short: one cell per row (byte-reversed lo)
-        const uint64_t rv = __builtin_bswap64(lo);
-        if (j0 < R) idxw[2 * g] = (uint32_t)rv;
-        if (j0 + 4 < R) idxw[2 * g + 1] = (uint32_t)(rv >> 32);
-      }
-    }
-  }
+  map_cells<MAP_THREADS>(d, cww, idx, tid);
   __syncthreads();
   MAP_PHASE(2);
   // ---- constellation + cyclic Q delay; chain: cell interleaver (framemapper:1973-1998) on the
@@ -850,79 +1012,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
     }
     return;
   }
-  const int r = blk % d.F;
-  const int shift = d.ci_shift[r];
-  uint16_t *dst = io.out_pairs + (int64_t)(blk / d.F) * io.frame_stride;   // frame data region
-  int r0 = r, nb = 1;
-  if (d.ti_on) {
-    const int ns = d.ti_nsmall * d.ti_small;
-    if (r < ns) { r0 = r - r % d.ti_small; nb = d.ti_small; }
-    else { r0 = r - (r - ns) % d.ti_big; nb = d.ti_big; }
-  }
-  const int rows = cs / 5, cols = 5 * nb;
-  const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
-  // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
-  // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
-  constexpr int MB = MAP_MB;
-  for (int j0 = tid; j0 < cs; j0 += MB * MAP_THREADS) {
-    int t[MB];
-#pragma unroll
-    for (int u = 0; u < MB; u++) {
-      const int j = min(j0 + u * MAP_THREADS, cs - 1);
-      t[u] = d.ci_perm[j] + shift;
-    }
-#pragma unroll
-    for (int u = 0; u < MB; u++) {
-      const int j = j0 + u * MAP_THREADS;
-      if (j < cs) {
-        const int tt = t[u] >= cs ? t[u] - cs : t[u];
-        const uint32_t lo = idx[j], hi = d.rotation ? idx[j == 0 ? cs - 1 : j - 1] : lo;
-        stage[tt] = (uint16_t)(lo | (hi << 8));
-      }
-    }
-  }
-  __syncthreads();
-  MAP_PHASE(3);
-  // time-interleaver store of the index pairs: row-major over (row, e), 5 consecutive cells
-  // (10 B) per TI row (32K: through the half partition); the constellation lookup (QAM +
-  // rotated-constellation Q delay) is fused into the OFDM kernel's bin scatter
-  const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
-  // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
-  const int16_t *pr = d.part ? d.part + (int64_t)r * cs : nullptr;   // block-major int16 table
-  for (int j0 = tid; j0 < cs; j0 += MB * MAP_THREADS) {
-    uint32_t dsl[MB];
-    int tt[MB];
-#pragma unroll
-    for (int u = 0; u < MB; u++) {
-      const int j = min(j0 + u * MAP_THREADS, cs - 1);
-      int o;
-      if (d.ti_on) {
-        const int row = j / 5, e = j - 5 * row;
-        tt[u] = e * rows + row;
-        o = row * cols + e;
-      } else {
-        tt[u] = j;
-        o = j;
-      }
-      dsl[u] = (uint32_t)fbase + (uint32_t)o + (uint32_t)(pr ? (int)pr[j] : 0);
-    }
-#pragma unroll
-    for (int u = 0; u < MB; u++) {
-      if (j0 + u * MAP_THREADS < cs) st_off(dst, dsl[u] * 2u, stage[tt[u]]);
-    }
-  }
-#if MAP_VARIANT & 1
-  __syncthreads();
-  MAP_PHASE(4);
-  if (tid == 0) {
-    uint32_t v[6] = {(uint32_t)g_map_ts[0], (uint32_t)(g_map_ts[1] - g_map_ts[0]), (uint32_t)(g_map_ts[2] - g_map_ts[0]),
-                     (uint32_t)(g_map_ts[3] - g_map_ts[0]), (uint32_t)(g_map_ts[4] - g_map_ts[0]), 0u};
-    for (int c = 0; c < 12; c++) {     // uint32 v[c/2], 16 bits per slot of TI-store index c
-      const int o = d.ti_on ? (c / 5) * cols + c % 5 : c;
-      dst[fbase + o + (d.part ? d.part[(int64_t)r * cs + c] : 0)] = (uint16_t)(v[c >> 1] >> (16 * (c & 1)));
-    }
-  }
-#endif
+  map_store_pairs<MAP_THREADS>(d, io.out_pairs, io.frame_stride, idx, stage, blk, tid);
 }
 
 hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {

@@ -24,6 +24,14 @@ def _have_gpu():
 
 @pytest.fixture(scope="session")
 def gpu():
+    # torch's HIP runtime (used by the stream / device-buffer tests) is brought up before the
+    # library's own, as in bench.py and the INTEGRATION.md examples
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
     if not _have_gpu():
         pytest.fail("gpu-marked test but no GPU / HIP library available")
     return True
