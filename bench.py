@@ -23,6 +23,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import subprocess
 import sys
 import tempfile
@@ -54,6 +55,9 @@ def parse():
                          "TS stream per rank (seed = rank + 1), SURVEY 8(e)'s two modes")
     ap.add_argument("--slots", type=int, default=2,
                     help="chain buffer slots = HIP streams the steps alternate over (1 = serial)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="independent TS streams per launch (seeds 1..S, dvbt2ll_chain_run_streams; BASELINE cfg4 "
+                         "x4 / cfg5 x8): each step encodes --frames // S frames of every stream")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -121,11 +125,12 @@ def pmc_passes(args):
     if rp is None:
         return None, "rocprofv3 not found"
     res = {k: {} for k in KERNELS}
+    names = set()
     for ctrs in (["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"]):
         d = tempfile.mkdtemp(prefix="t2pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = [rp, "--pmc", *ctrs, "--kernel-include-regex", "(fec|map|ofdm|ofdm32)_kernel", "-T", "-f", "csv", "-d", d,
                "-o", "pmc", "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--config", args.config,
-               "--frames", str(args.frames), "--steps", "2", "--warmup", "1"]
+               "--frames", str(args.frames), "--streams", str(args.streams), "--steps", "2", "--warmup", "1"]
         try:
             subprocess.run(cmd, check=True, timeout=240, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
         except Exception as e:  # noqa: BLE001
@@ -134,17 +139,19 @@ def pmc_passes(args):
         for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(fn) as fh:
                 for row in csv.DictReader(fh):
-                    for k in KERNELS:
-                        kn = row.get("Kernel_Name", "")
-                        if row.get("Counter_Name") in ctrs and (kn.startswith(k + "_kernel") or
-                                                                 (k == "ofdm" and kn.startswith("ofdm32_kernel"))):
-                            vals.setdefault((k, row["Counter_Name"]), []).append(float(row["Counter_Value"]))
+                    kn = row.get("Kernel_Name", "")
+                    names.add(kn[:60])
+                    m = re.search(r"\b(fec|map|ofdm)(32)?_kernel", kn)
+                    if m and row.get("Counter_Name") in ctrs:
+                        vals.setdefault((m.group(1), row["Counter_Name"]), []).append(float(row["Counter_Value"]))
         for (k, c), v in vals.items():
             res[k][c] = sum(v) / len(v)
         shutil.rmtree(d, ignore_errors=True)
     cal = _calibration()
     for k in KERNELS:
         r = res[k]
+        if "FETCH_SIZE" not in r:
+            r["kernel_names_seen"] = sorted(names)   # diagnostic: what the PMC pass recorded
         if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
             fr = cal.get("FETCH_SIZE rd %dB" % LOAD_WIDTH[k], 0.5)
             wr = cal.get("WRITE_SIZE wr %dB" % STORE_WIDTH[k], 1.0)
@@ -287,7 +294,7 @@ def one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per):
     direct launches and hipGraph mode"""
     import torch
     lat = []
-    first, base, n = ts_meta[0]
+    first, base, n, _ = ts_meta[0]
     for k in range(25):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -345,13 +352,26 @@ def main():
     rank_first, _ = frame_range(world * R * B, rank, world)
     seed = 1
     if args.shard == "streams":
-        rank_first, seed = 0, rank + 1
+        rank_first, seed = 0, rank * max(1, args.streams) + 1
+    NS = max(1, args.streams)
+    if NS > 1:
+        # multi-stream batch: NS independent TS streams (seeds seed..seed+NS-1), B // NS frames of each
+        # per step, one launch (dvbt2ll_chain_run_streams)
+        if B % NS:
+            raise SystemExit("--frames must be a multiple of --streams")
+        rank_first = frame_range(world * R * (B // NS), rank, world)[0] if args.shard == "frames" else 0
+    BS = B // NS
     ts_dev, ts_meta = [], []
     for r in range(R):
-        first = rank_first + r * B
-        ts, base = ts_for_frames(cfg, first, B, seed)
-        ts_dev.append(torch.from_numpy(ts).cuda())
-        ts_meta.append((first, base, len(ts)))
+        first = rank_first + r * BS
+        tss = [ts_for_frames(cfg, first, BS, seed + k) for k in range(NS)]
+        base, n = tss[0][1], len(tss[0][0])
+        stride = (n + 255) // 256 * 256
+        buf = np.zeros((NS, stride), np.uint8)
+        for k, (ts, _) in enumerate(tss):
+            buf[k, :n] = ts
+        ts_dev.append(torch.from_numpy(buf.reshape(-1)).cuda())
+        ts_meta.append((first, base, n, stride))
     # pipelined steps: the handle holds `slots` intermediate buffer sets and step s is issued on
     # stream s % slots into its own IQ buffer, so one step's kernels fill the CUs the previous
     # step's kernel tails leave idle (dvbt2ll_chain_set_slots); every step still does all the work
@@ -362,9 +382,13 @@ def main():
     torch.cuda.synchronize()
 
     def step(s, serial=False):
-        first, base, n = ts_meta[s % R]
+        first, base, n, stride = ts_meta[s % R]
         st = streams[0] if serial else streams[s % S]
-        chain.run_device(ts_dev[s % R].data_ptr(), base, n, first, B, out[0][s % S].data_ptr(), st.cuda_stream)
+        if NS > 1:
+            chain.run_streams(ts_dev[s % R].data_ptr(), stride, NS, base, n, first, BS, out[0][s % S].data_ptr(),
+                              st.cuda_stream)
+        else:
+            chain.run_device(ts_dev[s % R].data_ptr(), base, n, first, B, out[0][s % S].data_ptr(), st.cuda_stream)
 
     out = [iq]
     for s in range(args.warmup):
@@ -425,10 +449,10 @@ def main():
         sc16 = {"ms_per_step": e16 / args.steps * 1e3, "elapsed": e16,
                 "ofdm_avg_launch_ms": ms16[2] / max(1, n16[2])}
     latency = None
-    if not args.no_latency:
+    if not args.no_latency and NS == 1:
         latency = one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per)
     gathered = None
-    if dist and args.shard == "frames":
+    if dist and args.shard == "frames" and NS == 1:
         # secondary (not `value`): each step followed by the ordered IQ gather to rank 0, the
         # chain's one exchange step (point-to-point sends to the root over RCCL / xGMI)
         from dvbt2ll.distributed import gather_frames
@@ -498,10 +522,12 @@ def main():
             "metric": METRIC, "value": msps, "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "%s: TS->IQ full DVB-T2 chain, %d T2 frames per step per GPU "
+            "config": {"workload": "%s: TS->IQ full DVB-T2 chain, %d T2 frames per step per GPU%s "
                                    "(%d FEC blocks, %d IQ samples per frame)"
-                                   % (cfg.name, B, info["fec_blocks_per_frame"], per),
+                                   % (cfg.name, B, " (%d independent TS streams x %d frames, one launch)" % (NS, BS)
+                                      if NS > 1 else "", info["fec_blocks_per_frame"], per),
                        "frames_per_step_per_gpu": B, "slots_streams_per_gpu": S,
+                       "ts_streams_per_launch": NS,
                        "parallelism": "%s x%d (no data-path collective)"
                                       % ("frame-sharded" if args.shard == "frames" else "independent streams", world)},
             "fec_blocks_per_sec": fec_total / elapsed,

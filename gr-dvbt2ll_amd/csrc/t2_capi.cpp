@@ -844,9 +844,16 @@ extern "C" int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info
 
 extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_base, int64_t ts_len,
                                         int64_t first_frame, int nframes, void *iq_dev, void *stream) {
-  if (!h || !ts_dev || !iq_dev || nframes < 1 || nframes > h->max_frames || first_frame < 0 || ts_base < 0 ||
-      ts_base % 188 != 0)
+  return dvbt2ll_chain_run_streams(h, ts_dev, 0, 1, ts_base, ts_len, first_frame, nframes, iq_dev, stream);
+}
+
+extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_stride, int nstreams,
+                                         int64_t ts_base, int64_t ts_len, int64_t first_frame, int nframes,
+                                         void *iq_dev, void *stream) {
+  if (!h || !ts_dev || !iq_dev || nframes < 1 || nstreams < 1 || (int64_t)nframes * nstreams > h->max_frames ||
+      first_frame < 0 || ts_base < 0 || ts_base % 188 != 0 || (nstreams > 1 && ts_stride < ts_len))
     return DVBT2LL_EINVAL;
+  const int nf = nframes * nstreams;   // frames of the launch, stream-major
   hipStream_t s = stream ? (hipStream_t)stream : h->ctx.stream;
   const int F = h->frame.F;
   // the TS slice must cover every byte the frames consume plus the packet before the
@@ -878,13 +885,15 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   fio.first_block = first_frame * F;
   fio.out = h->fused ? nullptr : cw.as<uint8_t>();
   fio.cw_stride = h->cw_stride;
-  fio.nblocks = F * nframes;
+  fio.nblocks = F * nf;
   fio.sync_err = h->sync_err.as<uint32_t>();
+  fio.blocks_per_stream = nstreams > 1 ? F * nframes : 0;
+  fio.ts_stride = nstreams > 1 ? ts_stride : 0;
   mio.in = cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
   mio.out_pairs = pairs.as<uint16_t>();
   mio.frame_stride = h->pair_stride;
-  mio.nblocks = F * nframes;
+  mio.nblocks = F * nf;
   mio.packed_in = 1;
   mio.apply_ci = 1;
   oio.data = h->aux.as<float2>();
@@ -895,9 +904,10 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   oio.out = (float2 *)iq_dev;
   oio.out_stride = h->iq_per_frame;
   oio.first_frame = first_frame;
-  oio.nframes = nframes;
+  oio.nframes = nf;
+  oio.frames_per_stream = nstreams > 1 ? nframes : 0;
   if (h->use_graph) {
-    int r = h->graph_launch(fio, mio, oio, nframes, slot, s);
+    int r = h->graph_launch(fio, mio, oio, nf, slot, s);
     if (r) return r;
   } else {
     HIP_TRY(h->launch_chain(fio, mio, oio, s, h->timing ? ev[1] : nullptr, h->timing ? ev[2] : nullptr));

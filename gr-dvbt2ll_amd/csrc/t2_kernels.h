@@ -38,6 +38,10 @@ struct FecIO {
   int64_t cw_stride;
   int nblocks;
   uint32_t *sync_err;      // ts modes, optional: += TS sync bytes != 0x47 consumed (bbheader:675, 703)
+  // multi-stream batch (chain, ts modes): 0 = one stream; else launch block b belongs to stream
+  // b / blocks_per_stream, whose TS bytes start at in + stream * ts_stride (same ts_base, ts_len)
+  int blocks_per_stream;
+  int64_t ts_stride;
 };
 
 // ---------------------------------------------------------------- bit interleave + QAM + CI
@@ -106,6 +110,8 @@ struct OfdmIO {
   int64_t out_stride;
   int64_t first_frame;
   int nframes;
+  int frames_per_stream;    // multi-stream batch: launch frame f is frame first_frame + f % frames_per_stream
+                            // of stream f / frames_per_stream (0: one stream)
   int carriers_only;        // test hook: write pre-IFFT bins (natural bin order) instead
 };
 

@@ -348,12 +348,16 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
     bend = min((x + 1) * q, io.nblocks);
   }
   for (int bi = bstart; bi < bend; bi += bstep) {
-  const int64_t B = io.first_block + bi;
+  // stream-major multi-stream batch: launch block bi is block bi % bps of stream bi / bps, whose TS
+  // slice (same ts_base / ts_len layout for every stream) starts at in + stream * ts_stride
+  const int sidx = io.blocks_per_stream ? bi / io.blocks_per_stream : 0;
+  const int64_t B = io.first_block + (bi - sidx * io.blocks_per_stream);
+  const uint8_t *tin = io.in + (int64_t)sidx * io.ts_stride;
   FEC_PHASE(0);
   do {   // one FEC block; `break` ends it early (block-API modes)
   if (MODE == FEC_BITS_TO_BITS) {
     // pack nbch unpacked info bits
-    const uint8_t *src = io.in + (int64_t)bi * d.nbch;
+    const uint8_t *src = tin + (int64_t)bi * d.nbch;
     for (int k = tid; k < NB; k += FEC_THREADS) {
       uint32_t v = 0;
       for (int e = 0; e < 8; e++) v |= (uint32_t)(src[8 * k + e] & 1) << (7 - e);
@@ -393,15 +397,15 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
       uint32_t *rawst = (uint32_t *)(smem + SM_RAW);
       for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)crc8)[i] = ((const uint32_t *)d.crc8_tab)[i];
       for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)crcsh)[i] = ((const uint32_t *)d.crc8_shift)[i];
-      const bool aligned = (((uintptr_t)io.in) & 3) == 0;
+      const bool aligned = (((uintptr_t)tin) & 3) == 0;
       for (int i = tid; i < nw; i += FEC_THREADS) {
         const int64_t b = 4 * (w0 + i);
         uint32_t v = 0;
         if (aligned && b >= 0 && b + 4 <= io.ts_len) {
-          v = *(const uint32_t *)(io.in + b);
+          v = *(const uint32_t *)(tin + b);
         } else {
           for (int e = 0; e < 4; e++)
-            if (b + e >= 0 && b + e < io.ts_len) v |= (uint32_t)io.in[b + e] << (8 * e);
+            if (b + e >= 0 && b + e < io.ts_len) v |= (uint32_t)tin[b + e] << (8 * e);
         }
         rawst[i] = v;
       }
@@ -448,7 +452,7 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
       // byte 187 p (bbheader:673-680, warning at :675-677)
       const int64_t p0 = (J0 + 186) / 187;
       for (int64_t pk = p0 + tid; 187 * pk < J0 + npay; pk += FEC_THREADS)
-        if (io.in[188 * pk - io.ts_base] != 0x47) atomicAdd(io.sync_err, 1u);
+        if (tin[188 * pk - io.ts_base] != 0x47) atomicAdd(io.sync_err, 1u);
     }
     // BBHEADER (bbheader:272-325), uniform across the workgroup: MATYPE-1 = TS, SIS, CCM, ISSYI 0,
     // NPD 0, RO 0; ISI 0; bytes 0..7 big-endian in hw, byte 8 = SYNCD low, byte 9 = CRC-8
@@ -473,7 +477,7 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
       if (pidx == 9) return hcrc_rev;
       const int j = pidx - 10;
       if (j < npay) {
-        if (d.hem) return io.in[payload_pos(J0 + j, 1) - io.ts_base];
+        if (d.hem) return tin[payload_pos(J0 + j, 1) - io.ts_base];
         const int r = (count0 + j) % 188;
         return r == 0 ? (uint32_t)syncv[(j - first_slot) / 188] : (uint32_t)smem[SM_RAW + delta + 188 + j];
       }
@@ -1434,7 +1438,7 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const int u = xcd_major(blockIdx.x, gridDim.x);
   const int j = u / io.nframes;                   // symbol
   const int f = u - j * io.nframes;               // frame within launch
-  const int64_t frame = io.first_frame + f;
+  const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);   // stream-major batch
   const float2 *data = io.data;                   // uniform base: all gathers are base + u32 offset
   const uint32_t cbase = io.cell_off + (uint32_t)f * io.cell_stride;
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
@@ -1633,7 +1637,7 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   const int u = xcd_major(blockIdx.x, gridDim.x);
   const int j = u / io.nframes;                   // symbol
   const int f = u - j * io.nframes;               // frame within launch
-  const int64_t frame = io.first_frame + f;
+  const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);   // stream-major batch
   const float2 *data = io.data;
   const uint32_t cbase = io.cell_off + (uint32_t)f * io.cell_stride;
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;

@@ -64,7 +64,7 @@ for _b in BLOCKS:
                 ("create", "output_multiple", "forecast", "general_work", "destroy")]
 EXPORTS += ["dvbt2ll_framemapperfint_stream_items", "dvbt2ll_pilotgenp1insert_active_items",
             "dvbt2ll_pilotgenp1insert_debug_carriers", "dvbt2ll_bbheaderbch_sync_errors"]
-EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_host", "set_output", "set_slots", "set_graph", "set_timing",
+EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_streams", "run_host", "set_output", "set_slots", "set_graph", "set_timing",
                                            "get_timing", "debug_codewords", "debug_cell_pairs", "debug_cells",
                                            "synchronize", "sync_errors",
                                            "destroy")]
@@ -95,6 +95,7 @@ def lib():
     L.dvbt2ll_chain_create.argtypes = [ctypes.POINTER(_ChainParams), ci, ctypes.POINTER(vp)]
     L.dvbt2ll_chain_get_info.argtypes = [vp, ctypes.POINTER(_ChainInfo)]
     L.dvbt2ll_chain_run_device.argtypes = [vp, vp, i64, i64, i64, ci, vp, vp]
+    L.dvbt2ll_chain_run_streams.argtypes = [vp, vp, i64, ci, i64, i64, i64, ci, vp, vp]
     L.dvbt2ll_chain_run_host.argtypes = [vp, vp, i64, i64, i64, ci, vp]
     L.dvbt2ll_chain_set_output.argtypes = [vp, ctypes.c_float, ci]
     L.dvbt2ll_chain_set_slots.argtypes = [vp, ci]

@@ -62,6 +62,15 @@ class Chain:
                                              int(first_frame), int(nframes), ctypes.c_void_p(iq_ptr),
                                              ctypes.c_void_p(stream or None)), "chain run")
 
+    def run_streams(self, ts_ptr, ts_stride, nstreams, ts_base, ts_len, first_frame, nframes, iq_ptr, stream=0):
+        """nstreams independent TS streams (stream s at ts_ptr + s * ts_stride, each laid out as
+        run_device's buffer) -> IQ of frames [first_frame, first_frame + nframes) of every stream in one
+        launch, stream-major (dvbt2ll_chain_run_streams)"""
+        check(lib().dvbt2ll_chain_run_streams(self._h, ctypes.c_void_p(ts_ptr), int(ts_stride), int(nstreams),
+                                              int(ts_base), int(ts_len), int(first_frame), int(nframes),
+                                              ctypes.c_void_p(iq_ptr), ctypes.c_void_p(stream or None)),
+              "chain run streams")
+
     def run(self, first_frame, nframes, ts=None, ts_base=None, seed=1):
         """host convenience: synthetic TS (or the given buffer) -> IQ numpy array"""
         if ts is None:

@@ -172,6 +172,17 @@ int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info);
  * own stream).  Asynchronous on that stream. */
 int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_base, int64_t ts_len,
                              int64_t first_frame, int nframes, void *iq_dev, void *stream);
+/* multi-stream batch (BASELINE cfg4 "4 independent PLP streams", cfg5 "8-stream batch"): nstreams
+ * independent single-PLP T2 signals (the reference carries one PLP per instance,
+ * lib/framemapperfint_cc_impl.cc:153, so each stream is its own five-block chain) encoded in one launch of
+ * the three kernels.  Stream s's TS bytes are at ts_dev + s * ts_stride, every stream laid out as
+ * run_device's ts_dev (the same ts_base and ts_len; ts_stride >= ts_len); all streams encode frames
+ * [first_frame, first_frame + nframes).  IQ: stream s, frame first_frame + j at sample
+ * (s * nframes + j) * iq_samples_per_frame of iq_dev.  nstreams * nframes <= max_frames.
+ * run_device(...) == run_streams(h, ts, 0, 1, ...).  Asynchronous on stream. */
+int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_stride, int nstreams,
+                              int64_t ts_base, int64_t ts_len, int64_t first_frame, int nframes,
+                              void *iq_dev, void *stream);
 /* intermediate buffer slots (packed codewords + cell index pairs, ~310 MB per slot for 64 cfg3
  * frames): run calls take the slots round-robin, so calls issued on different streams run
  * concurrently on the GPU (one call's kernels fill the CUs the other call's kernel tails leave

@@ -206,3 +206,94 @@ def test_chain_graph_mode(gpu, name):
         np.testing.assert_array_equal(ch.run(first, n), ref.run(first, n))
     ch.set_graph(False)
     np.testing.assert_array_equal(ch.run(6, 1), ref.run(6, 1))
+
+
+def _stream_batch(cfg, S, first, B, graph=False, sc16=False):
+    """S independent TS streams (seeds 1..S) in one dvbt2ll_chain_run_streams launch; returns the
+    per-stream IQ and a single-stream reference handle's IQ of each stream's own TS"""
+    import torch
+    ch = dvbt2ll.Chain(cfg, max_frames=S * B)
+    ref = dvbt2ll.Chain(cfg, max_frames=B)
+    if graph:
+        ch.set_graph(True)
+    if sc16:
+        for c in (ch, ref):
+            c.set_output(0.2, dvbt2ll.IQ_SC16)
+    per = ch.iq_per_frame
+    tss = [ts_for_frames(cfg, first, B, seed=s + 1) for s in range(S)]
+    base, n = tss[0][1], len(tss[0][0])
+    stride = (n + 1000 + 255) // 256 * 256          # deliberately not the tight length
+    buf = np.zeros((S, stride), np.uint8)
+    for s, (ts, b) in enumerate(tss):
+        assert b == base and len(ts) == n
+        buf[s, :n] = ts
+    ts_dev = torch.from_numpy(buf.reshape(-1)).cuda()
+    dt = torch.int16 if sc16 else torch.float32
+    iq = torch.empty((S * B * per, 2), dtype=dt, device="cuda")
+    torch.cuda.synchronize()
+    ch.run_streams(ts_dev.data_ptr(), stride, S, base, n, first, B, iq.data_ptr(),
+                   torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = iq.cpu().numpy()
+    got = got.reshape(S, B * per, 2) if sc16 else got.view(np.complex64).reshape(S, B * per)
+    want = [ref.run(first, B, ts=ts, ts_base=b) for ts, b in tss]
+    return got, want, tss
+
+
+@pytest.mark.parametrize("name,S,first,B", [("cfg1", 3, 0, 2), ("cfg1q", 4, 5, 1), ("cfg4", 4, 0, 1),
+                                            ("cfg2", 2, 1, 1)])
+def test_chain_streams_batch(gpu, name, S, first, B):
+    """BASELINE cfg4 / cfg5 multi-stream batching: S independent streams in one launch give, per
+    stream, bit-exactly what a single-stream handle gives on that stream's TS; streams differ"""
+    got, want, _ = _stream_batch(CONFIGS[name], S, first, B)
+    for s in range(S):
+        np.testing.assert_array_equal(got[s].view(np.uint32), want[s].view(np.uint32), err_msg="stream %d" % s)
+    assert not np.array_equal(got[0], got[1])
+
+
+def test_chain_streams_batch_vs_oracle(gpu):
+    """stream 3 of a 4-stream cfg4-shaped (here cfg1) batch against the oracle chain on its own seed"""
+    cfg = CONFIGS["cfg1"]
+    got, _, tss = _stream_batch(cfg, 4, 0, 1)
+    ts, base = tss[3]
+    F = cfg.fecblocks
+    bits, _ = O.BB(*cfg.bb_args()).work(ts, F)
+    cells = O.IM(*cfg.im_args()).work(O.LDPC(cfg.framesize, cfg.rate).work(bits, F), F)
+    pg = O.PG(*cfg.pg_args())
+    car = pg.carriers(O.FM(*cfg.fm_args()).work(cells))
+    iq_check.check_frame(got[3], car, pg.vlength, pg.guard, pg.normalization, pg.p1(), "cfg1 stream 3")
+
+
+@pytest.mark.parametrize("mode", ["hem", "hem_inband", "nm_inband"])
+def test_chain_streams_batch_input_modes(gpu, mode):
+    """the per-stream TS pointer in the HEM and in-band payload paths"""
+    from test_cpu_plan import grid_cfg
+    from dvbt2ll import enums as E
+    over = dict(version=E.VERSION_131, tsrate=12345678)
+    if mode.startswith("hem"):
+        over["inputmode"] = E.INPUTMODE_HIEFF
+    if mode.endswith("inband"):
+        over["inband"] = E.INBAND_ON
+    cfg = grid_cfg(over)
+    got, want, _ = _stream_batch(cfg, 3, 2, 1)
+    for s in range(3):
+        np.testing.assert_array_equal(got[s].view(np.uint32), want[s].view(np.uint32), err_msg="stream %d" % s)
+
+
+def test_chain_streams_batch_graph_sc16(gpu):
+    """multi-stream batch through the hipGraph launch mode with the sc16 output step"""
+    got, want, _ = _stream_batch(CONFIGS["cfg1"], 3, 1, 2, graph=True, sc16=True)
+    for s in range(3):
+        np.testing.assert_array_equal(got[s], want[s], err_msg="stream %d" % s)
+
+
+def test_chain_streams_rejects_bad_args(gpu):
+    import torch
+    cfg = CONFIGS["cfg1"]
+    ch = dvbt2ll.Chain(cfg, max_frames=4)
+    ts, base = ts_for_frames(cfg, 0, 1)
+    d = torch.from_numpy(np.tile(ts, 5)).cuda()
+    iq = torch.empty((5 * ch.iq_per_frame, 2), dtype=torch.float32, device="cuda")
+    for stride, S, B in ((len(ts), 5, 1), (len(ts), 2, 3), (len(ts) - 1, 2, 1), (len(ts), 0, 1)):
+        with pytest.raises(dvbt2ll.DVBT2Error):
+            ch.run_streams(d.data_ptr(), stride, S, base, len(ts), 0, B, iq.data_ptr())

@@ -14,13 +14,22 @@ step tests && IQ_STATS=$PWD/$O/iq_stats.jsonl timeout -k 10 900 python -u -m pyt
   && tail -3 "$O/pytest.log" \
   && step smoke && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
   && cat "$O/smoke.log" \
-  && step calib && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T -d "$O/calib_fetch" -o calib -- ./tools/fetch_calib > /dev/null 2>&1 \
+  && if [ -n "$CALIB" ]; then step calib && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -T -d "$O/calib_fetch" -o calib -- ./tools/fetch_calib > /dev/null 2>&1 \
   && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -T -d "$O/calib_write" -o calib -- ./tools/fetch_calib > /dev/null 2>&1 \
   && python tools/fetch_calib.py "$O/calib_fetch" "$O/calib_write" > "$O/r2_fetch_calib.json" \
-  && cp "$O/r2_fetch_calib.json" profiles/r2_fetch_calib.json && cat "$O/r2_fetch_calib.json" \
+  && cp "$O/r2_fetch_calib.json" profiles/r2_fetch_calib.json && cat "$O/r2_fetch_calib.json"; fi \
   && step bench && timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" \
   && cat "$O/bench.json" \
-  && step trace && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace" -o trace -- \
+  && step trace && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace" -o trace -f csv -- \
        python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --slots 1 --steps 10 --warmup 2 \
        > "$O/trace_bench.json" 2> "$O/trace.err" \
   && echo "=== done ($(date +%T))"
+rc=$?
+[ $rc -eq 0 ] || exit $rc
+# multi-stream batches (BASELINE cfg4 x4, cfg5 x8 streams in one launch), when asked for
+if [ -n "$STREAMS" ]; then
+  step streams && timeout -k 10 300 python -u bench.py --config cfg4 --streams 4 --no-pmc --no-cpu-baseline --no-sc16 \
+       > "$O/bench_cfg4_x4.json" 2> "$O/bench_cfg4_x4.err" \
+    && timeout -k 10 300 python -u bench.py --config cfg5 --streams 8 --no-pmc --no-cpu-baseline --no-sc16 \
+       > "$O/bench_cfg5_x8.json" 2> "$O/bench_cfg5_x8.err" && echo "=== streams done"
+fi
