@@ -150,7 +150,7 @@ def pmc_passes(args):
     cal = _calibration()
     for k in KERNELS:
         r = res[k]
-        if "FETCH_SIZE" not in r:
+        if "FETCH_SIZE" not in r or "WRITE_SIZE" not in r:
             r["kernel_names_seen"] = sorted(names)   # diagnostic: what the PMC pass recorded
         if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
             fr = cal.get("FETCH_SIZE rd %dB" % LOAD_WIDTH[k], 0.5)
@@ -496,6 +496,9 @@ def main():
             e["frac"] = e["achieved"] / HBM_PEAK_GBS if e["achieved"] else None
             pm = (traffic or {}).get(name, {})
             e["traffic"] = pm.get("hbm_bytes")
+            if traffic is not None and e["traffic"] is None:
+                e["pmc_missing"] = {"counters": sorted(c for c in pm if c.isupper()),
+                                    "kernel_names_seen": pm.get("kernel_names_seen")}
             if e["traffic"] and t > 0:
                 e["traffic_GBs"] = e["traffic"] / t / 1e9
                 e["traffic_frac"] = e["traffic_GBs"] / HBM_PEAK_GBS

@@ -45,6 +45,16 @@ int t2probe_pilot(const int *p12, int *info, int32_t *bin_map, float *pilot_valu
   return 0;
 }
 
+// the OFDM kernels' twiddle tables: tw 128 + N/128 complex, tw1k 1024 complex
+int t2probe_twiddle(const int *p12, float *tw, float *tw1k) {
+  PgParams p{p12[0], p12[1], p12[2], p12[3], p12[4], p12[5], p12[6], p12[7], p12[8], p12[9], p12[10], p12[11]};
+  PilotPlan pp;
+  if (build_pilot(p, pp)) return -1;
+  if (tw) memcpy(tw, pp.twiddle.data(), pp.twiddle.size() * 8);
+  if (tw1k) memcpy(tw1k, pp.twiddle1k.data(), pp.twiddle1k.size() * 8);
+  return 0;
+}
+
 int t2probe_counts(int fftsize, int carriermode, int pp, int papr, int gi, int preamble, int *out5) {
   return frame_cell_counts(fftsize, carriermode, pp, papr, gi, preamble, out5);
 }

@@ -66,3 +66,19 @@ def check_frame(iq, carriers, N, G, norm, p1, ctx=""):
         rel, mx = check_symbol(y, carriers[j], N, G, norm, "%s sym %d" % (ctx, j))
         worst = [max(worst[0], rel), max(worst[1], mx)]
     return worst
+
+
+def check_frame_exact(iq, carriers, pg_args, G, norm, ctx="", gain=1.0, fmt=0):
+    """SURVEY 8(c)'s bit-exact bar between the CPU restatement and the GPU: the frame equals, bit for
+    bit, the oracle's carriers put through oracle/ifft_model.c (the OFDM kernels' operation order)
+    with the planner's P1 samples (the GPU copies them).  Returns the number of samples compared."""
+    import oracle_lib as O
+    import plan_probe as PP
+    want = O.model_frame(carriers, G, norm, PP.pilot_plan(pg_args)["p1"], gain, fmt)
+    got = np.asarray(iq)
+    assert got.shape == want.shape, (ctx, got.shape, want.shape)
+    a, b = got.view(np.uint32).reshape(-1), want.view(np.uint32).reshape(-1)
+    bad = np.nonzero(a != b)[0]
+    assert bad.size == 0, "%s: %d of %d IQ words differ from the CPU model of the GPU IFFT, first at %s" % (
+        ctx, bad.size, a.size, bad[:5])
+    return a.size

@@ -55,6 +55,8 @@ def lib():
         L.orc_pg_work.argtypes = [vp, vp, vp]
         L.orc_pg_p1.argtypes = [vp, vp]
         L.orc_pg_destroy.argtypes = [vp]
+        L.t2m_tables.argtypes = [ci, vp, vp]
+        L.t2m_symbols.argtypes = [ci, ci, ci, vp, ctypes.c_float, ctypes.c_float, ci, vp]
         L.orc_crc8_dvbs2.restype = ctypes.c_uint8
         L.orc_crc8_dvbs2.argtypes = [vp, ci]
         L.orc_crc32_bits.restype = ctypes.c_uint32
@@ -175,3 +177,33 @@ class PG:
     def __del__(self):
         if getattr(self, "h", None):
             lib().orc_pg_destroy(self.h)
+
+
+# ---------------------------------------------------------------- GPU-order IFFT model (oracle/ifft_model.c)
+def model_tables(N):
+    tw = np.zeros(128 + N // 128, np.complex64)
+    tw1k = np.zeros(1024, np.complex64)
+    assert lib().t2m_tables(N, _p(tw), _p(tw1k)) == 0
+    return tw, tw1k
+
+
+def model_symbols(carriers, G, norm, gain=1.0, fmt=0):
+    """carriers (nsym x N, pilotgen's pre-IFFT symbols) -> the OFDM symbols with guard intervals
+    exactly as the GPU kernels compute them (same operation order); complex64, or
+    int16 I/Q pairs for fmt 1"""
+    car = np.ascontiguousarray(carriers, np.complex64)
+    nsym, N = car.shape
+    out = np.zeros(nsym * (G + N), np.complex64) if fmt == 0 else np.zeros((nsym * (G + N), 2), np.int16)
+    assert lib().t2m_symbols(N, G, nsym, _p(car), float(norm), float(gain), fmt, _p(out)) == 0
+    return out
+
+
+def model_frame(carriers, G, norm, p1, gain=1.0, fmt=0):
+    """a whole T2 frame as the GPU writes it: P1 (the planner's precomputed samples) then the symbols"""
+    sy = model_symbols(carriers, G, norm, gain, fmt)
+    p1 = np.asarray(p1, np.complex64)
+    a = np.stack([p1.real, p1.imag], axis=1).astype(np.float32) * np.float32(gain)   # per component, as the GPU
+    if fmt == 0:
+        return np.concatenate([a.reshape(-1).view(np.complex64), sy])
+    q = np.clip(np.rint(a * np.float32(32767.0)), -32768, 32767).astype(np.int16)
+    return np.concatenate([q, sy])

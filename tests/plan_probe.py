@@ -74,6 +74,16 @@ def pilot_plan(pg_args):
                 bin_map=bm.reshape(Nsym, N), pilot_values=pv, p1=p1, isinc=isinc, norm=float(norm[0]))
 
 
+def twiddle_tables(pg_args):
+    """the OFDM kernels' two-level twiddle table (128 + N/128) and w_1024 table, as uploaded"""
+    N = int(pg_args[11])
+    p = np.array(pg_args, np.int32)
+    tw = np.zeros(128 + N // 128, np.complex64)
+    tw1k = np.zeros(1024, np.complex64)
+    assert lib().t2probe_twiddle(_p(p), _p(tw), _p(tw1k)) == 0
+    return tw, tw1k
+
+
 def cell_counts(fftsize, carriermode, pp, papr, gi, preamble):
     """framemapper cell-count table entry {N_P2, C_P2, C_DATA, N_FC, C_FC} or None"""
     out = np.zeros(5, np.int32)

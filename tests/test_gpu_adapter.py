@@ -52,6 +52,8 @@ def test_gr_adapter_flowgraph(gpu, tmp_path, name, nframes, seed):
         car = pg.carriers(fm.work(im.work(ld.work(bits, F), F)))
         iq_check.check_frame(iq[k * per:(k + 1) * per], car, pg.vlength, pg.guard, pg.normalization, pg.p1(),
                              "adapter %s frame %d" % (name, k))
+        iq_check.check_frame_exact(iq[k * per:(k + 1) * per], car, cfg.pg_args(), pg.guard, pg.normalization,
+                                   "adapter %s frame %d" % (name, k))
 
 
 def test_gr_adapter_sync_warnings(gpu, tmp_path):

@@ -101,7 +101,7 @@ def test_framemapper_bit_exact(gpu, name):
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
-@pytest.mark.parametrize("name", ["cfg1", "cfg3", "cfg4"])
+@pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
 def test_pilotgen_carriers_bit_exact_and_iq(gpu, name):
     cfg = CONFIGS[name]
     cells = _oracle_cells(cfg)
@@ -114,6 +114,7 @@ def test_pilotgen_carriers_bit_exact_and_iq(gpu, name):
     iq = np.zeros(pg.output_items, np.complex64)
     assert blk.general_work([mapped], [iq]) == pg.output_items
     iq_check.check_frame(iq, want_car, pg.vlength, pg.guard, pg.normalization, pg.p1(), "pilotgen " + name)
+    iq_check.check_frame_exact(iq, want_car, cfg.pg_args(), pg.guard, pg.normalization, "pilotgen " + name)
 
 
 ALL_CODES = [(1, r) for r in range(6)] + [(0, r) for r in range(8)]

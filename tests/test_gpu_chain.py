@@ -60,6 +60,8 @@ def _check_chain(cfg, nframes):
     for k in range(nframes):
         iq_check.check_frame(iq[k * per:(k + 1) * per], ref[k][0], pg.vlength, pg.guard, pg.normalization, p1,
                              "%s frame %d" % (cfg.name, k))
+        iq_check.check_frame_exact(iq[k * per:(k + 1) * per], ref[k][0], cfg.pg_args(), pg.guard, pg.normalization,
+                                   "%s frame %d" % (cfg.name, k))
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
@@ -109,6 +111,14 @@ def test_chain_output_gain_and_sc16(gpu, name):
     assert sc.dtype == np.int16 and sc.shape == (2 * ch.iq_per_frame, 2)
     ref = np.clip(np.rint(want.astype(np.float32) * np.float32(32767)), -32768, 32767).astype(np.int16)
     np.testing.assert_array_equal(sc.reshape(-1), ref)
+    # and both against the CPU model of the GPU IFFT with the output step (bit-exact)
+    ref, pg = oracle_chain(cfg, 2)
+    per = ch.iq_per_frame
+    for k in range(2):
+        iq_check.check_frame_exact(scaled[k * per:(k + 1) * per], ref[k][0], cfg.pg_args(), pg.guard,
+                                   pg.normalization, "%s x0.2 frame %d" % (name, k), gain=0.2)
+        iq_check.check_frame_exact(sc[k * per:(k + 1) * per], ref[k][0], cfg.pg_args(), pg.guard,
+                                   pg.normalization, "%s sc16 frame %d" % (name, k), gain=0.2, fmt=1)
     # saturation: a gain large enough to clip
     ch.set_output(40.0, dvbt2ll.IQ_SC16)
     big = ch.run(0, 1).reshape(-1)
@@ -262,6 +272,7 @@ def test_chain_streams_batch_vs_oracle(gpu):
     pg = O.PG(*cfg.pg_args())
     car = pg.carriers(O.FM(*cfg.fm_args()).work(cells))
     iq_check.check_frame(got[3], car, pg.vlength, pg.guard, pg.normalization, pg.p1(), "cfg1 stream 3")
+    iq_check.check_frame_exact(got[3], car, cfg.pg_args(), pg.guard, pg.normalization, "cfg1 stream 3")
 
 
 @pytest.mark.parametrize("mode", ["hem", "hem_inband", "nm_inband"])

@@ -33,3 +33,10 @@ if [ -n "$STREAMS" ]; then
     && timeout -k 10 300 python -u bench.py --config cfg5 --streams 8 --no-pmc --no-cpu-baseline --no-sc16 \
        > "$O/bench_cfg5_x8.json" 2> "$O/bench_cfg5_x8.err" && echo "=== streams done"
 fi
+# raw PMC passes of the bench child kept for inspection, when asked for
+if [ -n "$PMCDBG" ]; then
+  step pmcdbg && for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "(fec|map|ofdm|ofdm32)_kernel" -T -f csv \
+      -d "$O/pmc_$c" -o pmc -- python bench.py --pmc-child --steps 2 --warmup 1 > "$O/pmc_$c.log" 2>&1 || exit 1
+  done && echo "=== pmcdbg done"
+fi
