@@ -28,14 +28,27 @@ def kernel_stats(db):
     return out
 
 
+def kernel_stats_csv(path):
+    import csv
+    out = []
+    for r in csv.DictReader(open(path)):
+        out.append((r["Name"], int(r["Calls"]), float(r["AverageNs"]) / 1e3, float(r["MinNs"]) / 1e3,
+                    float(r["MaxNs"]) / 1e3, float(r["Percentage"])))
+    return out
+
+
 def main(tag, rnd):
     src = os.path.join("gpurun_out", tag)
     lines = ["# GPU session %s (%s)" % (tag, rnd), ""]
     dbs = glob.glob(os.path.join(src, "trace", "*.db"))
-    if dbs:
+    csvs = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    stats = kernel_stats(dbs[0]) if dbs else (kernel_stats_csv(csvs[0]) if csvs else None)
+    if csvs:
+        shutil.copy(csvs[0], os.path.join("profiles", "%s_%s_kernel_stats.csv" % (rnd, tag)))
+    if stats:
         lines += ["## kernel trace (`rocprofv3 --kernel-trace --stats`, bench.py --slots 1 --steps 10 --warmup 2)", "",
                   "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
-        for name, n, avg, mn, mx, pct in kernel_stats(dbs[0]):
+        for name, n, avg, mn, mx, pct in stats:
             lines.append("| %s | %d | %.1f | %.1f | %.1f | %.1f |" % (name[:60], n, avg, mn, mx, pct))
         lines.append("")
     bj = os.path.join(src, "bench.json")
