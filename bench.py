@@ -128,7 +128,9 @@ def pmc_passes(args):
     names = set()
     for ctrs in (["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"]):
         d = tempfile.mkdtemp(prefix="t2pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = [rp, "--pmc", *ctrs, "--kernel-include-regex", "(fec|map|ofdm|ofdm32)_kernel", "-T", "-f", "csv", "-d", d,
+        # (no --kernel-include-regex: with it rocprofv3 7.2 dropped ofdm32_kernel's dispatches; kernels are
+        # matched by name below)
+        cmd = [rp, "--pmc", *ctrs, "-T", "-f", "csv", "-d", d,
                "-o", "pmc", "--", sys.executable, str(ROOT / "bench.py"), "--pmc-child", "--config", args.config,
                "--frames", str(args.frames), "--streams", str(args.streams), "--steps", "2", "--warmup", "1"]
         try:

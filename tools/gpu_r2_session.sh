@@ -36,7 +36,7 @@ fi
 # raw PMC passes of the bench child kept for inspection, when asked for
 if [ -n "$PMCDBG" ]; then
   step pmcdbg && for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 120 rocprofv3 --pmc $c --kernel-include-regex "(fec|map|ofdm|ofdm32)_kernel" -T -f csv \
+    timeout -s KILL 120 rocprofv3 --pmc $c -T -f csv \
       -d "$O/pmc_$c" -o pmc -- python bench.py --pmc-child --steps 2 --warmup 1 > "$O/pmc_$c.log" 2>&1 || exit 1
   done && echo "=== pmcdbg done"
 fi
