@@ -142,6 +142,34 @@ struct MapTables {
   }
 };
 
+// ---------------------------------------------------------------- L1-post tables on device
+struct L1Tables {
+  DevBuf tmpl, crc_c, scr, sig_pos, bch_r, ldpc_ptr, ldpc_addr, sel, lut;
+  L1Dev dev{};
+  int init(const FramePlan &fp) {
+    const L1PostPlan &l = fp.l1;
+    int r;
+    if ((r = upload(tmpl, l.tmpl)) || (r = upload(crc_c, l.crc_c)) || (r = upload(scr, l.scr)) ||
+        (r = upload(sig_pos, l.sig_pos)) || (r = upload(bch_r, l.bch_r)) || (r = upload(ldpc_ptr, l.ldpc_ptr)) ||
+        (r = upload(ldpc_addr, l.ldpc_addr)) || (r = upload(sel, l.sel)) || (r = upload_raw(lut, l.lut, sizeof(l.lut))))
+      return r;
+    dev.tmpl = tmpl.as<uint32_t>();
+    dev.crc_c = crc_c.as<uint32_t>();
+    dev.scr = l.scr.empty() ? nullptr : scr.as<uint32_t>();
+    dev.sig_pos = sig_pos.as<uint16_t>();
+    dev.bch_r = bch_r.as<uint32_t>();
+    dev.ldpc_ptr = ldpc_ptr.as<uint16_t>();
+    dev.ldpc_addr = ldpc_addr.as<uint16_t>();
+    dev.sel = sel.as<uint16_t>();
+    dev.lut = lut.as<float2>();
+    dev.crc_k = l.crc_k;
+    dev.nsig = l.nsig; dev.fidx_pos = l.fidx_pos; dev.npost = l.npost; dev.lp = l.lp; dev.mode = l.mode;
+    dev.ncols = l.ncols; dev.rows = l.rows; dev.q = l.q; dev.pbits = l.pbits; dev.t2frames = fp.t2frames;
+    memcpy(dev.mux, l.mux, sizeof(dev.mux));
+    return 0;
+  }
+};
+
 }  // namespace
 
 // ============================================================================ common
@@ -364,7 +392,8 @@ static FmParams to_fm(const dvbt2ll_framemapperfint_params &p) {
 struct dvbt2ll_framemapperfint {
   DeviceCtx ctx;
   FramePlan plan;
-  DevBuf map, aux, din, dout;
+  L1Tables l1;
+  DevBuf map, aux, din, dout;   // aux: one row; its L1-post cells are rewritten per call on the GPU
   int t2_frame_num = 0;
 };
 extern "C" int dvbt2ll_framemapperfint_create(const dvbt2ll_framemapperfint_params *p, int device,
@@ -376,7 +405,8 @@ extern "C" int dvbt2ll_framemapperfint_create(const dvbt2ll_framemapperfint_para
   if (build_frame(to_fm(*p), h->plan)) return DVBT2LL_EINVAL;
   int r = h->ctx.init(device);
   if (r) return r;
-  if ((r = upload(h->map, h->plan.gather_in)) || (r = upload(h->aux, h->plan.aux))) return r;
+  if ((r = upload(h->map, h->plan.gather_in)) || (r = upload(h->aux, h->plan.aux)) || (r = h->l1.init(h->plan)))
+    return r;
   *out = h.release();
   return DVBT2LL_OK;
 }
@@ -398,11 +428,17 @@ extern "C" int dvbt2ll_framemapperfint_general_work(dvbt2ll_framemapperfint *h, 
   HIP_TRY(hipSetDevice(h->ctx.device));
   if (h->din.ensure((size_t)f.S * 8) || h->dout.ensure((size_t)f.M * 8)) return DVBT2LL_ENOMEM;
   HIP_TRY(hipMemcpyAsync(h->din.p, in, (size_t)f.S * 8, hipMemcpyHostToDevice, h->ctx.stream));
+  // this frame's L1-post cells (FRAME_IDX = t2_frame_num) into the aux row, then the gather
+  L1IO lio{};
+  lio.out = h->aux.as<float2>() + AUX_L1PRE + 1840;
+  lio.first_frame = h->t2_frame_num;
+  lio.nframes = 1;
+  HIP_TRY(launch_l1post(h->l1.dev, lio, h->ctx.stream));
   GatherIO io{};
   io.in = h->din.as<float2>();
   io.out = h->dout.as<float2>();
   io.map = h->map.as<int32_t>();
-  io.aux = h->aux.as<float2>() + (size_t)h->t2_frame_num * f.aux_len;
+  io.aux = h->aux.as<float2>();
   io.M = f.M;
   HIP_TRY(launch_gather(io, h->ctx.stream));
   HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)f.M * 8, hipMemcpyDeviceToHost, h->ctx.stream));
@@ -521,8 +557,8 @@ struct ChainGraph {
   int nframes = 0, fmt = -1, slot = -1;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
-  hipGraphNode_t node[3] = {};
-  hipKernelNodeParams base[3] = {};
+  hipGraphNode_t node[4] = {};
+  hipKernelNodeParams base[4] = {};
   ~ChainGraph() {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -544,6 +580,10 @@ struct dvbt2ll_chain {
   // calls issued on different streams overlap; a slot reused on another stream first waits for
   // its previous run (slot_done) -- see dvbt2ll_chain_set_slots
   DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], pairs[DVBT2LL_CHAIN_MAX_SLOTS];
+  // per-frame L1-post cells of a run (l1post_kernel -> the OFDM kernel's indirect aux entries)
+  L1Tables l1;
+  DevBuf l1buf[DVBT2LL_CHAIN_MAX_SLOTS];
+  uint32_t l1_stride = 0;
   hipEvent_t slot_done[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   hipStream_t slot_stream[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   bool slot_used[DVBT2LL_CHAIN_MAX_SLOTS] = {};
@@ -561,13 +601,15 @@ struct dvbt2ll_chain {
   int64_t iq_per_frame = 0;
   int64_t ts_per_frame = 0;
   int pay = 0;
-  // stage timing: 4 events per run (start, after fec, after map, after ofdm) recorded on the
-  // launch stream without host synchronisation; folded into ms[] by get_timing()
+  // stage timing: 5 events per run (start, after l1post, after fec, after map, after ofdm) recorded
+  // on the launch stream without host synchronisation; folded into ms[] by get_timing()
+  // (stages 0 fec, 1 map, 2 ofdm, 3 l1post)
+  static constexpr int NEV = 5;
   bool timing = false;
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
-  double ms[3] = {0, 0, 0};
-  int64_t launches[3] = {0, 0, 0};
+  double ms[4] = {0, 0, 0, 0};
+  int64_t launches[4] = {0, 0, 0, 0};
   hipEvent_t next_event() {
     if (evused == evpool.size()) {
       hipEvent_t e = nullptr;
@@ -581,14 +623,15 @@ struct dvbt2ll_chain {
   int fold_timing() {
     if (!evused) return 0;
     int st = 0;
-    for (size_t b = 0; b + 3 < evused && !st; b += 4) {
-      hipError_t e = hipEventSynchronize(evpool[b + 3]);
-      for (int k = 0; k < 3 && e == hipSuccess; k++) {
+    static const int stage_of[4] = {3, 0, 1, 2};   // event interval k -> stage
+    for (size_t b = 0; b + NEV - 1 < evused && !st; b += NEV) {
+      hipError_t e = hipEventSynchronize(evpool[b + NEV - 1]);
+      for (int k = 0; k < NEV - 1 && e == hipSuccess; k++) {
         float t = 0;
         e = hipEventElapsedTime(&t, evpool[b + k], evpool[b + k + 1]);
         if (e == hipSuccess) {
-          ms[k] += t;
-          launches[k] += 1;
+          ms[stage_of[k]] += t;
+          launches[stage_of[k]] += 1;
         }
       }
       if (e != hipSuccess) {
@@ -599,12 +642,15 @@ struct dvbt2ll_chain {
     evused = 0;
     return st;
   }
-  // the chain's kernels on stream s: fused FEC + map, or FEC then map; then OFDM.  ev (timing):
-  // recorded after the FEC (+ map) and after the map kernel
-  hipError_t launch_chain(const FecIO &fio, const MapIO &mio, const OfdmIO &oio, hipStream_t s, hipEvent_t ev1,
-                          hipEvent_t ev2) {
-    hipError_t e = fused ? launch_fec_map(fec.dev, fio, map.dev, mio.out_pairs, mio.frame_stride, s)
-                         : launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, s);
+  // the chain's kernels on stream s: the frames' L1-post cells, fused FEC + map or FEC then map,
+  // then OFDM.  evl, ev1, ev2 (timing): recorded after the L1-post, the FEC (+ map) and the map kernel
+  hipError_t launch_chain(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, hipStream_t s,
+                          hipEvent_t evl, hipEvent_t ev1, hipEvent_t ev2) {
+    hipError_t e = launch_l1post(l1.dev, lio, s);
+    if (e == hipSuccess && evl) e = hipEventRecord(evl, s);
+    if (e == hipSuccess)
+      e = fused ? launch_fec_map(fec.dev, fio, map.dev, mio.out_pairs, mio.frame_stride, s)
+                : launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, s);
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, s);
     if (e == hipSuccess && !fused) e = launch_map(map.dev, mio, s);
     if (e == hipSuccess && ev2) e = hipEventRecord(ev2, s);
@@ -616,8 +662,9 @@ struct dvbt2ll_chain {
   // re-armed after its previous launch has completed (host wait on the slot's completion event,
   // recorded after every run on the slot), so no in-flight launch ever sees arguments rewritten
   // under it; with several slots the calls still overlap on the device
-  int graph_launch(const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, int slot, hipStream_t s) {
-    const int nk = fused ? 2 : 3;
+  int graph_launch(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, int slot,
+                   hipStream_t s) {
+    const int nk = fused ? 3 : 4;
     ChainGraph *g = nullptr;
     for (auto &c : graphs)
       if (c->nframes == nframes && c->fmt == ofdm.dev.fmt && c->slot == slot) g = c.get();
@@ -629,7 +676,7 @@ struct dvbt2ll_chain {
       c->fmt = ofdm.dev.fmt;
       c->slot = slot;
       HIP_TRY(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
-      hipError_t e1 = launch_chain(fio, mio, oio, cap_stream, nullptr, nullptr);
+      hipError_t e1 = launch_chain(lio, fio, mio, oio, cap_stream, nullptr, nullptr, nullptr);
       hipError_t ec = hipStreamEndCapture(cap_stream, &c->graph);
       HIP_TRY(e1);
       HIP_TRY(ec);
@@ -675,18 +722,21 @@ struct dvbt2ll_chain {
       graphs.push_back(std::move(c));
     }
     if (slot_used[slot]) HIP_TRY(hipEventSynchronize(slot_done[slot]));
+    L1Dev ld = l1.dev;
     FecDev fd = fec.dev;
     MapDev md = map.dev, md0{};
     OfdmDev od = ofdm.dev;
+    L1IO li = lio;
     FecIO fi = fio;
     MapIO mi = mio;
     OfdmIO oi = oio;
     uint16_t *op = fused ? mio.out_pairs : nullptr;
     int64_t fs = fused ? mio.frame_stride : 0;
+    void *al[2] = {&ld, &li};
     void *a0[5] = {&fd, &fi, fused ? (void *)&md : (void *)&md0, &op, &fs};
     void *a1[2] = {&md, &mi}, *a2[2] = {&od, &oi};
-    void **args[3] = {a0, a1, a2};
-    if (fused) args[1] = a2;
+    void **args[4] = {al, a0, a1, a2};
+    if (fused) args[2] = a2;
     for (int k = 0; k < nk; k++) {
       hipKernelNodeParams p = g->base[k];
       p.kernelParams = args[k];
@@ -698,7 +748,7 @@ struct dvbt2ll_chain {
   }
   int alloc_slot(int k) {
     if ((!fused && cw[k].ensure((size_t)frame.F * max_frames * cw_stride)) ||
-        pairs[k].ensure((size_t)pair_stride * max_frames * 2))
+        pairs[k].ensure((size_t)pair_stride * max_frames * 2) || l1buf[k].ensure((size_t)l1_stride * max_frames * 8))
       return DVBT2LL_ENOMEM;
     if (!slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
     return 0;
@@ -767,12 +817,15 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
     h->map.dev.part = h->part.as<int16_t>();
   }
   const PilotPlan &pp = h->pilot;
+  // one aux row (pilot values, L1-pre, dummy cells): the L1-post cells come per frame from the GPU
   std::vector<cf32> auxv = h->frame.aux;
-  for (int v = 0; v < h->frame.t2frames; v++)
-    for (int i = 0; i < 12; i++) auxv[(size_t)v * h->frame.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
-  if ((r = h->ofdm.init(pp, layout.cmap, h->frame.aux_len, h->frame.t2frames))) return r;
+  for (int i = 0; i < 12; i++) auxv[AUX_PILOT0 + i] = pp.pilot_values[i];
+  if ((r = h->ofdm.init(pp, layout.cmap, h->frame.aux_len, 1))) return r;
   AuxLists al;
-  if (build_aux_lists(layout, pp.N, pp.Nsym, auxv, h->frame.aux_len, h->frame.t2frames, al)) return DVBT2LL_EINVAL;
+  if (build_aux_lists(layout, pp.N, pp.Nsym, auxv, h->frame.aux_len, 1, al, AUX_L1PRE + 1840, h->frame.Lp))
+    return DVBT2LL_EINVAL;
+  if ((r = h->l1.init(h->frame))) return r;
+  h->l1_stride = (uint32_t)((h->frame.Lp + 3) & ~3);
   for (auto &b : al.dbin)
     if (b != 0xFFFF) b = (uint16_t)ofdm_padded_bin(pp.N, b);
   for (auto &e : al.ind) e = ofdm_padded_bin(pp.N, e & 0x7FFFu) | (e & ~0x7FFFu);
@@ -806,7 +859,8 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   // (bbheader:327-355, fec_block == 0)
   h->ts_per_frame = (int64_t)h->frame.F * h->pay - (f.inband ? 13 : 0);
   // the OFDM kernel addresses index pairs and aux cells with 32-bit byte offsets
-  if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32))
+  if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32) ||
+      (uint64_t)h->l1_stride * h->max_frames * 8 >= (1ull << 32))
     return DVBT2LL_EINVAL;
   {
     // tuning knob for kernel experiments (tools/gpu_fused_ab.sh): DVBT2LL_CHAIN_FUSED=1 runs FEC and
@@ -869,16 +923,22 @@ extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, i
   const int slot = h->next_slot;
   if (h->slot_used[slot] && h->slot_stream[slot] != s) HIP_TRY(hipStreamWaitEvent(s, h->slot_done[slot], 0));
   DevBuf &cw = h->cw[slot], &pairs = h->pairs[slot];
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[dvbt2ll_chain::NEV] = {};
   if (h->timing && !h->use_graph) {   // per-stage events only on the direct launch path
-    if (h->evused + 4 > 4096 && h->fold_timing()) return DVBT2LL_EDEVICE;
+    if (h->evused + dvbt2ll_chain::NEV > 4096 && h->fold_timing()) return DVBT2LL_EDEVICE;
     for (auto &e : ev)
       if (!(e = h->next_event())) return DVBT2LL_EDEVICE;
     HIP_TRY(hipEventRecord(ev[0], s));
   }
+  L1IO lio{};
   FecIO fio{};
   MapIO mio{};
   OfdmIO oio{};
+  lio.out = h->l1buf[slot].as<float2>();
+  lio.out_stride = h->l1_stride;
+  lio.first_frame = first_frame;
+  lio.nframes = nf;
+  lio.frames_per_stream = nstreams > 1 ? nframes : 0;
   fio.in = (const uint8_t *)ts_dev;
   fio.ts_base = ts_base;
   fio.ts_len = ts_len;
@@ -906,12 +966,14 @@ extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, i
   oio.first_frame = first_frame;
   oio.nframes = nf;
   oio.frames_per_stream = nstreams > 1 ? nframes : 0;
+  oio.l1 = h->l1buf[slot].as<float2>();
+  oio.l1_stride = h->l1_stride;
   if (h->use_graph) {
-    int r = h->graph_launch(fio, mio, oio, nf, slot, s);
+    int r = h->graph_launch(lio, fio, mio, oio, nf, slot, s);
     if (r) return r;
   } else {
-    HIP_TRY(h->launch_chain(fio, mio, oio, s, h->timing ? ev[1] : nullptr, h->timing ? ev[2] : nullptr));
-    if (h->timing) HIP_TRY(hipEventRecord(ev[3], s));
+    HIP_TRY(h->launch_chain(lio, fio, mio, oio, s, ev[1], ev[2], ev[3]));
+    if (h->timing) HIP_TRY(hipEventRecord(ev[4], s));
   }
   HIP_TRY(hipEventRecord(h->slot_done[slot], s));
   h->slot_used[slot] = true;
@@ -971,13 +1033,13 @@ extern "C" int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable) {
   if (!h) return DVBT2LL_EINVAL;
   if (h->fold_timing()) return DVBT2LL_EDEVICE;
   h->timing = enable != 0;
-  for (int k = 0; k < 3; k++) { h->ms[k] = 0; h->launches[k] = 0; }
+  for (int k = 0; k < 4; k++) { h->ms[k] = 0; h->launches[k] = 0; }
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages) {
   if (!h || !ms || nstages < 1) return DVBT2LL_EINVAL;
   if (h->fold_timing()) return DVBT2LL_EDEVICE;
-  for (int k = 0; k < nstages && k < 3; k++) {
+  for (int k = 0; k < nstages && k < 4; k++) {
     ms[k] = h->ms[k];
     if (launches) launches[k] = h->launches[k];
   }

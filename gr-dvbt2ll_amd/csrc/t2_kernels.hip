@@ -1446,6 +1446,8 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u, d.abin, d.aval, d.aind, nullptr,
                 nullptr};
   if (d.inv) {
+    src.data = io.l1;                              // indirect entries: this frame's L1-post cells
+    src.abase = (uint32_t)f * io.l1_stride - 1u;
     src.d0 = (uint32_t)d.sym_d0[j];
     src.dn = (uint32_t)d.sym_n[j];
     src.dn0 = (uint32_t)d.sym_n0[j];
@@ -1669,7 +1671,7 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     // scatter mode, one half of the bins (m2 < 16, then m2 >= 16) at a time
     float *qre = (float *)(smem + O32_QAM), *qim = qre + 256;
     const float2 tq = tid < 256 ? d.qam[tid] : make_float2(0.f, 0.f);
-    BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, (uint32_t)d.sym_d0[j], (uint32_t)d.sym_n[j],
+    BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv, io.pairs, qre, qim, (uint32_t)d.sym_d0[j], (uint32_t)d.sym_n[j],
                   (uint32_t)d.sym_n0[j], d.abin, d.aval, d.aind, d.agrp + 2 * j, d.azr + 2 * j};
     const uint32_t dummy = (uint32_t)(O32_H + (O32_H >> O32_PS)) + (uint32_t)(tid & 63);
 #pragma unroll
@@ -1761,6 +1763,144 @@ hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
     case 32768: return launch_ofdm_t<32768>(d, io, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+// ============================================================================ L1-post
+// One 256-thread workgroup per T2 frame of the launch: that frame's L1-post cells
+// (framemapper:1536-1910) from the t2_plan L1PostPlan.  The codeword lives in LDS as 16200 bits
+// packed MSB first: information bits 0..7031 (shortened positions zero), BCH parity 7032..7199,
+// LDPC parity 7200..16199 (word-aligned at word 225).
+constexpr int L1_NT = 256, L1_CW_WORDS = (16200 + 31) / 32, L1_SIG_WORDS = 16;
+
+__device__ __forceinline__ uint32_t l1_bit(const uint32_t *w, int i) { return (w[i >> 5] >> (31 - (i & 31))) & 1u; }
+
+// XOR of v over the workgroup (every thread gets the result); red: L1_NT / 64 words of LDS
+__device__ __forceinline__ uint32_t l1_xor_all(uint32_t v, uint32_t *red, int tid) {
+  v = rd_lane_u32(wave_prefix_xor(v), 63);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+#pragma unroll
+  for (int k = 0; k < L1_NT / 64; k++) t ^= red[k];
+  return t;
+}
+
+__global__ __launch_bounds__(L1_NT) void l1post_kernel(L1Dev d, L1IO io) {
+  __shared__ uint32_t cw[L1_CW_WORDS];
+  __shared__ uint32_t sig[L1_SIG_WORDS];
+  __shared__ uint32_t red[L1_NT / 64 * 6];
+  const int tid = threadIdx.x, f = blockIdx.x;
+  const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);
+  const uint32_t fidx = (uint32_t)(frame % d.t2frames);   // FRAME_IDX = t2_frame_num (:1648-1651)
+  const int nsw = (d.nsig + 31) >> 5, L = d.nsig - 32;
+  for (int w = tid; w < L1_CW_WORDS; w += L1_NT) cw[w] = 0;
+  // signal bits: the template with this frame's FRAME_IDX (8 bits, MSB first, at fidx_pos)
+  if (tid < nsw) {
+    uint32_t v = d.tmpl[tid];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int p = d.fidx_pos + k;
+      if ((p >> 5) == tid && ((fidx >> (7 - k)) & 1u)) v |= 1u << (31 - (p & 31));
+    }
+    sig[tid] = v;
+  }
+  __syncthreads();
+  // CRC-32 (:1203-1224) over the first L bits: crc_k ^ XOR of the set bits' contributions
+  uint32_t c = 0;
+  for (int i = tid; i < L; i += L1_NT)
+    if (l1_bit(sig, i)) c ^= d.crc_c[i];
+  const uint32_t crc = d.crc_k ^ l1_xor_all(c, red, tid);
+  if (tid < 32 && ((crc >> (31 - tid)) & 1u)) atomicOr(&sig[(L + tid) >> 5], 1u << (31 - ((L + tid) & 31)));
+  __syncthreads();
+  if (d.scr && tid < nsw) sig[tid] ^= d.scr[tid];   // L1 scrambler (:1928-1940), v1.3.1
+  __syncthreads();
+  // shortening: signal bit i -> information position sig_pos[i]; BCH(168) parity = XOR of the
+  // per-position remainders of the set bits (6 words, parity bit n at word n / 32, MSB first)
+  uint32_t b[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = tid; i < d.nsig; i += L1_NT) {
+    if (!l1_bit(sig, i)) continue;
+    const int pos = d.sig_pos[i];
+    atomicOr(&cw[pos >> 5], 1u << (31 - (pos & 31)));
+#pragma unroll
+    for (int k = 0; k < 6; k++) b[k] ^= d.bch_r[i * 6 + k];
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) b[k] = rd_lane_u32(wave_prefix_xor(b[k]), 63);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 6; k++) red[(tid >> 6) * 6 + k] = b[k];
+  __syncthreads();
+  if (tid < 168) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int r = 0; r < L1_NT / 64; r++) w ^= red[r * 6 + (tid >> 5)];
+    if ((w >> (31 - (tid & 31))) & 1u) {
+      const int pos = 7032 + tid;
+      atomicOr(&cw[pos >> 5], 1u << (31 - (pos & 31)));
+    }
+  }
+  __syncthreads();
+  // LDPC (:1314-1364): information bit 360 g + n feeds parity (x + n q) mod pbits for each address x
+  // of group g; only the signal positions and the BCH parity can be set
+  uint32_t *par = cw + 225;
+  for (int i = tid; i < d.nsig + 168; i += L1_NT) {
+    const int pos = i < d.nsig ? (int)d.sig_pos[i] : 7032 + (i - d.nsig);
+    if (!l1_bit(cw, pos)) continue;
+    const int g = pos / 360, n = pos - 360 * g;
+    for (int e = d.ldpc_ptr[g]; e < d.ldpc_ptr[g + 1]; e++) {
+      const int j = (d.ldpc_addr[e] + n * d.q) % d.pbits;
+      atomicXor(&par[j >> 5], 1u << (31 - (j & 31)));
+    }
+  }
+  __syncthreads();
+  // accumulate p[j] ^= p[j - 1]: inclusive prefix XOR within each word (from the MSB), then the
+  // exclusive prefix of the word parities over the wave, five words per lane
+  if (tid < 64) {
+    const int nwp = (d.pbits + 31) >> 5, per = (nwp + 63) / 64;
+    uint32_t x[5], par_l = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const int w = tid * per + k;
+      uint32_t v = (k < per && w < nwp) ? par[w] : 0u;
+      v ^= v >> 1; v ^= v >> 2; v ^= v >> 4; v ^= v >> 8; v ^= v >> 16;
+      x[k] = v;
+      par_l ^= v & 1u;   // the word's total parity sits in its last bit
+    }
+    const uint32_t before = wave_prefix_xor(par_l) ^ par_l;
+    uint32_t carry = before;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const int w = tid * per + k;
+      if (k < per && w < nwp) par[w] = carry ? ~x[k] : x[k];
+      carry ^= x[k] & 1u;
+    }
+  }
+  __syncthreads();
+  // puncture / select the N_post transmitted bits and map them (BPSK, QPSK, or the 16/64QAM column
+  // interleaver + demux, :1832-1908)
+  float2 *out = io.out + (int64_t)f * io.out_stride;
+  for (int cidx = tid; cidx < d.lp; cidx += L1_NT) {
+    float2 v;
+    if (d.mode == 0) {
+      v = make_float2(l1_bit(cw, d.sel[cidx]) ? -1.0f : 1.0f, 0.0f);
+    } else if (d.mode == 1) {
+      v = d.lut[(l1_bit(cw, d.sel[2 * cidx]) << 1) | l1_bit(cw, d.sel[2 * cidx + 1])];
+    } else {
+      const int k = cidx >> 1, half = d.ncols >> 1, e0 = (cidx & 1) ? half : 0;
+      uint32_t pack = 0;
+      for (int e = e0; e < e0 + half; e++) pack = (pack << 1) | l1_bit(cw, d.sel[d.rows * d.mux[e] + k]);
+      v = d.lut[pack];
+    }
+    out[cidx] = v;
+  }
+}
+
+hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s) {
+  if (io.nframes <= 0) return hipSuccess;
+  if (d.nsig > 32 * L1_SIG_WORDS || d.nsig < 33 || d.pbits != 9000 || d.q <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(l1post_kernel, dim3(io.nframes), dim3(L1_NT), 0, s, d, io);
+  return hipGetLastError();
 }
 
 // ============================================================================ gather

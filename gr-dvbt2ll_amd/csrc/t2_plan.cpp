@@ -461,7 +461,7 @@ void l1_encode(std::vector<uint8_t> &cw, int k, int nbch, int rate_id) {
 
 }  // namespace
 
-int build_frame(const FmParams &p, FramePlan &fp) {
+int build_frame(const FmParams &p, FramePlan &fp, bool host_l1post) {
   int normal = p.framesize == 1;
   fp.cs = cell_size_of(normal, p.constellation);
   if (!fp.cs || p.fecblocks < 1 || p.t2frames < 1 || p.t2frames > 255 || p.numdatasyms < 1) return -1;
@@ -480,7 +480,7 @@ int build_frame(const FmParams &p, FramePlan &fp) {
   if (p.l1constellation < 0 || p.l1constellation > 3) return -1;
   fp.eta = eta_of[p.l1constellation];
   // L1-post size (framemapper:978-987)
-  const int KSIG_POST = 350, KBCH12 = 7032, NBCH12 = 7200, KBCH14 = 3072, NBCH14 = 3240;
+  const int KSIG_POST = 350, KBCH12 = 7032, KBCH14 = 3072, NBCH14 = 3240;
   int npunc_t = (6 * (KBCH12 - KSIG_POST)) / 5;
   int npost_t = KSIG_POST + 168 + 9000 - npunc_t;
   if (fp.N_P2 == 1) fp.N_post = (int)std::ceil((float)npost_t / (2 * (float)fp.eta)) * 2 * fp.eta;
@@ -601,13 +601,10 @@ int build_frame(const FmParams &p, FramePlan &fp) {
   }
 
   // ---- L1 signalling cells
-  int qmod;
-  cf32 l1lut[64];
-  static const int l1c[4] = {0, QPSK, QAM16, QAM64};
-  if (p.l1constellation > 0) qam_table(l1c[p.l1constellation], 0, l1lut, &qmod);
   bool v131 = p.version == 2, resv = p.reservedbiasbits && v131;
   fp.aux_len = AUX_L1PRE + 1840 + Lp + fp.D;
-  fp.aux.assign((size_t)fp.t2frames * fp.aux_len, cf32{0.f, 0.f});
+  fp.aux_variants = host_l1post ? fp.t2frames : 1;
+  fp.aux.assign((size_t)fp.aux_variants * fp.aux_len, cf32{0.f, 0.f});
   // L1-pre (framemapper:1366-1534): BPSK, shortened/punctured LDPC(16200) 1/4
   std::vector<cf32> pre(1840);
   {
@@ -635,77 +632,202 @@ int build_frame(const FmParams &p, FramePlan &fp) {
       if (!punct[w]) pre[k++] = bpsk(cw[NBCH14 + w]);
     if (k != 1840) return -1;
   }
-  // L1-post (framemapper:1536-1910) for every FRAME_IDX value
-  std::vector<uint8_t> l1rand(KBCH12);
-  prbs15(l1rand.data(), KBCH12);
-  const uint8_t *pad = p.l1constellation == 2 ? T2_L1_POST_PADDING_16QAM
-                     : p.l1constellation == 3 ? T2_L1_POST_PADDING_64QAM : T2_L1_POST_PADDING_BQPSK;
-  const uint8_t *pun = p.l1constellation == 2 ? T2_L1_POST_PUNCTURE_16QAM
-                     : p.l1constellation == 3 ? T2_L1_POST_PUNCTURE_64QAM : T2_L1_POST_PUNCTURE_BQPSK;
+  // L1-post (framemapper:1536-1910): the per-frame GPU plan; with host_l1post also every FRAME_IDX
+  // variant encoded here (the CPU tests' cross-check of the plan and of the oracle)
   std::vector<uint8_t> dummybits(fp.D > 0 ? fp.D : 1);
   prbs15(dummybits.data(), (int)dummybits.size());
-  for (int v = 0; v < fp.t2frames; v++) {
-    Bits b;
-    b.put(1, 15); b.put(1, 8); b.put(0, 4); b.put(0, 8); b.put(0, 3); b.put(729833333u, 32);
-    b.put(0, 8); b.put(1, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3); b.put(0, 8); b.put(1, 8);
-    b.put(p.rate, 3); b.put(p.constellation, 3); b.put(p.rotation, 1); b.put(p.framesize, 2);
-    b.put(p.fecblocks, 10); b.put(1, 8); b.put(p.tiblocks, 8); b.put(0, 1); b.put(0, 1);
-    b.put((p.inband && v131) ? 1 : 0, 1); b.put(resv ? 0x7ff : 0, 11);
-    b.put(p.version == 0 ? 0 : p.inputmode + 1, 2); b.put(0, 1); b.put(0, 1); b.put(0, 2);
-    b.put(resv ? 0x3fffffff : 0, 30); b.put(v, 8); b.put(0, 22); b.put(0, 22); b.put(0, 8);
-    b.put(0, 3); b.put(resv ? 0xff : 0, 8); b.put(0, 8); b.put(0, 22); b.put(p.fecblocks, 10);
-    b.put(resv ? 0xff : 0, 8); b.put(resv ? 0xff : 0, 8);
-    b.put(crc32_mpeg2(b.b), 32);
-    int nsig = (int)b.b.size();
-    if (v131 && p.l1scrambled)
-      for (int i = 0; i < nsig; i++) b.b[i] ^= l1rand[i];
-    // shortening: groups in padding order, partial group filled from its end
-    std::vector<uint8_t> shortened(KBCH12, 0);
-    int m, last;
-    if (nsig <= 360) { m = 19; last = 360 - nsig; }
-    else { m = (KBCH12 - nsig) / 360; last = KBCH12 - nsig - 360 * m; }
-    for (int n = 0; n < m; n++) {
-      int len = pad[n] == 19 ? 192 : 360;
-      for (int w = 0; w < len; w++) shortened[pad[n] * 360 + w] = 1;
-    }
-    int gl = pad[m] == 19 ? 192 : 360;
-    for (int w = 0; w < last; w++) shortened[pad[m] * 360 + gl - last + w] = 1;
-    std::vector<uint8_t> cw(kShort, 0);
-    for (int n = 0, i = 0; n < KBCH12; n++) cw[n] = shortened[n] ? 0 : b.b[i++];
-    l1_encode(cw, KBCH12, NBCH12, 101);
-    std::vector<uint8_t> punct(kShort - NBCH12, 0);
-    for (int cg = 0; cg <= fp.N_punc / 360; cg++) {
-      int cnt = cg < fp.N_punc / 360 ? 360 : fp.N_punc % 360;
-      for (int c2 = 0; c2 < cnt; c2++) punct[c2 * 25 + pun[cg]] = 1;
-    }
-    std::vector<uint8_t> post;
-    for (int w = 0; w < KBCH12; w++) if (!shortened[w]) post.push_back(cw[w]);
-    for (int w = 0; w < 168; w++) post.push_back(cw[KBCH12 + w]);
-    for (int w = 0; w < kShort - NBCH12; w++) if (!punct[w]) post.push_back(cw[NBCH12 + w]);
-    if ((int)post.size() != fp.N_post) return -1;
-    cf32 *dst = &fp.aux[(size_t)v * fp.aux_len + AUX_L1PRE + 1840];
-    int produced = 0;
-    if (p.l1constellation == 0) {
-      for (int d = 0; d < fp.N_post; d++) dst[produced++] = cf32{post[d] ? -1.0f : 1.0f, 0.0f};
-    } else if (p.l1constellation == 1) {
-      for (int d = 0; d < fp.N_post / 2; d++) dst[produced++] = l1lut[(post[2 * d] << 1) | post[2 * d + 1]];
-    } else {
-      // column-row bit interleaver then demux by source index (framemapper:1832-1908)
-      int ncols = p.l1constellation == 2 ? 8 : 12, rows = fp.N_post / ncols, half = ncols / 2;
-      const uint8_t *mux = p.l1constellation == 2 ? T2_L1_MUX16 : T2_L1_MUX64;
-      for (int k = 0; k < rows; k++) {
-        int pack = 0;
-        for (int e = 0; e < ncols; e++) pack = (pack << 1) | post[rows * mux[e] + k];
-        dst[produced++] = l1lut[pack >> half];
-        dst[produced++] = l1lut[pack & ((1 << half) - 1)];
-      }
-    }
-    if (produced != Lp) return -1;
+  for (int v = 0; v < fp.aux_variants; v++) {
     cf32 *row = &fp.aux[(size_t)v * fp.aux_len];
     std::copy(pre.begin(), pre.end(), row + AUX_L1PRE);
     for (int i = 0; i < fp.D; i++) row[aux_dummy + i] = cf32{dummybits[i] ? -1.0f : 1.0f, 0.0f};
   }
+  if (build_l1post_plan(p, fp)) return -1;
+  if (host_l1post)
+    for (int v = 0; v < fp.t2frames; v++)
+      if (l1post_host(p, fp, v, &fp.aux[(size_t)v * fp.aux_len + AUX_L1PRE + 1840])) return -1;
   return 0;
+}
+
+namespace {
+// L1-post signalling bits before the CRC-32 (framemapper:1560-1830, single PLP, no auxiliary
+// streams): FRAME_IDX (8 bits at *fidx_pos) = frame_idx
+std::vector<uint8_t> l1post_signal(const FmParams &p, int frame_idx, int *fidx_pos) {
+  const bool v131 = p.version == 2, resv = p.reservedbiasbits && v131;
+  Bits b;
+  b.put(1, 15); b.put(1, 8); b.put(0, 4); b.put(0, 8); b.put(0, 3); b.put(729833333u, 32);
+  b.put(0, 8); b.put(1, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3); b.put(0, 8); b.put(1, 8);
+  b.put(p.rate, 3); b.put(p.constellation, 3); b.put(p.rotation, 1); b.put(p.framesize, 2);
+  b.put(p.fecblocks, 10); b.put(1, 8); b.put(p.tiblocks, 8); b.put(0, 1); b.put(0, 1);
+  b.put((p.inband && v131) ? 1 : 0, 1); b.put(resv ? 0x7ff : 0, 11);
+  b.put(p.version == 0 ? 0 : p.inputmode + 1, 2); b.put(0, 1); b.put(0, 1); b.put(0, 2);
+  b.put(resv ? 0x3fffffff : 0, 30);
+  if (fidx_pos) *fidx_pos = (int)b.b.size();
+  b.put((uint64_t)frame_idx, 8); b.put(0, 22); b.put(0, 22); b.put(0, 8);
+  b.put(0, 3); b.put(resv ? 0xff : 0, 8); b.put(0, 8); b.put(0, 22); b.put(p.fecblocks, 10);
+  b.put(resv ? 0xff : 0, 8); b.put(resv ? 0xff : 0, 8);
+  return b.b;
+}
+
+const int KBCH12 = 7032, NBCH12 = 7200;
+
+// shortening (framemapper:2190-2214): which of the 7032 information positions stay zero
+std::vector<uint8_t> l1post_shortened(const FmParams &p, int nsig) {
+  const uint8_t *pad = p.l1constellation == 2 ? T2_L1_POST_PADDING_16QAM
+                     : p.l1constellation == 3 ? T2_L1_POST_PADDING_64QAM : T2_L1_POST_PADDING_BQPSK;
+  std::vector<uint8_t> shortened(KBCH12, 0);
+  int m, last;
+  if (nsig <= 360) { m = 19; last = 360 - nsig; }
+  else { m = (KBCH12 - nsig) / 360; last = KBCH12 - nsig - 360 * m; }
+  for (int n = 0; n < m; n++) {
+    int len = pad[n] == 19 ? 192 : 360;
+    for (int w = 0; w < len; w++) shortened[pad[n] * 360 + w] = 1;
+  }
+  int gl = pad[m] == 19 ? 192 : 360;
+  for (int w = 0; w < last; w++) shortened[pad[m] * 360 + gl - last + w] = 1;
+  return shortened;
+}
+
+// puncturing (framemapper:2215-2233): which LDPC parity bits are not transmitted
+std::vector<uint8_t> l1post_punctured(const FmParams &p, const FramePlan &fp) {
+  const uint8_t *pun = p.l1constellation == 2 ? T2_L1_POST_PUNCTURE_16QAM
+                     : p.l1constellation == 3 ? T2_L1_POST_PUNCTURE_64QAM : T2_L1_POST_PUNCTURE_BQPSK;
+  std::vector<uint8_t> punct(kShort - NBCH12, 0);
+  for (int cg = 0; cg <= fp.N_punc / 360; cg++) {
+    int cnt = cg < fp.N_punc / 360 ? 360 : fp.N_punc % 360;
+    for (int c2 = 0; c2 < cnt; c2++) punct[c2 * 25 + pun[cg]] = 1;
+  }
+  return punct;
+}
+}  // namespace
+
+int build_l1post_plan(const FmParams &p, FramePlan &fp) {
+  L1PostPlan &l = fp.l1;
+  l = L1PostPlan();
+  const bool v131 = p.version == 2;
+  std::vector<uint8_t> sig = l1post_signal(p, 0, &l.fidx_pos);
+  const int L = (int)sig.size();           // CRC-covered bits
+  l.nsig = L + 32;
+  if (l.nsig > 512 || l.fidx_pos + 8 > L) return -1;
+  const int nw = (l.nsig + 31) / 32;
+  l.tmpl.assign(nw, 0);
+  for (int i = 0; i < L; i++)
+    if (sig[i]) l.tmpl[i >> 5] |= 1u << (31 - (i & 31));
+  // CRC-32/MPEG-2 (register init all ones, no final XOR) is affine in the message: crc(m) = crc(0^L)
+  // ^ XOR of c_i over the set bits, c_i = the register after a lone 1 at position i
+  l.crc_k = crc32_mpeg2(std::vector<uint8_t>((size_t)L, 0));
+  l.crc_c.assign(L, 0);
+  uint32_t c = 0x04C11DB7u;                 // a 1 in the last message bit
+  for (int i = L - 1; i >= 0; i--) {
+    l.crc_c[i] = c;
+    c = (c << 1) ^ ((c >> 31) ? 0x04C11DB7u : 0u);
+  }
+  if (v131 && p.l1scrambled) {
+    std::vector<uint8_t> r(KBCH12);
+    prbs15(r.data(), KBCH12);
+    l.scr.assign(nw, 0);
+    for (int i = 0; i < l.nsig; i++)
+      if (r[i]) l.scr[i >> 5] |= 1u << (31 - (i & 31));
+  }
+  const std::vector<uint8_t> shortened = l1post_shortened(p, l.nsig);
+  for (int n = 0; n < KBCH12; n++)
+    if (!shortened[n]) l.sig_pos.push_back((uint16_t)n);
+  if ((int)l.sig_pos.size() != l.nsig) return -1;
+  // BCH(168): the parity of a lone 1 at information position q is x^(168 + 7031 - q) mod g(x)
+  static const Poly192 g = bch_generator(false, 168);
+  Poly192 v;
+  v.w[0] = 1;
+  for (int i = 0; i < 168; i++) v = times_x(v, g, 168);
+  std::vector<Poly192> rem(KBCH12);
+  for (int q = KBCH12 - 1; q >= 0; q--) {
+    rem[q] = v;
+    v = times_x(v, g, 168);
+  }
+  l.bch_r.assign((size_t)l.nsig * 6, 0);
+  for (int i = 0; i < l.nsig; i++) {
+    const Poly192 &r = rem[l.sig_pos[i]];
+    for (int n = 0; n < 168; n++)
+      if (r.bit(167 - n)) l.bch_r[(size_t)i * 6 + (n >> 5)] |= 1u << (31 - (n & 31));
+  }
+  // LDPC 1/2 short (the L1-post code, framemapper:1314-1364)
+  const t2_ldpc_code_t *code = find_code(0, 101);
+  if (!code || code->nrows * 360 != NBCH12) return -1;
+  l.q = code->q;
+  l.pbits = kShort - NBCH12;
+  int off = code->addr_off;
+  l.ldpc_ptr.assign(code->nrows + 1, 0);
+  for (int gi = 0; gi < code->nrows; gi++) {
+    l.ldpc_ptr[gi] = (uint16_t)l.ldpc_addr.size();
+    const int cnt = T2_LDPC_ROWLEN[code->row_off + gi];
+    for (int e = 0; e < cnt; e++) l.ldpc_addr.push_back((uint16_t)T2_LDPC_ADDR[off + e]);
+    off += cnt;
+  }
+  l.ldpc_ptr[code->nrows] = (uint16_t)l.ldpc_addr.size();
+  // transmitted bits: unshortened information, BCH parity, unpunctured LDPC parity
+  const std::vector<uint8_t> punct = l1post_punctured(p, fp);
+  for (int i = 0; i < l.nsig; i++) l.sel.push_back(l.sig_pos[i]);
+  for (int n = 0; n < 168; n++) l.sel.push_back((uint16_t)(KBCH12 + n));
+  for (int w = 0; w < l.pbits; w++)
+    if (!punct[w]) l.sel.push_back((uint16_t)(NBCH12 + w));
+  l.npost = (int)l.sel.size();
+  if (l.npost != fp.N_post) return -1;
+  l.lp = fp.Lp;
+  l.mode = p.l1constellation;
+  static const int l1c[4] = {0, QPSK, QAM16, QAM64};
+  int qmod = 0;
+  if (l.mode > 0) qam_table(l1c[l.mode], 0, l.lut, &qmod);
+  if (l.mode >= 2) {
+    l.ncols = l.mode == 2 ? 8 : 12;
+    l.rows = fp.N_post / l.ncols;
+    const uint8_t *mux = l.mode == 2 ? T2_L1_MUX16 : T2_L1_MUX64;
+    for (int e = 0; e < l.ncols; e++) l.mux[e] = mux[e];
+  }
+  return 0;
+}
+
+// Host encoder of one FRAME_IDX variant's L1-post cells (tests only): the reference's order of
+// operations, one bit at a time (framemapper:1536-1910)
+int l1post_host(const FmParams &p, const FramePlan &fp, int frame_idx, cf32 *dst) {
+  const bool v131 = p.version == 2;
+  std::vector<uint8_t> bits = l1post_signal(p, frame_idx, nullptr);
+  const uint32_t crc = crc32_mpeg2(bits);
+  for (int i = 31; i >= 0; i--) bits.push_back((crc >> i) & 1);
+  const int nsig = (int)bits.size();
+  if (v131 && p.l1scrambled) {
+    std::vector<uint8_t> l1rand(KBCH12);
+    prbs15(l1rand.data(), KBCH12);
+    for (int i = 0; i < nsig; i++) bits[i] ^= l1rand[i];
+  }
+  const std::vector<uint8_t> shortened = l1post_shortened(p, nsig);
+  std::vector<uint8_t> cw(kShort, 0);
+  for (int n = 0, i = 0; n < KBCH12; n++) cw[n] = shortened[n] ? 0 : bits[i++];
+  l1_encode(cw, KBCH12, NBCH12, 101);
+  const std::vector<uint8_t> punct = l1post_punctured(p, fp);
+  std::vector<uint8_t> post;
+  for (int w = 0; w < KBCH12; w++) if (!shortened[w]) post.push_back(cw[w]);
+  for (int w = 0; w < 168; w++) post.push_back(cw[KBCH12 + w]);
+  for (int w = 0; w < kShort - NBCH12; w++) if (!punct[w]) post.push_back(cw[NBCH12 + w]);
+  if ((int)post.size() != fp.N_post) return -1;
+  cf32 l1lut[64];
+  int qmod;
+  static const int l1c[4] = {0, QPSK, QAM16, QAM64};
+  if (p.l1constellation > 0) qam_table(l1c[p.l1constellation], 0, l1lut, &qmod);
+  int produced = 0;
+  if (p.l1constellation == 0) {
+    for (int d = 0; d < fp.N_post; d++) dst[produced++] = cf32{post[d] ? -1.0f : 1.0f, 0.0f};
+  } else if (p.l1constellation == 1) {
+    for (int d = 0; d < fp.N_post / 2; d++) dst[produced++] = l1lut[(post[2 * d] << 1) | post[2 * d + 1]];
+  } else {
+    // column-row bit interleaver then demux by source index (framemapper:1832-1908)
+    int ncols = p.l1constellation == 2 ? 8 : 12, rows = fp.N_post / ncols, half = ncols / 2;
+    const uint8_t *mux = p.l1constellation == 2 ? T2_L1_MUX16 : T2_L1_MUX64;
+    for (int k = 0; k < rows; k++) {
+      int pack = 0;
+      for (int e = 0; e < ncols; e++) pack = (pack << 1) | post[rows * mux[e] + k];
+      dst[produced++] = l1lut[pack >> half];
+      dst[produced++] = l1lut[pack & ((1 << half) - 1)];
+    }
+  }
+  return produced == fp.Lp ? 0 : -1;
 }
 
 // ============================================================================ pilots + OFDM
@@ -1042,14 +1164,16 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
 }
 
 int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf32> &auxv, int aux_len,
-                    int t2frames, AuxLists &al) {
+                    int t2frames, AuxLists &al, int l1_lo, int l1_len) {
   const bool split = ofdm_split(N);
   const int nsub = split ? N / 2 : N, ngrp = 2 * Nsym;
   if ((int64_t)aux_len * t2frames > (int64_t)auxv.size() || nsub > 32768) return -1;
   al.dbin.clear(); al.dval.clear(); al.ind.clear();
   al.grp.assign((size_t)4 * ngrp, 0);
   al.zrun.assign((size_t)2 * ngrp, 0);
+  auto is_l1 = [&](int a) { return a >= l1_lo && a < l1_lo + l1_len; };
   auto same_in_all = [&](int a) {
+    if (is_l1(a)) return false;
     for (int v = 1; v < t2frames; v++) {
       const cf32 x = auxv[a], y = auxv[(size_t)v * aux_len + a];
       if (std::memcmp(&x, &y, sizeof(cf32))) return false;
@@ -1099,8 +1223,11 @@ int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf
         al.dbin.push_back((uint16_t)k);
         al.dval.push_back(v);
       } else {
-        if (-c >= (1 << 17)) return -1;
-        al.ind.push_back((uint32_t)k | ((uint32_t)(-c) << 15));
+        // per-frame cells: L1-post cell a - l1_lo of the frame (code a - l1_lo + 1), or (no L1
+        // range) aux index a of the frame's t2_frame_num variant (code a + 1)
+        const int code = is_l1(a) ? a - l1_lo + 1 : a + 1;
+        if (code >= (1 << 17)) return -1;
+        al.ind.push_back((uint32_t)k | ((uint32_t)code << 15));
       }
     }
     while (al.dbin.size() & 3) {   // pad to a quad: bin 0xFFFF goes to the kernel's dummy slot

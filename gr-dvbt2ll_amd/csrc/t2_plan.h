@@ -66,6 +66,34 @@ struct FmParams {
 constexpr int AUX_ZERO = 0;
 constexpr int AUX_PILOT0 = 1;
 constexpr int AUX_L1PRE = 13;
+// L1-post signalling (framemapper:1536-1910), generated per T2 frame on the GPU (l1post_kernel):
+// the configurable + dynamic fields as a bit template whose only per-frame field is FRAME_IDX
+// (= t2_frame_num, :1648-1651), CRC-32 (:1203-1224) as the XOR of per-bit contributions, the
+// optional L1 scrambler (:1928-1940), shortening into the 7032-bit BCH information word (padding
+// groups :2190-2233), BCH(168) as the XOR of per-position remainders x^(168 + 7031 - p) mod g(x)
+// (:1269-1312), the LDPC 1/2 (16K) accumulate over its address table (:1314-1364), puncturing,
+// and the L1 constellation with the 16/64QAM bit interleaver + demux (:1832-1908).
+struct L1PostPlan {
+  int nsig = 0;                    // signalling bits including the CRC-32
+  int fidx_pos = 0;                // bit position of FRAME_IDX (8 bits, MSB first)
+  int npost = 0, lp = 0;           // transmitted bits N_post, cells Lp
+  int mode = 0;                    // L1 constellation: 0 BPSK, 1 QPSK, 2 16QAM, 3 64QAM
+  int ncols = 0, rows = 0;         // 16/64QAM bit interleaver geometry
+  int q = 0, pbits = 0;            // LDPC: 25, 9000
+  uint32_t crc_k = 0;              // CRC-32 of the all-zero message (the 0xFFFFFFFF init's share)
+  std::vector<uint32_t> tmpl;      // ceil(nsig / 32) words, MSB first; FRAME_IDX and CRC fields 0
+  std::vector<uint32_t> crc_c;     // nsig - 32: CRC-32 contribution of message bit i
+  std::vector<uint32_t> scr;       // ceil(nsig / 32) words of L1 scrambler PRBS, empty when off
+  std::vector<uint16_t> sig_pos;   // nsig: position of signal bit i in the 7032-bit BCH info word
+  std::vector<uint32_t> bch_r;     // nsig x 6 words: BCH parity of a 1 at sig_pos[i] (parity bit n
+                                   //   at word n / 32, bit 31 - n % 32)
+  std::vector<uint16_t> ldpc_ptr;  // 21: address list of information group g at [ptr[g], ptr[g + 1])
+  std::vector<uint16_t> ldpc_addr; // parity addresses x: info bit 360 g + n feeds (x + n q) mod pbits
+  std::vector<uint16_t> sel;       // npost: codeword index (info | BCH parity | LDPC parity) per bit
+  uint8_t mux[12] = {};
+  cf32 lut[64] = {};
+};
+
 struct FramePlan {
   int cs = 0, F = 0, S = 0, M = 0, N_P2 = 0, C_P2 = 0, C_DATA = 0, N_FC = 0, C_FC = 0;
   int eta = 0, N_post = 0, N_punc = 0, Lp = 0, D = 0, num_data_symbols = 0, t2frames = 0;
@@ -75,9 +103,19 @@ struct FramePlan {
   std::vector<int32_t> gather_d;         // M: mapped cell -> frame data-region index (TI output order) | aux
   int ti_on = 0, ti_small = 1, ti_big = 1, ti_nsmall = 0;   // TI blocks: ti_nsmall of ti_small FEC blocks, then ti_big
   std::vector<int32_t> gather_in;        // M: mapped cell -> framemapper input index | aux
-  std::vector<cf32> aux;                 // t2frames x aux_len
+  // host_l1post: t2frames x aux_len with every variant's L1-post cells (the CPU tests' cross-check);
+  // else one variant whose L1-post cells [AUX_L1PRE + 1840, + Lp) are left zero for the GPU
+  std::vector<cf32> aux;
+  int aux_variants = 0;
+  L1PostPlan l1;
 };
-int build_frame(const FmParams &p, FramePlan &fp);
+// host_l1post: also encode every t2_frame_num variant's L1-post on the host (tests only; the
+// product generates L1-post per frame on the GPU from fp.l1)
+int build_frame(const FmParams &p, FramePlan &fp, bool host_l1post = false);
+// fp.l1 from the parameters and fp's L1 geometry (called by build_frame)
+int build_l1post_plan(const FmParams &p, FramePlan &fp);
+// one FRAME_IDX variant's Lp L1-post cells, encoded bit by bit on the host (tests only)
+int l1post_host(const FmParams &p, const FramePlan &fp, int frame_idx, cf32 *dst);
 
 // ----------------------------------------------------------------------------- pilots + OFDM
 struct PgParams {
@@ -126,8 +164,8 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
 // LDS buffer, then writes:
 //   direct entries (bin, value): aux cells equal in every t2_frame_num variant (pilots,
 //     L1-pre, dummy cells), each group padded to a multiple of 4 with bin 0xFFFF;
-//   indirect entries bin | code << 15: the rest (L1-post), read from the per-variant aux
-//     table at abase + code (code = -cmap).
+//   indirect entries bin | code << 15: the per-frame L1-post cells, read from the frame's row of
+//     the L1 buffer at abase + code (see build_aux_lists).
 // Null bins and +0 aux values are left out (the zero fill covers them).
 struct AuxLists {
   std::vector<uint16_t> dbin;
@@ -138,8 +176,11 @@ struct AuxLists {
   // as a range; every other zero bin is a direct entry with value 0
   std::vector<int32_t> zrun;
 };
+// aux indices [l1_lo, l1_lo + l1_len) are the per-frame L1-post cells: always indirect, code = index
+// within the L1-post cells + 1 (the chain reads them from the frame's row of the L1 buffer the
+// l1post kernel writes); l1_len = 0: indirect codes are aux index + 1 into the frame's variant
 int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf32> &auxv, int aux_len,
-                    int t2frames, AuxLists &al);
+                    int t2frames, AuxLists &al, int l1_lo = 0, int l1_len = 0);
 // time-interleaver output index (frame data order) of cell-interleaved cell t of FEC block r
 int64_t ti_dest(const FramePlan &fp, int r, int t);
 

@@ -17,7 +17,7 @@ int t2probe_frame(const int *p20, int *info, int32_t *gather_in, int32_t *gather
   FmParams p{p20[0], p20[1], p20[2], p20[3], p20[4], p20[5], p20[6], p20[7], p20[8], p20[9],
              p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
   FramePlan fp;
-  if (build_frame(p, fp)) return -1;
+  if (build_frame(p, fp, true)) return -1;   // with every variant's L1-post encoded on the host
   int v[17] = {fp.M, fp.S, fp.aux_len, fp.t2frames, fp.cs, fp.F, fp.N_P2, fp.C_P2, fp.C_DATA, fp.N_FC, fp.C_FC,
                fp.Lp, fp.D, fp.ti_on, fp.ti_small, fp.ti_big, fp.ti_nsmall};
   memcpy(info, v, sizeof(v));
@@ -117,23 +117,89 @@ int t2probe_aux_lists(const int *p20, const int *pg3, int *sizes, uint16_t *dbin
              p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
   PgParams g{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
              f.preamble, pg3[0], pg3[1], pg3[2], fft_points(f.fftsize)};
-  FramePlan fp;
+  FramePlan fp, fh;
   PilotPlan pp;
   ChainLayout cl;
-  if (build_frame(f, fp) || build_pilot(g, pp) || build_chain_layout(fp, pp, cl)) return -1;
-  std::vector<cf32> auxv = fp.aux;
+  if (build_frame(f, fp) || build_frame(f, fh, true) || build_pilot(g, pp) || build_chain_layout(fp, pp, cl))
+    return -1;
+  // as t2_capi.cpp builds them: one aux row, the L1-post range per frame from the GPU
+  std::vector<cf32> row = fp.aux;
+  for (int i = 0; i < 12; i++) row[AUX_PILOT0 + i] = pp.pilot_values[i];
+  AuxLists al;
+  if (build_aux_lists(cl, pp.N, pp.Nsym, row, fp.aux_len, 1, al, AUX_L1PRE + 1840, fp.Lp)) return -2;
+  // the checker's table: every t2_frame_num variant with its host-encoded L1-post
+  std::vector<cf32> auxv = fh.aux;
   for (int v = 0; v < fp.t2frames; v++)
     for (int i = 0; i < 12; i++) auxv[(size_t)v * fp.aux_len + AUX_PILOT0 + i] = pp.pilot_values[i];
-  AuxLists al;
-  if (build_aux_lists(cl, pp.N, pp.Nsym, auxv, fp.aux_len, fp.t2frames, al)) return -2;
   sizes[0] = (int)al.dbin.size(); sizes[1] = (int)al.ind.size(); sizes[2] = (int)al.grp.size() / 4;
-  sizes[3] = fp.aux_len; sizes[4] = fp.t2frames;
+  sizes[3] = fp.aux_len; sizes[4] = fp.t2frames; sizes[5] = AUX_L1PRE + 1840;
   if (dbin) memcpy(dbin, al.dbin.data(), al.dbin.size() * 2);
   if (dval) memcpy(dval, al.dval.data(), al.dval.size() * 8);
   if (ind) memcpy(ind, al.ind.data(), al.ind.size() * 4);
   if (grp) memcpy(grp, al.grp.data(), al.grp.size() * 4);
   if (auxv_out) memcpy(auxv_out, auxv.data(), (size_t)fp.aux_len * fp.t2frames * 8);
   if (zrun) memcpy(zrun, al.zrun.data(), al.zrun.size() * 4);
+  return 0;
+}
+
+// L1-post of one FRAME_IDX: cells from the GPU plan applied on the host in the l1post kernel's
+// order of operations (plan = 1) or from the bit-by-bit host encoder (plan = 0); out: Lp complex.
+// info (optional): [nsig, npost, Lp, mode]
+int t2probe_l1post(const int *p20, int frame_idx, int plan, float *out, int *info) {
+  FmParams p{p20[0], p20[1], p20[2], p20[3], p20[4], p20[5], p20[6], p20[7], p20[8], p20[9],
+             p20[10], p20[11], p20[12], p20[13], p20[14], p20[15], p20[16], p20[17], p20[18], p20[19]};
+  FramePlan fp;
+  if (build_frame(p, fp)) return -1;
+  const L1PostPlan &l = fp.l1;
+  if (info) { info[0] = l.nsig; info[1] = l.npost; info[2] = l.lp; info[3] = l.mode; }
+  if (!out) return 0;
+  cf32 *o = (cf32 *)out;
+  if (!plan) return l1post_host(p, fp, frame_idx, o);
+  auto bit = [](const std::vector<uint32_t> &w, int i) { return (w[i >> 5] >> (31 - (i & 31))) & 1u; };
+  auto set = [](std::vector<uint32_t> &w, int i) { w[i >> 5] |= 1u << (31 - (i & 31)); };
+  std::vector<uint32_t> sig = l.tmpl;
+  const uint32_t fidx = (uint32_t)(frame_idx % fp.t2frames);
+  for (int k = 0; k < 8; k++)
+    if ((fidx >> (7 - k)) & 1u) set(sig, l.fidx_pos + k);
+  const int L = l.nsig - 32;
+  uint32_t crc = l.crc_k;
+  for (int i = 0; i < L; i++)
+    if (bit(sig, i)) crc ^= l.crc_c[i];
+  for (int k = 0; k < 32; k++)
+    if ((crc >> (31 - k)) & 1u) set(sig, L + k);
+  if (!l.scr.empty())
+    for (size_t w = 0; w < sig.size(); w++) sig[w] ^= l.scr[w];
+  std::vector<uint32_t> cw((16200 + 31) / 32, 0);
+  uint32_t b[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < l.nsig; i++)
+    if (bit(sig, i)) {
+      set(cw, l.sig_pos[i]);
+      for (int k = 0; k < 6; k++) b[k] ^= l.bch_r[(size_t)i * 6 + k];
+    }
+  for (int n = 0; n < 168; n++)
+    if ((b[n >> 5] >> (31 - (n & 31))) & 1u) set(cw, 7032 + n);
+  std::vector<uint8_t> par(l.pbits, 0);
+  for (int i = 0; i < l.nsig + 168; i++) {
+    const int pos = i < l.nsig ? (int)l.sig_pos[i] : 7032 + (i - l.nsig);
+    if (!bit(cw, pos)) continue;
+    const int g = pos / 360, n = pos % 360;
+    for (int e = l.ldpc_ptr[g]; e < l.ldpc_ptr[g + 1]; e++) par[(l.ldpc_addr[e] + n * l.q) % l.pbits] ^= 1;
+  }
+  for (int j = 1; j < l.pbits; j++) par[j] ^= par[j - 1];
+  for (int j = 0; j < l.pbits; j++)
+    if (par[j]) set(cw, 7200 + j);
+  for (int c = 0; c < l.lp; c++) {
+    if (l.mode == 0) {
+      o[c] = cf32{bit(cw, l.sel[c]) ? -1.0f : 1.0f, 0.0f};
+    } else if (l.mode == 1) {
+      o[c] = l.lut[(bit(cw, l.sel[2 * c]) << 1) | bit(cw, l.sel[2 * c + 1])];
+    } else {
+      const int k = c >> 1, half = l.ncols >> 1, e0 = (c & 1) ? half : 0;
+      uint32_t pack = 0;
+      for (int e = e0; e < e0 + half; e++) pack = (pack << 1) | bit(cw, l.sel[l.rows * l.mux[e] + k]);
+      o[c] = l.lut[pack];
+    }
+  }
   return 0;
 }
 }

@@ -89,9 +89,10 @@ class Chain:
         check(lib().dvbt2ll_chain_set_timing(self._h, int(bool(enable))), "timing")
 
     def timing(self):
-        ms = (ctypes.c_double * 3)()
-        n = (ctypes.c_int64 * 3)()
-        check(lib().dvbt2ll_chain_get_timing(self._h, ms, n, 3), "timing")
+        """accumulated HIP-event milliseconds and launch counts of the stages (fec, map, ofdm, l1post)"""
+        ms = (ctypes.c_double * 4)()
+        n = (ctypes.c_int64 * 4)()
+        check(lib().dvbt2ll_chain_get_timing(self._h, ms, n, 4), "timing")
         return list(ms), list(n)
 
     def debug_codewords(self, nblocks):

@@ -29,6 +29,7 @@ def lib():
         L.t2probe_chain.argtypes = [vp] * 9
         L.t2probe_counts.argtypes = [ctypes.c_int] * 6 + [vp]
         L.t2probe_aux_lists.argtypes = [vp] * 9
+        L.t2probe_l1post.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
         _L = L
     return _L
 
@@ -151,9 +152,9 @@ def aux_lists(cfg):
     zrun (groups: the [z0, z1) run of zero bins the kernel zeroes as a range)"""
     p = np.array(cfg.fm_args(), np.int32)
     g = np.array([cfg.misogroup, cfg.equalization, cfg.bandwidth], np.int32)
-    sz = np.zeros(5, np.int32)
+    sz = np.zeros(6, np.int32)
     assert lib().t2probe_aux_lists(_p(p), _p(g), _p(sz), None, None, None, None, None, None) == 0
-    nd, ni, ng, aux_len, t2f = (int(x) for x in sz)
+    nd, ni, ng, aux_len, t2f, l1_lo = (int(x) for x in sz)
     dbin = np.zeros(nd, np.uint16)
     dval = np.zeros(nd, np.complex64)
     ind = np.zeros(max(ni, 1), np.uint32)
@@ -163,7 +164,18 @@ def aux_lists(cfg):
     assert lib().t2probe_aux_lists(_p(p), _p(g), _p(sz), _p(dbin), _p(dval), _p(ind), _p(grp), _p(auxv),
                                    _p(zrun)) == 0
     return dict(dbin=dbin.astype(np.int64), dval=dval, ind=ind[:ni].astype(np.int64), grp=grp.reshape(ng, 4),
-                auxv=auxv.reshape(t2f, aux_len), zrun=zrun.reshape(ng, 2))
+                auxv=auxv.reshape(t2f, aux_len), zrun=zrun.reshape(ng, 2), l1_lo=l1_lo)
+
+
+def l1post(fm_args, frame_idx, plan=True):
+    """one FRAME_IDX's L1-post cells: the GPU plan applied on the host in the kernel's order
+    (plan=True) or the bit-by-bit host encoder (plan=False)"""
+    p = np.array(fm_args, np.int32)
+    info = np.zeros(4, np.int32)
+    assert lib().t2probe_l1post(_p(p), 0, 1, None, _p(info)) == 0
+    out = np.zeros(int(info[2]), np.complex64)
+    assert lib().t2probe_l1post(_p(p), int(frame_idx), int(bool(plan)), _p(out), None) == 0
+    return out
 
 
 def stored_to_natural(row, N, split):

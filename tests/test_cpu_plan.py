@@ -177,8 +177,8 @@ def test_chain_aux_lists_match_cmap(name, over):
                 assert (al["dval"][d0:d0 + dn][~real] == 0).all()
                 got[b[real]] = al["dval"][d0:d0 + dn][real]
                 np.add.at(hits, b[real], 1)
-                e = al["ind"][i0:i0 + ni]
-                got[e & 0x7FFF] = auxv[v][(e >> 15) - 1]
+                e = al["ind"][i0:i0 + ni]     # L1-post cell (e >> 15) - 1 of the frame
+                got[e & 0x7FFF] = auxv[v][al["l1_lo"] + (e >> 15) - 1]
                 np.add.at(hits, e & 0x7FFF, 1)
                 assert hits.max(initial=0) <= 1
                 assert (code[hits > 0] < 0).all()
@@ -265,3 +265,30 @@ def test_qam_tables(const, rot):
     assert np.allclose(np.abs(unrot.real), np.abs(unrot.real).round(6), atol=1e-5)
     levels = np.unique(np.round(unrot.real * np.sqrt({0: 2, 1: 10, 2: 42, 3: 170}[const]), 4))
     assert len(levels) == int(np.sqrt(n)) * (2 if const == 0 else 1) // (2 if const == 0 else 1)
+
+
+@pytest.mark.parametrize("name,over", GRID + [(n, None) for n in BENCH_CFGS],
+                         ids=[g[0] for g in GRID] + BENCH_CFGS)
+def test_l1post_plan_matches_host_encoder(name, over):
+    """the L1-post plan the GPU kernel runs (template + FRAME_IDX, CRC-32 as XOR of per-bit
+    contributions, scrambler, shortening, BCH as XOR of per-position remainders, LDPC accumulate,
+    puncturing, L1 constellation), applied on the host in the kernel's order, equals the bit-by-bit
+    host encoder (itself checked against the oracle through test_framemapper_map_matches_oracle)
+    for several FRAME_IDX values"""
+    cfg = CONFIGS[name] if over is None else grid_cfg(over)
+    for fi in sorted({0, 1, cfg.t2frames - 1, (7 * cfg.t2frames) // 11}):
+        a = PP.l1post(cfg.fm_args(), fi, plan=True)
+        b = PP.l1post(cfg.fm_args(), fi, plan=False)
+        np.testing.assert_array_equal(a.view(np.uint64), b.view(np.uint64), err_msg="FRAME_IDX %d" % fi)
+
+
+@pytest.mark.parametrize("l1c", [0, 1, 2, 3])
+@pytest.mark.parametrize("extra", [dict(), dict(version=2, l1scrambled=1, reservedbiasbits=1)], ids=["v111", "v131"])
+def test_l1post_plan_all_frame_idx(l1c, extra):
+    """t2frames = 255: every FRAME_IDX value, every L1 constellation, with and without the v1.3.1
+    L1 scrambler / bias bits"""
+    cfg = grid_cfg(dict(l1constellation=l1c, t2frames=255, **extra))
+    for fi in range(255):
+        a = PP.l1post(cfg.fm_args(), fi, plan=True)
+        b = PP.l1post(cfg.fm_args(), fi, plan=False)
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), "FRAME_IDX %d" % fi
