@@ -516,7 +516,7 @@ def main():
                     e["salu_wave_instr_per_block"] = pm.get("SQ_INSTS_SALU", 0) / nb
                     e["valu_issue_frac"] = pm["SQ_INSTS_VALU"] / t / VALU_ISSUE_PEAK
             rooflines[name] = e
-        if len(stage_ms) > 3 and launches[3]:
+        if len(stage_ms) > 3 and launches[3] and info.get("fused_fec_map"):
             stages["l1post"] = {"avg_launch_ms": stage_ms[3] / launches[3],
                                 "note": "per-frame L1-post signalling (CRC-32, BCH, LDPC, map) on the GPU"}
         dom = max((n for n in stages if n in KERNELS), key=lambda n: stages[n]["avg_launch_ms"])

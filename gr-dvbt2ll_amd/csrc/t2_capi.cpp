@@ -646,13 +646,14 @@ struct dvbt2ll_chain {
   // then OFDM.  evl, ev1, ev2 (timing): recorded after the L1-post, the FEC (+ map) and the map kernel
   hipError_t launch_chain(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, hipStream_t s,
                           hipEvent_t evl, hipEvent_t ev1, hipEvent_t ev2) {
-    hipError_t e = launch_l1post(l1.dev, lio, s);
+    // L1-post: workgroups of the map kernel's launch, or (fused FEC + map) a launch of its own
+    hipError_t e = fused ? launch_l1post(l1.dev, lio, s) : hipSuccess;
     if (e == hipSuccess && evl) e = hipEventRecord(evl, s);
     if (e == hipSuccess)
       e = fused ? launch_fec_map(fec.dev, fio, map.dev, mio.out_pairs, mio.frame_stride, s)
                 : launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, s);
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, s);
-    if (e == hipSuccess && !fused) e = launch_map(map.dev, mio, s);
+    if (e == hipSuccess && !fused) e = launch_map(map.dev, mio, s, &l1.dev, &lio);
     if (e == hipSuccess && ev2) e = hipEventRecord(ev2, s);
     if (e == hipSuccess) e = launch_ofdm(ofdm.dev, oio, s);
     return e;
@@ -664,7 +665,7 @@ struct dvbt2ll_chain {
   // under it; with several slots the calls still overlap on the device
   int graph_launch(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, int slot,
                    hipStream_t s) {
-    const int nk = fused ? 3 : 4;
+    const int nk = 3;   // fec, map (+ L1-post), ofdm; fused: l1post, fec + map, ofdm
     ChainGraph *g = nullptr;
     for (auto &c : graphs)
       if (c->nframes == nframes && c->fmt == ofdm.dev.fmt && c->slot == slot) g = c.get();
@@ -734,9 +735,9 @@ struct dvbt2ll_chain {
     int64_t fs = fused ? mio.frame_stride : 0;
     void *al[2] = {&ld, &li};
     void *a0[5] = {&fd, &fi, fused ? (void *)&md : (void *)&md0, &op, &fs};
-    void *a1[2] = {&md, &mi}, *a2[2] = {&od, &oi};
-    void **args[4] = {al, a0, a1, a2};
-    if (fused) args[2] = a2;
+    void *a1[4] = {&md, &mi, &ld, &li}, *a2[2] = {&od, &oi};
+    void **args[3] = {a0, a1, a2};
+    if (fused) { args[0] = al; args[1] = a0; }
     for (int k = 0; k < nk; k++) {
       hipKernelNodeParams p = g->base[k];
       p.kernelParams = args[k];

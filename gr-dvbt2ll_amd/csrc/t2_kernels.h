@@ -44,6 +44,29 @@ struct FecIO {
   int64_t ts_stride;
 };
 
+// ---------------------------------------------------------------- L1-post signalling (t2_plan.h L1PostPlan)
+struct L1Dev {
+  const uint32_t *tmpl;      // signal bits, FRAME_IDX and CRC zero
+  const uint32_t *crc_c;     // nsig - 32
+  const uint32_t *scr;       // L1 scrambler bits or null
+  const uint16_t *sig_pos;   // nsig
+  const uint32_t *bch_r;     // nsig x 6
+  const uint16_t *ldpc_ptr;  // 21
+  const uint16_t *ldpc_addr;
+  const uint16_t *sel;       // npost
+  const float2 *lut;         // 64 (QPSK / 16QAM / 64QAM)
+  uint32_t crc_k;
+  int nsig, fidx_pos, npost, lp, mode, ncols, rows, q, pbits, t2frames;
+  uint8_t mux[12];
+};
+struct L1IO {
+  float2 *out;               // frame f's Lp cells at out + f * out_stride
+  int64_t out_stride;
+  int64_t first_frame;       // frame f has t2_frame_num (first_frame + f % frames_per_stream) % t2frames
+  int nframes;
+  int frames_per_stream;     // 0: one stream
+};
+
 // ---------------------------------------------------------------- bit interleave + QAM + CI
 struct MapDev {
   const float2 *lut;       // 256
@@ -119,29 +142,6 @@ struct OfdmIO {
   uint32_t l1_stride;
 };
 
-// ---------------------------------------------------------------- L1-post signalling (t2_plan.h L1PostPlan)
-struct L1Dev {
-  const uint32_t *tmpl;      // signal bits, FRAME_IDX and CRC zero
-  const uint32_t *crc_c;     // nsig - 32
-  const uint32_t *scr;       // L1 scrambler bits or null
-  const uint16_t *sig_pos;   // nsig
-  const uint32_t *bch_r;     // nsig x 6
-  const uint16_t *ldpc_ptr;  // 21
-  const uint16_t *ldpc_addr;
-  const uint16_t *sel;       // npost
-  const float2 *lut;         // 64 (QPSK / 16QAM / 64QAM)
-  uint32_t crc_k;
-  int nsig, fidx_pos, npost, lp, mode, ncols, rows, q, pbits, t2frames;
-  uint8_t mux[12];
-};
-struct L1IO {
-  float2 *out;               // frame f's Lp cells at out + f * out_stride
-  int64_t out_stride;
-  int64_t first_frame;       // frame f has t2_frame_num (first_frame + f % frames_per_stream) % t2frames
-  int nframes;
-  int frames_per_stream;     // 0: one stream
-};
-
 // ---------------------------------------------------------------- frame-mapper gather
 struct GatherIO {
   const float2 *in;
@@ -157,7 +157,9 @@ hipError_t launch_fec_map(const FecDev &d, const FecIO &io, const MapDev &md, ui
                           int64_t frame_stride, hipStream_t s);
 // LDS bytes of the fused kernel for a constellation's cell size / 0 when it would not fit
 int fec_map_lds(int cs, int nldpc);
-hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s);
+// l1d / l1io (optional, the chain): the frames' L1-post cells by extra workgroups of the same launch
+hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1Dev *l1d = nullptr,
+                      const L1IO *l1io = nullptr);
 hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s);
 hipError_t launch_gather(const GatherIO &io, hipStream_t s);
 hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s);

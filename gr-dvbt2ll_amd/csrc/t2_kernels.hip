@@ -963,10 +963,167 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   }
 }
 
-__global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
+// ============================================================================ L1-post
+// One 256-thread workgroup per T2 frame of the launch: that frame's L1-post cells
+// (framemapper:1536-1910) from the t2_plan L1PostPlan.  The codeword lives in LDS as 16200 bits
+// packed MSB first: information bits 0..7031 (shortened positions zero), BCH parity 7032..7199,
+// LDPC parity 7200..16199 (word-aligned at word 225).
+constexpr int L1_NT = 256, L1_CW_WORDS = (16200 + 31) / 32, L1_SIG_WORDS = 16;
+
+__device__ __forceinline__ uint32_t l1_bit(const uint32_t *w, int i) { return (w[i >> 5] >> (31 - (i & 31))) & 1u; }
+
+// XOR of v over the workgroup (every thread gets the result); red: L1_NT / 64 words of LDS
+__device__ __forceinline__ uint32_t l1_xor_all(uint32_t v, uint32_t *red, int tid) {
+  v = rd_lane_u32(wave_prefix_xor(v), 63);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+#pragma unroll
+  for (int k = 0; k < L1_NT / 64; k++) t ^= red[k];
+  return t;
+}
+
+// LDS words the L1-post of one frame needs (codeword, signal bits, reduction scratch)
+constexpr int L1_LDS_WORDS = L1_CW_WORDS + L1_SIG_WORDS + L1_NT / 64 * 6;
+
+// frame f's L1-post cells by one 256-thread workgroup; lds: L1_LDS_WORDS words
+__device__ void l1post_frame(const L1Dev &d, const L1IO &io, int f, uint32_t *lds) {
+  uint32_t *cw = lds, *sig = lds + L1_CW_WORDS, *red = sig + L1_SIG_WORDS;
+  const int tid = threadIdx.x;
+  const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);
+  const uint32_t fidx = (uint32_t)(frame % d.t2frames);   // FRAME_IDX = t2_frame_num (:1648-1651)
+  const int nsw = (d.nsig + 31) >> 5, L = d.nsig - 32;
+  for (int w = tid; w < L1_CW_WORDS; w += L1_NT) cw[w] = 0;
+  // signal bits: the template with this frame's FRAME_IDX (8 bits, MSB first, at fidx_pos)
+  if (tid < nsw) {
+    uint32_t v = d.tmpl[tid];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int p = d.fidx_pos + k;
+      if ((p >> 5) == tid && ((fidx >> (7 - k)) & 1u)) v |= 1u << (31 - (p & 31));
+    }
+    sig[tid] = v;
+  }
+  __syncthreads();
+  // CRC-32 (:1203-1224) over the first L bits: crc_k ^ XOR of the set bits' contributions
+  uint32_t c = 0;
+  for (int i = tid; i < L; i += L1_NT)
+    if (l1_bit(sig, i)) c ^= d.crc_c[i];
+  const uint32_t crc = d.crc_k ^ l1_xor_all(c, red, tid);
+  if (tid < 32 && ((crc >> (31 - tid)) & 1u)) atomicOr(&sig[(L + tid) >> 5], 1u << (31 - ((L + tid) & 31)));
+  __syncthreads();
+  if (d.scr && tid < nsw) sig[tid] ^= d.scr[tid];   // L1 scrambler (:1928-1940), v1.3.1
+  __syncthreads();
+  // shortening: signal bit i -> information position sig_pos[i]; BCH(168) parity = XOR of the
+  // per-position remainders of the set bits (6 words, parity bit n at word n / 32, MSB first)
+  uint32_t b[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = tid; i < d.nsig; i += L1_NT) {
+    if (!l1_bit(sig, i)) continue;
+    const int pos = d.sig_pos[i];
+    atomicOr(&cw[pos >> 5], 1u << (31 - (pos & 31)));
+#pragma unroll
+    for (int k = 0; k < 6; k++) b[k] ^= d.bch_r[i * 6 + k];
+  }
+#pragma unroll
+  for (int k = 0; k < 6; k++) b[k] = rd_lane_u32(wave_prefix_xor(b[k]), 63);
+  if ((tid & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 6; k++) red[(tid >> 6) * 6 + k] = b[k];
+  __syncthreads();
+  if (tid < 168) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int r = 0; r < L1_NT / 64; r++) w ^= red[r * 6 + (tid >> 5)];
+    if ((w >> (31 - (tid & 31))) & 1u) {
+      const int pos = 7032 + tid;
+      atomicOr(&cw[pos >> 5], 1u << (31 - (pos & 31)));
+    }
+  }
+  __syncthreads();
+  // LDPC (:1314-1364): information bit 360 g + n feeds parity (x + n q) mod pbits for each address x
+  // of group g; only the signal positions and the BCH parity can be set
+  uint32_t *par = cw + 225;
+  for (int i = tid; i < d.nsig + 168; i += L1_NT) {
+    const int pos = i < d.nsig ? (int)d.sig_pos[i] : 7032 + (i - d.nsig);
+    if (!l1_bit(cw, pos)) continue;
+    const int g = pos / 360, n = pos - 360 * g;
+    for (int e = d.ldpc_ptr[g]; e < d.ldpc_ptr[g + 1]; e++) {
+      const int j = (d.ldpc_addr[e] + n * d.q) % d.pbits;
+      atomicXor(&par[j >> 5], 1u << (31 - (j & 31)));
+    }
+  }
+  __syncthreads();
+  // accumulate p[j] ^= p[j - 1]: inclusive prefix XOR within each word (from the MSB), then the
+  // exclusive prefix of the word parities over the wave, five words per lane
+  if (tid < 64) {
+    const int nwp = (d.pbits + 31) >> 5, per = (nwp + 63) / 64;
+    uint32_t x[5], par_l = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const int w = tid * per + k;
+      uint32_t v = (k < per && w < nwp) ? par[w] : 0u;
+      v ^= v >> 1; v ^= v >> 2; v ^= v >> 4; v ^= v >> 8; v ^= v >> 16;
+      x[k] = v;
+      par_l ^= v & 1u;   // the word's total parity sits in its last bit
+    }
+    const uint32_t before = wave_prefix_xor(par_l) ^ par_l;
+    uint32_t carry = before;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+      const int w = tid * per + k;
+      if (k < per && w < nwp) par[w] = carry ? ~x[k] : x[k];
+      carry ^= x[k] & 1u;
+    }
+  }
+  __syncthreads();
+  // puncture / select the N_post transmitted bits and map them (BPSK, QPSK, or the 16/64QAM column
+  // interleaver + demux, :1832-1908)
+  float2 *out = io.out + (int64_t)f * io.out_stride;
+  for (int cidx = tid; cidx < d.lp; cidx += L1_NT) {
+    float2 v;
+    if (d.mode == 0) {
+      v = make_float2(l1_bit(cw, d.sel[cidx]) ? -1.0f : 1.0f, 0.0f);
+    } else if (d.mode == 1) {
+      v = d.lut[(l1_bit(cw, d.sel[2 * cidx]) << 1) | l1_bit(cw, d.sel[2 * cidx + 1])];
+    } else {
+      const int k = cidx >> 1, half = d.ncols >> 1, e0 = (cidx & 1) ? half : 0;
+      uint32_t pack = 0;
+      for (int e = e0; e < e0 + half; e++) pack = (pack << 1) | l1_bit(cw, d.sel[d.rows * d.mux[e] + k]);
+      v = d.lut[pack];
+    }
+    out[cidx] = v;
+  }
+}
+
+__global__ __launch_bounds__(L1_NT) void l1post_kernel(L1Dev d, L1IO io) {
+  __shared__ uint32_t lds[L1_LDS_WORDS];
+  l1post_frame(d, io, blockIdx.x, lds);
+}
+
+static bool l1_args_ok(const L1Dev &d) {
+  return d.nsig <= 32 * L1_SIG_WORDS && d.nsig >= 33 && d.pbits == 9000 && d.q > 0 && d.t2frames > 0;
+}
+
+hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s) {
+  if (io.nframes <= 0) return hipSuccess;
+  if (!l1_args_ok(d)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(l1post_kernel, dim3(io.nframes), dim3(L1_NT), 0, s, d, io);
+  return hipGetLastError();
+}
+
+// The chain's launches prepend ceil8(L1 frames) workgroups that generate the frames' L1-post cells
+// (they run beside the map workgroups instead of as a launch of their own; a multiple of 8 keeps
+// each map workgroup's XCD)
+__global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io, L1Dev l1d, L1IO l1io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
-  const int blk = xcd_major(blockIdx.x, gridDim.x);
+  const int nl1 = (l1io.nframes + 7) & ~7;
+  if ((int)blockIdx.x < nl1) {
+    if ((int)blockIdx.x < l1io.nframes) l1post_frame(l1d, l1io, blockIdx.x, (uint32_t *)smem);
+    return;
+  }
+  const int blk = xcd_major((int)blockIdx.x - nl1, (int)gridDim.x - nl1);
   float2 *lut = (float2 *)smem;
   uint8_t *idx = smem + 2048;
   uint8_t *cw = smem + 2048 + map_idx_bytes(d.cs);
@@ -1019,13 +1176,22 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
   map_store_pairs<MAP_THREADS>(d, io.out_pairs, io.frame_stride, idx, stage, blk, tid);
 }
 
-hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {
+hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1Dev *l1d, const L1IO *l1io) {
   if (io.nblocks <= 0) return hipSuccess;
   int smem = map_smem(d.cs, d.nldpc / 8 + 4, io.apply_ci);
+  L1Dev ld{};
+  L1IO li{};
+  if (l1d && l1io && l1io->nframes > 0) {
+    if (!l1_args_ok(*l1d)) return hipErrorInvalidValue;
+    ld = *l1d;
+    li = *l1io;
+    smem = smem > L1_LDS_WORDS * 4 ? smem : L1_LDS_WORDS * 4;
+  }
   if (smem > MAP_LDS_MAX) return hipErrorInvalidValue;
   hipError_t e = lds_limit((const void *)map_kernel, MAP_LDS_MAX);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(map_kernel, dim3(io.nblocks), dim3(MAP_THREADS), smem, s, d, io);
+  const int nl1 = (li.nframes + 7) & ~7;
+  hipLaunchKernelGGL(map_kernel, dim3(io.nblocks + nl1), dim3(MAP_THREADS), smem, s, d, io, ld, li);
   return hipGetLastError();
 }
 
@@ -1529,11 +1695,13 @@ constexpr int O32_TW2 = O32_TW1K + 1024 * 8;                      // two-level t
 constexpr int O32_QAM = O32_TW2 + 384 * 8;                        // constellation re[256], im[256]
 constexpr int O32_LDS = O32_QAM + 256 * 8;
 static_assert(O32_LDS <= 160 * 1024, "32K OFDM LDS");
+static_assert((16384 + 2 * 32) * 8 <= O32_DATA, "exchange slots fit the data area");
 
 // bins within a half as the scatter stores them (one pad slot per 32, t2_kernels.h)
 __device__ __forceinline__ uint32_t o32_bin(uint32_t k) { return k + (k >> O32_PS); }
-// exchange slots: one pad per 512 (stride-512 lane patterns spread over the banks)
-__device__ __forceinline__ uint32_t o32_x(uint32_t e) { return e + (e >> 9); }
+// exchange slots: two pad slots per 512 (stride-512 lane patterns spread over the banks, and even
+// slots stay 16-byte aligned so exchange 1 reads its value pairs as ds_read_b128)
+__device__ __forceinline__ uint32_t o32_x(uint32_t e) { return e + 2u * (e >> 9); }
 
 // v[r] *= w^(e r) for r = 1..31 from the seven table values w^(e k) (k = 1, 2, 3, 4, 8, 12, 16):
 // r = 16 t + 4 h + l -> top^t hi[h] lo[l]
@@ -1549,6 +1717,87 @@ __device__ __forceinline__ void o32_twiddle(float2 *v, const Lookup &tw) {
     float2 w = h == 0 ? lo[l] : (l == 0 ? hi[h] : cmulf(hi[h], lo[l]));
     if (t) w = (h == 0 && l == 0) ? top : cmulf(top, w);
     v[r] = cmulf(v[r], w);
+  }
+}
+
+// Scatter inputs of one half (group), loaded into registers ahead of time: the first aux quad and
+// the first four data quads of each thread (a 32K half has at most 16384 data slots = 4096 quads
+// + 1 for the run's misalignment, and typically < 1024 aux quads); the rest, and the indirect
+// L1-post entries, are loaded when written (o32_put).  Both halves are prefetched before the
+// first is written, so their global-load latencies overlap instead of adding up.
+struct O32Pre {
+  uint2 ab;
+  float4 av0, av1;
+  uint2 b[4], c[4];
+};
+__device__ __forceinline__ void o32_prefetch(O32Pre &p, const BinSource &src, int h, uint32_t r0, uint32_t rn,
+                                             uint32_t tid) {
+  constexpr uint32_t NT = 1024;
+  const int4 gr = src.agrp[h];
+  const uint32_t naq = (uint32_t)gr.y >> 2;
+  // (the aux lists end with four padding entries, so quad gr.x is readable even when naq = 0)
+  const uint32_t e0 = (uint32_t)gr.x + 4u * (tid < naq ? tid : 0u);
+  p.ab = ld_off((const uint2 *)src.abin, e0 * 2u);
+  p.av0 = ld_off((const float4 *)src.aval, e0 * 8u);
+  p.av1 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
+  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const uint32_t g = tid + NT * (uint32_t)u;
+    const uint32_t s = q0 + 4u * (g < nq ? g : 0u);
+    p.b[u] = ld_off((const uint2 *)src.inv, s * 2u);
+    p.c[u] = ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u);
+  }
+}
+__device__ __forceinline__ void o32_put_quad(float2 *lds, const BinSource &src, uint2 b, uint2 c, uint32_t s,
+                                             uint32_t r0, uint32_t rn, uint32_t dummy) {
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const uint32_t bw = e < 2 ? b.x : b.y, cw = e < 2 ? c.x : c.y;
+    const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;
+    const uint32_t pr = cw >> (16 * (e & 1));
+    const bool in_run = s + (uint32_t)e - r0 < rn;
+    lds[in_run ? bin : dummy] = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+  }
+}
+// write one group from its prefetched registers (+ the remainder loads), every bin exactly once
+__device__ __forceinline__ void o32_put(float2 *lds, const BinSource &src, const O32Pre &p, int h, uint32_t r0,
+                                        uint32_t rn, uint32_t dummy, uint32_t tid) {
+  constexpr uint32_t NT = 1024;
+  const int4 gr = src.agrp[h];
+  const uint32_t naq = (uint32_t)gr.y >> 2;
+  if (tid < naq) {
+    const uint32_t k0 = p.ab.x & 0xFFFFu, k1 = p.ab.x >> 16, k2 = p.ab.y & 0xFFFFu, k3 = p.ab.y >> 16;
+    lds[k0 != 0xFFFFu ? k0 : dummy] = make_float2(p.av0.x, p.av0.y);
+    lds[k1 != 0xFFFFu ? k1 : dummy] = make_float2(p.av0.z, p.av0.w);
+    lds[k2 != 0xFFFFu ? k2 : dummy] = make_float2(p.av1.x, p.av1.y);
+    lds[k3 != 0xFFFFu ? k3 : dummy] = make_float2(p.av1.z, p.av1.w);
+  }
+  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const uint32_t g = tid + NT * (uint32_t)u;
+    if (g < nq) o32_put_quad(lds, src, p.b[u], p.c[u], q0 + 4u * g, r0, rn, dummy);
+  }
+  for (uint32_t q = tid + NT; q < naq; q += NT) {      // aux quads past the first per thread
+    const uint32_t e0 = (uint32_t)gr.x + 4u * q;
+    const uint2 b = ld_off((const uint2 *)src.abin, e0 * 2u);
+    const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
+    const float4 v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
+    const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
+    lds[k0 != 0xFFFFu ? k0 : dummy] = make_float2(v01.x, v01.y);
+    lds[k1 != 0xFFFFu ? k1 : dummy] = make_float2(v01.z, v01.w);
+    lds[k2 != 0xFFFFu ? k2 : dummy] = make_float2(v23.x, v23.y);
+    lds[k3 != 0xFFFFu ? k3 : dummy] = make_float2(v23.z, v23.w);
+  }
+  for (uint32_t g = tid + 4u * NT; g < nq; g += NT) {   // data quads past the fourth per thread
+    const uint32_t s = q0 + 4u * g;
+    o32_put_quad(lds, src, ld_off((const uint2 *)src.inv, s * 2u), ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u),
+                 s, r0, rn, dummy);
+  }
+  for (uint32_t i = tid; i < (uint32_t)gr.w; i += NT) {   // per-frame L1-post cells (P2 symbols)
+    const uint32_t e = src.aind[(uint32_t)gr.z + i];
+    lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
   }
 }
 
@@ -1573,11 +1822,23 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
     }
     __syncthreads();
     if (mine) {
+      if (SPLIT == 8) {
+        // values r, r + 1 are adjacent, 16-byte aligned slots: one ds_read_b128 per pair (lanes
+        // b = 0..15 at a stride of 514 slots cover the 64 banks; the compiler would otherwise pair
+        // the 8-byte reads into ds_read2_b64, at half the LDS rate)
 #pragma unroll
-      for (uint32_t r = 0; r < 32; r++) {
-        const uint32_t e = SPLIT == 8 ? (r & 15u) + 16u * (a & 15u) + 256u * (r >> 4) + 512u * b
-                                      : (b & 15u) + 16u * (a & 15u) + 256u * (a >> 4) + 512u * r;
-        v[r] = lds[o32_x(e)];
+        for (uint32_t r = 0; r < 32; r += 2) {
+          const uint32_t e = (r & 15u) + 16u * (a & 15u) + 256u * (r >> 4) + 512u * b;
+          const float4 q = *(const float4 *)(lds + o32_x(e));
+          v[r] = make_float2(q.x, q.y);
+          v[r + 1] = make_float2(q.z, q.w);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t r = 0; r < 32; r++) {
+          const uint32_t e = (b & 15u) + 16u * (a & 15u) + 256u * (a >> 4) + 512u * r;
+          v[r] = lds[o32_x(e)];
+        }
       }
     }
   }
@@ -1674,6 +1935,10 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv, io.pairs, qre, qim, (uint32_t)d.sym_d0[j], (uint32_t)d.sym_n[j],
                   (uint32_t)d.sym_n0[j], d.abin, d.aval, d.aind, d.agrp + 2 * j, d.azr + 2 * j};
     const uint32_t dummy = (uint32_t)(O32_H + (O32_H >> O32_PS)) + (uint32_t)(tid & 63);
+    const uint32_t r00 = src.d0, rn0 = src.dn0, r01 = src.d0 + src.dn0, rn1 = src.dn - src.dn0;
+    O32Pre p0, p1;
+    o32_prefetch(p0, src, 0, r00, rn0, (uint32_t)tid);
+    o32_prefetch(p1, src, 1, r01, rn1, (uint32_t)tid);
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       if (h) __syncthreads();                     // half 0 read back before half 1 overwrites it
@@ -1686,8 +1951,8 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
         }
         __syncthreads();                          // constellation visible to the scatter
       }
-      const uint32_t r0 = src.d0 + (h ? src.dn0 : 0u), rn = h ? src.dn - src.dn0 : src.dn0;
-      scatter_group<NT, 4>(lds, src, h, r0, rn, dummy, tid);
+      if (h == 0) o32_put(lds, src, p0, 0, r00, rn0, dummy, (uint32_t)tid);
+      else o32_put(lds, src, p1, 1, r01, rn1, dummy, (uint32_t)tid);
       __syncthreads();
       if (h == 0) OFDM_PHASE(1);
 #pragma unroll
@@ -1763,144 +2028,6 @@ hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
     case 32768: return launch_ofdm_t<32768>(d, io, s);
     default: return hipErrorInvalidValue;
   }
-}
-
-// ============================================================================ L1-post
-// One 256-thread workgroup per T2 frame of the launch: that frame's L1-post cells
-// (framemapper:1536-1910) from the t2_plan L1PostPlan.  The codeword lives in LDS as 16200 bits
-// packed MSB first: information bits 0..7031 (shortened positions zero), BCH parity 7032..7199,
-// LDPC parity 7200..16199 (word-aligned at word 225).
-constexpr int L1_NT = 256, L1_CW_WORDS = (16200 + 31) / 32, L1_SIG_WORDS = 16;
-
-__device__ __forceinline__ uint32_t l1_bit(const uint32_t *w, int i) { return (w[i >> 5] >> (31 - (i & 31))) & 1u; }
-
-// XOR of v over the workgroup (every thread gets the result); red: L1_NT / 64 words of LDS
-__device__ __forceinline__ uint32_t l1_xor_all(uint32_t v, uint32_t *red, int tid) {
-  v = rd_lane_u32(wave_prefix_xor(v), 63);
-  __syncthreads();
-  if ((tid & 63) == 0) red[tid >> 6] = v;
-  __syncthreads();
-  uint32_t t = 0;
-#pragma unroll
-  for (int k = 0; k < L1_NT / 64; k++) t ^= red[k];
-  return t;
-}
-
-__global__ __launch_bounds__(L1_NT) void l1post_kernel(L1Dev d, L1IO io) {
-  __shared__ uint32_t cw[L1_CW_WORDS];
-  __shared__ uint32_t sig[L1_SIG_WORDS];
-  __shared__ uint32_t red[L1_NT / 64 * 6];
-  const int tid = threadIdx.x, f = blockIdx.x;
-  const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);
-  const uint32_t fidx = (uint32_t)(frame % d.t2frames);   // FRAME_IDX = t2_frame_num (:1648-1651)
-  const int nsw = (d.nsig + 31) >> 5, L = d.nsig - 32;
-  for (int w = tid; w < L1_CW_WORDS; w += L1_NT) cw[w] = 0;
-  // signal bits: the template with this frame's FRAME_IDX (8 bits, MSB first, at fidx_pos)
-  if (tid < nsw) {
-    uint32_t v = d.tmpl[tid];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const int p = d.fidx_pos + k;
-      if ((p >> 5) == tid && ((fidx >> (7 - k)) & 1u)) v |= 1u << (31 - (p & 31));
-    }
-    sig[tid] = v;
-  }
-  __syncthreads();
-  // CRC-32 (:1203-1224) over the first L bits: crc_k ^ XOR of the set bits' contributions
-  uint32_t c = 0;
-  for (int i = tid; i < L; i += L1_NT)
-    if (l1_bit(sig, i)) c ^= d.crc_c[i];
-  const uint32_t crc = d.crc_k ^ l1_xor_all(c, red, tid);
-  if (tid < 32 && ((crc >> (31 - tid)) & 1u)) atomicOr(&sig[(L + tid) >> 5], 1u << (31 - ((L + tid) & 31)));
-  __syncthreads();
-  if (d.scr && tid < nsw) sig[tid] ^= d.scr[tid];   // L1 scrambler (:1928-1940), v1.3.1
-  __syncthreads();
-  // shortening: signal bit i -> information position sig_pos[i]; BCH(168) parity = XOR of the
-  // per-position remainders of the set bits (6 words, parity bit n at word n / 32, MSB first)
-  uint32_t b[6] = {0, 0, 0, 0, 0, 0};
-  for (int i = tid; i < d.nsig; i += L1_NT) {
-    if (!l1_bit(sig, i)) continue;
-    const int pos = d.sig_pos[i];
-    atomicOr(&cw[pos >> 5], 1u << (31 - (pos & 31)));
-#pragma unroll
-    for (int k = 0; k < 6; k++) b[k] ^= d.bch_r[i * 6 + k];
-  }
-#pragma unroll
-  for (int k = 0; k < 6; k++) b[k] = rd_lane_u32(wave_prefix_xor(b[k]), 63);
-  if ((tid & 63) == 0)
-#pragma unroll
-    for (int k = 0; k < 6; k++) red[(tid >> 6) * 6 + k] = b[k];
-  __syncthreads();
-  if (tid < 168) {
-    uint32_t w = 0;
-#pragma unroll
-    for (int r = 0; r < L1_NT / 64; r++) w ^= red[r * 6 + (tid >> 5)];
-    if ((w >> (31 - (tid & 31))) & 1u) {
-      const int pos = 7032 + tid;
-      atomicOr(&cw[pos >> 5], 1u << (31 - (pos & 31)));
-    }
-  }
-  __syncthreads();
-  // LDPC (:1314-1364): information bit 360 g + n feeds parity (x + n q) mod pbits for each address x
-  // of group g; only the signal positions and the BCH parity can be set
-  uint32_t *par = cw + 225;
-  for (int i = tid; i < d.nsig + 168; i += L1_NT) {
-    const int pos = i < d.nsig ? (int)d.sig_pos[i] : 7032 + (i - d.nsig);
-    if (!l1_bit(cw, pos)) continue;
-    const int g = pos / 360, n = pos - 360 * g;
-    for (int e = d.ldpc_ptr[g]; e < d.ldpc_ptr[g + 1]; e++) {
-      const int j = (d.ldpc_addr[e] + n * d.q) % d.pbits;
-      atomicXor(&par[j >> 5], 1u << (31 - (j & 31)));
-    }
-  }
-  __syncthreads();
-  // accumulate p[j] ^= p[j - 1]: inclusive prefix XOR within each word (from the MSB), then the
-  // exclusive prefix of the word parities over the wave, five words per lane
-  if (tid < 64) {
-    const int nwp = (d.pbits + 31) >> 5, per = (nwp + 63) / 64;
-    uint32_t x[5], par_l = 0;
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      const int w = tid * per + k;
-      uint32_t v = (k < per && w < nwp) ? par[w] : 0u;
-      v ^= v >> 1; v ^= v >> 2; v ^= v >> 4; v ^= v >> 8; v ^= v >> 16;
-      x[k] = v;
-      par_l ^= v & 1u;   // the word's total parity sits in its last bit
-    }
-    const uint32_t before = wave_prefix_xor(par_l) ^ par_l;
-    uint32_t carry = before;
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-      const int w = tid * per + k;
-      if (k < per && w < nwp) par[w] = carry ? ~x[k] : x[k];
-      carry ^= x[k] & 1u;
-    }
-  }
-  __syncthreads();
-  // puncture / select the N_post transmitted bits and map them (BPSK, QPSK, or the 16/64QAM column
-  // interleaver + demux, :1832-1908)
-  float2 *out = io.out + (int64_t)f * io.out_stride;
-  for (int cidx = tid; cidx < d.lp; cidx += L1_NT) {
-    float2 v;
-    if (d.mode == 0) {
-      v = make_float2(l1_bit(cw, d.sel[cidx]) ? -1.0f : 1.0f, 0.0f);
-    } else if (d.mode == 1) {
-      v = d.lut[(l1_bit(cw, d.sel[2 * cidx]) << 1) | l1_bit(cw, d.sel[2 * cidx + 1])];
-    } else {
-      const int k = cidx >> 1, half = d.ncols >> 1, e0 = (cidx & 1) ? half : 0;
-      uint32_t pack = 0;
-      for (int e = e0; e < e0 + half; e++) pack = (pack << 1) | l1_bit(cw, d.sel[d.rows * d.mux[e] + k]);
-      v = d.lut[pack];
-    }
-    out[cidx] = v;
-  }
-}
-
-hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s) {
-  if (io.nframes <= 0) return hipSuccess;
-  if (d.nsig > 32 * L1_SIG_WORDS || d.nsig < 33 || d.pbits != 9000 || d.q <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(l1post_kernel, dim3(io.nframes), dim3(L1_NT), 0, s, d, io);
-  return hipGetLastError();
 }
 
 // ============================================================================ gather

@@ -214,7 +214,9 @@ int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, in
 int dvbt2ll_chain_set_output(dvbt2ll_chain *h, float gain, int format);
 /* per-stage kernel timing with HIP events on the launch stream: enable, then read the
  * accumulated milliseconds and launch counts of stages {0: fec (+ map when fused), 1: map, 2: ofdm,
- * 3: l1post (the frames' L1-post signalling, generated on the GPU per run)}; nstages <= 4. */
+ * 3: l1post}; nstages <= 4.  The frames' L1-post signalling is generated on the GPU every run: by
+ * extra workgroups of the map launch (counted in stage 1; stage 3 then times an empty interval), or,
+ * with the fused FEC + map kernel, by a launch of its own (stage 3). */
 int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable);
 int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages);
 /* test hooks (host outputs, synchronous), last run's frame 0: packed codewords (tempu
