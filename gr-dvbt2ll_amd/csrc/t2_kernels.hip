@@ -1701,7 +1701,10 @@ static_assert((16384 + 2 * 32) * 8 <= O32_DATA, "exchange slots fit the data are
 __device__ __forceinline__ uint32_t o32_bin(uint32_t k) { return k + (k >> O32_PS); }
 // exchange slots: two pad slots per 512 (stride-512 lane patterns spread over the banks, and even
 // slots stay 16-byte aligned so exchange 1 reads its value pairs as ds_read_b128)
-__device__ __forceinline__ uint32_t o32_x(uint32_t e) { return e + 2u * (e >> 9); }
+#ifndef O32_X2PAD
+#define O32_X2PAD 1   // experiment switch: 0 = one pad slot per 512 and 8-byte exchange-1 reads
+#endif
+__device__ __forceinline__ uint32_t o32_x(uint32_t e) { return e + (O32_X2PAD ? 2u : 1u) * (e >> 9); }
 
 // v[r] *= w^(e r) for r = 1..31 from the seven table values w^(e k) (k = 1, 2, 3, 4, 8, 12, 16):
 // r = 16 t + 4 h + l -> top^t hi[h] lo[l]
@@ -1717,87 +1720,6 @@ __device__ __forceinline__ void o32_twiddle(float2 *v, const Lookup &tw) {
     float2 w = h == 0 ? lo[l] : (l == 0 ? hi[h] : cmulf(hi[h], lo[l]));
     if (t) w = (h == 0 && l == 0) ? top : cmulf(top, w);
     v[r] = cmulf(v[r], w);
-  }
-}
-
-// Scatter inputs of one half (group), loaded into registers ahead of time: the first aux quad and
-// the first four data quads of each thread (a 32K half has at most 16384 data slots = 4096 quads
-// + 1 for the run's misalignment, and typically < 1024 aux quads); the rest, and the indirect
-// L1-post entries, are loaded when written (o32_put).  Both halves are prefetched before the
-// first is written, so their global-load latencies overlap instead of adding up.
-struct O32Pre {
-  uint2 ab;
-  float4 av0, av1;
-  uint2 b[4], c[4];
-};
-__device__ __forceinline__ void o32_prefetch(O32Pre &p, const BinSource &src, int h, uint32_t r0, uint32_t rn,
-                                             uint32_t tid) {
-  constexpr uint32_t NT = 1024;
-  const int4 gr = src.agrp[h];
-  const uint32_t naq = (uint32_t)gr.y >> 2;
-  // (the aux lists end with four padding entries, so quad gr.x is readable even when naq = 0)
-  const uint32_t e0 = (uint32_t)gr.x + 4u * (tid < naq ? tid : 0u);
-  p.ab = ld_off((const uint2 *)src.abin, e0 * 2u);
-  p.av0 = ld_off((const float4 *)src.aval, e0 * 8u);
-  p.av1 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
-  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
-#pragma unroll
-  for (int u = 0; u < 4; u++) {
-    const uint32_t g = tid + NT * (uint32_t)u;
-    const uint32_t s = q0 + 4u * (g < nq ? g : 0u);
-    p.b[u] = ld_off((const uint2 *)src.inv, s * 2u);
-    p.c[u] = ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u);
-  }
-}
-__device__ __forceinline__ void o32_put_quad(float2 *lds, const BinSource &src, uint2 b, uint2 c, uint32_t s,
-                                             uint32_t r0, uint32_t rn, uint32_t dummy) {
-#pragma unroll
-  for (int e = 0; e < 4; e++) {
-    const uint32_t bw = e < 2 ? b.x : b.y, cw = e < 2 ? c.x : c.y;
-    const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;
-    const uint32_t pr = cw >> (16 * (e & 1));
-    const bool in_run = s + (uint32_t)e - r0 < rn;
-    lds[in_run ? bin : dummy] = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-  }
-}
-// write one group from its prefetched registers (+ the remainder loads), every bin exactly once
-__device__ __forceinline__ void o32_put(float2 *lds, const BinSource &src, const O32Pre &p, int h, uint32_t r0,
-                                        uint32_t rn, uint32_t dummy, uint32_t tid) {
-  constexpr uint32_t NT = 1024;
-  const int4 gr = src.agrp[h];
-  const uint32_t naq = (uint32_t)gr.y >> 2;
-  if (tid < naq) {
-    const uint32_t k0 = p.ab.x & 0xFFFFu, k1 = p.ab.x >> 16, k2 = p.ab.y & 0xFFFFu, k3 = p.ab.y >> 16;
-    lds[k0 != 0xFFFFu ? k0 : dummy] = make_float2(p.av0.x, p.av0.y);
-    lds[k1 != 0xFFFFu ? k1 : dummy] = make_float2(p.av0.z, p.av0.w);
-    lds[k2 != 0xFFFFu ? k2 : dummy] = make_float2(p.av1.x, p.av1.y);
-    lds[k3 != 0xFFFFu ? k3 : dummy] = make_float2(p.av1.z, p.av1.w);
-  }
-  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
-#pragma unroll
-  for (int u = 0; u < 4; u++) {
-    const uint32_t g = tid + NT * (uint32_t)u;
-    if (g < nq) o32_put_quad(lds, src, p.b[u], p.c[u], q0 + 4u * g, r0, rn, dummy);
-  }
-  for (uint32_t q = tid + NT; q < naq; q += NT) {      // aux quads past the first per thread
-    const uint32_t e0 = (uint32_t)gr.x + 4u * q;
-    const uint2 b = ld_off((const uint2 *)src.abin, e0 * 2u);
-    const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
-    const float4 v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
-    const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
-    lds[k0 != 0xFFFFu ? k0 : dummy] = make_float2(v01.x, v01.y);
-    lds[k1 != 0xFFFFu ? k1 : dummy] = make_float2(v01.z, v01.w);
-    lds[k2 != 0xFFFFu ? k2 : dummy] = make_float2(v23.x, v23.y);
-    lds[k3 != 0xFFFFu ? k3 : dummy] = make_float2(v23.z, v23.w);
-  }
-  for (uint32_t g = tid + 4u * NT; g < nq; g += NT) {   // data quads past the fourth per thread
-    const uint32_t s = q0 + 4u * g;
-    o32_put_quad(lds, src, ld_off((const uint2 *)src.inv, s * 2u), ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u),
-                 s, r0, rn, dummy);
-  }
-  for (uint32_t i = tid; i < (uint32_t)gr.w; i += NT) {   // per-frame L1-post cells (P2 symbols)
-    const uint32_t e = src.aind[(uint32_t)gr.z + i];
-    lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
   }
 }
 
@@ -1822,7 +1744,7 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
     }
     __syncthreads();
     if (mine) {
-      if (SPLIT == 8) {
+      if (SPLIT == 8 && O32_X2PAD) {
         // values r, r + 1 are adjacent, 16-byte aligned slots: one ds_read_b128 per pair (lanes
         // b = 0..15 at a stride of 514 slots cover the 64 banks; the compiler would otherwise pair
         // the 8-byte reads into ds_read2_b64, at half the LDS rate)
@@ -1836,7 +1758,8 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
       } else {
 #pragma unroll
         for (uint32_t r = 0; r < 32; r++) {
-          const uint32_t e = (b & 15u) + 16u * (a & 15u) + 256u * (a >> 4) + 512u * r;
+          const uint32_t e = SPLIT == 8 ? (r & 15u) + 16u * (a & 15u) + 256u * (r >> 4) + 512u * b
+                                        : (b & 15u) + 16u * (a & 15u) + 256u * (a >> 4) + 512u * r;
           v[r] = lds[o32_x(e)];
         }
       }
@@ -1925,8 +1848,9 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     for (int i = tid; i < 2048; i += NT) p.put((uint32_t)i, d.p1[i]);
   }
   OFDM_PHASE(0);
-  tw1k[tid] = d.twiddle1k[tid];
-  if (tid < 384) tw2[tid] = d.twiddle[tid];
+  // twiddle tables: loaded here, stored to LDS once the scatter inputs are in flight
+  const float2 t1k = d.twiddle1k[tid];
+  const float2 t2 = tid < 384 ? d.twiddle[tid] : make_float2(0.f, 0.f);
   float2 v[32];
   if (d.inv) {
     // scatter mode, one half of the bins (m2 < 16, then m2 >= 16) at a time
@@ -1935,10 +1859,8 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv, io.pairs, qre, qim, (uint32_t)d.sym_d0[j], (uint32_t)d.sym_n[j],
                   (uint32_t)d.sym_n0[j], d.abin, d.aval, d.aind, d.agrp + 2 * j, d.azr + 2 * j};
     const uint32_t dummy = (uint32_t)(O32_H + (O32_H >> O32_PS)) + (uint32_t)(tid & 63);
-    const uint32_t r00 = src.d0, rn0 = src.dn0, r01 = src.d0 + src.dn0, rn1 = src.dn - src.dn0;
-    O32Pre p0, p1;
-    o32_prefetch(p0, src, 0, r00, rn0, (uint32_t)tid);
-    o32_prefetch(p1, src, 1, r01, rn1, (uint32_t)tid);
+    // (measured and dropped: both halves' scatter inputs prefetched into registers before the
+    // first half is written, in one batch or half 1 behind half 0's arrival: +11 % kernel time)
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       if (h) __syncthreads();                     // half 0 read back before half 1 overwrites it
@@ -1949,16 +1871,20 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
           qre[tid] = tq.x;
           qim[tid] = tq.y;
         }
+        tw1k[tid] = t1k;
+        if (tid < 384) tw2[tid] = t2;
         __syncthreads();                          // constellation visible to the scatter
       }
-      if (h == 0) o32_put(lds, src, p0, 0, r00, rn0, dummy, (uint32_t)tid);
-      else o32_put(lds, src, p1, 1, r01, rn1, dummy, (uint32_t)tid);
+      const uint32_t r0 = src.d0 + (h ? src.dn0 : 0u), rn = h ? src.dn - src.dn0 : src.dn0;
+      scatter_group<NT, 4>(lds, src, h, r0, rn, dummy, tid);
       __syncthreads();
       if (h == 0) OFDM_PHASE(1);
 #pragma unroll
       for (uint32_t r = 0; r < 16; r++) v[16 * h + r] = lds[o32_bin(kin + 1024u * r)];
     }
   } else {
+  tw1k[tid] = t1k;
+  if (tid < 384) tw2[tid] = t2;
 #pragma unroll
   for (int c0 = 0; c0 < 32; c0 += 8) {
     uint32_t off[8];
