@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sc16", action="store_true", help="skip the secondary sc16-output timing")
     ap.add_argument("--no-latency", action="store_true", help="skip the one-frame latency calls")
+    ap.add_argument("--no-blocks", action="store_true", help="skip the per-block general_work timing")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--shard", choices=("frames", "streams"), default="frames",
                     help="frames: one TS stream, disjoint frame ranges per rank; streams: an independent "
@@ -290,6 +291,46 @@ def cpu_baseline(cfg, seconds, all_configs=True):
     return out
 
 
+def per_block_rate(cfg, frames=6):
+    """the drop-in path GNU Radio would drive: the five blocks' C-ABI general_work calls on host
+    (pageable numpy) buffers, one T2 frame per framemapper / pilotgen call, each call synchronous
+    (H2D + kernels + D2H); secondary figure, not `value`"""
+    import numpy as np
+    import dvbt2ll
+    from dvbt2ll.configs import ts_for_frames
+    F = cfg.fecblocks
+    bb = dvbt2ll.bbheaderbch_bb(*cfg.bb_args()); ld = dvbt2ll.ldpc_bb(cfg.framesize, cfg.rate)
+    im = dvbt2ll.interleavermod_bc(*cfg.im_args()); fm = dvbt2ll.framemapperfint_cc(*cfg.fm_args())
+    pg = dvbt2ll.pilotgenp1insert_cc(*cfg.pg_args())
+    nbch, nldpc, cs = bb.output_multiple(), ld.output_multiple(), im.output_multiple()
+    bits = np.zeros(F * nbch, np.uint8); cw = np.zeros(F * nldpc, np.uint8)
+    cells = np.zeros(F * cs, np.complex64); mapped = np.zeros(fm.output_multiple(), np.complex64)
+    iq = np.zeros(pg.output_multiple(), np.complex64)
+    ts, _ = ts_for_frames(cfg, 0, frames + 1)
+    off = 0
+    names = ("bbheaderbch", "ldpc", "interleavermod", "framemapperfint", "pilotgenp1insert")
+    tot = dict.fromkeys(names, 0.0)
+    t_all = 0.0
+    for k in range(frames + 1):
+        t = [time.perf_counter()]
+        bb.general_work([ts[off:]], [bits]); off += bb.last_consumed; t.append(time.perf_counter())
+        ld.general_work([bits], [cw]); t.append(time.perf_counter())
+        im.general_work([cw], [cells]); t.append(time.perf_counter())
+        fm.general_work([cells], [mapped]); t.append(time.perf_counter())
+        pg.general_work([mapped], [iq]); t.append(time.perf_counter())
+        if k:                               # frame 0 is the warm-up
+            for i, n in enumerate(names):
+                tot[n] += t[i + 1] - t[i]
+            t_all += t[-1] - t[0]
+    per = len(iq)
+    return {"value": frames * per / t_all / 1e6, "unit": "Msamples/s", "frames": frames,
+            "ms_per_frame": {n: v / frames * 1e3 for n, v in tot.items()},
+            "x_realtime": frames * per / t_all / RT_SPS,
+            "note": "secondary: the per-block drop-in path (bbheaderbch -> ldpc -> interleavermod -> "
+                    "framemapperfint -> pilotgenp1insert general_work through the C ABI on pageable host "
+                    "buffers, synchronous per call, one stream); PCIe-bound, not `value`"}
+
+
 def one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per):
     """per-frame latency (the reference's stated aim, README:21-29): one T2 frame per call, TS
     resident in HBM, from the call to the frame's IQ complete in HBM; median / p90 of 20 calls,
@@ -453,6 +494,9 @@ def main():
     latency = None
     if not args.no_latency and NS == 1:
         latency = one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per)
+    blocks = None
+    if not args.no_blocks and world == 1 and rank == 0:
+        blocks = per_block_rate(cfg)
     gathered = None
     if dist and args.shard == "frames" and NS == 1:
         # secondary (not `value`): each step followed by the ordered IQ gather to rank 0, the
@@ -558,6 +602,8 @@ def main():
             out["latency_1_frame"] = latency
         if gathered:
             out["gather_to_rank0"] = gathered
+        if blocks:
+            out["per_block_general_work"] = blocks
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only (host cores are shared)
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
             # the box's CPU share is 16 threads (os.cpu_count() reports the whole machine)

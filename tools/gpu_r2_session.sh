@@ -21,7 +21,7 @@ step tests && IQ_STATS=$PWD/$O/iq_stats.jsonl timeout -k 10 900 python -u -m pyt
   && step bench && timeout -k 10 900 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" \
   && cat "$O/bench.json" \
   && step trace && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace" -o trace -f csv -- \
-       python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --slots 1 --steps 10 --warmup 2 \
+       python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --no-blocks --slots 1 --steps 10 --warmup 2 \
        > "$O/trace_bench.json" 2> "$O/trace.err" \
   && echo "=== done ($(date +%T))"
 rc=$?
