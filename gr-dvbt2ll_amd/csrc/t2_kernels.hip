@@ -1728,11 +1728,20 @@ __device__ __forceinline__ void o32_twiddle(float2 *v, const Lookup &tw) {
 // n2 = r) and reads (m0 = a, m1 = r, n2 = b) at (m1 & 15) + 16 (m0 & 15) + 256 (m1 >> 4) + 512 n2;
 // exchange 2 (SPLIT 9) writes (n2 = b, m0 = a, n1 = r) and reads (n2 = b, m0 = r, n1 = a) at
 // (n2 & 15) + 16 (n1 & 15) + 256 (n1 >> 4) + 512 m0
+#ifndef O32_EXCH_EXP
+#define O32_EXCH_EXP 0   // experiment switch (wrong output): 1 = barriers only, 2 = LDS traffic only, 3 = neither
+#endif
 template <int SPLIT>
 __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t tid, uint32_t a, uint32_t b) {
+#if O32_EXCH_EXP == 1
+  __syncthreads(); __syncthreads(); __syncthreads(); __syncthreads();
+  return;
+#elif O32_EXCH_EXP == 3
+  return;
+#endif
 #pragma unroll
   for (uint32_t h = 0; h < 2; h++) {
-    __syncthreads();
+    if (O32_EXCH_EXP != 2) __syncthreads();
     const bool mine = ((tid >> SPLIT) & 1u) == h;
     if (mine) {
 #pragma unroll
@@ -1742,7 +1751,7 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
         lds[o32_x(e)] = v[r];
       }
     }
-    __syncthreads();
+    if (O32_EXCH_EXP != 2) __syncthreads();
     if (mine) {
       if (SPLIT == 8 && O32_X2PAD) {
         // values r, r + 1 are adjacent, 16-byte aligned slots: one ds_read_b128 per pair (lanes
