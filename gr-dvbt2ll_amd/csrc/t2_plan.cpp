@@ -1142,24 +1142,36 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
   for (int s = 0; s < fp.S; s++)
     if (!seen[s]) return -1;
   cl.sym_n0 = cl.sym_n;
-  cl.part.clear();
-  if (ofdm_split(pp.N)) {
-    const int half = pp.N / 2;
-    cl.part.assign(fp.S, 0);
-    std::vector<uint16_t> inv2(fp.S);
-    for (int j = 0; j < pp.Nsym; j++) {
-      const int d0 = cl.sym_d0[j], n = cl.sym_n[j];
-      int n0 = 0;
+  // Slot order within each symbol (32K: within each half, bins < N/2 first): FEC-block-major, TI
+  // order within a block.  The OFDM kernels stream any order (inv follows it); this one gives the
+  // map kernel, which stores one FEC block per workgroup, one contiguous run per symbol (half)
+  // instead of 10-byte TI-row runs scattered over the symbol.
+  std::vector<int32_t> blk_of(fp.S);
+  for (int r = 0; r < fp.F; r++)
+    for (int t = 0; t < fp.cs; t++) blk_of[ti_dest(fp, r, t)] = r;
+  const bool split = ofdm_split(pp.N);
+  const int half = pp.N / 2;
+  cl.part.assign(fp.S, 0);
+  std::vector<int32_t> order;
+  for (int j = 0; j < pp.Nsym; j++) {
+    const int d0 = cl.sym_d0[j], n = cl.sym_n[j];
+    int n0 = 0;
+    if (split)
       for (int s = d0; s < d0 + n; s++) n0 += cl.inv[s] < half;
-      int a = d0, b = d0 + n0;
-      for (int s = d0; s < d0 + n; s++) cl.part[s] = cl.inv[s] < half ? a++ : b++;
-      cl.sym_n0[j] = n0;
-    }
-    for (int s = 0; s < fp.S; s++) inv2[cl.part[s]] = cl.inv[s];
-    cl.inv.swap(inv2);
-    for (auto &c : cl.cmap)
-      if (c >= 0) c = cl.part[c];
+    order.resize(n);
+    for (int k = 0; k < n; k++) order[k] = d0 + k;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+      const int hx = split && cl.inv[x] >= half, hy = split && cl.inv[y] >= half;
+      return hx != hy ? hx < hy : blk_of[x] < blk_of[y];
+    });
+    for (int k = 0; k < n; k++) cl.part[order[k]] = d0 + k;
+    cl.sym_n0[j] = split ? n0 : n;
   }
+  std::vector<uint16_t> inv2(fp.S);
+  for (int s = 0; s < fp.S; s++) inv2[cl.part[s]] = cl.inv[s];
+  cl.inv.swap(inv2);
+  for (auto &c : cl.cmap)
+    if (c >= 0) c = cl.part[c];
   return 0;
 }
 
