@@ -1522,6 +1522,15 @@ struct OfdmShape {
   static constexpr int LDS_BYTES = QAM_OFF + 256 * 8;                // + constellation re[256], im[256]
 };
 
+// experiment switch: 0 = one sample per IQ store (o32_store and the plain loop of ofdm_kernel)
+#ifndef O32_STORE_X2
+#define O32_STORE_X2 1
+#endif
+// value of lane l ^ 1 (DPP quad_perm [1,0,3,2])
+__device__ __forceinline__ float swap_adjacent_lane(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
+
 // IQ sample writer: the normalised sample times the output gain (the flowgraph's
 // blocks_multiply_const_xx after pilotgen, apps/vv009-4kshort.grc:335-385; 1 = the block's own
 // output), stored as complex64 (FMT 0) or as saturated round-to-nearest-even int16 I/Q at
@@ -1540,6 +1549,21 @@ struct IqOut {
       const uint32_t w = ((uint32_t)(int)i & 0xFFFFu) | ((uint32_t)(int)q << 16);
       __builtin_nontemporal_store(w, (uint32_t *)(base + n * 4u));
     }
+  }
+  // samples n, n + 1 (n even, already multiplied by the gain) as one store
+  __device__ __forceinline__ void put2(uint32_t n, float2 a, float2 b) const {
+    if (FMT == 0) {
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(f4v{a.x, a.y, b.x, b.y}, (f4v *)(base + n * 8u));
+    } else {
+      typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(u2v{sc16(a), sc16(b)}, (u2v *)(base + n * 4u));
+    }
+  }
+  static __device__ __forceinline__ uint32_t sc16(float2 a) {
+    const float i = fminf(fmaxf(rintf(a.x * 32767.f), -32768.f), 32767.f);
+    const float q = fminf(fmaxf(rintf(a.y * 32767.f), -32768.f), 32767.f);
+    return ((uint32_t)(int)i & 0xFFFFu) | ((uint32_t)(int)q << 16);
   }
 };
 
@@ -1647,16 +1671,36 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   OFDM_PHASE(0);
   sub_ifft<N, V>(v, lds, src, d.isinc, twl, tid, tabs);
   OFDM_PHASE(3);
+  if (O32_STORE_X2 && ((((uintptr_t)o.base + (uint32_t)G * SB) & (2u * SB - 1u)) == 0)) {
+    // two consecutive samples per lane and store: lanes t, t ^ 1 swap half of their values
+    // (as o32_store_pairs), so the even lane stores (t, t + 1) of every even m and the odd lane
+    // those of every odd m, m = uu + UL r
+    const bool odd = tid & 1;
+    const uint32_t n0 = (uint32_t)tid & ~1u;
 #pragma unroll
-  for (int uu = 0; uu < UL; uu++)
-#pragma unroll
-    for (int r = 0; r < RL; r++) {
-      const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
-      float2 a = v[uu * RL + r];
-      a = cscale(a, nrm);
-      o.put((uint32_t)G + n, a);
-      if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
+    for (int p = 0; p < V / 2; p++) {
+      const int m0 = 2 * p, m1 = 2 * p + 1;
+      const float2 e = cscale(cscale(v[(m0 % UL) * RL + m0 / UL], nrm), o.gain);
+      const float2 dd = cscale(cscale(v[(m1 % UL) * RL + m1 / UL], nrm), o.gain);
+      const float2 re = make_float2(swap_adjacent_lane(e.x), swap_adjacent_lane(e.y));
+      const float2 rd = make_float2(swap_adjacent_lane(dd.x), swap_adjacent_lane(dd.y));
+      const float2 lo = odd ? rd : e, hi = odd ? dd : re;
+      const uint32_t n = n0 + (uint32_t)NT * (uint32_t)(m0 + (odd ? 1 : 0));
+      o.put2((uint32_t)G + n, lo, hi);
+      if (n >= (uint32_t)(N - G)) o.put2(n - (uint32_t)(N - G), lo, hi);
     }
+  } else {
+#pragma unroll
+    for (int uu = 0; uu < UL; uu++)
+#pragma unroll
+      for (int r = 0; r < RL; r++) {
+        const uint32_t n = (uint32_t)(tid + NT * (uu + UL * r));
+        float2 a = v[uu * RL + r];
+        a = cscale(a, nrm);
+        o.put((uint32_t)G + n, a);
+        if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
+      }
+  }
 #if OFDM_VARIANT & 8
   __syncthreads();
   OFDM_PHASE(8);
@@ -1817,6 +1861,29 @@ __device__ __forceinline__ void o32_store(const float2 *v, const IqOut<FMT> &o, 
   }
 }
 
+// The same store with two consecutive samples per lane (one 16-byte, or 8-byte sc16, store
+// instead of two): lanes b and b ^ 1 swap half of their values (DPP quad_perm [1,0,3,2]) so the
+// even-b lane holds samples (b, b + 1) of every even r and the odd-b lane those of every odd r.
+// Each store instruction then writes eight runs of 16 samples per wave, half the instructions of
+// o32_store (the per-CU store issue rate, not HBM, bounds the store phase).  Needs the symbol's
+// sample 0 aligned to two samples (always true for the chain's frame layout; checked by the caller).
+template <int FMT>
+__device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT> &o, uint32_t nout, float nrm, int G) {
+  constexpr uint32_t N = 32768;
+  const bool odd = nout & 1u;
+  const uint32_t n0 = nout & ~1u;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++) {
+    const float2 e = cscale(cscale(v[2 * k], nrm), o.gain), d = cscale(cscale(v[2 * k + 1], nrm), o.gain);
+    const float2 re = make_float2(swap_adjacent_lane(e.x), swap_adjacent_lane(e.y));
+    const float2 rd = make_float2(swap_adjacent_lane(d.x), swap_adjacent_lane(d.y));
+    const float2 lo = odd ? rd : e, hi = odd ? d : re;
+    const uint32_t n = n0 + 1024u * (2u * k + (odd ? 1u : 0u));
+    o.put2((uint32_t)G + n, lo, hi);
+    if (n >= N - (uint32_t)G) o.put2(n - (N - (uint32_t)G), lo, hi);
+  }
+}
+
 // 32K symbols, one workgroup per (symbol, frame): scatter mode (the fused chain), gather mode (the
 // pilotgen block: cells already in carrier order) and the carriers-only test hook
 template <int FMT>
@@ -1918,7 +1985,10 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   OFDM_PHASE(2);
   o32_fft(v, lds, tw1k, tw2, (uint32_t)tid, ta, tb);   // its first barrier publishes the tables
   const IqOut<FMT> o{(char *)io.out + ((int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + d.G)) * SB, d.gain};
-  o32_store<FMT, 0, 32>(v, o, tb + 32u * ta, d.norm, d.G);
+  if (O32_STORE_X2 && ((((uintptr_t)o.base + (uint32_t)d.G * SB) & (2u * SB - 1u)) == 0))
+    o32_store_pairs<FMT>(v, o, tb + 32u * ta, d.norm, d.G);
+  else
+    o32_store<FMT, 0, 32>(v, o, tb + 32u * ta, d.norm, d.G);
 #if OFDM_VARIANT & 8
   __syncthreads();
   OFDM_PHASE(8);
