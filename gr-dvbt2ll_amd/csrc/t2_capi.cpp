@@ -87,14 +87,14 @@ struct DeviceCtx {
 // ---------------------------------------------------------------- FEC tables on device
 struct FecTables {
   FecPlan plan;
-  DevBuf hcrc, tab, m1, m64, rowptr, ent, prbs, crc8, crcsh;
+  DevBuf hcrc, tab, m1, m64, ctab, rowptr, ent, prbs, crc8, crcsh;
   FecDev dev{};
   int init(int framesize, int rate, int constellation, int mode, int inband, int fecblocks, int tsrate) {
     // tuning knob for kernel experiments (tools/): waves sharing the BCH division, default 1
     const char *bw = std::getenv("DVBT2LL_FEC_BCH_WAVES");
     if (build_fec(framesize, rate, constellation, plan, bw ? std::atoi(bw) : 1)) return DVBT2LL_EINVAL;
     int r;
-    if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) || (r = upload(m64, plan.bch_m64)) ||
+    if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) || (r = upload(m64, plan.bch_m64)) || (r = upload(ctab, plan.bch_ctab)) ||
         (r = upload(rowptr, plan.ldpc_rowptr)) || (r = upload(ent, plan.ldpc_ent)) ||
         (r = upload(prbs, plan.prbs_bytes)) || (r = upload(crc8, plan.crc8_tab)) || (r = upload(crcsh, plan.crc8_shift)) ||
         (r = upload(hcrc, plan.hcrc_bits)))
@@ -102,6 +102,7 @@ struct FecTables {
     dev.bch_tab = tab.as<uint64_t>();
     dev.bch_m1 = m1.as<uint64_t>();
     dev.bch_m64 = m64.as<uint64_t>();
+    dev.bch_ctab = ctab.as<uint64_t>();
     dev.ldpc_rowptr = rowptr.as<uint16_t>();
     dev.ldpc_ent = ent.as<uint32_t>();
     dev.prbs = prbs.as<uint8_t>();

@@ -18,6 +18,7 @@ struct FecDev {
   const uint64_t *bch_tab;      // 256 x 3
   const uint64_t *bch_m1;       // 192 x 3: x^(8 chunk) mod g (one wave's Horner step)
   const uint64_t *bch_m64;      // 192 x 3: x^(8 * 64 chunk) mod g (combine of the four waves)
+  const uint64_t *bch_ctab;     // [P/4][16][64] x 4: lane shift nibble tables (FecPlan::bch_ctab)
   const uint16_t *ldpc_rowptr;  // q + 1
   const uint32_t *ldpc_ent;     // nent
   const uint8_t *prbs;          // kbch / 8

@@ -134,6 +134,12 @@ __shared__ uint64_t g_fec_ts[16];
 #else
 #define FEC_PHASE(i) do { } while (0)
 #endif
+#ifndef FEC_BCH_TAB
+#define FEC_BCH_TAB 1    // 1: chunk remainders combined by per-lane nibble tables; 0: Horner over the lanes
+#endif
+#ifndef FEC_BCH_TAB_JB
+#define FEC_BCH_TAB_JB 4  // table lookups in flight per lane (8: spills)
+#endif
 #ifndef FEC_BCH_PRIO
 #define FEC_BCH_PRIO 1   // wave priority (s_setprio) of the BCH wave while it runs (0: off)
 #endif
@@ -238,13 +244,16 @@ __device__ __forceinline__ void load_rows(uint64_t m[3][3], const uint64_t *g, i
 // P is a template parameter so the register geometry (top byte, masks) is compile-time.
 template <int P>
 __device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64_t *btab, const uint64_t *m1g,
-                                              int L, int C, int NC, int t, int lane, uint64_t a[3]) {
+                                              const uint64_t *ctab, int L, int C, int NC, int t, int lane,
+                                              uint64_t a[3]) {
   const int lo = L - (NC - t) * C, hi = L - (NC - 1 - t) * C;
   constexpr int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
   constexpr uint64_t k1 = P >= 128 ? ~0ull : (1ull << (P - 64)) - 1;
   constexpr uint64_t k2 = P >= 192 ? ~0ull : P <= 128 ? 0ull : (1ull << (P - 128)) - 1;
+#if !FEC_BCH_TAB
   uint64_t m1[3][3];
   load_rows(m1, m1g, lane);
+#endif
   uint64_t r0 = 0, r1 = 0, r2 = 0;
   // byte-table division; the next message byte is read before the table lookup's wait (LDS
   // returns in order, so it costs no extra round trip)
@@ -263,6 +272,47 @@ __device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64
     r1 ^= btab[idx * 3 + 1];
     r2 ^= btab[idx * 3 + 2];
   }
+#if FEC_VARIANT & 2
+  FEC_PHASE(5);   // experiment: byte-table division done (phase 5 = division, 6 = shift + combine)
+#endif
+#if FEC_BCH_TAB
+  // each lane moves its remainder to the end of the wave's chunks by nibble-table lookups (no
+  // dependency between lanes), then one XOR reduction over the wave
+  constexpr int NJ = P / 4, JB = FEC_BCH_TAB_JB;
+  uint64_t s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll 1
+  for (int j0 = 0; j0 < NJ; j0 += JB) {
+    uint4 e01[JB];
+    uint2 e2[JB];
+#pragma unroll
+    for (int u = 0; u < JB; u++) {
+      const int j = j0 + u;
+      if (j < NJ) {
+        const uint64_t rw = j < 16 ? r0 : j < 32 ? r1 : r2;
+        const uint32_t v = (uint32_t)(rw >> (4 * (j & 15))) & 15u;
+        const uint32_t off = (((uint32_t)j * 16u + v) * 64u + (uint32_t)lane) * 32u;
+        e01[u] = ld_off((const uint4 *)ctab, off);
+        e2[u] = ld_off((const uint2 *)ctab, off + 16u);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < JB; u++) {
+      if (j0 + u < NJ) {
+        s0 ^= ((uint64_t)e01[u].y << 32) | e01[u].x;
+        s1 ^= ((uint64_t)e01[u].w << 32) | e01[u].z;
+        s2 ^= ((uint64_t)e2[u].y << 32) | e2[u].x;
+      }
+    }
+  }
+  auto wave_xor64 = [](uint64_t x) -> uint64_t {
+    const uint32_t lo = rd_lane_u32(wave_prefix_xor((uint32_t)x), 63);
+    const uint32_t hi = rd_lane_u32(wave_prefix_xor((uint32_t)(x >> 32)), 63);
+    return ((uint64_t)hi << 32) | lo;
+  };
+  a[0] = wave_xor64(s0);
+  a[1] = wave_xor64(s1);
+  a[2] = P > 128 ? wave_xor64(s2) : 0ull;
+#else
   uint64_t a0 = rd_lane_u64(r0, 0), a1 = rd_lane_u64(r1, 0), a2 = rd_lane_u64(r2, 0);
   for (int l = 1; l < 64; l++) {
     gf2_matvec(m1, a0, a1, a2);
@@ -273,6 +323,7 @@ __device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64
   a[0] = a0;
   a[1] = a1;
   a[2] = a2;
+#endif
 }
 
 // the nw wave remainders R_w (LDS, 3 words each) -> (..(R0 M64 + R1) M64 + ..) M64 + R_(nw-1),
@@ -515,7 +566,9 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
     }
     __syncthreads();
     FEC_PHASE(4);
+#if !(FEC_VARIANT & 2)
     FEC_PHASE(5);
+#endif
 
     // ---- BCH: waves 0 .. bch_waves - 1 divide 64 chunks each and Horner-combine them
     //      (bch_wave_part); wave 0 then combines the wave remainders and writes the parity.  The
@@ -528,10 +581,10 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
     if (wave < nbw) {
       uint64_t a[3];
       switch (P) {   // compile-time register geometry per BCH parity length (t = 12, 10, 8; short 12)
-        case 192: bch_wave_part<192>(frame, btab, d.bch_m1, L, d.chunk, nchunks, tid, lane, a); break;
-        case 168: bch_wave_part<168>(frame, btab, d.bch_m1, L, d.chunk, nchunks, tid, lane, a); break;
-        case 160: bch_wave_part<160>(frame, btab, d.bch_m1, L, d.chunk, nchunks, tid, lane, a); break;
-        default: bch_wave_part<128>(frame, btab, d.bch_m1, L, d.chunk, nchunks, tid, lane, a); break;
+        case 192: bch_wave_part<192>(frame, btab, d.bch_m1, d.bch_ctab, L, d.chunk, nchunks, tid, lane, a); break;
+        case 168: bch_wave_part<168>(frame, btab, d.bch_m1, d.bch_ctab, L, d.chunk, nchunks, tid, lane, a); break;
+        case 160: bch_wave_part<160>(frame, btab, d.bch_m1, d.bch_ctab, L, d.chunk, nchunks, tid, lane, a); break;
+        default: bch_wave_part<128>(frame, btab, d.bch_m1, d.bch_ctab, L, d.chunk, nchunks, tid, lane, a); break;
       }
       if (lane < 3) wres[3 * wave + lane] = lane == 0 ? a[0] : lane == 1 ? a[1] : a[2];
     }

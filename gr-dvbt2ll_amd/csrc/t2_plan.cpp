@@ -166,6 +166,30 @@ int build_fec(int framesize, int rate, int constellation, FecPlan &fp, int bch_w
   fp.bch_chunk = (L + 64 * bch_waves - 1) / (64 * bch_waves);
   fp.bch_m1 = shift_matrix(g, P, 8L * fp.bch_chunk);
   fp.bch_m64 = shift_matrix(g, P, 8L * 64 * fp.bch_chunk);
+  // the chunk remainder of lane l moves to the end of its wave's 64 chunks: r_l x^(8 chunk (63 - l))
+  // mod g, as the XOR of P/4 nibble-table entries (one lookup per 4-bit digit of r_l)
+  {
+    const int NJ = P / 4;
+    fp.bch_ctab.assign((size_t)NJ * 16 * 64 * 4, 0);
+    Poly192 base;
+    base.set(0);   // lane 63: x^0
+    for (int l = 63; l >= 0; l--) {
+      Poly192 pj = base;   // base x^(4 j)
+      for (int j = 0; j < NJ; j++) {
+        Poly192 q[4];
+        q[0] = pj;
+        for (int k = 1; k < 4; k++) q[k] = times_x(q[k - 1], g, P);
+        for (int v = 0; v < 16; v++) {
+          uint64_t *e = &fp.bch_ctab[(((size_t)j * 16 + v) * 64 + l) * 4];
+          for (int k = 0; k < 4; k++)
+            if ((v >> k) & 1)
+              for (int w = 0; w < 3; w++) e[w] ^= q[k].w[w];
+        }
+        pj = times_x(q[3], g, P);
+      }
+      for (long i = 0; i < 8L * fp.bch_chunk; i++) base = times_x(base, g, P);
+    }
+  }
   // LDPC: info group gidx (360 bits) with address x lands in parity row a = x mod q with
   // cyclic offset b = x div q (columns c = (b + n) mod 360, since pbits = 360 q)
   const t2_ldpc_code_t *c = find_code(normal, rate);

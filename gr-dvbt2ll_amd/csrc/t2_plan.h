@@ -33,6 +33,9 @@ struct FecPlan {
   std::vector<uint64_t> bch_tab;      // 256 x 3 words: d(x) * x^P mod g(x)
   std::vector<uint64_t> bch_m1;       // 192 rows x 3 words: v -> v * x^(8*chunk) mod g
   std::vector<uint64_t> bch_m64;      // 192 rows x 3 words: v -> v * x^(8*64*chunk) mod g
+  // per-lane chunk shift as nibble tables: entry [j][v][lane] (4 words, the 4th zero) =
+  // v x^(4 j) x^(8 chunk (63 - lane)) mod g for nibble j < P/4, value v < 16, lane < 64
+  std::vector<uint64_t> bch_ctab;
   std::vector<uint16_t> ldpc_rowptr;  // q + 1
   std::vector<uint32_t> ldpc_ent;     // (group << 16) | rotation, grouped by parity row
   std::vector<uint8_t> prbs_bytes;    // BB scrambler, kbch/8 bytes

@@ -80,6 +80,16 @@ int t2probe_fec(int framesize, int rate, int constellation, int *info, uint32_t 
   return 0;
 }
 
+// BCH tables of the FEC kernel: info [P, chunk, L]; tab 256 x 3 words; ctab (P/4) x 16 x 64 x 4 words
+int t2probe_bch(int framesize, int rate, int *info, uint64_t *tab, uint64_t *ctab) {
+  FecPlan fp;
+  if (build_fec(framesize, rate, 3, fp)) return -1;
+  info[0] = fp.nparity; info[1] = fp.bch_chunk; info[2] = fp.kbch / 8;
+  if (tab) memcpy(tab, fp.bch_tab.data(), fp.bch_tab.size() * 8);
+  if (ctab) memcpy(ctab, fp.bch_ctab.data(), fp.bch_ctab.size() * 8);
+  return 0;
+}
+
 // fused-chain layout: cmap Nsym x N (stored row order), inv S, sym_d0/sym_n Nsym;
 // info [Nsym, N, S, split]
 int t2probe_chain(const int *p20, const int *pg3, int *info, int32_t *cmap, uint16_t *inv, int32_t *d0,

@@ -26,6 +26,7 @@ def lib():
         L.t2probe_pilot.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.t2probe_map.argtypes = [ctypes.c_int] * 4 + [vp, vp]
         L.t2probe_fec.argtypes = [ctypes.c_int] * 3 + [vp, vp, vp]
+        L.t2probe_bch.argtypes = [ctypes.c_int] * 2 + [vp, vp, vp]
         L.t2probe_chain.argtypes = [vp] * 9
         L.t2probe_counts.argtypes = [ctypes.c_int] * 6 + [vp]
         L.t2probe_aux_lists.argtypes = [vp] * 9
@@ -108,6 +109,18 @@ def fec_plan(framesize, rate, constellation=3):
     rp = np.zeros(q + 1, np.uint16)
     assert lib().t2probe_fec(framesize, rate, constellation, _p(info), _p(ent), _p(rp)) == 0
     return dict(kbch=kbch, nbch=nbch, P=P, q=q, ent=ent, rowptr=rp, chunk=chunk, parity_il=pil)
+
+
+def bch_tables(framesize, rate):
+    """the FEC kernel's BCH tables: byte table (256 x 3 words) and the per-lane chunk-shift
+    nibble tables ((P/4) x 16 x 64 x 4 words), with P, the chunk length and the BBFRAME bytes"""
+    info = np.zeros(3, np.int32)
+    assert lib().t2probe_bch(framesize, rate, _p(info), None, None) == 0
+    P, chunk, L = (int(x) for x in info)
+    tab = np.zeros(256 * 3, np.uint64)
+    ctab = np.zeros((P // 4) * 16 * 64 * 4, np.uint64)
+    assert lib().t2probe_bch(framesize, rate, _p(info), _p(tab), _p(ctab)) == 0
+    return dict(P=P, chunk=chunk, L=L, tab=tab.reshape(256, 3), ctab=ctab.reshape(P // 4, 16, 64, 4))
 
 
 def ti_dest(plan, r, t):

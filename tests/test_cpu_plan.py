@@ -9,6 +9,7 @@ from dvbt2ll import enums as E
 from dvbt2ll.configs import CONFIGS, T2Config
 import oracle_lib as O
 import plan_probe as PP
+import std_tables as T
 
 rng = np.random.default_rng(7)
 
@@ -292,3 +293,47 @@ def test_l1post_plan_all_frame_idx(l1c, extra):
         a = PP.l1post(cfg.fm_args(), fi, plan=True)
         b = PP.l1post(cfg.fm_args(), fi, plan=False)
         assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), "FRAME_IDX %d" % fi
+
+
+def _gf2_mod(v, g):
+    """remainder of the GF(2) polynomial v (int, bit i = x^i) modulo g (int)"""
+    dg = g.bit_length() - 1
+    while v.bit_length() - 1 >= dg:
+        v ^= g << (v.bit_length() - 1 - dg)
+    return v
+
+
+@pytest.mark.parametrize("framesize,rate", [(1, r) for r in range(6)] + [(0, r) for r in range(8)])
+def test_bch_lane_shift_tables(framesize, rate):
+    """The FEC kernel's BCH (t2_kernels.hip bch_wave_part, FEC_BCH_TAB): 64 lanes divide
+    consecutive chunks of the BBFRAME by the byte table, then each lane moves its remainder to
+    the end of the message with P/4 nibble-table lookups and the lanes' results are XORed.  That
+    must equal the byte-table division of the whole message, and message || parity must be a
+    multiple of the generator (bbheaderbch:504-531)."""
+    t = PP.bch_tables(framesize, rate)
+    P, C, L = t["P"], t["chunk"], t["L"]
+    tab = [int(a) | int(b) << 64 | int(c) << 128 for a, b, c in t["tab"]]
+    ctab = t["ctab"]
+    mask = (1 << P) - 1
+
+    def divide(msg):
+        r = 0
+        for byte in msg:
+            r = ((r << 8) & mask) ^ tab[((r >> (P - 8)) & 0xFF) ^ int(byte)]
+        return r
+
+    gl = T.bch_generator(framesize == 1, P)   # highest power first, degree P
+    g = int("".join(str(int(b)) for b in gl), 2)
+    rng = np.random.default_rng(1000 + 10 * framesize + rate)
+    for _ in range(2):
+        msg = rng.integers(0, 256, L, dtype=np.uint8)
+        total = 0
+        for lane in range(64):
+            lo, hi = max(L - (64 - lane) * C, 0), max(L - (63 - lane) * C, 0)
+            r = divide(msg[lo:hi])
+            for j in range(P // 4):
+                e = ctab[j, (r >> (4 * j)) & 15, lane]
+                total ^= int(e[0]) | int(e[1]) << 64 | int(e[2]) << 128
+        assert total == divide(msg)
+        m = int.from_bytes(msg.tobytes(), "big")
+        assert _gf2_mod((m << P) | total, g) == 0
