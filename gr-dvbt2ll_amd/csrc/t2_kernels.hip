@@ -362,6 +362,27 @@ template <int NT>
 __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
                                 uint16_t *stage, int blk, int tid);
 
+// LDPC parity rows: row a, word w of p[a][c] = XOR over the row's entries (g, b) of the window
+// d_g[(c - b) mod 360], c = 32 w; 12 words per row at rowA
+__device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, const uint32_t *ents, const uint16_t *rp,
+                                          int q, int t0, int nt) {
+  for (int it = t0; it < q * 12; it += nt) {
+    const int a = it / 12, w = it - a * 12;
+    uint32_t acc = 0;
+    for (int e = rp[a]; e < rp[a + 1]; e++) {
+      const uint32_t ent = ents[e];
+      const int g = ent >> 16, b = ent & 0xFFFF;
+      int o = 32 * w - b;            // window start (c - b) mod 360 for c = 32 w
+      o += o < 0 ? 360 : 0;
+      const uint32_t *dg = D + g * FEC_DW + (o >> 5);
+      const uint64_t win = ((uint64_t)dg[0] << 32) | dg[1];
+      acc ^= (uint32_t)(win >> (32 - (o & 31)));
+    }
+    if (w == 11) acc &= 0xFF000000u;
+    rowA[it] = acc;
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io, MapDev md,
                                                                         uint16_t *out_pairs, int64_t frame_stride) {
@@ -642,22 +663,7 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
   // row a, word w of p[a][c] = XOR over entries (g, b) of d_g[(c - b) mod 360]
   const int q = d.q;
   uint32_t *rowA = D + ngroups * FEC_DW;
-  const uint16_t *rp = d.ldpc_rowptr;
-  for (int it = tid; it < q * 12; it += FEC_THREADS) {
-    int a = it / 12, w = it - a * 12;
-    uint32_t acc = 0;
-    for (int e = rp[a]; e < rp[a + 1]; e++) {
-      uint32_t ent = ents[e];
-      int g = ent >> 16, b = ent & 0xFFFF;
-      int o = 32 * w - b;            // window start (c - b) mod 360 for c = 32 w
-      o += o < 0 ? 360 : 0;
-      const uint32_t *dg = D + g * FEC_DW + (o >> 5);
-      uint64_t win = ((uint64_t)dg[0] << 32) | dg[1];
-      acc ^= (uint32_t)(win >> (32 - (o & 31)));
-    }
-    if (w == 11) acc &= 0xFF000000u;
-    rowA[it] = acc;
-  }
+  ldpc_rows(D, rowA, ents, d.ldpc_rowptr, q, tid, FEC_THREADS);
   __syncthreads();
   FEC_PHASE(8);
   // inclusive prefix XOR over rows a, in place: wave w scans word columns 3w..3w+2, 64 rows
