@@ -140,6 +140,13 @@ __shared__ uint64_t g_fec_ts[16];
 #ifndef FEC_BCH_TAB_JB
 #define FEC_BCH_TAB_JB 4  // table lookups in flight per lane (8: spills)
 #endif
+#ifndef FEC_BCH_COOP
+#define FEC_BCH_COOP 0   // experiment switch (measured: fec 0.30 -> 0.38 ms, dropped): 1 (one BCH wave, nibble
+                         // tables) = all four waves share the combine's lookups
+#endif
+#ifndef FEC_BCH_COOP_JB
+#define FEC_BCH_COOP_JB 4   // cooperative combine: table lookups in flight per thread
+#endif
 #ifndef FEC_BCH_PRIO
 #define FEC_BCH_PRIO 1   // wave priority (s_setprio) of the BCH wave while it runs (0: off)
 #endif
@@ -147,7 +154,13 @@ constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
 constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 233280 / 360)
 constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g || d_g[0..56)
-constexpr int FEC_WG_PER_CU = 6;
+#ifndef FEC_BTAB_GLOBAL
+#define FEC_BTAB_GLOBAL 0   // 1: BCH byte table read from global memory (no LDS copy per workgroup)
+#endif
+#ifndef FEC_WGS
+#define FEC_WGS 6           // resident FEC workgroups per CU (persistent grid)
+#endif
+constexpr int FEC_WG_PER_CU = FEC_WGS;
 // dynamic LDS carve (bytes): a persistent part (the workgroup loops over FEC blocks; tables are
 // staged once), then the per-block area, reused by phase:
 //   BB/CRC phase: [frame | raw TS bytes | CRC-8 table | CRC-8 zero-extension tables]
@@ -155,7 +168,7 @@ constexpr int FEC_WG_PER_CU = 6;
 //   fused map phase (FEC_TS_TO_PAIRS): [cell indices | index pairs] over the whole per-block area,
 //   the interleaver-input words (built from frame + rows) beyond it (fec_map_lds)
 constexpr int SM_BTAB = 0;                                   // 256*3*8 = 6144
-constexpr int SM_ENT = SM_BTAB + 6144;                       // 648*4
+constexpr int SM_ENT = SM_BTAB + (FEC_BTAB_GLOBAL ? 0 : 6144);  // 648*4
 constexpr int SM_HCRC = SM_ENT + FEC_MAX_ENT * 4;            // 72 (+8)
 constexpr int SM_SYNC = SM_HCRC + 80;                        // 48 (<= 36 sync slots)
 constexpr int SM_W = SM_SYNC + 48;                           // 12*4
@@ -168,10 +181,14 @@ constexpr int SM_CRC8 = SM_RAW + ((FEC_RAW_BYTES + 15) & ~15);   // 256
 constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
 constexpr int SM_D = SM_PHASE;                               // rows follow D at word ngroups * 13
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
-constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_BYTES ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_BYTES);
+// cooperative BCH combine (FEC_BCH_COOP): the 64 chunk remainders (3 words each) sit after D
+__host__ __device__ constexpr int fec_rem_off(int ngroups) { return (FEC_DW * 4 * ngroups + 15) & ~15; }
+constexpr int FEC_REM_BYTES = 64 * 3 * 8;
+constexpr int FEC_LDPC_AREA = FEC_LDPC_BYTES > fec_rem_off(150) + FEC_REM_BYTES ? FEC_LDPC_BYTES : fec_rem_off(150) + FEC_REM_BYTES;
+constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_AREA ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_AREA);
 static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0 && SM_BLK % 16 == 0, "LDS carve alignment");
 static_assert(SM_SYNC % 8 == 0 && SM_BLK - SM_SYNC >= 4 * 3 * 8, "BCH wave remainders in SM_SYNC + SM_W");
-static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "six FEC workgroups per CU");
+static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "FEC_WGS workgroups per CU");
 
 // stream position of payload byte J (counted over the payload bytes of the whole stream)
 __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
@@ -242,21 +259,14 @@ __device__ __forceinline__ void load_rows(uint64_t m[3][3], const uint64_t *g, i
 // ones may be empty) by the byte table, then a Horner pass over the wave's 64 lanes with M1 (v -> v x^(8C)
 // mod g) as wave ballots.  Returns the wave's remainder sum_l r_l x^(8C (63 - l)) (uniform).
 // P is a template parameter so the register geometry (top byte, masks) is compile-time.
+// byte-table division of frame[lo, hi) (lo clamped at 0) into the P-bit remainder r; the next message
+// byte is read before the table lookup's wait (LDS returns in order, so it costs no extra round trip)
 template <int P>
-__device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64_t *btab, const uint64_t *m1g,
-                                              const uint64_t *ctab, int L, int C, int NC, int t, int lane,
-                                              uint64_t a[3]) {
-  const int lo = L - (NC - t) * C, hi = L - (NC - 1 - t) * C;
+__device__ __forceinline__ void bch_divide(const uint8_t *frame, const uint64_t *btab, int lo, int hi, uint64_t &r0,
+                                           uint64_t &r1, uint64_t &r2) {
   constexpr int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
   constexpr uint64_t k1 = P >= 128 ? ~0ull : (1ull << (P - 64)) - 1;
   constexpr uint64_t k2 = P >= 192 ? ~0ull : P <= 128 ? 0ull : (1ull << (P - 128)) - 1;
-#if !FEC_BCH_TAB
-  uint64_t m1[3][3];
-  load_rows(m1, m1g, lane);
-#endif
-  uint64_t r0 = 0, r1 = 0, r2 = 0;
-  // byte-table division; the next message byte is read before the table lookup's wait (LDS
-  // returns in order, so it costs no extra round trip)
   int i = max(lo, 0);
   uint32_t nxt = i < hi ? frame[i] : 0u;
 #pragma unroll 2
@@ -272,6 +282,65 @@ __device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64
     r1 ^= btab[idx * 3 + 1];
     r2 ^= btab[idx * 3 + 2];
   }
+}
+
+__device__ __forceinline__ uint64_t wave_xor64(uint64_t x) {
+  const uint32_t lo = rd_lane_u32(wave_prefix_xor((uint32_t)x), 63);
+  const uint32_t hi = rd_lane_u32(wave_prefix_xor((uint32_t)(x >> 32)), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Cooperative combine (one BCH wave): the chunk remainders r_l (rem, LDS, 3 words each) are moved
+// to the end of the 64 chunks, r_l x^(8C(63 - l)) mod g, as the XOR of P/4 nibble-table entries
+// each; the 64 (P/4) lookups are spread over the whole workgroup (thread t: lane l = t & 63, digits
+// j = t / 64 + 4 k), so each thread has P/16 of them instead of the BCH wave's P/4, and the
+// workgroup's partial sums are XOR-reduced (DPP wave scans, then wsum in LDS, 4 x 3 words)
+template <int P>
+__device__ __forceinline__ void bch_coop_sum(const uint64_t *rem, const uint64_t *ctab, uint64_t *wsum, int tid) {
+  constexpr int NJ = P / 4, K = (NJ + 3) / 4, JB = FEC_BCH_COOP_JB;
+  const int l = tid & 63, j0 = tid >> 6;
+  const uint64_t r0 = rem[3 * l], r1 = rem[3 * l + 1], r2 = rem[3 * l + 2];
+  uint64_t s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+  for (int kb = 0; kb < K; kb += JB) {
+    uint4 e01[JB];
+    uint2 e2[JB];
+#pragma unroll
+    for (int u = 0; u < JB; u++) {
+      const int k = kb + u < K ? kb + u : K - 1;
+      const int j = j0 + 4 * k < NJ ? j0 + 4 * k : 0;   // out-of-range digits: a valid entry, masked below
+      const uint64_t rw = 4 * k < 16 ? r0 : 4 * k < 32 ? r1 : r2;   // j0 < 4: j's word is k's
+      const uint32_t v = (uint32_t)(rw >> (4 * (j & 15))) & 15u;
+      const uint32_t off = (((uint32_t)j * 16u + v) * 64u + (uint32_t)l) * 32u;
+      e01[u] = ld_off((const uint4 *)ctab, off);
+      e2[u] = ld_off((const uint2 *)ctab, off + 16u);
+    }
+#pragma unroll
+    for (int u = 0; u < JB; u++) {
+      const bool ok = kb + u < K && j0 + 4 * (kb + u) < NJ;
+      const uint32_t m = ok ? ~0u : 0u;
+      s0 ^= ((uint64_t)(e01[u].y & m) << 32) | (e01[u].x & m);
+      s1 ^= ((uint64_t)(e01[u].w & m) << 32) | (e01[u].z & m);
+      s2 ^= ((uint64_t)(e2[u].y & m) << 32) | (e2[u].x & m);
+    }
+  }
+  s0 = wave_xor64(s0);
+  s1 = wave_xor64(s1);
+  s2 = P > 128 ? wave_xor64(s2) : 0ull;
+  if ((tid & 63) < 3) wsum[3 * (tid >> 6) + (tid & 63)] = (tid & 63) == 0 ? s0 : (tid & 63) == 1 ? s1 : s2;
+}
+
+template <int P>
+__device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64_t *btab, const uint64_t *m1g,
+                                              const uint64_t *ctab, int L, int C, int NC, int t, int lane,
+                                              uint64_t a[3]) {
+  const int lo = L - (NC - t) * C, hi = L - (NC - 1 - t) * C;
+#if !FEC_BCH_TAB
+  uint64_t m1[3][3];
+  load_rows(m1, m1g, lane);
+#endif
+  uint64_t r0 = 0, r1 = 0, r2 = 0;
+  bch_divide<P>(frame, btab, lo, hi, r0, r1, r2);
 #if FEC_VARIANT & 2
   FEC_PHASE(5);   // experiment: byte-table division done (phase 5 = division, 6 = shift + combine)
 #endif
@@ -304,11 +373,6 @@ __device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64
       }
     }
   }
-  auto wave_xor64 = [](uint64_t x) -> uint64_t {
-    const uint32_t lo = rd_lane_u32(wave_prefix_xor((uint32_t)x), 63);
-    const uint32_t hi = rd_lane_u32(wave_prefix_xor((uint32_t)(x >> 32)), 63);
-    return ((uint64_t)hi << 32) | lo;
-  };
   a[0] = wave_xor64(s0);
   a[1] = wave_xor64(s1);
   a[2] = P > 128 ? wave_xor64(s2) : 0ull;
@@ -396,14 +460,19 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
   uint8_t *crcsh = smem + SM_CRCSH;
   uint8_t *hcrc8 = smem + SM_HCRC;
   uint8_t *syncv = smem + SM_SYNC;
+#if FEC_BTAB_GLOBAL
+  const uint64_t *btab = d.bch_tab;
+#else
   uint64_t *btab = (uint64_t *)(smem + SM_BTAB);
+#endif
   uint32_t *D = (uint32_t *)(smem + SM_D);
   uint32_t *Wv = (uint32_t *)(smem + SM_W);
   uint32_t *ents = (uint32_t *)(smem + SM_ENT);
   uint64_t *wres = (uint64_t *)(smem + SM_SYNC);   // BCH wave remainders (SM_SYNC + SM_W, free then)
 
   // ---- constant tables into LDS, once: the workgroup then loops over FEC blocks
-  for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
+  if (!FEC_BTAB_GLOBAL)
+    for (int i = tid; i < 768; i += FEC_THREADS) ((uint64_t *)(smem + SM_BTAB))[i] = d.bch_tab[i];
   for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
   if (MODE != FEC_BITS_TO_BITS)
     for (int i = tid; i < 72; i += FEC_THREADS) hcrc8[i] = d.hcrc_bits[i];
@@ -596,6 +665,59 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
     //      other waves meanwhile (chain mode) lay out the LDPC info groups that hold no BCH parity.
     const int ngroups = d.nbch / 360;
     const int nbw = d.bch_waves, nchunks = 64 * nbw;
+    bool bch_done = false;
+#if FEC_BCH_COOP && FEC_BCH_TAB
+    if (nbw == 1) {
+      // wave 0 divides the 64 chunks while waves 1..3 lay out the LDPC info groups without parity;
+      // then the whole workgroup shares the combine's table lookups (bch_coop_sum)
+      uint64_t *rem = (uint64_t *)(smem + SM_D + fec_rem_off(ngroups));
+      if (wave == 0) {
+#if FEC_BCH_PRIO
+        __builtin_amdgcn_s_setprio(FEC_BCH_PRIO);
+#endif
+        uint64_t r0 = 0, r1 = 0, r2 = 0;
+        const int C = d.chunk, lo = L - (64 - lane) * C, hi = L - (63 - lane) * C;
+        switch (P) {
+          case 192: bch_divide<192>(frame, btab, lo, hi, r0, r1, r2); break;
+          case 168: bch_divide<168>(frame, btab, lo, hi, r0, r1, r2); break;
+          case 160: bch_divide<160>(frame, btab, lo, hi, r0, r1, r2); break;
+          default: bch_divide<128>(frame, btab, lo, hi, r0, r1, r2); break;
+        }
+        rem[3 * lane] = r0;
+        rem[3 * lane + 1] = r1;
+        rem[3 * lane + 2] = r2;
+#if FEC_BCH_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
+      } else if (MODE == FEC_TS_TO_TEMPU || MODE == FEC_TS_TO_PAIRS) {
+        for (int it = tid - 64; it < (ngroups - 1) * FEC_DW; it += FEC_THREADS - 64) {
+          const int g = it / FEC_DW;
+          ldpc_group_word(D, frame, g, it - g * FEC_DW);
+        }
+      }
+      __syncthreads();
+      switch (P) {
+        case 192: bch_coop_sum<192>(rem, d.bch_ctab, wres, tid); break;
+        case 168: bch_coop_sum<168>(rem, d.bch_ctab, wres, tid); break;
+        case 160: bch_coop_sum<160>(rem, d.bch_ctab, wres, tid); break;
+        default: bch_coop_sum<128>(rem, d.bch_ctab, wres, tid); break;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        const uint64_t acc[3] = {wres[0] ^ wres[3] ^ wres[6] ^ wres[9], wres[1] ^ wres[4] ^ wres[7] ^ wres[10],
+                                 wres[2] ^ wres[5] ^ wres[8] ^ wres[11]};
+        if (lane < P / 8) frame[L + lane] = get_byte192(acc, P - 8 - 8 * lane);
+        if (MODE == FEC_TS_TO_TEMPU || MODE == FEC_TS_TO_PAIRS) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          if (lane < FEC_DW) ldpc_group_word(D, frame, ngroups - 1, lane);
+        }
+      }
+      bch_done = true;
+    }
+#endif
+    if (!bch_done) {
 #if FEC_BCH_PRIO
     if (wave < nbw) __builtin_amdgcn_s_setprio(FEC_BCH_PRIO);   // the BCH is the block's critical path
 #endif
@@ -639,6 +761,7 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
 #if FEC_BCH_PRIO
     if (wave < nbw) __builtin_amdgcn_s_setprio(0);
 #endif
+    }
     __syncthreads();
     FEC_PHASE(6);
     FEC_PHASE(7);
@@ -873,6 +996,13 @@ __device__ __forceinline__ int xcd_major(int i, int n) {
 #ifndef MAP_VARIANT
 #define MAP_VARIANT 0
 #endif
+#ifndef MAP_SKIP
+#define MAP_SKIP 0     // experiment switch (wrong output): bit 0 = no TI store, 1 = no cell interleave, 2 = no demux
+#endif
+#ifndef MAP_RMAJOR
+#define MAP_RMAJOR 0   // experiment switch (measured: map neutral, OFDM +7 %, dropped): 1 = blocks in r-major
+                      // logical order (see map_kernel); 0 = frame-major
+#endif
 #if MAP_VARIANT & 1
 __shared__ uint64_t g_map_ts[8];
 #define MAP_PHASE(i) do { if (threadIdx.x == 0) g_map_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -973,7 +1103,7 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
   // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
   constexpr int MB = MAP_MB;
-  for (int j0 = tid; j0 < cs; j0 += MB * NT) {
+  for (int j0 = tid; j0 < ((MAP_SKIP & 2) ? 0 : cs); j0 += MB * NT) {
     int t[MB];
 #pragma unroll
     for (int u = 0; u < MB; u++) {
@@ -998,7 +1128,7 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
   // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
   const int16_t *pr = d.part ? d.part + (int64_t)r * cs : nullptr;   // block-major int16 table
-  for (int j0 = tid; j0 < cs; j0 += MB * NT) {
+  for (int j0 = tid; j0 < ((MAP_SKIP & 1) ? 0 : cs); j0 += MB * NT) {
     uint32_t dsl[MB];
     int tt[MB];
 #pragma unroll
@@ -1182,7 +1312,13 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io, L1
     if ((int)blockIdx.x < l1io.nframes) l1post_frame(l1d, l1io, blockIdx.x, (uint32_t *)smem);
     return;
   }
-  const int blk = xcd_major((int)blockIdx.x - nl1, (int)gridDim.x - nl1);
+  int blk = xcd_major((int)blockIdx.x - nl1, (int)gridDim.x - nl1);
+  if (MAP_RMAJOR && io.apply_ci && io.nblocks % d.F == 0) {
+    // logical order r-major over (block-in-frame r, frame): each XCD's contiguous share covers a
+    // few r for every frame, so the r-indexed partition rows it reads stay in its L2
+    const int nf = io.nblocks / d.F, r = blk / nf;
+    blk = (blk - r * nf) * d.F + r;
+  }
   float2 *lut = (float2 *)smem;
   uint8_t *idx = smem + 2048;
   uint8_t *cw = smem + 2048 + map_idx_bytes(d.cs);
@@ -1216,7 +1352,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io, L1
   }
   __syncthreads();
   MAP_PHASE(1);
-  map_cells<MAP_THREADS>(d, cww, idx, tid);
+  if (!(MAP_SKIP & 4)) map_cells<MAP_THREADS>(d, cww, idx, tid);
   __syncthreads();
   MAP_PHASE(2);
   // ---- constellation + cyclic Q delay; chain: cell interleaver (framemapper:1973-1998) on the
@@ -1796,7 +1932,10 @@ constexpr int O32_DATA = (O32_H + (O32_H >> O32_PS) + 64) * 8;   // padded half 
 constexpr int O32_TW1K = O32_DATA;                                // w_1024^m, m < 1024
 constexpr int O32_TW2 = O32_TW1K + 1024 * 8;                      // two-level table, 128 + 256
 constexpr int O32_QAM = O32_TW2 + 384 * 8;                        // constellation re[256], im[256]
-constexpr int O32_LDS = O32_QAM + 256 * 8;
+                                                                  // (code mode: value table re[512], im[512])
+constexpr int O32_LDS = O32_QAM + 512 * 8;
+constexpr uint32_t O32_HALF_SLOTS = O32_H + (O32_H >> O32_PS);   // half 1's padded bins start here (code mode)
+static_assert((2 * O32_HALF_SLOTS + 64) * 4 <= O32_DATA, "code-mode slots fit the data area");
 static_assert(O32_LDS <= 160 * 1024, "32K OFDM LDS");
 static_assert((16384 + 2 * 32) * 8 <= O32_DATA, "exchange slots fit the data area");
 
@@ -1879,6 +2018,81 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
   }
 }
 
+// Exchange with 16-byte LDS slots (O32_XCHG128, the default).  Thread t <-> a = t4 | t3 << 1 |
+// t[6..7] << 2 | t8 << 4, b = t5 | t[0..2] << 1 | t9 << 4 (o32_ta / o32_tb), so b's bit 0 pairs lanes
+// l, l ^ 32 and a's bit 0 lanes l, l ^ 16.  Before exchange 1 the lanes b, b ^ 1 swap v[r + 1] of the
+// lower lane with v[r] of the upper one (v_permlane32_swap): each lane then holds, per even r, the
+// two values (m1 = 2p, 2p + 1) of one n2 = r + b0, which is the pair the reader wants in adjacent
+// registers.  Exchange 2 does the same on a's bit 0 (v_permlane16_swap, pairs m0 = 2p, 2p + 1 of one
+// n1).  Both sides then move 16 bytes per lane (ds_write_b128 / ds_read_b128), half the LDS
+// instructions of 8-byte slots, and the wide stores reach their rate with few waves per SIMD.
+// A half holds 512 rows x 16 slots of 16 bytes (128 KB, no padding): row = (kept coordinate & 15)
+// + 16 * (the coordinate that travels with r), column = pair index ^ g, g = ((n2 >> 1) & 7) |
+// (bit 1 of the remaining coordinate) << 3, which puts every lane group of ds_write_b128 (8 lanes,
+// t0..t2) and of ds_read_b128 (16 lanes over t0..t4) on distinct banks (MI355X_MICROARCH.md LDS).
+#ifndef O32_XCHG128
+#define O32_XCHG128 0   // experiment switch (measured: +3 % OFDM time, dropped): 1 = 16-byte slots and the lane
+                       // mapping above; 0 = 8-byte slots, lanes b = t[0..3]
+#endif
+__device__ __forceinline__ uint32_t o32_ta(uint32_t t) {
+  if (O32_XCHG128) return ((t >> 4) & 1u) | (((t >> 3) & 1u) << 1) | (((t >> 6) & 3u) << 2) | (((t >> 8) & 1u) << 4);
+  return ((t >> 4) & 15u) | (((t >> 8) & 1u) << 4);
+}
+__device__ __forceinline__ uint32_t o32_tb(uint32_t t) {
+  if (O32_XCHG128) return ((t >> 5) & 1u) | ((t & 7u) << 1) | (((t >> 9) & 1u) << 4);
+  return (t & 15u) | (((t >> 9) & 1u) << 4);
+}
+// swap the upper lanes' lo with the lower lanes' hi across lane bit 5 (W = 32) or 4 (W = 16)
+template <int W>
+__device__ __forceinline__ void lane_pair_swap(float2 &lo, float2 &hi) {
+  uint32_t x0 = __float_as_uint(lo.x), x1 = __float_as_uint(hi.x), y0 = __float_as_uint(lo.y), y1 = __float_as_uint(hi.y);
+  if (W == 32) {
+    const auto sx = __builtin_amdgcn_permlane32_swap(x0, x1, false, false);
+    const auto sy = __builtin_amdgcn_permlane32_swap(y0, y1, false, false);
+    x0 = sx[0]; x1 = sx[1]; y0 = sy[0]; y1 = sy[1];
+  } else {
+    const auto sx = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(y0, y1, false, false);
+    x0 = sx[0]; x1 = sx[1]; y0 = sy[0]; y1 = sy[1];
+  }
+  lo = make_float2(__uint_as_float(x0), __uint_as_float(y0));
+  hi = make_float2(__uint_as_float(x1), __uint_as_float(y1));
+}
+template <int SPLIT>
+__device__ __forceinline__ void o32_exchange128(float2 *v, float2 *lds, uint32_t tid, uint32_t a, uint32_t b) {
+#pragma unroll
+  for (int r = 0; r < 32; r += 2) lane_pair_swap<SPLIT == 8 ? 32 : 16>(v[r], v[r + 1]);
+  float4 *x = (float4 *)lds;
+  const uint32_t lo = SPLIT == 8 ? (b & 1u) : (a & 1u);
+  const uint32_t a1 = (a >> 1) & 1u;
+  const uint32_t rbase = 16u * (SPLIT == 8 ? (a & 15u) + 16u * b : (b & 15u) + 16u * a);
+  const uint32_t rg = ((b >> 1) & 7u) | (a1 << 3);
+#pragma unroll
+  for (uint32_t h = 0; h < 2; h++) {
+    __syncthreads();
+    const bool mine = ((tid >> SPLIT) & 1u) == h;
+    if (mine) {
+#pragma unroll
+      for (uint32_t r = 0; r < 32; r += 2) {
+        const uint32_t n = r + lo;
+        const uint32_t row = (SPLIT == 8 ? (a & 15u) : (b & 15u)) + 16u * n;
+        const uint32_t g = SPLIT == 8 ? (((n >> 1) & 7u) | (a1 << 3)) : (((b >> 1) & 7u) | (((n >> 1) & 1u) << 3));
+        const uint32_t col = ((SPLIT == 8 ? b : a) >> 1) ^ g;
+        x[16u * row + col] = make_float4(v[r].x, v[r].y, v[r + 1].x, v[r + 1].y);
+      }
+    }
+    __syncthreads();
+    if (mine) {
+#pragma unroll
+      for (uint32_t q = 0; q < 16; q++) {
+        const float4 f = x[rbase + (q ^ rg)];
+        v[2 * q] = make_float2(f.x, f.y);
+        v[2 * q + 1] = make_float2(f.z, f.w);
+      }
+    }
+  }
+}
+
 // stages A, B, C with the two exchanges: v[r] = bin kin + 1024 r on entry (kin = a + 32 b), sample
 // b + 32 a + 1024 r on exit.  Every thread is past its last LDS access of the symbol on return.
 __device__ __forceinline__ void o32_fft(float2 *v, float2 *lds, const float2 *tw1k, const float2 *tw2, uint32_t tid,
@@ -1892,14 +2106,14 @@ __device__ __forceinline__ void o32_fft(float2 *v, float2 *lds, const float2 *tw
     return cmulf(tw2[128 + (i >> 7)], tw2[i & 127u]);
   });
   OFDM_PHASE(3);
-  o32_exchange<8>(v, lds, tid, ta, tb);
+  if (O32_XCHG128) o32_exchange128<8>(v, lds, tid, ta, tb); else o32_exchange<8>(v, lds, tid, ta, tb);
   OFDM_PHASE(4);
   // stage B: DFT over m1, twiddle w_1024^(m0 n1) = w_1024^(a r)
   __builtin_amdgcn_sched_barrier(0);
   Dft<32>::run(v);
   o32_twiddle(v, [&](int k) { return tw1k[(ta * (uint32_t)k) & 1023u]; });
   OFDM_PHASE(5);
-  o32_exchange<9>(v, lds, tid, ta, tb);
+  if (O32_XCHG128) o32_exchange128<9>(v, lds, tid, ta, tb); else o32_exchange<9>(v, lds, tid, ta, tb);
   OFDM_PHASE(6);
   // stage C: DFT over m0 -> x[b + 32 a + 1024 r]
   __builtin_amdgcn_sched_barrier(0);
@@ -1931,6 +2145,19 @@ __device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT
   constexpr uint32_t N = 32768;
   const bool odd = nout & 1u;
   const uint32_t n0 = nout & ~1u;
+  if (O32_XCHG128) {
+    // b's bit 0 is lane bit 5: after the swap the lower lane holds samples (b, b + 1) of r = 2k and
+    // the upper lane those of r = 2k + 1, with no select
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+      float2 e = cscale(cscale(v[2 * k], nrm), o.gain), d = cscale(cscale(v[2 * k + 1], nrm), o.gain);
+      lane_pair_swap<32>(e, d);
+      const uint32_t n = n0 + 1024u * (2u * k + (odd ? 1u : 0u));
+      o.put2((uint32_t)G + n, e, d);
+      if (n >= N - (uint32_t)G) o.put2(n - (N - (uint32_t)G), e, d);
+    }
+    return;
+  }
 #pragma unroll
   for (uint32_t k = 0; k < 16; k++) {
     const float2 e = cscale(cscale(v[2 * k], nrm), o.gain), d = cscale(cscale(v[2 * k + 1], nrm), o.gain);
@@ -1943,6 +2170,67 @@ __device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT
   }
 }
 
+#ifndef O32_CODES
+#define O32_CODES 0   // experiment switch (measured: bit-exact, OFDM 0.413 -> 0.440 ms, dropped): 1 = single-
+                      // pass scatter of 4-byte value codes for symbols without L1-post cells
+#endif
+// Code-mode scatter of a whole 32K symbol (both halves in one pass): every bin's LDS word is a value
+// code re | im << 9 (t2_capi: vtab = constellation, then the direct aux values), so the words are
+// 4 bytes and the symbol's 32768 bins (with one pad word per 32) fit the LDS at once; the
+// constellation lookup moves to the read-back.  Half 1's stored bins are offset by O32_HALF_SLOTS,
+// which makes the word of bin k sit at o32_bin(k) over the whole symbol.
+__device__ __forceinline__ void o32_scatter_codes(uint32_t *c32, const OfdmDev &d, const uint16_t *pairs, uint32_t cbase,
+                                                  int j, uint32_t tid) {
+  constexpr uint32_t NT = O32_NT;
+  const uint32_t dummy = 2u * O32_HALF_SLOTS + (tid & 63u);
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int2 zr = d.azr[2 * j + h];
+    const uint32_t off = h ? O32_HALF_SLOTS : 0u;
+    for (uint32_t i = (uint32_t)zr.x + tid; i < (uint32_t)zr.y; i += NT) c32[off + i] = d.zcode;
+  }
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int4 gr = d.agrp[2 * j + h];
+    const uint32_t off = h ? O32_HALF_SLOTS : 0u;
+    for (uint32_t q = tid; q < (uint32_t)gr.y >> 2; q += NT) {
+      const uint32_t e0 = (uint32_t)gr.x + 4u * q;
+      const uint2 b = ld_off((const uint2 *)d.abin, e0 * 2u);
+      const uint4 c = ld_off((const uint4 *)d.acode, e0 * 4u);
+      const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
+      c32[k0 != 0xFFFFu ? off + k0 : dummy] = c.x;
+      c32[k1 != 0xFFFFu ? off + k1 : dummy] = c.y;
+      c32[k2 != 0xFFFFu ? off + k2 : dummy] = c.z;
+      c32[k3 != 0xFFFFu ? off + k3 : dummy] = c.w;
+    }
+  }
+  const uint32_t r0 = (uint32_t)d.sym_d0[j], rn = (uint32_t)d.sym_n[j], h1 = r0 + (uint32_t)d.sym_n0[j];
+  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2, lastq = nq - 1u;
+  constexpr int SQ = 4;
+  for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
+    uint2 b[SQ], c[SQ];
+#pragma unroll
+    for (int u = 0; u < SQ; u++) {
+      const uint32_t s = q0 + 4u * min(g0 + tid + NT * (uint32_t)u, lastq);
+      b[u] = ld_off((const uint2 *)d.inv, s * 2u);
+      c[u] = ld_off((const uint2 *)pairs, (cbase + s) * 2u);
+    }
+#pragma unroll
+    for (int u = 0; u < SQ; u++) {
+      const uint32_t s = q0 + 4u * min(g0 + tid + NT * (uint32_t)u, lastq);
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
+        const uint32_t se = s + (uint32_t)e;
+        const uint32_t bin = ((bw >> (16 * (e & 1))) & 0xFFFFu) + (se >= h1 ? O32_HALF_SLOTS : 0u);
+        const uint32_t pr = cw >> (16 * (e & 1));
+        const uint32_t code = (pr & 0xFFu) | (((pr >> 8) & 0xFFu) << 9);
+        c32[se - r0 < rn ? bin : dummy] = code;
+      }
+    }
+  }
+}
+
 // 32K symbols, one workgroup per (symbol, frame): scatter mode (the fused chain), gather mode (the
 // pilotgen block: cells already in carrier order) and the carriers-only test hook
 template <int FMT>
@@ -1952,8 +2240,7 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   float2 *lds = (float2 *)smem;
   float2 *tw1k = (float2 *)(smem + O32_TW1K), *tw2 = (float2 *)(smem + O32_TW2);
   const int tid = threadIdx.x;
-  const uint32_t ta = (((uint32_t)tid >> 4) & 15u) | ((((uint32_t)tid >> 8) & 1u) << 4);
-  const uint32_t tb = ((uint32_t)tid & 15u) | ((((uint32_t)tid >> 9) & 1u) << 4);
+  const uint32_t ta = o32_ta((uint32_t)tid), tb = o32_tb((uint32_t)tid);
   const uint32_t kin = ta + 32u * tb;             // stage-A input bins kin + 1024 r
   const int u = xcd_major(blockIdx.x, gridDim.x);
   const int j = u / io.nframes;                   // symbol
@@ -1987,7 +2274,26 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   const float2 t1k = d.twiddle1k[tid];
   const float2 t2 = tid < 384 ? d.twiddle[tid] : make_float2(0.f, 0.f);
   float2 v[32];
-  if (d.inv) {
+  if (O32_CODES && d.inv && d.acode && d.sym_code[j]) {
+    // code mode: the whole symbol's value codes in one pass, values looked up at the read-back
+    uint32_t *c32 = (uint32_t *)smem;
+    float *vre = (float *)(smem + O32_QAM), *vim = vre + 512;
+    const float2 tv0 = d.vtab[tid & 511];
+    o32_scatter_codes(c32, d, io.pairs, cbase, j, (uint32_t)tid);
+    if (tid < 512) {
+      vre[tid] = tv0.x;
+      vim[tid] = tv0.y;
+    }
+    tw1k[tid] = t1k;
+    if (tid < 384) tw2[tid] = t2;
+    __syncthreads();
+    OFDM_PHASE(1);
+#pragma unroll
+    for (uint32_t r = 0; r < 32; r++) {
+      const uint32_t c = c32[o32_bin(kin + 1024u * r)];
+      v[r] = make_float2(vre[c & 511u], vim[c >> 9]);
+    }
+  } else if (d.inv) {
     // scatter mode, one half of the bins (m2 < 16, then m2 >= 16) at a time
     float *qre = (float *)(smem + O32_QAM), *qim = qre + 256;
     const float2 tq = tid < 256 ? d.qam[tid] : make_float2(0.f, 0.f);
