@@ -784,7 +784,9 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if ((r = h->fec.init(f.framesize, f.rate, f.constellation, f.inputmode, f.inband, f.fecblocks, p->tsrate)))
     return r;
   if ((r = h->map.init(f.framesize, f.rate, f.constellation, f.rotation, h->fec.plan))) return r;
-  if ((r = upload(h->perm, h->frame.ci_perm)) || (r = upload(h->shift, h->frame.ci_shift))) return r;
+  std::vector<int16_t> cip(h->frame.ci_perm.begin(), h->frame.ci_perm.end());
+  cip.resize(((cip.size() + 3) & ~(size_t)3) + 4, 0);   // the map kernel reads aligned quads
+  if ((r = upload(h->perm, cip)) || (r = upload(h->shift, h->frame.ci_shift))) return r;
   h->map.dev.ci_perm = h->perm.as<int16_t>();
   h->map.dev.ci_shift = h->shift.as<int32_t>();
   h->map.dev.F = h->frame.F;
@@ -808,16 +810,18 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
     // reorder to the map kernel's store order: block r, index j = 5 row + e (TI on) or t
     const FramePlan &fp = h->frame;
     // stored as int16 deltas from the TI position (a cell only moves within its symbol)
-    std::vector<int16_t> pb((size_t)fp.S);
+    const int csp = (fp.cs + 3) & ~3;   // rows padded for the kernel's aligned quad loads
+    std::vector<int16_t> pb((size_t)fp.F * csp + 4, 0);
     for (int rr = 0; rr < fp.F; rr++)
       for (int jj = 0; jj < fp.cs; jj++) {
         const int t = fp.ti_on ? (jj % 5) * (fp.cs / 5) + jj / 5 : jj;
         const int64_t s = ti_dest(fp, rr, t), delta = layout.part[s] - s;
         if (delta < INT16_MIN || delta > INT16_MAX) return DVBT2LL_EINVAL;
-        pb[(size_t)rr * fp.cs + jj] = (int16_t)delta;
+        pb[(size_t)rr * csp + jj] = (int16_t)delta;
       }
     if ((r = upload(h->part, pb))) return r;
     h->map.dev.part = h->part.as<int16_t>();
+    h->map.dev.part_stride = csp;
   }
   const PilotPlan &pp = h->pilot;
   // one aux row (pilot values, L1-pre, dummy cells): the L1-post cells come per frame from the GPU

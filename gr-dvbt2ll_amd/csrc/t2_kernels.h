@@ -75,7 +75,9 @@ struct MapDev {
   const int32_t *ci_shift; // F  (chain only)
   int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
-  const int16_t *part;     // chain, 32K only: slot - TI position of (block r, TI-store index j), at r*cs + j
+  const int16_t *part;     // chain, 32K only: slot - TI position of (block r, TI-store index j), at
+                           // r*part_stride + j (rows padded to a multiple of 4 for 8-byte quad loads)
+  int part_stride;
   uint8_t twist[16], mux[16];
   uint8_t colsel[16];      // column e whose bit lands at position b of the row word (W-1-mux[e] = b), 255: none
 };

@@ -999,6 +999,9 @@ __device__ __forceinline__ int xcd_major(int i, int n) {
 #ifndef MAP_SKIP
 #define MAP_SKIP 0     // experiment switch (wrong output): bit 0 = no TI store, 1 = no cell interleave, 2 = no demux
 #endif
+#ifndef MAP_QUADS
+#define MAP_QUADS 1    // 1: TI store with quad loads of the partition deltas (see map_store_pairs)
+#endif
 #ifndef MAP_RMAJOR
 #define MAP_RMAJOR 0   // experiment switch (measured: map neutral, OFDM +7 %, dropped): 1 = blocks in r-major
                       // logical order (see map_kernel); 0 = frame-major
@@ -1103,6 +1106,37 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
   // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
   constexpr int MB = MAP_MB;
+  if (MAP_QUADS) {
+    // four consecutive cells per thread: one 8-byte load of their permutation entries and one
+    // 4-byte LDS read of their indices (plus the previous cell's byte for the rotation)
+    constexpr int MQ = MB / 2;
+    const int nq = (cs + 3) >> 2;
+    const uint32_t *idxw = (const uint32_t *)idx;
+    for (int q0 = tid; q0 < ((MAP_SKIP & 2) ? 0 : nq); q0 += MQ * NT) {
+      uint2 pq[MQ];
+#pragma unroll
+      for (int u = 0; u < MQ; u++) pq[u] = ld_off((const uint2 *)d.ci_perm, (uint32_t)min(q0 + u * NT, nq - 1) * 8u);
+#pragma unroll
+      for (int u = 0; u < MQ; u++) {
+        const int q = q0 + u * NT;
+        if (q < nq) {
+          const uint32_t w = idxw[q];
+          uint32_t prev = idx[q == 0 ? cs - 1 : 4 * q - 1];
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int j = 4 * q + k;
+            const uint32_t lo = (w >> (8 * k)) & 0xFFu, hi = d.rotation ? prev : lo;
+            prev = lo;
+            if (j < cs) {
+              int tt = (int)(int16_t)(((k < 2 ? pq[u].x : pq[u].y) >> (16 * (k & 1))) & 0xFFFFu) + shift;
+              tt = tt >= cs ? tt - cs : tt;
+              stage[tt] = (uint16_t)(lo | (hi << 8));
+            }
+          }
+        }
+      }
+    }
+  } else
   for (int j0 = tid; j0 < ((MAP_SKIP & 2) ? 0 : cs); j0 += MB * NT) {
     int t[MB];
 #pragma unroll
@@ -1127,7 +1161,37 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   // rotated-constellation Q delay) is fused into the OFDM kernel's bin scatter
   const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
   // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
-  const int16_t *pr = d.part ? d.part + (int64_t)r * cs : nullptr;   // block-major int16 table
+  const int16_t *pr = d.part ? d.part + (int64_t)r * d.part_stride : nullptr;   // block-major int16 table
+  if (MAP_QUADS && pr) {
+    // four consecutive TI-store indices per thread: one 8-byte load of their partition deltas
+    // instead of four 2-byte loads (the memory instruction count, not the bytes, sets this loop's
+    // rate; the pair stores stay 2 bytes per cell)
+    constexpr int MQ = MB / 2;
+    const int nq = (cs + 3) >> 2;
+    for (int q0 = tid; q0 < ((MAP_SKIP & 1) ? 0 : nq); q0 += MQ * NT) {
+      uint2 pq[MQ];
+#pragma unroll
+      for (int u = 0; u < MQ; u++) pq[u] = ld_off((const uint2 *)pr, (uint32_t)min(q0 + u * NT, nq - 1) * 8u);
+#pragma unroll
+      for (int u = 0; u < MQ; u++) {
+        const int q = q0 + u * NT;
+        if (q < nq) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) {
+            const int j = 4 * q + k;
+            if (j < cs) {
+              const int row = j / 5, e = j - 5 * row;
+              const int tt = d.ti_on ? e * rows + row : j, oo = d.ti_on ? row * cols + e : j;
+              const int16_t dl = (int16_t)(((k < 2 ? pq[u].x : pq[u].y) >> (16 * (k & 1))) & 0xFFFFu);
+              const uint32_t o = (uint32_t)fbase + (uint32_t)oo + (uint32_t)(int)dl;
+              st_off(dst, o * 2u, stage[tt]);
+            }
+          }
+        }
+      }
+    }
+    return;
+  }
   for (int j0 = tid; j0 < ((MAP_SKIP & 1) ? 0 : cs); j0 += MB * NT) {
     uint32_t dsl[MB];
     int tt[MB];
@@ -1391,6 +1455,10 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1D
 }
 
 // ============================================================================ OFDM kernels
+#ifndef O32_FASTQ
+#define O32_FASTQ 0   // experiment switch (measured: OFDM +1.5 %, dropped): 1 = range checks only on the edge
+                      // quads of a scatter run, no gain multiply at gain 1
+#endif
 #ifndef OFDM_SQ16
 #define OFDM_SQ16 8   // data-slot quads per thread per scatter round (N <= 16K)
 #endif
@@ -1641,14 +1709,27 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
 #pragma unroll
     for (int u = 0; u < SQ; u++) {
       const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
+      // interior quads (all four slots in the run: every quad but the run's first and last) skip
+      // the per-slot range checks
+      const bool full = O32_FASTQ && s - r0 < rn && s + 3u - r0 < rn;
+      if (full) {
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
-        const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the group
-        const uint32_t pr = cw >> (16 * (e & 1));
-        const bool in_run = s + (uint32_t)e - r0 < rn;
-        const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-        lds[in_run ? bin : dummy] = v;
+        for (int e = 0; e < 4; e++) {
+          const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
+          const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;
+          const uint32_t pr = cw >> (16 * (e & 1));
+          lds[bin] = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
+          const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the group
+          const uint32_t pr = cw >> (16 * (e & 1));
+          const bool in_run = s + (uint32_t)e - r0 < rn;
+          const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+          lds[in_run ? bin : dummy] = v;
+        }
       }
     }
   }
@@ -2145,6 +2226,20 @@ __device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT
   constexpr uint32_t N = 32768;
   const bool odd = nout & 1u;
   const uint32_t n0 = nout & ~1u;
+  if (O32_FASTQ && o.gain == 1.f && !O32_XCHG128) {
+    // the block's own output (gain 1, the multiply is exact): one multiply per value
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+      const float2 e = cscale(v[2 * k], nrm), d = cscale(v[2 * k + 1], nrm);
+      const float2 re = make_float2(swap_adjacent_lane(e.x), swap_adjacent_lane(e.y));
+      const float2 rd = make_float2(swap_adjacent_lane(d.x), swap_adjacent_lane(d.y));
+      const float2 lo = odd ? rd : e, hi = odd ? d : re;
+      const uint32_t n = n0 + 1024u * (2u * k + (odd ? 1u : 0u));
+      o.put2((uint32_t)G + n, lo, hi);
+      if (n >= N - (uint32_t)G) o.put2(n - (N - (uint32_t)G), lo, hi);
+    }
+    return;
+  }
   if (O32_XCHG128) {
     // b's bit 0 is lane bit 5: after the swap the lower lane holds samples (b, b + 1) of r = 2k and
     // the upper lane those of r = 2k + 1, with no select
