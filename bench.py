@@ -291,9 +291,10 @@ def cpu_baseline(cfg, seconds, all_configs=True):
     return out
 
 
-def per_block_rate(cfg, frames=6):
+def per_block_rate(cfg, frames=6, pinned=False):
     """the drop-in path GNU Radio would drive: the five blocks' C-ABI general_work calls on host
-    (pageable numpy) buffers, one T2 frame per framemapper / pilotgen call, each call synchronous
+    buffers (pageable numpy, or page-locked with `pinned`: the DMA then reads / writes the caller's
+    buffers directly), one T2 frame per framemapper / pilotgen call, each call synchronous
     (H2D + kernels + D2H); secondary figure, not `value`"""
     import numpy as np
     import dvbt2ll
@@ -303,10 +304,21 @@ def per_block_rate(cfg, frames=6):
     im = dvbt2ll.interleavermod_bc(*cfg.im_args()); fm = dvbt2ll.framemapperfint_cc(*cfg.fm_args())
     pg = dvbt2ll.pilotgenp1insert_cc(*cfg.pg_args())
     nbch, nldpc, cs = bb.output_multiple(), ld.output_multiple(), im.output_multiple()
-    bits = np.zeros(F * nbch, np.uint8); cw = np.zeros(F * nldpc, np.uint8)
-    cells = np.zeros(F * cs, np.complex64); mapped = np.zeros(fm.output_multiple(), np.complex64)
-    iq = np.zeros(pg.output_multiple(), np.complex64)
+
+    def host(n, dt):
+        if not pinned:
+            return np.zeros(n, dt)
+        import torch
+        tdt = {np.uint8: torch.uint8, np.complex64: torch.complex64}[dt]
+        return torch.zeros(n, dtype=tdt).pin_memory().numpy()
+    bits = host(F * nbch, np.uint8); cw = host(F * nldpc, np.uint8)
+    cells = host(F * cs, np.complex64); mapped = host(fm.output_multiple(), np.complex64)
+    iq = host(pg.output_multiple(), np.complex64)
     ts, _ = ts_for_frames(cfg, 0, frames + 1)
+    if pinned:
+        tsp = host(len(ts), np.uint8)
+        tsp[:] = ts
+        ts = tsp
     off = 0
     names = ("bbheaderbch", "ldpc", "interleavermod", "framemapperfint", "pilotgenp1insert")
     tot = dict.fromkeys(names, 0.0)
@@ -323,12 +335,18 @@ def per_block_rate(cfg, frames=6):
                 tot[n] += t[i + 1] - t[i]
             t_all += t[-1] - t[0]
     per = len(iq)
+    hbytes = (len(ts) // (frames + 1) + 2 * bits.nbytes + 2 * cw.nbytes + 2 * cells.nbytes + 2 * mapped.nbytes
+              + iq.nbytes)
     return {"value": frames * per / t_all / 1e6, "unit": "Msamples/s", "frames": frames,
             "ms_per_frame": {n: v / frames * 1e3 for n, v in tot.items()},
             "x_realtime": frames * per / t_all / RT_SPS,
+            "host_bytes_per_frame": hbytes, "pcie_GBs": hbytes * frames / t_all / 1e9,
+            "host_buffers": "pinned" if pinned else "pageable",
             "note": "secondary: the per-block drop-in path (bbheaderbch -> ldpc -> interleavermod -> "
-                    "framemapperfint -> pilotgenp1insert general_work through the C ABI on pageable host "
-                    "buffers, synchronous per call, one stream); PCIe-bound, not `value`"}
+                    "framemapperfint -> pilotgenp1insert general_work through the C ABI on %s host "
+                    "buffers, synchronous per call, one stream); PCIe-bound (the blocks exchange unpacked "
+                    "bits and complex64 cells, as the reference's streams do), not `value`"
+                    % ("page-locked" if pinned else "pageable")}
 
 
 def one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per):
@@ -497,6 +515,7 @@ def main():
     blocks = None
     if not args.no_blocks and world == 1 and rank == 0:
         blocks = per_block_rate(cfg)
+        blocks["pinned"] = per_block_rate(cfg, pinned=True)
     gathered = None
     if dist and args.shard == "frames" and NS == 1:
         # secondary (not `value`): each step followed by the ordered IQ gather to rank 0, the

@@ -576,7 +576,6 @@ struct dvbt2ll_chain {
   OfdmTables ofdm;
   DevBuf aux, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
   DevBuf abin, aval, aind, agrp, azr;   // non-data bins as compact lists (t2_plan.h AuxLists)
-  DevBuf acode, vtab, sym_code;          // 32K code-mode scatter (ofdm32_kernel, O32_CODES)
   DevBuf sync_err;                      // TS sync bytes != 0x47 consumed by run calls (bbheader:675, 703)
   // intermediate buffer slots (codewords, index pairs): run calls take them round-robin, so
   // calls issued on different streams overlap; a slot reused on another stream first waits for
@@ -848,37 +847,6 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if ((r = upload(h->abin, al.dbin)) || (r = upload(h->aval, al.dval)) || (r = upload(h->aind, al.ind)) ||
       (r = upload(h->agrp, al.grp)) || (r = upload(h->azr, zr)))
     return r;
-  if (pp.N == 32768) {
-    // value codes for the single-pass 32K scatter: vtab = the constellation, then the distinct
-    // direct aux values (value 0 first); a symbol takes the code path when its groups have no
-    // indirect (per-frame L1-post) entries.  More than 256 distinct values: codes off.
-    std::vector<cf32> vt(h->map.plan.lut, h->map.plan.lut + 256);
-    std::vector<uint32_t> code(al.dval.size(), 0);
-    auto value_index = [&](const cf32 &x) -> int {
-      for (size_t i = 256; i < vt.size(); i++)
-        if (!std::memcmp(&vt[i], &x, sizeof(cf32))) return (int)i;
-      if (vt.size() >= 512) return -1;
-      vt.push_back(x);
-      return (int)vt.size() - 1;
-    };
-    bool ok = value_index(cf32{0.f, 0.f}) == 256;
-    for (size_t i = 0; ok && i < al.dval.size(); i++) {
-      const int vi = value_index(al.dval[i]);
-      if (vi < 0) ok = false;
-      else code[i] = (uint32_t)vi | ((uint32_t)vi << 9);
-    }
-    std::vector<int32_t> sc((size_t)pp.Nsym, 0);
-    for (int j = 0; ok && j < pp.Nsym; j++) sc[j] = al.grp[4 * (2 * j) + 3] == 0 && al.grp[4 * (2 * j + 1) + 3] == 0;
-    if (ok) {
-      vt.resize(512, cf32{0.f, 0.f});
-      code.resize(((code.size() + 3) & ~(size_t)3) + 4, 0);
-      if ((r = upload(h->acode, code)) || (r = upload(h->vtab, vt)) || (r = upload(h->sym_code, sc))) return r;
-      h->ofdm.dev.acode = h->acode.as<uint32_t>();
-      h->ofdm.dev.vtab = h->vtab.as<float2>();
-      h->ofdm.dev.sym_code = h->sym_code.as<int32_t>();
-      h->ofdm.dev.zcode = 256u | (256u << 9);
-    }
-  }
   h->ofdm.dev.abin = h->abin.as<uint16_t>();
   h->ofdm.dev.aval = h->aval.as<float2>();
   h->ofdm.dev.aind = h->aind.as<uint32_t>();

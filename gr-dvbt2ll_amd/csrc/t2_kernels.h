@@ -120,12 +120,6 @@ struct OfdmDev {
   const uint32_t *aind;     // indirect: padded bin | code << 15, value at aux abase + code
   const int4 *agrp;
   const int2 *azr;          // per group: padded LDS slot range [x, y) zeroed as a run (AuxLists::zrun)
-  // 32K scatter by value codes (symbols with sym_code[j] != 0): a bin's LDS word is re | im << 9,
-  // indices into vtab (512: the 256-entry constellation, then the distinct direct aux values)
-  const uint32_t *acode;    // per direct aux entry (parallel to abin); null: codes off
-  const float2 *vtab;
-  const int32_t *sym_code;
-  uint32_t zcode;           // the code of value 0 (zero runs)
   int N, G, Nsym, aux_len, t2frames;
   float norm;
   float gain;               // output gain after the normalisation (1 = pilotgen's own output)

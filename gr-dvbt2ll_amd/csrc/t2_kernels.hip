@@ -140,13 +140,6 @@ __shared__ uint64_t g_fec_ts[16];
 #ifndef FEC_BCH_TAB_JB
 #define FEC_BCH_TAB_JB 4  // table lookups in flight per lane (8: spills)
 #endif
-#ifndef FEC_BCH_COOP
-#define FEC_BCH_COOP 0   // experiment switch (measured: fec 0.30 -> 0.38 ms, dropped): 1 (one BCH wave, nibble
-                         // tables) = all four waves share the combine's lookups
-#endif
-#ifndef FEC_BCH_COOP_JB
-#define FEC_BCH_COOP_JB 4   // cooperative combine: table lookups in flight per thread
-#endif
 #ifndef FEC_BCH_PRIO
 #define FEC_BCH_PRIO 1   // wave priority (s_setprio) of the BCH wave while it runs (0: off)
 #endif
@@ -181,11 +174,7 @@ constexpr int SM_CRC8 = SM_RAW + ((FEC_RAW_BYTES + 15) & ~15);   // 256
 constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
 constexpr int SM_D = SM_PHASE;                               // rows follow D at word ngroups * 13
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
-// cooperative BCH combine (FEC_BCH_COOP): the 64 chunk remainders (3 words each) sit after D
-__host__ __device__ constexpr int fec_rem_off(int ngroups) { return (FEC_DW * 4 * ngroups + 15) & ~15; }
-constexpr int FEC_REM_BYTES = 64 * 3 * 8;
-constexpr int FEC_LDPC_AREA = FEC_LDPC_BYTES > fec_rem_off(150) + FEC_REM_BYTES ? FEC_LDPC_BYTES : fec_rem_off(150) + FEC_REM_BYTES;
-constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_AREA ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_AREA);
+constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_BYTES ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_BYTES);
 static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0 && SM_BLK % 16 == 0, "LDS carve alignment");
 static_assert(SM_SYNC % 8 == 0 && SM_BLK - SM_SYNC >= 4 * 3 * 8, "BCH wave remainders in SM_SYNC + SM_W");
 static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "FEC_WGS workgroups per CU");
@@ -288,46 +277,6 @@ __device__ __forceinline__ uint64_t wave_xor64(uint64_t x) {
   const uint32_t lo = rd_lane_u32(wave_prefix_xor((uint32_t)x), 63);
   const uint32_t hi = rd_lane_u32(wave_prefix_xor((uint32_t)(x >> 32)), 63);
   return ((uint64_t)hi << 32) | lo;
-}
-
-// Cooperative combine (one BCH wave): the chunk remainders r_l (rem, LDS, 3 words each) are moved
-// to the end of the 64 chunks, r_l x^(8C(63 - l)) mod g, as the XOR of P/4 nibble-table entries
-// each; the 64 (P/4) lookups are spread over the whole workgroup (thread t: lane l = t & 63, digits
-// j = t / 64 + 4 k), so each thread has P/16 of them instead of the BCH wave's P/4, and the
-// workgroup's partial sums are XOR-reduced (DPP wave scans, then wsum in LDS, 4 x 3 words)
-template <int P>
-__device__ __forceinline__ void bch_coop_sum(const uint64_t *rem, const uint64_t *ctab, uint64_t *wsum, int tid) {
-  constexpr int NJ = P / 4, K = (NJ + 3) / 4, JB = FEC_BCH_COOP_JB;
-  const int l = tid & 63, j0 = tid >> 6;
-  const uint64_t r0 = rem[3 * l], r1 = rem[3 * l + 1], r2 = rem[3 * l + 2];
-  uint64_t s0 = 0, s1 = 0, s2 = 0;
-#pragma unroll
-  for (int kb = 0; kb < K; kb += JB) {
-    uint4 e01[JB];
-    uint2 e2[JB];
-#pragma unroll
-    for (int u = 0; u < JB; u++) {
-      const int k = kb + u < K ? kb + u : K - 1;
-      const int j = j0 + 4 * k < NJ ? j0 + 4 * k : 0;   // out-of-range digits: a valid entry, masked below
-      const uint64_t rw = 4 * k < 16 ? r0 : 4 * k < 32 ? r1 : r2;   // j0 < 4: j's word is k's
-      const uint32_t v = (uint32_t)(rw >> (4 * (j & 15))) & 15u;
-      const uint32_t off = (((uint32_t)j * 16u + v) * 64u + (uint32_t)l) * 32u;
-      e01[u] = ld_off((const uint4 *)ctab, off);
-      e2[u] = ld_off((const uint2 *)ctab, off + 16u);
-    }
-#pragma unroll
-    for (int u = 0; u < JB; u++) {
-      const bool ok = kb + u < K && j0 + 4 * (kb + u) < NJ;
-      const uint32_t m = ok ? ~0u : 0u;
-      s0 ^= ((uint64_t)(e01[u].y & m) << 32) | (e01[u].x & m);
-      s1 ^= ((uint64_t)(e01[u].w & m) << 32) | (e01[u].z & m);
-      s2 ^= ((uint64_t)(e2[u].y & m) << 32) | (e2[u].x & m);
-    }
-  }
-  s0 = wave_xor64(s0);
-  s1 = wave_xor64(s1);
-  s2 = P > 128 ? wave_xor64(s2) : 0ull;
-  if ((tid & 63) < 3) wsum[3 * (tid >> 6) + (tid & 63)] = (tid & 63) == 0 ? s0 : (tid & 63) == 1 ? s1 : s2;
 }
 
 template <int P>
@@ -665,59 +614,6 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
     //      other waves meanwhile (chain mode) lay out the LDPC info groups that hold no BCH parity.
     const int ngroups = d.nbch / 360;
     const int nbw = d.bch_waves, nchunks = 64 * nbw;
-    bool bch_done = false;
-#if FEC_BCH_COOP && FEC_BCH_TAB
-    if (nbw == 1) {
-      // wave 0 divides the 64 chunks while waves 1..3 lay out the LDPC info groups without parity;
-      // then the whole workgroup shares the combine's table lookups (bch_coop_sum)
-      uint64_t *rem = (uint64_t *)(smem + SM_D + fec_rem_off(ngroups));
-      if (wave == 0) {
-#if FEC_BCH_PRIO
-        __builtin_amdgcn_s_setprio(FEC_BCH_PRIO);
-#endif
-        uint64_t r0 = 0, r1 = 0, r2 = 0;
-        const int C = d.chunk, lo = L - (64 - lane) * C, hi = L - (63 - lane) * C;
-        switch (P) {
-          case 192: bch_divide<192>(frame, btab, lo, hi, r0, r1, r2); break;
-          case 168: bch_divide<168>(frame, btab, lo, hi, r0, r1, r2); break;
-          case 160: bch_divide<160>(frame, btab, lo, hi, r0, r1, r2); break;
-          default: bch_divide<128>(frame, btab, lo, hi, r0, r1, r2); break;
-        }
-        rem[3 * lane] = r0;
-        rem[3 * lane + 1] = r1;
-        rem[3 * lane + 2] = r2;
-#if FEC_BCH_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
-      } else if (MODE == FEC_TS_TO_TEMPU || MODE == FEC_TS_TO_PAIRS) {
-        for (int it = tid - 64; it < (ngroups - 1) * FEC_DW; it += FEC_THREADS - 64) {
-          const int g = it / FEC_DW;
-          ldpc_group_word(D, frame, g, it - g * FEC_DW);
-        }
-      }
-      __syncthreads();
-      switch (P) {
-        case 192: bch_coop_sum<192>(rem, d.bch_ctab, wres, tid); break;
-        case 168: bch_coop_sum<168>(rem, d.bch_ctab, wres, tid); break;
-        case 160: bch_coop_sum<160>(rem, d.bch_ctab, wres, tid); break;
-        default: bch_coop_sum<128>(rem, d.bch_ctab, wres, tid); break;
-      }
-      __syncthreads();
-      if (wave == 0) {
-        const uint64_t acc[3] = {wres[0] ^ wres[3] ^ wres[6] ^ wres[9], wres[1] ^ wres[4] ^ wres[7] ^ wres[10],
-                                 wres[2] ^ wres[5] ^ wres[8] ^ wres[11]};
-        if (lane < P / 8) frame[L + lane] = get_byte192(acc, P - 8 - 8 * lane);
-        if (MODE == FEC_TS_TO_TEMPU || MODE == FEC_TS_TO_PAIRS) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (lane < FEC_DW) ldpc_group_word(D, frame, ngroups - 1, lane);
-        }
-      }
-      bch_done = true;
-    }
-#endif
-    if (!bch_done) {
 #if FEC_BCH_PRIO
     if (wave < nbw) __builtin_amdgcn_s_setprio(FEC_BCH_PRIO);   // the BCH is the block's critical path
 #endif
@@ -761,7 +657,6 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
 #if FEC_BCH_PRIO
     if (wave < nbw) __builtin_amdgcn_s_setprio(0);
 #endif
-    }
     __syncthreads();
     FEC_PHASE(6);
     FEC_PHASE(7);
@@ -1001,10 +896,6 @@ __device__ __forceinline__ int xcd_major(int i, int n) {
 #endif
 #ifndef MAP_QUADS
 #define MAP_QUADS 1    // 1: TI store with quad loads of the partition deltas (see map_store_pairs)
-#endif
-#ifndef MAP_RMAJOR
-#define MAP_RMAJOR 0   // experiment switch (measured: map neutral, OFDM +7 %, dropped): 1 = blocks in r-major
-                      // logical order (see map_kernel); 0 = frame-major
 #endif
 #if MAP_VARIANT & 1
 __shared__ uint64_t g_map_ts[8];
@@ -1376,13 +1267,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io, L1
     if ((int)blockIdx.x < l1io.nframes) l1post_frame(l1d, l1io, blockIdx.x, (uint32_t *)smem);
     return;
   }
-  int blk = xcd_major((int)blockIdx.x - nl1, (int)gridDim.x - nl1);
-  if (MAP_RMAJOR && io.apply_ci && io.nblocks % d.F == 0) {
-    // logical order r-major over (block-in-frame r, frame): each XCD's contiguous share covers a
-    // few r for every frame, so the r-indexed partition rows it reads stay in its L2
-    const int nf = io.nblocks / d.F, r = blk / nf;
-    blk = (blk - r * nf) * d.F + r;
-  }
+  const int blk = xcd_major((int)blockIdx.x - nl1, (int)gridDim.x - nl1);
   float2 *lut = (float2 *)smem;
   uint8_t *idx = smem + 2048;
   uint8_t *cw = smem + 2048 + map_idx_bytes(d.cs);
@@ -1455,10 +1340,6 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1D
 }
 
 // ============================================================================ OFDM kernels
-#ifndef O32_FASTQ
-#define O32_FASTQ 0   // experiment switch (measured: OFDM +1.5 %, dropped): 1 = range checks only on the edge
-                      // quads of a scatter run, no gain multiply at gain 1
-#endif
 #ifndef OFDM_SQ16
 #define OFDM_SQ16 8   // data-slot quads per thread per scatter round (N <= 16K)
 #endif
@@ -1709,27 +1590,14 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
 #pragma unroll
     for (int u = 0; u < SQ; u++) {
       const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
-      // interior quads (all four slots in the run: every quad but the run's first and last) skip
-      // the per-slot range checks
-      const bool full = O32_FASTQ && s - r0 < rn && s + 3u - r0 < rn;
-      if (full) {
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
-          const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;
-          const uint32_t pr = cw >> (16 * (e & 1));
-          lds[bin] = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
-          const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the group
-          const uint32_t pr = cw >> (16 * (e & 1));
-          const bool in_run = s + (uint32_t)e - r0 < rn;
-          const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-          lds[in_run ? bin : dummy] = v;
-        }
+      for (int e = 0; e < 4; e++) {
+        const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
+        const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the group
+        const uint32_t pr = cw >> (16 * (e & 1));
+        const bool in_run = s + (uint32_t)e - r0 < rn;
+        const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+        lds[in_run ? bin : dummy] = v;
       }
     }
   }
@@ -2013,10 +1881,7 @@ constexpr int O32_DATA = (O32_H + (O32_H >> O32_PS) + 64) * 8;   // padded half 
 constexpr int O32_TW1K = O32_DATA;                                // w_1024^m, m < 1024
 constexpr int O32_TW2 = O32_TW1K + 1024 * 8;                      // two-level table, 128 + 256
 constexpr int O32_QAM = O32_TW2 + 384 * 8;                        // constellation re[256], im[256]
-                                                                  // (code mode: value table re[512], im[512])
-constexpr int O32_LDS = O32_QAM + 512 * 8;
-constexpr uint32_t O32_HALF_SLOTS = O32_H + (O32_H >> O32_PS);   // half 1's padded bins start here (code mode)
-static_assert((2 * O32_HALF_SLOTS + 64) * 4 <= O32_DATA, "code-mode slots fit the data area");
+constexpr int O32_LDS = O32_QAM + 256 * 8;
 static_assert(O32_LDS <= 160 * 1024, "32K OFDM LDS");
 static_assert((16384 + 2 * 32) * 8 <= O32_DATA, "exchange slots fit the data area");
 
@@ -2226,20 +2091,6 @@ __device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT
   constexpr uint32_t N = 32768;
   const bool odd = nout & 1u;
   const uint32_t n0 = nout & ~1u;
-  if (O32_FASTQ && o.gain == 1.f && !O32_XCHG128) {
-    // the block's own output (gain 1, the multiply is exact): one multiply per value
-#pragma unroll
-    for (uint32_t k = 0; k < 16; k++) {
-      const float2 e = cscale(v[2 * k], nrm), d = cscale(v[2 * k + 1], nrm);
-      const float2 re = make_float2(swap_adjacent_lane(e.x), swap_adjacent_lane(e.y));
-      const float2 rd = make_float2(swap_adjacent_lane(d.x), swap_adjacent_lane(d.y));
-      const float2 lo = odd ? rd : e, hi = odd ? d : re;
-      const uint32_t n = n0 + 1024u * (2u * k + (odd ? 1u : 0u));
-      o.put2((uint32_t)G + n, lo, hi);
-      if (n >= N - (uint32_t)G) o.put2(n - (N - (uint32_t)G), lo, hi);
-    }
-    return;
-  }
   if (O32_XCHG128) {
     // b's bit 0 is lane bit 5: after the swap the lower lane holds samples (b, b + 1) of r = 2k and
     // the upper lane those of r = 2k + 1, with no select
@@ -2262,67 +2113,6 @@ __device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT
     const uint32_t n = n0 + 1024u * (2u * k + (odd ? 1u : 0u));
     o.put2((uint32_t)G + n, lo, hi);
     if (n >= N - (uint32_t)G) o.put2(n - (N - (uint32_t)G), lo, hi);
-  }
-}
-
-#ifndef O32_CODES
-#define O32_CODES 0   // experiment switch (measured: bit-exact, OFDM 0.413 -> 0.440 ms, dropped): 1 = single-
-                      // pass scatter of 4-byte value codes for symbols without L1-post cells
-#endif
-// Code-mode scatter of a whole 32K symbol (both halves in one pass): every bin's LDS word is a value
-// code re | im << 9 (t2_capi: vtab = constellation, then the direct aux values), so the words are
-// 4 bytes and the symbol's 32768 bins (with one pad word per 32) fit the LDS at once; the
-// constellation lookup moves to the read-back.  Half 1's stored bins are offset by O32_HALF_SLOTS,
-// which makes the word of bin k sit at o32_bin(k) over the whole symbol.
-__device__ __forceinline__ void o32_scatter_codes(uint32_t *c32, const OfdmDev &d, const uint16_t *pairs, uint32_t cbase,
-                                                  int j, uint32_t tid) {
-  constexpr uint32_t NT = O32_NT;
-  const uint32_t dummy = 2u * O32_HALF_SLOTS + (tid & 63u);
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const int2 zr = d.azr[2 * j + h];
-    const uint32_t off = h ? O32_HALF_SLOTS : 0u;
-    for (uint32_t i = (uint32_t)zr.x + tid; i < (uint32_t)zr.y; i += NT) c32[off + i] = d.zcode;
-  }
-#pragma unroll
-  for (int h = 0; h < 2; h++) {
-    const int4 gr = d.agrp[2 * j + h];
-    const uint32_t off = h ? O32_HALF_SLOTS : 0u;
-    for (uint32_t q = tid; q < (uint32_t)gr.y >> 2; q += NT) {
-      const uint32_t e0 = (uint32_t)gr.x + 4u * q;
-      const uint2 b = ld_off((const uint2 *)d.abin, e0 * 2u);
-      const uint4 c = ld_off((const uint4 *)d.acode, e0 * 4u);
-      const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
-      c32[k0 != 0xFFFFu ? off + k0 : dummy] = c.x;
-      c32[k1 != 0xFFFFu ? off + k1 : dummy] = c.y;
-      c32[k2 != 0xFFFFu ? off + k2 : dummy] = c.z;
-      c32[k3 != 0xFFFFu ? off + k3 : dummy] = c.w;
-    }
-  }
-  const uint32_t r0 = (uint32_t)d.sym_d0[j], rn = (uint32_t)d.sym_n[j], h1 = r0 + (uint32_t)d.sym_n0[j];
-  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2, lastq = nq - 1u;
-  constexpr int SQ = 4;
-  for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
-    uint2 b[SQ], c[SQ];
-#pragma unroll
-    for (int u = 0; u < SQ; u++) {
-      const uint32_t s = q0 + 4u * min(g0 + tid + NT * (uint32_t)u, lastq);
-      b[u] = ld_off((const uint2 *)d.inv, s * 2u);
-      c[u] = ld_off((const uint2 *)pairs, (cbase + s) * 2u);
-    }
-#pragma unroll
-    for (int u = 0; u < SQ; u++) {
-      const uint32_t s = q0 + 4u * min(g0 + tid + NT * (uint32_t)u, lastq);
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
-        const uint32_t se = s + (uint32_t)e;
-        const uint32_t bin = ((bw >> (16 * (e & 1))) & 0xFFFFu) + (se >= h1 ? O32_HALF_SLOTS : 0u);
-        const uint32_t pr = cw >> (16 * (e & 1));
-        const uint32_t code = (pr & 0xFFu) | (((pr >> 8) & 0xFFu) << 9);
-        c32[se - r0 < rn ? bin : dummy] = code;
-      }
-    }
   }
 }
 
@@ -2369,26 +2159,7 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   const float2 t1k = d.twiddle1k[tid];
   const float2 t2 = tid < 384 ? d.twiddle[tid] : make_float2(0.f, 0.f);
   float2 v[32];
-  if (O32_CODES && d.inv && d.acode && d.sym_code[j]) {
-    // code mode: the whole symbol's value codes in one pass, values looked up at the read-back
-    uint32_t *c32 = (uint32_t *)smem;
-    float *vre = (float *)(smem + O32_QAM), *vim = vre + 512;
-    const float2 tv0 = d.vtab[tid & 511];
-    o32_scatter_codes(c32, d, io.pairs, cbase, j, (uint32_t)tid);
-    if (tid < 512) {
-      vre[tid] = tv0.x;
-      vim[tid] = tv0.y;
-    }
-    tw1k[tid] = t1k;
-    if (tid < 384) tw2[tid] = t2;
-    __syncthreads();
-    OFDM_PHASE(1);
-#pragma unroll
-    for (uint32_t r = 0; r < 32; r++) {
-      const uint32_t c = c32[o32_bin(kin + 1024u * r)];
-      v[r] = make_float2(vre[c & 511u], vim[c >> 9]);
-    }
-  } else if (d.inv) {
+  if (d.inv) {
     // scatter mode, one half of the bins (m2 < 16, then m2 >= 16) at a time
     float *qre = (float *)(smem + O32_QAM), *qim = qre + 256;
     const float2 tq = tid < 256 ? d.qam[tid] : make_float2(0.f, 0.f);
