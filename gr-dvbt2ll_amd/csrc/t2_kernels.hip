@@ -373,7 +373,7 @@ __host__ __device__ inline int fec_map_smem(int cs, int nldpc) {
 template <int NT> __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, int tid);
 template <int NT>
 __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
-                                uint16_t *stage, int blk, int tid);
+                                uint16_t *stage, int blk, int tid, bool alias = false);
 
 // LDPC parity rows: row a, word w of p[a][c] = XOR over the row's entries (g, b) of the window
 // d_g[(c - b) mod 360], c = 32 w; 12 words per row at rowA
@@ -873,7 +873,21 @@ constexpr int MAP_LDS_MAX = 160 * 1024 - 256;   // leaves room for static LDS of
 // LDS: [LUT 2 KB][cell indices, cs bytes][codeword bytes | cell-interleaved index pairs (2 cs)]
 // (<= 99 KB for QPSK normal, 26 KB for 256-QAM normal)
 __host__ __device__ inline int map_idx_bytes(int cs) { return (cs + 15) & ~15; }
+// Compact chain layout (cs <= 4 MAP_CQ MAP_THREADS, e.g. 256-QAM normal): [codeword | cell indices]
+// in 2 idx-bytes, the cell-interleaved pairs (2 cs bytes) overlaying both once the indices are in
+// registers (map_store_pairs alias mode); no LUT (the chain's constellation lookup is in the OFDM
+// kernel).  16 KB instead of 26 KB for 256-QAM normal: 8 workgroups per CU instead of 6.
+#ifndef MAP_CQ
+#define MAP_CQ 8
+#endif
+#ifndef MAP_COMPACT
+#define MAP_COMPACT 1
+#endif
+__host__ __device__ inline bool map_compact(int cs, int cw_bytes, int apply_ci) {
+  return MAP_COMPACT && apply_ci && (cs + 3) / 4 <= MAP_CQ * MAP_THREADS && cw_bytes <= map_idx_bytes(cs);
+}
 __host__ __device__ inline int map_smem(int cs, int cw_bytes, int apply_ci) {
+  if (map_compact(cs, cw_bytes, apply_ci)) return 2 * map_idx_bytes(cs);
   int region = cw_bytes;
   if (apply_ci && 2 * cs > region) region = 2 * cs;
   return 2048 + map_idx_bytes(cs) + ((region + 15) & ~15);
@@ -981,7 +995,7 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
 // data region out_pairs + (blk / F) frame_stride
 template <int NT>
 __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
-                                uint16_t *stage, int blk, int tid) {
+                                uint16_t *stage, int blk, int tid, bool alias) {
   const int cs = d.cs;
   const int r = blk % d.F;
   const int shift = d.ci_shift[r];
@@ -997,7 +1011,40 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
   // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
   constexpr int MB = MAP_MB;
-  if (MAP_QUADS) {
+  if (alias) {
+    // compact LDS (map_compact): stage overlays the cell indices, so every thread first takes its
+    // (at most MAP_CQ) quads of indices and permutation entries into registers, then all write
+    const int nq = (cs + 3) >> 2;
+    const uint32_t *idxw = (const uint32_t *)idx;
+    uint2 pq[MAP_CQ];
+    uint32_t wv[MAP_CQ], pv[MAP_CQ];
+#pragma unroll
+    for (int k = 0; k < MAP_CQ; k++) {
+      const int q = min(tid + k * NT, nq - 1);
+      pq[k] = ld_off((const uint2 *)d.ci_perm, (uint32_t)q * 8u);
+      wv[k] = idxw[q];
+      pv[k] = idx[q == 0 ? cs - 1 : 4 * q - 1];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < MAP_CQ; k++) {
+      const int q = tid + k * NT;
+      if (q < nq && !(MAP_SKIP & 2)) {
+        uint32_t prev = pv[k];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const int j = 4 * q + e;
+          const uint32_t lo = (wv[k] >> (8 * e)) & 0xFFu, hi = d.rotation ? prev : lo;
+          prev = lo;
+          if (j < cs) {
+            int tt = (int)(int16_t)(((e < 2 ? pq[k].x : pq[k].y) >> (16 * (e & 1))) & 0xFFFFu) + shift;
+            tt = tt >= cs ? tt - cs : tt;
+            stage[tt] = (uint16_t)(lo | (hi << 8));
+          }
+        }
+      }
+    }
+  } else if (MAP_QUADS) {
     // four consecutive cells per thread: one 8-byte load of their permutation entries and one
     // 4-byte LDS read of their indices (plus the previous cell's byte for the rotation)
     constexpr int MQ = MB / 2;
@@ -1259,7 +1306,10 @@ hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s) {
 // The chain's launches prepend ceil8(L1 frames) workgroups that generate the frames' L1-post cells
 // (they run beside the map workgroups instead of as a launch of their own; a multiple of 8 keeps
 // each map workgroup's XCD)
-__global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io, L1Dev l1d, L1IO l1io) {
+#ifndef MAP_MINWG
+#define MAP_MINWG 8    // resident workgroups per CU the register allocation must allow (compact LDS: 8 fit)
+#endif
+__global__ __launch_bounds__(MAP_THREADS, MAP_MINWG) void map_kernel(MapDev d, MapIO io, L1Dev l1d, L1IO l1io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int nl1 = (l1io.nframes + 7) & ~7;
@@ -1268,13 +1318,16 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io, L1
     return;
   }
   const int blk = xcd_major((int)blockIdx.x - nl1, (int)gridDim.x - nl1);
+  const bool compact = map_compact(d.cs, d.nldpc / 8 + 4, io.apply_ci);
   float2 *lut = (float2 *)smem;
-  uint8_t *idx = smem + 2048;
-  uint8_t *cw = smem + 2048 + map_idx_bytes(d.cs);
-  uint16_t *stage = (uint16_t *)cw;    // chain: (idx[j], idx[j-1]) at cell-interleaved position t
+  uint8_t *idx = compact ? smem + map_idx_bytes(d.cs) : smem + 2048;
+  uint8_t *cw = compact ? smem : smem + 2048 + map_idx_bytes(d.cs);
+  // chain: (idx[j], idx[j-1]) at cell-interleaved position t
+  uint16_t *stage = compact ? (uint16_t *)smem : (uint16_t *)cw;
   const int cs = d.cs, nl = d.nldpc;
   MAP_PHASE(0);
-  for (int i = tid; i < 256; i += MAP_THREADS) lut[i] = d.lut[i];
+  if (!io.apply_ci)
+    for (int i = tid; i < 256; i += MAP_THREADS) lut[i] = d.lut[i];
   // ---- interleaver input bits (tempu) into LDS as big-endian words: bit i of the codeword is
   //      bit 31 - (i & 31) of word i >> 5
   uint32_t *cww = (uint32_t *)cw;
@@ -1317,7 +1370,7 @@ __global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io, L1
     }
     return;
   }
-  map_store_pairs<MAP_THREADS>(d, io.out_pairs, io.frame_stride, idx, stage, blk, tid);
+  map_store_pairs<MAP_THREADS>(d, io.out_pairs, io.frame_stride, idx, stage, blk, tid, compact);
 }
 
 hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1Dev *l1d, const L1IO *l1io) {
