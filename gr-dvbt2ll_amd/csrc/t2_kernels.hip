@@ -138,7 +138,7 @@ __shared__ uint64_t g_fec_ts[16];
 #define FEC_BCH_TAB 1    // 1: chunk remainders combined by per-lane nibble tables; 0: Horner over the lanes
 #endif
 #ifndef FEC_BCH_TAB_JB
-#define FEC_BCH_TAB_JB 4  // table lookups in flight per lane (8: spills)
+#define FEC_BCH_TAB_JB 2  // table lookups in flight per lane (4 spills more at the 72-VGPR budget of 7 WGs/CU)
 #endif
 #ifndef FEC_BCH_PRIO
 #define FEC_BCH_PRIO 1   // wave priority (s_setprio) of the BCH wave while it runs (0: off)
@@ -151,7 +151,7 @@ constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g ||
 #define FEC_BTAB_GLOBAL 0   // 1: BCH byte table read from global memory (no LDS copy per workgroup)
 #endif
 #ifndef FEC_WGS
-#define FEC_WGS 6           // resident FEC workgroups per CU (persistent grid)
+#define FEC_WGS 7           // most resident FEC workgroups per CU (register budget; LDS may allow fewer)
 #endif
 constexpr int FEC_WG_PER_CU = FEC_WGS;
 // dynamic LDS carve (bytes): a persistent part (the workgroup loops over FEC blocks; tables are
@@ -177,7 +177,20 @@ constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes o
 constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_BYTES ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_BYTES);
 static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0 && SM_BLK % 16 == 0, "LDS carve alignment");
 static_assert(SM_SYNC % 8 == 0 && SM_BLK - SM_SYNC >= 4 * 3 * 8, "BCH wave remainders in SM_SYNC + SM_W");
-static_assert(FEC_SMEM <= 160 * 1024 / FEC_WG_PER_CU, "FEC_WGS workgroups per CU");
+// the carve a plan actually needs (frame, raw TS and LDPC areas sized for its code): the launch
+// fits as many persistent workgroups per CU as it allows, up to FEC_WGS (the register budget)
+struct FecCarve {
+  int phase, crc8, crcsh, total;
+};
+__host__ __device__ inline FecCarve fec_carve(int kbch, int nbch, int q) {
+  FecCarve c;
+  c.phase = SM_FRAME + ((nbch / 8 + 15) & ~15);
+  c.crc8 = c.phase + ((188 + (kbch - 80) / 8 + 16 + 15) & ~15);
+  c.crcsh = c.crc8 + 256;
+  const int ldpc = 4 * (FEC_DW * (nbch / 360) + 12 * q);
+  c.total = c.crcsh + 2048 > c.phase + ldpc ? c.crcsh + 2048 : c.phase + ldpc;
+  return c;
+}
 
 // stream position of payload byte J (counted over the payload bytes of the whole stream)
 __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
@@ -405,8 +418,10 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
   const int NB = d.nbch >> 3;          // info bytes (BBFRAME + BCH parity)
   const int P = d.P;
   uint8_t *frame = smem + SM_FRAME;
-  uint8_t *crc8 = smem + SM_CRC8;
-  uint8_t *crcsh = smem + SM_CRCSH;
+  const FecCarve cv = fec_carve(d.kbch, d.nbch, d.q);
+  uint8_t *crc8 = smem + cv.crc8;
+  uint8_t *crcsh = smem + cv.crcsh;
+  uint8_t *const phase = smem + cv.phase;   // raw TS bytes (NM), then the LDPC groups and rows
   uint8_t *hcrc8 = smem + SM_HCRC;
   uint8_t *syncv = smem + SM_SYNC;
 #if FEC_BTAB_GLOBAL
@@ -414,7 +429,7 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
 #else
   uint64_t *btab = (uint64_t *)(smem + SM_BTAB);
 #endif
-  uint32_t *D = (uint32_t *)(smem + SM_D);
+  uint32_t *D = (uint32_t *)phase;
   uint32_t *Wv = (uint32_t *)(smem + SM_W);
   uint32_t *ents = (uint32_t *)(smem + SM_ENT);
   uint64_t *wres = (uint64_t *)(smem + SM_SYNC);   // BCH wave remainders (SM_SYNC + SM_W, free then)
@@ -474,17 +489,17 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
     // ---- CRC-8 of each packet whose sync slot falls in this block (NM only):
     //      8 lanes per packet, 24-byte chunks combined with zero-extension tables
     // NM: stage the raw stream bytes [pos0 - 188, pos0 + npay) once (independent dword loads;
-    // raw byte i = stream byte rs + i lives at LDS byte SM_RAW + delta + i); the CRC-8 chains and
+    // raw byte i = stream byte rs + i lives at LDS byte cv.phase + delta + i); the CRC-8 chains and
     // the payload words then read LDS
     const int64_t rs = pos0 - 188;
     int delta = 0, first_slot = 0;
-    const uint32_t *raww = (const uint32_t *)(smem + SM_RAW);
+    const uint32_t *raww = (const uint32_t *)phase;
     if (!d.hem) {
       const int64_t rel = rs - io.ts_base;                 // >= -188
       const int64_t w0 = (rel >= 0 ? rel : rel - 3) / 4;   // floor
       delta = (int)(rel - 4 * w0);
       const int nw = (delta + npay + 188 + 3) >> 2;
-      uint32_t *rawst = (uint32_t *)(smem + SM_RAW);
+      uint32_t *rawst = (uint32_t *)phase;
       for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)crc8)[i] = ((const uint32_t *)d.crc8_tab)[i];
       for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)crcsh)[i] = ((const uint32_t *)d.crc8_shift)[i];
       const bool aligned = (((uintptr_t)tin) & 3) == 0;
@@ -499,7 +514,7 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
         }
         rawst[i] = v;
       }
-      const uint8_t *raw = smem + SM_RAW + delta;
+      const uint8_t *raw = phase + delta;
       __syncthreads();
       FEC_PHASE(2);
       first_slot = (188 - count0) % 188;
@@ -569,7 +584,7 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
       if (j < npay) {
         if (d.hem) return tin[payload_pos(J0 + j, 1) - io.ts_base];
         const int r = (count0 + j) % 188;
-        return r == 0 ? (uint32_t)syncv[(j - first_slot) / 188] : (uint32_t)smem[SM_RAW + delta + 188 + j];
+        return r == 0 ? (uint32_t)syncv[(j - first_slot) / 188] : (uint32_t)phase[delta + 188 + j];
       }
       const int k = j - npay;   // in-band type B (bbheader:327-355): 01, 65 zero bits, TS rate (27 bits), 10 zeros
       if (!padding || k >= 13) return 0u;
@@ -826,17 +841,20 @@ static bool fec_plan_fits(const FecDev &d) {
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
   if (!fec_plan_fits(d)) return hipErrorInvalidValue;
-  dim3 grid(fec_grid(io.nblocks, FEC_WG_PER_CU)), block(FEC_THREADS);
+  const int lds = fec_carve(d.kbch, d.nbch, d.q).total;
+  int per_cu = (160 * 1024) / lds;
+  per_cu = per_cu < 1 ? 1 : per_cu > FEC_WG_PER_CU ? FEC_WG_PER_CU : per_cu;
+  dim3 grid(fec_grid(io.nblocks, per_cu)), block(FEC_THREADS);
   const MapDev md{};
   switch (mode) {
     case FEC_TS_TO_TEMPU:
-      hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, FEC_SMEM, s, d, io, md, nullptr, (int64_t)0);
+      hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, lds, s, d, io, md, nullptr, (int64_t)0);
       break;
     case FEC_TS_TO_BITS:
-      hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_BITS>, grid, block, FEC_SMEM, s, d, io, md, nullptr, (int64_t)0);
+      hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_BITS>, grid, block, lds, s, d, io, md, nullptr, (int64_t)0);
       break;
     default:
-      hipLaunchKernelGGL(fec_kernel<FEC_BITS_TO_BITS>, grid, block, FEC_SMEM, s, d, io, md, nullptr, (int64_t)0);
+      hipLaunchKernelGGL(fec_kernel<FEC_BITS_TO_BITS>, grid, block, lds, s, d, io, md, nullptr, (int64_t)0);
       break;
   }
   return hipGetLastError();
