@@ -1411,6 +1411,9 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1D
 }
 
 // ============================================================================ OFDM kernels
+#ifndef OFDM_SKIP
+#define OFDM_SKIP 0   // experiment switch (wrong output): bit 0 = no data-slot scatter, 1 = no direct aux entries
+#endif
 #ifndef OFDM_SQ16
 #define OFDM_SQ16 8   // data-slot quads per thread per scatter round (N <= 16K)
 #endif
@@ -1633,7 +1636,7 @@ template <int NT, int SQ>
 __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src, int g, uint32_t r0, uint32_t rn,
                                               uint32_t dummy, int tid) {
   const int4 gr = src.agrp[g];
-  for (uint32_t q = (uint32_t)tid; q < (uint32_t)gr.y >> 2; q += NT) {
+  for (uint32_t q = (uint32_t)tid; q < ((OFDM_SKIP & 2) ? 0u : (uint32_t)gr.y >> 2); q += NT) {
     const uint32_t e0 = (uint32_t)gr.x + 4u * q;
     const uint2 b = ld_off((const uint2 *)src.abin, e0 * 2u);
     const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
@@ -1648,7 +1651,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
     const uint32_t e = src.aind[(uint32_t)gr.z + i];
     lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
   }
-  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
+  const uint32_t q0 = r0 & ~3u, nq = (OFDM_SKIP & 1) ? 0u : (r0 + rn - q0 + 3u) >> 2;
   const uint32_t lastq = nq - 1u;
   for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
     uint2 b[SQ], c[SQ];
