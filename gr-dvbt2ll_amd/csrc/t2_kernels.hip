@@ -17,7 +17,6 @@
 #include "t2_kernels.h"
 
 #include <atomic>
-#include <cstdlib>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -829,7 +828,6 @@ static int fec_grid(int nblocks, int per_cu) {
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
     ncu[dev].store(n, std::memory_order_relaxed);
   }
-  if (const char *g = std::getenv("DVBT2LL_FEC_GRID_CU")) n = std::atoi(g) > 0 ? std::atoi(g) : n;   // experiment
   return nblocks < n * per_cu ? nblocks : n * per_cu;
 }
 
@@ -2194,23 +2192,16 @@ __device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT
 
 // 32K symbols, one workgroup per (symbol, frame): scatter mode (the fused chain), gather mode (the
 // pilotgen block: cells already in carrier order) and the carriers-only test hook
-#ifndef O32_PERSIST
-#define O32_PERSIST 0   // experiment switch (measured neutral, session h): 1 = one resident workgroup per CU
-                        // loops over the launch's symbols
-#endif
 template <int FMT>
-__device__ __forceinline__ void ofdm32_symbol(const OfdmDev &d, const OfdmIO &io, int u) {
+__global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   constexpr int N = 32768, NT = O32_NT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2 *lds = (float2 *)smem;
   float2 *tw1k = (float2 *)(smem + O32_TW1K), *tw2 = (float2 *)(smem + O32_TW2);
-  // the thread index is re-read per symbol behind an empty asm, so the persistent loop cannot hoist
-  // the per-thread address arithmetic out of it (hoisted, it stays live and spills)
-  uint32_t tidv = threadIdx.x;
-  if (O32_PERSIST) asm volatile("" : "+v"(tidv));
-  const int tid = (int)tidv;
+  const int tid = threadIdx.x;
   const uint32_t ta = o32_ta((uint32_t)tid), tb = o32_tb((uint32_t)tid);
   const uint32_t kin = ta + 32u * tb;             // stage-A input bins kin + 1024 r
+  const int u = xcd_major(blockIdx.x, gridDim.x);
   const int j = u / io.nframes;                   // symbol
   const int f = u - j * io.nframes;               // frame within launch
   const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);   // stream-major batch
@@ -2315,30 +2306,12 @@ __device__ __forceinline__ void ofdm32_symbol(const OfdmDev &d, const OfdmIO &io
 #endif
 }
 
-template <int FMT>
-__global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
-  const int total = d.Nsym * io.nframes;
-  if (O32_PERSIST) {
-    // persistent: workgroup b takes launch indices b, b + grid, ... (grid a multiple of 8, so every
-    // index stays on b's XCD and xcd_major gives that XCD a contiguous run of symbols); the next
-    // symbol starts without a workgroup dispatch
-    for (int i = blockIdx.x; i < total; i += gridDim.x) {
-      ofdm32_symbol<FMT>(d, io, xcd_major(i, total));
-      __syncthreads();                            // last LDS reads done before the next symbol's writes
-    }
-  } else {
-    ofdm32_symbol<FMT>(d, io, xcd_major(blockIdx.x, gridDim.x));
-  }
-}
-
-static int o32_grid(int total);
 template <int N, int FMT>
 static hipError_t launch_ofdm_f(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
   if (N == 32768) {
     hipError_t e = lds_limit((const void *)ofdm32_kernel<FMT>, O32_LDS);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((ofdm32_kernel<FMT>), dim3(O32_PERSIST ? o32_grid(d.Nsym * io.nframes) : d.Nsym * io.nframes),
-                       dim3(O32_NT), O32_LDS, s, d, io);
+    hipLaunchKernelGGL((ofdm32_kernel<FMT>), dim3(d.Nsym * io.nframes), dim3(O32_NT), O32_LDS, s, d, io);
     return hipGetLastError();
   }
   constexpr int NN = N > 16384 ? 16384 : N;
@@ -2347,13 +2320,6 @@ static hipError_t launch_ofdm_f(const OfdmDev &d, const OfdmIO &io, hipStream_t 
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((ofdm_kernel<NN, FMT>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
   return hipGetLastError();
-}
-// persistent 32K grid: one workgroup per CU, a multiple of 8 (XCD mapping), at most the symbol count
-static int o32_grid(int total) {
-  int n = fec_grid(1 << 30, 1);
-  if (const char *g = std::getenv("DVBT2LL_O32_GRID")) n = std::atoi(g) > 0 ? std::atoi(g) : n;   // experiment
-  n = n >= 8 ? n & ~7 : n;
-  return total < n ? total : n;
 }
 template <int N>
 static hipError_t launch_ofdm_t(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
