@@ -147,6 +147,9 @@ constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
 constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 233280 / 360)
 constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g || d_g[0..56)
+#ifndef MAP_CQ
+#define MAP_CQ 8
+#endif
 #ifndef FEC_BTAB_GLOBAL
 #define FEC_BTAB_GLOBAL 0   // 1: BCH byte table read from global memory (no LDS copy per workgroup)
 #endif
@@ -267,8 +270,8 @@ template <int P>
 __device__ __forceinline__ void bch_divide(const uint8_t *frame, const uint64_t *btab, int lo, int hi, uint64_t &r0,
                                            uint64_t &r1, uint64_t &r2) {
   constexpr int tw = (P - 8) >> 6, tsft = (P - 8) & 63;
-  constexpr uint64_t k1 = P >= 128 ? ~0ull : (1ull << (P - 64)) - 1;
-  constexpr uint64_t k2 = P >= 192 ? ~0ull : P <= 128 ? 0ull : (1ull << (P - 128)) - 1;
+  constexpr uint64_t k1 = P >= 128 ? ~0ull : (1ull << ((P - 64) & 63)) - 1;
+  constexpr uint64_t k2 = P >= 192 ? ~0ull : P <= 128 ? 0ull : (1ull << ((P - 128) & 63)) - 1;
   int i = max(lo, 0);
   uint32_t nxt = i < hi ? frame[i] : 0u;
 #pragma unroll 2
@@ -384,7 +387,7 @@ __host__ __device__ inline int fec_map_smem(int cs, int nldpc) {
 }
 
 template <int NT> __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, int tid);
-template <int NT>
+template <int NT, int CQ = MAP_CQ>
 __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
                                 uint16_t *stage, int blk, int tid, bool alias = false);
 
@@ -895,14 +898,19 @@ __host__ __device__ inline int map_idx_bytes(int cs) { return (cs + 15) & ~15; }
 // in 2 idx-bytes, the cell-interleaved pairs (2 cs bytes) overlaying both once the indices are in
 // registers (map_store_pairs alias mode); no LUT (the chain's constellation lookup is in the OFDM
 // kernel).  16 KB instead of 26 KB for 256-QAM normal: 8 workgroups per CU instead of 6.
-#ifndef MAP_CQ
-#define MAP_CQ 8
-#endif
 #ifndef MAP_COMPACT
 #define MAP_COMPACT 1
 #endif
+// register staging per thread of the compact layout: MAP_CQ quads (cs <= 8192: eight workgroups per
+// CU at 64 VGPRs) or 2 MAP_CQ (cs <= 16384, e.g. 64-QAM and 16-QAM normal: a second kernel
+// instantiation with a 96-VGPR budget, five to seven workgroups per CU by LDS); 0: not compact
+__host__ __device__ inline int map_compact_cq(int cs, int cw_bytes, int apply_ci) {
+  if (!MAP_COMPACT || !apply_ci || cw_bytes > map_idx_bytes(cs)) return 0;
+  const int nq = (cs + 3) / 4;
+  return nq <= MAP_CQ * MAP_THREADS ? MAP_CQ : nq <= 2 * MAP_CQ * MAP_THREADS ? 2 * MAP_CQ : 0;
+}
 __host__ __device__ inline bool map_compact(int cs, int cw_bytes, int apply_ci) {
-  return MAP_COMPACT && apply_ci && (cs + 3) / 4 <= MAP_CQ * MAP_THREADS && cw_bytes <= map_idx_bytes(cs);
+  return map_compact_cq(cs, cw_bytes, apply_ci) != 0;
 }
 __host__ __device__ inline int map_smem(int cs, int cw_bytes, int apply_ci) {
   if (map_compact(cs, cw_bytes, apply_ci)) return 2 * map_idx_bytes(cs);
@@ -1011,7 +1019,7 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
 // chain: cell interleaver (framemapper:1973-1998) of block blk's (index, previous index) pairs through
 // LDS (stage, 2 cs bytes), then the time-interleaver (framemapper:1999-2028) store into the frame
 // data region out_pairs + (blk / F) frame_stride
-template <int NT>
+template <int NT, int CQ>
 __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
                                 uint16_t *stage, int blk, int tid, bool alias) {
   const int cs = d.cs;
@@ -1034,10 +1042,10 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
     // (at most MAP_CQ) quads of indices and permutation entries into registers, then all write
     const int nq = (cs + 3) >> 2;
     const uint32_t *idxw = (const uint32_t *)idx;
-    uint2 pq[MAP_CQ];
-    uint32_t wv[MAP_CQ], pv[MAP_CQ];
+    uint2 pq[CQ];
+    uint32_t wv[CQ], pv[CQ];
 #pragma unroll
-    for (int k = 0; k < MAP_CQ; k++) {
+    for (int k = 0; k < CQ; k++) {
       const int q = min(tid + k * NT, nq - 1);
       pq[k] = ld_off((const uint2 *)d.ci_perm, (uint32_t)q * 8u);
       wv[k] = idxw[q];
@@ -1045,7 +1053,7 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < MAP_CQ; k++) {
+    for (int k = 0; k < CQ; k++) {
       const int q = tid + k * NT;
       if (q < nq && !(MAP_SKIP & 2)) {
         uint32_t prev = pv[k];
@@ -1327,7 +1335,8 @@ hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s) {
 #ifndef MAP_MINWG
 #define MAP_MINWG 8    // resident workgroups per CU the register allocation must allow (compact LDS: 8 fit)
 #endif
-__global__ __launch_bounds__(MAP_THREADS, MAP_MINWG) void map_kernel(MapDev d, MapIO io, L1Dev l1d, L1IO l1io) {
+template <int CQ>
+__global__ __launch_bounds__(MAP_THREADS, CQ <= MAP_CQ ? MAP_MINWG : 5) void map_kernel(MapDev d, MapIO io, L1Dev l1d, L1IO l1io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int nl1 = (l1io.nframes + 7) & ~7;
@@ -1336,7 +1345,7 @@ __global__ __launch_bounds__(MAP_THREADS, MAP_MINWG) void map_kernel(MapDev d, M
     return;
   }
   const int blk = xcd_major((int)blockIdx.x - nl1, (int)gridDim.x - nl1);
-  const bool compact = map_compact(d.cs, d.nldpc / 8 + 4, io.apply_ci);
+  const bool compact = map_compact_cq(d.cs, d.nldpc / 8 + 4, io.apply_ci) == CQ;
   float2 *lut = (float2 *)smem;
   uint8_t *idx = compact ? smem + map_idx_bytes(d.cs) : smem + 2048;
   uint8_t *cw = compact ? smem : smem + 2048 + map_idx_bytes(d.cs);
@@ -1388,7 +1397,7 @@ __global__ __launch_bounds__(MAP_THREADS, MAP_MINWG) void map_kernel(MapDev d, M
     }
     return;
   }
-  map_store_pairs<MAP_THREADS>(d, io.out_pairs, io.frame_stride, idx, stage, blk, tid, compact);
+  map_store_pairs<MAP_THREADS, CQ>(d, io.out_pairs, io.frame_stride, idx, stage, blk, tid, compact);
 }
 
 hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1Dev *l1d, const L1IO *l1io) {
@@ -1403,10 +1412,15 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1D
     smem = smem > L1_LDS_WORDS * 4 ? smem : L1_LDS_WORDS * 4;
   }
   if (smem > MAP_LDS_MAX) return hipErrorInvalidValue;
-  hipError_t e = lds_limit((const void *)map_kernel, MAP_LDS_MAX);
+  const bool big = map_compact_cq(d.cs, d.nldpc / 8 + 4, io.apply_ci) == 2 * MAP_CQ;
+  const void *fn = big ? (const void *)map_kernel<2 * MAP_CQ> : (const void *)map_kernel<MAP_CQ>;
+  hipError_t e = lds_limit(fn, MAP_LDS_MAX);
   if (e != hipSuccess) return e;
   const int nl1 = (li.nframes + 7) & ~7;
-  hipLaunchKernelGGL(map_kernel, dim3(io.nblocks + nl1), dim3(MAP_THREADS), smem, s, d, io, ld, li);
+  if (big)
+    hipLaunchKernelGGL(map_kernel<2 * MAP_CQ>, dim3(io.nblocks + nl1), dim3(MAP_THREADS), smem, s, d, io, ld, li);
+  else
+    hipLaunchKernelGGL(map_kernel<MAP_CQ>, dim3(io.nblocks + nl1), dim3(MAP_THREADS), smem, s, d, io, ld, li);
   return hipGetLastError();
 }
 
