@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=64, help="T2 frames per step per GPU")
+    ap.add_argument("--frames", type=int, default=192, help="T2 frames per step per GPU (192 cfg3 frames = 44 s of airtime)")
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
