@@ -1464,6 +1464,9 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1D
 #ifndef OFDM_SKIP
 #define OFDM_SKIP 0   // experiment switch (wrong output): bit 0 = no data-slot scatter, 1 = no direct aux entries
 #endif
+#ifndef O32_OCT
+#define O32_OCT 1   // 1: the 32K scatter loads its data slots as aligned octets (16-byte loads)
+#endif
 #ifndef OFDM_SQ16
 #define OFDM_SQ16 8   // data-slot quads per thread per scatter round (N <= 16K)
 #endif
@@ -1700,6 +1703,36 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
   for (uint32_t i = (uint32_t)tid; i < (uint32_t)gr.w; i += NT) {
     const uint32_t e = src.aind[(uint32_t)gr.z + i];
     lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
+  }
+  if (O32_OCT && SQ == 4 && !(OFDM_SKIP & 1)) {
+    // 32K kernel: slots in aligned octets, one 16-byte load of bins and one of index pairs per
+    // octet (half the load instructions of quads; the pair rows are padded to a multiple of 8)
+    const uint32_t o0 = r0 & ~7u, no = (r0 + rn - o0 + 7u) >> 3;
+    const uint32_t lasto = no - 1u;
+    for (uint32_t g0 = 0; g0 < no; g0 += 2u * NT) {
+      uint4 b[2], c[2];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint32_t s = o0 + 8u * min(g0 + (uint32_t)(tid + NT * u), lasto);
+        b[u] = ld_off((const uint4 *)src.inv, s * 2u);
+        c[u] = ld_off((const uint4 *)src.pairs, (src.cbase + s) * 2u);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const uint32_t s = o0 + 8u * min(g0 + (uint32_t)(tid + NT * u), lasto);
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const uint32_t bw = e < 2 ? b[u].x : e < 4 ? b[u].y : e < 6 ? b[u].z : b[u].w;
+          const uint32_t cw = e < 2 ? c[u].x : e < 4 ? c[u].y : e < 6 ? c[u].z : c[u].w;
+          const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the group
+          const uint32_t pr = cw >> (16 * (e & 1));
+          const bool in_run = s + (uint32_t)e - r0 < rn;
+          const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+          lds[in_run ? bin : dummy] = v;
+        }
+      }
+    }
+    return;
   }
   const uint32_t q0 = r0 & ~3u, nq = (OFDM_SKIP & 1) ? 0u : (r0 + rn - q0 + 3u) >> 2;
   const uint32_t lastq = nq - 1u;
