@@ -6,9 +6,13 @@ One "step" = the whole hot path (TS bytes -> BBFRAME/BCH/LDPC -> bit interleave/
 interleave -> time/frame/frequency interleave + pilots + IFFT + GI + P1) over a batch of
 --frames T2 frames per GPU, TS input already resident in HBM, IQ written to HBM.
 
-Multi-GPU: frame-sharded, one process per GPU (torchrun); each rank encodes its own
-disjoint T2 frames with closed-form stream state, no data-path collective ("weak" scaling).
-Rank 0 prints one JSON line.  Synthetic data: splitmix64 TS packets (dvbt2ll.configs).
+Multi-GPU: frame-sharded, one process per GPU; each rank encodes its own disjoint T2 frames with
+closed-form stream state, no data-path collective ("weak" scaling).  `--gpus N` under torchrun
+(WORLD_SIZE set) checks WORLD_SIZE == N; without it, this process spawns the N rank processes
+itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, after its PMC passes and before anything
+touches the GPU) and relays rank 0's line.  `--dry-run` (gloo, no HIP) exercises the same spawn ->
+frame_range -> barrier -> all_reduce -> gather_frames path on CPU.  Rank 0 prints one JSON line.
+Synthetic data: splitmix64 TS packets (dvbt2ll.configs).
 
 Steps are pipelined: the chain handle holds --slots intermediate buffer sets and step s is
 issued on HIP stream s % slots (dvbt2ll_chain_set_slots), so consecutive steps overlap on the GPU.
@@ -59,6 +63,11 @@ def parse():
     ap.add_argument("--streams", type=int, default=1,
                     help="independent TS streams per launch (seeds 1..S, dvbt2ll_chain_run_streams; BASELINE cfg4 "
                          "x4 / cfg5 x8): each step encodes --frames // S frames of every stream")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no HIP: exercise the multi-rank spawn / frame sharding / barrier / all_reduce / "
+                         "ordered gather path with placeholder frames (CPU tensors, gloo)")
+    ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL; gloo for "
+                                                    "--dry-run)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -76,10 +85,7 @@ def algorithmic_bytes(cfg, info):
     s2 = F * (nldpc // 8 + 8 * cs)
     s3 = 8 * S + 8 * M
     s4 = 8 * M + 8 * IQ
-    # kernel stages: fec = S1 (+ LDPC), map = S2, ofdm = S3 + S4 (fused); fec = S1 + S2 when the
-    # FEC and map kernels are one
-    if info.get("fused_fec_map"):
-        return {"fec": s1 + s2, "map": 0, "ofdm": s3 + s4}
+    # kernel stages: fec = S1 (+ LDPC), map = S2, ofdm = S3 + S4 (fused)
     return {"fec": s1, "map": s2, "ofdm": s3 + s4}
 
 
@@ -93,8 +99,6 @@ def minimal_bytes(cfg, info, iq_bytes=8):
     nldpc = 64800 if cfg.framesize == 1 else 16200
     kbch = KBCH[(cfg.framesize, cfg.rate)]
     cs, S, IQ = info["cell_size"], info["stream_items"], info["iq_samples_per_frame"]
-    if info.get("fused_fec_map"):   # one kernel: TS in, index pairs out, codewords only in LDS
-        return {"fec": F * ((kbch - 80) // 8 + 2 * cs), "map": 0, "ofdm": 2 * S + iq_bytes * IQ}
     return {"fec": F * ((kbch - 80) // 8 + nldpc // 8), "map": F * (nldpc // 8 + 2 * cs),
             "ofdm": 2 * S + iq_bytes * IQ}
 
@@ -102,10 +106,11 @@ def minimal_bytes(cfg, info, iq_bytes=8):
 KERNELS = ("fec", "map", "ofdm")
 # rocprofv3 FETCH_SIZE / WRITE_SIZE (KiB) -> bytes.  gfx950 tallies 128-B read requests at 64 B
 # (MI355X_MICROARCH.md, HBM): x2 on the read side, calibrated per access width by tools/fetch_calib
-# (profiles/r2_fetch_calib.json); the kernels' dominant widths: fec 4 B (TS words), map 4 B
-# (codeword words), ofdm 8 B (slot bins, index pairs)
-LOAD_WIDTH = {"fec": 4, "map": 4, "ofdm": 8}
-STORE_WIDTH = {"fec": 4, "map": 2, "ofdm": 8}
+# (profiles/r2_fetch_calib.json); the kernels' dominant access widths: fec 16-B TS staging loads and
+# 4-B codeword stores, map 16-B codeword loads and 2-B index-pair stores, ofdm 16-B data-slot loads
+# and 16-B IQ stores (two samples per lane)
+LOAD_WIDTH = {"fec": 16, "map": 16, "ofdm": 16}
+STORE_WIDTH = {"fec": 4, "map": 2, "ofdm": 16}
 
 
 def _calibration():
@@ -161,6 +166,7 @@ def pmc_passes(args):
             r["fetch_bytes"] = r["FETCH_SIZE"] * 1024 / fr
             r["write_bytes"] = r["WRITE_SIZE"] * 1024 / wr
             r["hbm_bytes"] = r["fetch_bytes"] + r["write_bytes"]
+            r["fetch_write_bytes"] = [r["fetch_bytes"], r["write_bytes"]]
             r["calibration"] = {"fetch_counter_per_byte": fr, "write_counter_per_byte": wr,
                                 "source": "profiles/r2_fetch_calib.json" if cal else "MI355X_MICROARCH.md default"}
     return res, None
@@ -382,14 +388,119 @@ def one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per):
     return latency
 
 
+def metric_for(cfg_name):
+    """BASELINE.json's metric string for cfg3 (the configuration it is quoted on); the same metric
+    named by its configuration for the others"""
+    if cfg_name == "cfg3":
+        return METRIC
+    from dvbt2ll.configs import CONFIGS
+    return "IQ Msamples/sec (whole node) + FEC blocks/sec, " + CONFIGS[cfg_name].name
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(args):
+    """`bench.py --gpus N` outside torchrun: the PMC passes (child processes on one GPU; per-launch
+    traffic does not depend on N under weak scaling), then N rank processes of this script with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set -- started before this process
+    touches the GPU (it never does) -- and rank 0's JSON line relayed.  Any rank failing fails the run."""
+    n = args.gpus
+    env0 = dict(os.environ)
+    if not args.dry_run and not args.no_pmc:
+        traffic, note = pmc_passes(args)
+        fd, path = tempfile.mkstemp(prefix="t2pmc_", suffix=".json", dir=os.environ.get("TMPDIR", "/tmp"))
+        with os.fdopen(fd, "w") as fh:
+            json.dump({"traffic": traffic, "note": note}, fh)
+        env0["DVBT2LL_BENCH_PMC_JSON"] = path
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DVBT2LL_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, str(ROOT / "bench.py")] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    out0 = procs[0].communicate()[0]
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    if env0.get("DVBT2LL_BENCH_PMC_JSON"):
+        os.unlink(env0["DVBT2LL_BENCH_PMC_JSON"])
+    if any(rcs):
+        sys.stderr.write("bench.py: rank exit codes %s\n" % rcs)
+        return max(1, max(abs(c) for c in rcs))
+    for line in out0.splitlines():        # rank 0's JSON line to stdout, its other output to stderr
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line + "\n")
+    sys.stdout.flush()
+    return 0
+
+
+def dry_run(args, rank, world):
+    """the multi-rank plumbing without HIP: placeholder frames (frame k's samples all hold k) are
+    produced per rank from its frame_range shard, K steps are timed between barriers with the
+    max over ranks by all_reduce, and the ordered gather to rank 0 is checked frame by frame"""
+    import torch
+    import torch.distributed as dist
+    from dvbt2ll.distributed import frame_range, gather_frames
+    if world > 1:
+        dist.init_process_group(args.backend or "gloo")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+    B, per = min(args.frames, 16), 1024
+    first, count = frame_range(world * B, rank, world)
+    buf = torch.empty((count * per, 2), dtype=torch.float32)
+
+    def step():
+        buf.view(count, per, 2)[:] = torch.arange(first, first + count, dtype=torch.float32)[:, None, None]
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.barrier()
+    e = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    shards = [list(frame_range(world * B, r, world)) for r in range(world)]
+    g = gather_frames(buf, world * B, per) if world > 1 else buf
+    if rank == 0:
+        got = g.view(world * B, per, 2)
+        ok = bool((got == torch.arange(world * B, dtype=torch.float32)[:, None, None]).all())
+        print(json.dumps({"metric": "dry run: placeholder frames/s (no HIP)", "value": world * B * args.steps / float(e),
+                          "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "dry_run": True, "backend": args.backend or "gloo",
+                          "world_size_verified": world == args.gpus, "shards": shards, "gather_in_order": ok,
+                          "launcher": "bench.py spawn" if os.environ.get("DVBT2LL_BENCH_SPAWNED") else
+                                      ("external" if world > 1 else "single process")}))
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.pmc_child:
+        return spawn_ranks(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not args.pmc_child:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
+    if args.dry_run:
+        return dry_run(args, rank, world)
     traffic, pmc_note = None, "skipped"
-    if world == 1 and not args.pmc_child and not args.no_pmc:
+    if os.environ.get("DVBT2LL_BENCH_PMC_JSON"):        # measured by the spawning parent (spawn_ranks)
+        with open(os.environ["DVBT2LL_BENCH_PMC_JSON"]) as fh:
+            pm = json.load(fh)
+        traffic, pmc_note = pm["traffic"], pm["note"]
+    elif world == 1 and not args.pmc_child and not args.no_pmc:
         traffic, pmc_note = pmc_passes(args)          # before any GPU initialisation here
+    elif world > 1:
+        pmc_note = "not collected under an external launcher (bench.py --gpus N spawns its ranks after its PMC passes)"
 
     import numpy as np
     import torch
@@ -401,7 +512,8 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local_rank))
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     B = args.frames
     chain = dvbt2ll.Chain(cfg, max_frames=B, device=local_rank)
     info = chain.info
@@ -547,13 +659,12 @@ def main():
         mb = minimal_bytes(cfg, info)
         stages, rooflines = {}, {}
         for k, name in enumerate(KERNELS):
-            if name == "map" and info.get("fused_fec_map"):
-                continue                  # FEC and map run as one kernel ("fec")
             avg_ms = stage_ms[k] / max(1, launches[k])
             t = avg_ms * 1e-3
             stages[name] = {"avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": ab[name] * B,
                             "achieved_GBs": ab[name] * B / t / 1e9 if t > 0 else None}
-            e = {"kernel": name + "_kernel", "bound": "hbm", "avg_launch_ms": avg_ms, "peak": HBM_PEAK_GBS,
+            kname = "ofdm32_kernel" if name == "ofdm" and info["fft_size"] == 32768 else name + "_kernel"
+            e = {"kernel": kname, "bound": "hbm", "avg_launch_ms": avg_ms, "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "min_bytes_per_launch": mb[name] * B,
                  "achieved": mb[name] * B / t / 1e9 if t > 0 else None,
                  "stage_bytes_per_launch": ab[name] * B,
@@ -568,6 +679,7 @@ def main():
                 e["traffic_GBs"] = e["traffic"] / t / 1e9
                 e["traffic_frac"] = e["traffic_GBs"] / HBM_PEAK_GBS
                 e["traffic_over_min"] = e["traffic"] / (mb[name] * B)
+                e["traffic_fetch_write"] = pm.get("fetch_write_bytes")
                 e["calibration"] = pm.get("calibration")
             if name == "fec":
                 nb = info["fec_blocks_per_frame"] * B
@@ -579,9 +691,6 @@ def main():
                     e["salu_wave_instr_per_block"] = pm.get("SQ_INSTS_SALU", 0) / nb
                     e["valu_issue_frac"] = pm["SQ_INSTS_VALU"] / t / VALU_ISSUE_PEAK
             rooflines[name] = e
-        if len(stage_ms) > 3 and launches[3] and info.get("fused_fec_map"):
-            stages["l1post"] = {"avg_launch_ms": stage_ms[3] / launches[3],
-                                "note": "per-frame L1-post signalling (CRC-32, BCH, LDPC, map) on the GPU"}
         dom = max((n for n in stages if n in KERNELS), key=lambda n: stages[n]["avg_launch_ms"])
         roof = dict(rooflines[dom])
         roof["note"] = ("frac = the kernel's minimal HBM bytes (DESIGN.md 5) / its HIP-event launch time / 8 TB/s; "
@@ -590,7 +699,7 @@ def main():
         if traffic is None:
             roof["traffic_note"] = pmc_note
         out = {
-            "metric": METRIC, "value": msps, "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric_for(args.config), "value": msps, "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "%s: TS->IQ full DVB-T2 chain, %d T2 frames per step per GPU%s "
@@ -600,7 +709,9 @@ def main():
                        "frames_per_step_per_gpu": B, "slots_streams_per_gpu": S,
                        "ts_streams_per_launch": NS,
                        "parallelism": "%s x%d (no data-path collective)"
-                                      % ("frame-sharded" if args.shard == "frames" else "independent streams", world)},
+                                      % ("frame-sharded" if args.shard == "frames" else "independent streams", world),
+                       "launcher": "bench.py spawn" if os.environ.get("DVBT2LL_BENCH_SPAWNED") else
+                                   ("external" if world > 1 else "single process")},
             "fec_blocks_per_sec": fec_total / elapsed,
             "serial_1_stream": {"value": samples_total / serial_elapsed / 1e6,
                                 "ms_per_step": serial_elapsed / args.steps * 1e3,
@@ -634,4 +745,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

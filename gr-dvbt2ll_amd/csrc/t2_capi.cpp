@@ -87,21 +87,17 @@ struct DeviceCtx {
 // ---------------------------------------------------------------- FEC tables on device
 struct FecTables {
   FecPlan plan;
-  DevBuf hcrc, tab, m1, m64, ctab, rowptr, ent, prbs, crc8, crcsh;
+  DevBuf hcrc, tab, ctab, rowptr, ent, prbs, crc8, crcsh;
   FecDev dev{};
   int init(int framesize, int rate, int constellation, int mode, int inband, int fecblocks, int tsrate) {
-    // tuning knob for kernel experiments (tools/): waves sharing the BCH division, default 1
-    const char *bw = std::getenv("DVBT2LL_FEC_BCH_WAVES");
-    if (build_fec(framesize, rate, constellation, plan, bw ? std::atoi(bw) : 1)) return DVBT2LL_EINVAL;
+    if (build_fec(framesize, rate, constellation, plan)) return DVBT2LL_EINVAL;
     int r;
-    if ((r = upload(tab, plan.bch_tab)) || (r = upload(m1, plan.bch_m1)) || (r = upload(m64, plan.bch_m64)) || (r = upload(ctab, plan.bch_ctab)) ||
+    if ((r = upload(tab, plan.bch_tab)) || (r = upload(ctab, plan.bch_ctab)) ||
         (r = upload(rowptr, plan.ldpc_rowptr)) || (r = upload(ent, plan.ldpc_ent)) ||
         (r = upload(prbs, plan.prbs_bytes)) || (r = upload(crc8, plan.crc8_tab)) || (r = upload(crcsh, plan.crc8_shift)) ||
         (r = upload(hcrc, plan.hcrc_bits)))
       return r;
     dev.bch_tab = tab.as<uint64_t>();
-    dev.bch_m1 = m1.as<uint64_t>();
-    dev.bch_m64 = m64.as<uint64_t>();
     dev.bch_ctab = ctab.as<uint64_t>();
     dev.ldpc_rowptr = rowptr.as<uint16_t>();
     dev.ldpc_ent = ent.as<uint32_t>();
@@ -111,7 +107,6 @@ struct FecTables {
     dev.hcrc_bits = hcrc.as<uint8_t>();
     dev.kbch = plan.kbch; dev.nbch = plan.nbch; dev.P = plan.nparity; dev.nldpc = plan.nldpc;
     dev.q = plan.q; dev.nent = (int)plan.ldpc_ent.size(); dev.chunk = plan.bch_chunk;
-    dev.bch_waves = plan.bch_waves;
     dev.parity_il = plan.parity_interleave ? 1 : 0;
     dev.hem = mode ? 1 : 0;
     dev.inband = inband ? 1 : 0;
@@ -594,18 +589,15 @@ struct dvbt2ll_chain {
   hipStream_t cap_stream = nullptr;
   std::vector<std::unique_ptr<ChainGraph>> graphs;
   int max_frames = 0;
-  // fused: FEC and map in one kernel (fec_kernel FEC_TS_TO_PAIRS, the codeword never leaves LDS);
-  // an experiment switch, see dvbt2ll_chain_create
-  bool fused = false;
   int64_t pair_stride = 0;   // pairs buffer: frame k's slots at k * pair_stride (multiple of 8)
   int64_t cw_stride = 0;
   int64_t iq_per_frame = 0;
   int64_t ts_per_frame = 0;
   int pay = 0;
-  // stage timing: 5 events per run (start, after l1post, after fec, after map, after ofdm) recorded
+  // stage timing: 4 events per run (start, after fec, after map + L1-post, after ofdm) recorded
   // on the launch stream without host synchronisation; folded into ms[] by get_timing()
-  // (stages 0 fec, 1 map, 2 ofdm, 3 l1post)
-  static constexpr int NEV = 5;
+  // (stages 0 fec, 1 map, 2 ofdm; stage 3 is reserved and stays 0)
+  static constexpr int NEV = 4;
   bool timing = false;
   std::vector<hipEvent_t> evpool;
   size_t evused = 0;
@@ -624,7 +616,7 @@ struct dvbt2ll_chain {
   int fold_timing() {
     if (!evused) return 0;
     int st = 0;
-    static const int stage_of[4] = {3, 0, 1, 2};   // event interval k -> stage
+    static const int stage_of[NEV - 1] = {0, 1, 2};   // event interval k -> stage
     for (size_t b = 0; b + NEV - 1 < evused && !st; b += NEV) {
       hipError_t e = hipEventSynchronize(evpool[b + NEV - 1]);
       for (int k = 0; k < NEV - 1 && e == hipSuccess; k++) {
@@ -643,18 +635,13 @@ struct dvbt2ll_chain {
     evused = 0;
     return st;
   }
-  // the chain's kernels on stream s: the frames' L1-post cells, fused FEC + map or FEC then map,
-  // then OFDM.  evl, ev1, ev2 (timing): recorded after the L1-post, the FEC (+ map) and the map kernel
+  // the chain's kernels on stream s: FEC, map (its extra workgroups generate the frames' L1-post
+  // cells), OFDM.  ev1, ev2 (timing): recorded after the FEC and the map kernel
   hipError_t launch_chain(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, hipStream_t s,
-                          hipEvent_t evl, hipEvent_t ev1, hipEvent_t ev2) {
-    // L1-post: workgroups of the map kernel's launch, or (fused FEC + map) a launch of its own
-    hipError_t e = fused ? launch_l1post(l1.dev, lio, s) : hipSuccess;
-    if (e == hipSuccess && evl) e = hipEventRecord(evl, s);
-    if (e == hipSuccess)
-      e = fused ? launch_fec_map(fec.dev, fio, map.dev, mio.out_pairs, mio.frame_stride, s)
-                : launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, s);
+                          hipEvent_t ev1, hipEvent_t ev2) {
+    hipError_t e = launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, s);
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, s);
-    if (e == hipSuccess && !fused) e = launch_map(map.dev, mio, s, &l1.dev, &lio);
+    if (e == hipSuccess) e = launch_map(map.dev, mio, s, &l1.dev, &lio);
     if (e == hipSuccess && ev2) e = hipEventRecord(ev2, s);
     if (e == hipSuccess) e = launch_ofdm(ofdm.dev, oio, s);
     return e;
@@ -666,7 +653,7 @@ struct dvbt2ll_chain {
   // under it; with several slots the calls still overlap on the device
   int graph_launch(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, int slot,
                    hipStream_t s) {
-    const int nk = 3;   // fec, map (+ L1-post), ofdm; fused: l1post, fec + map, ofdm
+    const int nk = 3;   // fec, map (+ L1-post), ofdm
     ChainGraph *g = nullptr;
     for (auto &c : graphs)
       if (c->nframes == nframes && c->fmt == ofdm.dev.fmt && c->slot == slot) g = c.get();
@@ -678,7 +665,7 @@ struct dvbt2ll_chain {
       c->fmt = ofdm.dev.fmt;
       c->slot = slot;
       HIP_TRY(hipStreamBeginCapture(cap_stream, hipStreamCaptureModeThreadLocal));
-      hipError_t e1 = launch_chain(lio, fio, mio, oio, cap_stream, nullptr, nullptr, nullptr);
+      hipError_t e1 = launch_chain(lio, fio, mio, oio, cap_stream, nullptr, nullptr);
       hipError_t ec = hipStreamEndCapture(cap_stream, &c->graph);
       HIP_TRY(e1);
       HIP_TRY(ec);
@@ -726,19 +713,14 @@ struct dvbt2ll_chain {
     if (slot_used[slot]) HIP_TRY(hipEventSynchronize(slot_done[slot]));
     L1Dev ld = l1.dev;
     FecDev fd = fec.dev;
-    MapDev md = map.dev, md0{};
+    MapDev md = map.dev;
     OfdmDev od = ofdm.dev;
     L1IO li = lio;
     FecIO fi = fio;
     MapIO mi = mio;
     OfdmIO oi = oio;
-    uint16_t *op = fused ? mio.out_pairs : nullptr;
-    int64_t fs = fused ? mio.frame_stride : 0;
-    void *al[2] = {&ld, &li};
-    void *a0[5] = {&fd, &fi, fused ? (void *)&md : (void *)&md0, &op, &fs};
-    void *a1[4] = {&md, &mi, &ld, &li}, *a2[2] = {&od, &oi};
+    void *a0[2] = {&fd, &fi}, *a1[4] = {&md, &mi, &ld, &li}, *a2[2] = {&od, &oi};
     void **args[3] = {a0, a1, a2};
-    if (fused) { args[0] = al; args[1] = a0; }
     for (int k = 0; k < nk; k++) {
       hipKernelNodeParams p = g->base[k];
       p.kernelParams = args[k];
@@ -749,7 +731,7 @@ struct dvbt2ll_chain {
     return 0;
   }
   int alloc_slot(int k) {
-    if ((!fused && cw[k].ensure((size_t)frame.F * max_frames * cw_stride)) ||
+    if (cw[k].ensure((size_t)frame.F * max_frames * cw_stride) ||
         pairs[k].ensure((size_t)pair_stride * max_frames * 2) || l1buf[k].ensure((size_t)l1_stride * max_frames * 8))
       return DVBT2LL_ENOMEM;
     if (!slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
@@ -868,15 +850,6 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32) ||
       (uint64_t)h->l1_stride * h->max_frames * 8 >= (1ull << 32))
     return DVBT2LL_EINVAL;
-  {
-    // tuning knob for kernel experiments (tools/gpu_fused_ab.sh): DVBT2LL_CHAIN_FUSED=1 runs FEC and
-    // map as one kernel where its LDS allows 3+ workgroups per CU.  Off by default: measured slower
-    // (cfg3 0.707 ms against 0.343 + 0.269 ms per 64 frames; the map phases' table loads are not
-    // hidden at 4 workgroups per CU), kept parity-tested for the record
-    const char *fu = std::getenv("DVBT2LL_CHAIN_FUSED");
-    const int lds = fec_map_lds(h->frame.cs, h->fec.plan.nldpc);
-    h->fused = lds && (160 * 1024) / lds >= 3 && fu && std::atoi(fu);
-  }
   if ((r = h->alloc_slot(0))) return r;
   if ((r = upload(h->aux, auxv))) return r;
   if (h->sync_err.ensure(4)) return DVBT2LL_ENOMEM;
@@ -898,7 +871,6 @@ extern "C" int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info
   info->fft_size = h->pilot.N;
   info->guard_interval = h->pilot.G;
   info->cw_stride_bytes = h->cw_stride;
-  info->fused_fec_map = h->fused ? 1 : 0;
   return DVBT2LL_OK;
 }
 
@@ -949,7 +921,7 @@ extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, i
   fio.ts_base = ts_base;
   fio.ts_len = ts_len;
   fio.first_block = first_frame * F;
-  fio.out = h->fused ? nullptr : cw.as<uint8_t>();
+  fio.out = cw.as<uint8_t>();
   fio.cw_stride = h->cw_stride;
   fio.nblocks = F * nf;
   fio.sync_err = h->sync_err.as<uint32_t>();
@@ -978,8 +950,8 @@ extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, i
     int r = h->graph_launch(lio, fio, mio, oio, nf, slot, s);
     if (r) return r;
   } else {
-    HIP_TRY(h->launch_chain(lio, fio, mio, oio, s, ev[1], ev[2], ev[3]));
-    if (h->timing) HIP_TRY(hipEventRecord(ev[4], s));
+    HIP_TRY(h->launch_chain(lio, fio, mio, oio, s, ev[1], ev[2]));
+    if (h->timing) HIP_TRY(hipEventRecord(ev[3], s));
   }
   HIP_TRY(hipEventRecord(h->slot_done[slot], s));
   h->slot_used[slot] = true;
@@ -1004,7 +976,7 @@ extern "C" int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots) {
     if (r) return r;
   }
   for (int k = nslots; k < DVBT2LL_CHAIN_MAX_SLOTS; k++) {
-    h->cw[k].release();   // (never allocated when fused)
+    h->cw[k].release();
     h->pairs[k].release();
     h->slot_used[k] = false;
   }
@@ -1052,8 +1024,7 @@ extern "C" int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *l
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes) {
-  // the fused kernel keeps codewords in LDS: only the two-kernel path has them
-  if (!h || !out || bytes < 0 || h->fused || (size_t)bytes > h->cw[h->last_slot].n) return DVBT2LL_EINVAL;
+  if (!h || !out || bytes < 0 || (size_t)bytes > h->cw[h->last_slot].n) return DVBT2LL_EINVAL;
   const DevBuf &cw = h->cw[h->last_slot];
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipDeviceSynchronize());

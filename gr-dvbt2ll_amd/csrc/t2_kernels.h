@@ -10,14 +10,10 @@ enum FecMode {
   FEC_TS_TO_TEMPU = 0,   // chain: TS bytes -> packed interleaver-input codeword
   FEC_TS_TO_BITS = 1,    // bbheaderbch block: TS bytes -> unpacked nbch bits
   FEC_BITS_TO_BITS = 2,  // ldpc block: unpacked nbch bits -> unpacked nldpc bits (natural)
-  FEC_TS_TO_PAIRS = 3,   // fused chain: TS bytes -> codeword in LDS -> bit interleave + demux + cell
-                         // and time interleave -> constellation index pairs (FEC and map kernels in one)
 };
 
 struct FecDev {
   const uint64_t *bch_tab;      // 256 x 3
-  const uint64_t *bch_m1;       // 192 x 3: x^(8 chunk) mod g (one wave's Horner step)
-  const uint64_t *bch_m64;      // 192 x 3: x^(8 * 64 chunk) mod g (combine of the four waves)
   const uint64_t *bch_ctab;     // [P/4][16][64] x 4: lane shift nibble tables (FecPlan::bch_ctab)
   const uint16_t *ldpc_rowptr;  // q + 1
   const uint32_t *ldpc_ent;     // nent
@@ -25,8 +21,7 @@ struct FecDev {
   const uint8_t *crc8_tab;      // 256
   const uint8_t *crc8_shift;    // 8 x 256
   const uint8_t *hcrc_bits;     // 72: BBHEADER CRC-8 contribution of each header bit
-  int kbch, nbch, P, nldpc, q, nent, chunk, parity_il;
-  int bch_waves;                // waves sharing the BCH division (t2_plan FecPlan::bch_waves)
+  int kbch, nbch, P, nldpc, q, nent, chunk, parity_il;   // chunk: BCH message bytes per lane (64 lanes)
   int hem, inband, fec_blocks, ts_rate;
 };
 
@@ -155,11 +150,6 @@ struct GatherIO {
 };
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s);
-// fused FEC + map (FEC_TS_TO_PAIRS): index pairs of launch block b into out_pairs + (b / F) * frame_stride
-hipError_t launch_fec_map(const FecDev &d, const FecIO &io, const MapDev &md, uint16_t *out_pairs,
-                          int64_t frame_stride, hipStream_t s);
-// LDS bytes of the fused kernel for a constellation's cell size / 0 when it would not fit
-int fec_map_lds(int cs, int nldpc);
 // l1d / l1io (optional, the chain): the frames' L1-post cells by extra workgroups of the same launch
 hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1Dev *l1d = nullptr,
                       const L1IO *l1io = nullptr);

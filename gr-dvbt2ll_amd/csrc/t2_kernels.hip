@@ -1,18 +1,18 @@
 // t2_kernels.hip -- gfx950 (MI355X / CDNA4) kernels of the DVB-T2 transmit chain.
 //
-//   fec_kernel   one workgroup per FEC block: BBFRAME build (header, CRC-8 sync
-//                replacement, scrambling) + BCH (256-lane chunked byte-table division,
-//                Horner-combined with GF(2) shift matrices via wave ballots) + LDPC as a
+//   fec_kernel   persistent 256-thread workgroups looping over FEC blocks: BBFRAME build
+//                (header, CRC-8 sync replacement, scrambling) + BCH (64-lane chunked byte-table
+//                division, chunk remainders moved by per-lane nibble tables) + LDPC as a
 //                quasi-cyclic array of 360-bit rotations with a bit-packed accumulate scan.
 //                Reference: lib/bbheaderbch_bb_impl.cc:648-742 (+ ldpc_calculate :625-646).
-//   map_kernel   one workgroup per FEC block: column-twist bit interleave + demux + QAM LUT
-//                + rotated-constellation Q delay, optionally cell-interleaved through LDS.
-//                Reference: lib/interleavermod_bc_impl.cc:270-704, framemapper :1973-1998.
-//   ofdm_kernel  one workgroup per OFDM symbol: gather (frame map + time/frequency
-//                interleave + pilots, all pre-composed into one int32 map) fused into the
-//                first pass of a 3-pass register/LDS IFFT, normalisation, guard interval, P1.
-//                Reference: lib/framemapperfint_cc_impl.cc:1999-2142,
-//                           lib/pilotgenp1insert_cc_impl.cc:2784-2907.
+//   map_kernel   one workgroup per FEC block: column-twist bit interleave + demux, then either
+//                the QAM LUT (interleavermod block) or the cell + time interleaver store of
+//                constellation index pairs (chain); extra workgroups generate the L1-post cells.
+//                Reference: lib/interleavermod_bc_impl.cc:270-704, framemapper :1973-2028.
+//   ofdm*_kernel one workgroup per (OFDM symbol, frame): bins scattered (chain) or gathered
+//                (pilotgen block) into a register/LDS IFFT, normalisation, output gain, guard
+//                interval, P1.  Reference: lib/framemapperfint_cc_impl.cc:1999-2142,
+//                lib/pilotgenp1insert_cc_impl.cc:2784-2907.
 // No MFMA: these are bitwise / permutation / complex-FFT paths.
 #include "t2_kernels.h"
 
@@ -26,44 +26,29 @@ namespace t2 {
 // ============================================================================ helpers
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-#ifndef CMUL_PACKED
-#define CMUL_PACKED 1
-#endif
 typedef float f2v __attribute__((ext_vector_type(2)));
 // complex product as two packed-FP32 ops: t = (ax bx, ax by); (ay (-by) + t.x, ay bx + t.y)
 // (operand swizzles and the negation ride on op_sel / neg_lo instead of extra moves)
 __device__ __forceinline__ float2 cmulf(float2 a, float2 b) {
-#if CMUL_PACKED
   const f2v av = {a.x, a.y}, bv = {b.x, b.y};
   f2v t, r;
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(av), "v"(bv));
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]" : "=v"(r) : "v"(av), "v"(bv), "v"(t));
   return make_float2(r.x, r.y);
-#else
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-#endif
 }
 // a + i b and a - i b as one packed add each (b's halves swapped and one negated by op_sel /
 // neg_lo / neg_hi); a * s for a real s as one packed multiply
 __device__ __forceinline__ float2 cadd_i(float2 a, float2 b) {
-#if CMUL_PACKED
   const f2v av = {a.x, a.y}, bv = {b.x, b.y};
   f2v r;
   asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(av), "v"(bv));
   return make_float2(r.x, r.y);
-#else
-  return make_float2(a.x - b.y, a.y + b.x);
-#endif
 }
 __device__ __forceinline__ float2 csub_i(float2 a, float2 b) {
-#if CMUL_PACKED
   const f2v av = {a.x, a.y}, bv = {b.x, b.y};
   f2v r;
   asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(av), "v"(bv));
   return make_float2(r.x, r.y);
-#else
-  return make_float2(a.x + b.y, a.y - b.x);
-#endif
 }
 __device__ __forceinline__ float2 cscale(float2 a, float sc) {
   const f2v r = f2v{a.x, a.y} * f2v{sc, sc};
@@ -82,23 +67,9 @@ __device__ __forceinline__ void st_off(T *base, uint32_t byte_off, T v) {
 }
 
 // streaming store (nontemporal): final IQ samples are never re-read by the chain
-// (experiment switch OFDM_STORE: 0 = one 64-bit nontemporal store, 1 = two 32-bit, 2 = plain)
-#ifndef OFDM_STORE
-#define OFDM_STORE 0
-#endif
 __device__ __forceinline__ void st_nt(float2 *base, uint32_t byte_off, float2 v) {
   float2 *p = (float2 *)((char *)base + byte_off);
-#if defined(OFDM_NOSTORE)
-  if (v.x == v.x) return;   // experiment: drop (nearly) every IQ store, keep the arithmetic
-#endif
-#if OFDM_STORE == 0
   __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, v), (uint64_t *)p);
-#elif OFDM_STORE == 1
-  __builtin_nontemporal_store(v.x, &p->x);
-  __builtin_nontemporal_store(v.y, &p->y);
-#else
-  *p = v;
-#endif
 }
 
 __device__ __forceinline__ uint32_t rd_lane_u32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -123,71 +94,28 @@ static hipError_t lds_limit(const void *fn, int bytes) {
 }
 
 // ============================================================================ FEC kernel
-// experiment switch (product builds: 0): bit 0 = phase timestamps of each block written over
-// the first 44 bytes of its codeword (wrong output; tools/fec_phases.py decodes them)
-#ifndef FEC_VARIANT
-#define FEC_VARIANT 0
-#endif
-#if FEC_VARIANT & 1
-__shared__ uint64_t g_fec_ts[16];
-#define FEC_PHASE(i) do { if (threadIdx.x == 0) g_fec_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define FEC_PHASE(i) do { } while (0)
-#endif
-#ifndef FEC_BCH_TAB
-#define FEC_BCH_TAB 1    // 1: chunk remainders combined by per-lane nibble tables; 0: Horner over the lanes
-#endif
-#ifndef FEC_BCH_TAB_JB
-#define FEC_BCH_TAB_JB 2  // table lookups in flight per lane (4 spills more at the 72-VGPR budget of 7 WGs/CU)
-#endif
-#ifndef FEC_BCH_PRIO
-#define FEC_BCH_PRIO 1   // wave priority (s_setprio) of the BCH wave while it runs (0: off)
-#endif
 constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
 constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 233280 / 360)
 constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g || d_g[0..56)
-#ifndef MAP_CQ
-#define MAP_CQ 8
-#endif
-#ifndef MAP_CW16
-#define MAP_CW16 1      // 1: the map kernel loads the codeword with 16-byte loads (0: 4-byte)
-#endif
-#ifndef FEC_STAGE16
-#define FEC_STAGE16 1   // 1: raw TS staged with 16-byte loads (0: 4-byte)
-#endif
-#ifndef FEC_BTAB_GLOBAL
-#define FEC_BTAB_GLOBAL 0   // 1: BCH byte table read from global memory (no LDS copy per workgroup)
-#endif
-#ifndef FEC_WGS
-#define FEC_WGS 7           // most resident FEC workgroups per CU (register budget; LDS may allow fewer)
-#endif
-constexpr int FEC_WG_PER_CU = FEC_WGS;
+constexpr int FEC_WG_PER_CU = 7;        // most resident FEC workgroups per CU (72-VGPR budget; LDS may allow fewer)
+constexpr int FEC_BCH_JB = 2;           // nibble-table lookups in flight per lane in the BCH combine
 // dynamic LDS carve (bytes): a persistent part (the workgroup loops over FEC blocks; tables are
 // staged once), then the per-block area, reused by phase:
 //   BB/CRC phase: [frame | raw TS bytes | CRC-8 table | CRC-8 zero-extension tables]
 //   LDPC: [frame | D: ngroups x 13 words | rows: q x 12 words], ngroups + q = nldpc / 360 (<= 180)
-//   fused map phase (FEC_TS_TO_PAIRS): [cell indices | index pairs] over the whole per-block area,
-//   the interleaver-input words (built from frame + rows) beyond it (fec_map_lds)
 constexpr int SM_BTAB = 0;                                   // 256*3*8 = 6144
-constexpr int SM_ENT = SM_BTAB + (FEC_BTAB_GLOBAL ? 0 : 6144);  // 648*4
+constexpr int SM_ENT = SM_BTAB + 6144;                       // 648*4
 constexpr int SM_HCRC = SM_ENT + FEC_MAX_ENT * 4;            // 72 (+8)
 constexpr int SM_SYNC = SM_HCRC + 80;                        // 48 (<= 36 sync slots)
 constexpr int SM_W = SM_SYNC + 48;                           // 12*4
 constexpr int SM_BLK = SM_W + 48;                            // per-block area
 constexpr int SM_FRAME = SM_BLK;
 constexpr int SM_PHASE = SM_FRAME + FEC_FRAME_BYTES;
-constexpr int SM_RAW = SM_PHASE;                             // raw TS bytes of the block (NM)
-constexpr int FEC_RAW_BYTES = 188 + 6720 + 32;               // one packet before + max payload + slack
-constexpr int SM_CRC8 = SM_RAW + ((FEC_RAW_BYTES + 15) & ~15);   // 256
-constexpr int SM_CRCSH = SM_CRC8 + 256;                      // 2048
-constexpr int SM_D = SM_PHASE;                               // rows follow D at word ngroups * 13
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
-constexpr int FEC_SMEM = (SM_CRCSH + 2048 > SM_PHASE + FEC_LDPC_BYTES ? SM_CRCSH + 2048 : SM_PHASE + FEC_LDPC_BYTES);
-static_assert(SM_BTAB % 16 == 0 && SM_D % 16 == 0 && SM_ENT % 16 == 0 && SM_BLK % 16 == 0, "LDS carve alignment");
-static_assert(SM_SYNC % 8 == 0 && SM_BLK - SM_SYNC >= 4 * 3 * 8, "BCH wave remainders in SM_SYNC + SM_W");
+static_assert(SM_BTAB % 16 == 0 && SM_PHASE % 16 == 0 && SM_ENT % 16 == 0 && SM_BLK % 16 == 0, "LDS carve alignment");
 // the carve a plan actually needs (frame, raw TS and LDPC areas sized for its code): the launch
-// fits as many persistent workgroups per CU as it allows, up to FEC_WGS (the register budget)
+// fits as many persistent workgroups per CU as it allows, up to FEC_WG_PER_CU (the register budget)
 struct FecCarve {
   int phase, crc8, crcsh, total;
 };
@@ -209,9 +137,6 @@ __device__ __forceinline__ int64_t payload_pos(int64_t J, int hem) {
 // inclusive prefix XOR over the 64 lanes of a wave with DPP moves (VALU latency, no LDS
 // crossbar): row_shr 1, 2, 4, 8 within each 16-lane row, then row_bcast:15 into rows 1 and 3 and
 // row_bcast:31 into rows 2 and 3 (GFX9-family DPP)
-#ifndef FEC_DPP_SCAN
-#define FEC_DPP_SCAN 1
-#endif
 __device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t v) {
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
@@ -220,18 +145,6 @@ __device__ __forceinline__ uint32_t wave_prefix_xor(uint32_t v) {
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
   return v;
-}
-
-// parity of (row . a) over GF(2) for a 192-bit matrix row m and the uniform 192-bit vector a:
-// the six 32-bit AND products folded with v_bitop3 ((x & y) ^ z, truth table 0x6A), one popcount
-__device__ __forceinline__ uint32_t row_parity(const uint64_t m[3], uint64_t a0, uint64_t a1, uint64_t a2) {
-  uint32_t acc = (uint32_t)m[0] & (uint32_t)a0;
-  acc = __builtin_amdgcn_bitop3_b32((uint32_t)(m[0] >> 32), (uint32_t)(a0 >> 32), acc, 0x6A);
-  acc = __builtin_amdgcn_bitop3_b32((uint32_t)m[1], (uint32_t)a1, acc, 0x6A);
-  acc = __builtin_amdgcn_bitop3_b32((uint32_t)(m[1] >> 32), (uint32_t)(a1 >> 32), acc, 0x6A);
-  acc = __builtin_amdgcn_bitop3_b32((uint32_t)m[2], (uint32_t)a2, acc, 0x6A);
-  acc = __builtin_amdgcn_bitop3_b32((uint32_t)(m[2] >> 32), (uint32_t)(a2 >> 32), acc, 0x6A);
-  return __builtin_popcount(acc) & 1u;
 }
 
 __device__ __forceinline__ uint8_t get_byte192(const uint64_t w[3], int lowbit) {
@@ -248,30 +161,9 @@ __device__ __forceinline__ void ldpc_group_word(uint32_t *D, const uint8_t *fram
                       ((uint32_t)gb[(b + 2) % 45] << 8) | (uint32_t)gb[(b + 3) % 45];
 }
 
-// new = M . a over GF(2) for the uniform 192-bit vector a, as three wave ballots: lane l holds rows
-// l, l + 64, l + 128 of M (m[s] = row l + 64 s)
-__device__ __forceinline__ void gf2_matvec(const uint64_t m[3][3], uint64_t &a0, uint64_t &a1, uint64_t &a2) {
-  const uint64_t n0 = __ballot(row_parity(m[0], a0, a1, a2));
-  const uint64_t n1 = __ballot(row_parity(m[1], a0, a1, a2));
-  const uint64_t n2 = __ballot(row_parity(m[2], a0, a1, a2));
-  a0 = n0;
-  a1 = n1;
-  a2 = n2;
-}
-
-__device__ __forceinline__ void load_rows(uint64_t m[3][3], const uint64_t *g, int lane) {
-  asm volatile("" : "+s"(g));   // keep the row loads out of the loop-carried register set
-  for (int s = 0; s < 3; s++)
-    for (int k = 0; k < 3; k++) m[s][k] = g[(lane + 64 * s) * 3 + k];
-}
-
-// One wave's share of the BCH parity of the BBFRAME frame[0..L): lane t = 64 w + lane divides chunk
-// t of the NC = 64 bch_waves chunks of C bytes (t2_plan: bch_chunk; the chunks end at L, leading
-// ones may be empty) by the byte table, then a Horner pass over the wave's 64 lanes with M1 (v -> v x^(8C)
-// mod g) as wave ballots.  Returns the wave's remainder sum_l r_l x^(8C (63 - l)) (uniform).
-// P is a template parameter so the register geometry (top byte, masks) is compile-time.
 // byte-table division of frame[lo, hi) (lo clamped at 0) into the P-bit remainder r; the next message
-// byte is read before the table lookup's wait (LDS returns in order, so it costs no extra round trip)
+// byte is read before the table lookup's wait (LDS returns in order, so it costs no extra round trip).
+// P is a template parameter so the register geometry (top byte, masks) is compile-time.
 template <int P>
 __device__ __forceinline__ void bch_divide(const uint8_t *frame, const uint64_t *btab, int lo, int hi, uint64_t &r0,
                                            uint64_t &r1, uint64_t &r2) {
@@ -301,24 +193,18 @@ __device__ __forceinline__ uint64_t wave_xor64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// BCH parity of the BBFRAME frame[0..L) by one wave (bbheader:504-531): lane l divides chunk l of the
+// 64 chunks of C bytes (t2_plan: bch_chunk; the chunks end at L, leading ones may be empty) by the
+// byte table, then moves its remainder to the end of the message, r_l x^(8C (63 - l)) mod g, by
+// per-lane nibble-table lookups (no dependency between lanes), and the wave XOR-reduces them.
+// Returns the P-bit parity (uniform).
 template <int P>
-__device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64_t *btab, const uint64_t *m1g,
-                                              const uint64_t *ctab, int L, int C, int NC, int t, int lane,
-                                              uint64_t a[3]) {
-  const int lo = L - (NC - t) * C, hi = L - (NC - 1 - t) * C;
-#if !FEC_BCH_TAB
-  uint64_t m1[3][3];
-  load_rows(m1, m1g, lane);
-#endif
+__device__ __forceinline__ void bch_wave(const uint8_t *frame, const uint64_t *btab, const uint64_t *ctab, int L,
+                                         int C, int lane, uint64_t a[3]) {
+  const int lo = L - (64 - lane) * C, hi = L - (63 - lane) * C;
   uint64_t r0 = 0, r1 = 0, r2 = 0;
   bch_divide<P>(frame, btab, lo, hi, r0, r1, r2);
-#if FEC_VARIANT & 2
-  FEC_PHASE(5);   // experiment: byte-table division done (phase 5 = division, 6 = shift + combine)
-#endif
-#if FEC_BCH_TAB
-  // each lane moves its remainder to the end of the wave's chunks by nibble-table lookups (no
-  // dependency between lanes), then one XOR reduction over the wave
-  constexpr int NJ = P / 4, JB = FEC_BCH_TAB_JB;
+  constexpr int NJ = P / 4, JB = FEC_BCH_JB;
   uint64_t s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll 1
   for (int j0 = 0; j0 < NJ; j0 += JB) {
@@ -347,55 +233,7 @@ __device__ __forceinline__ void bch_wave_part(const uint8_t *frame, const uint64
   a[0] = wave_xor64(s0);
   a[1] = wave_xor64(s1);
   a[2] = P > 128 ? wave_xor64(s2) : 0ull;
-#else
-  uint64_t a0 = rd_lane_u64(r0, 0), a1 = rd_lane_u64(r1, 0), a2 = rd_lane_u64(r2, 0);
-  for (int l = 1; l < 64; l++) {
-    gf2_matvec(m1, a0, a1, a2);
-    a0 ^= rd_lane_u64(r0, l);
-    a1 ^= rd_lane_u64(r1, l);
-    a2 ^= rd_lane_u64(r2, l);
-  }
-  a[0] = a0;
-  a[1] = a1;
-  a[2] = a2;
-#endif
 }
-
-// the nw wave remainders R_w (LDS, 3 words each) -> (..(R0 M64 + R1) M64 + ..) M64 + R_(nw-1),
-// written MSB (x^(P-1)) first as the BCH parity bytes frame[L..L + P/8) (bbheader:504-531)
-template <int P>
-__device__ __forceinline__ void bch_combine(uint8_t *frame, const uint64_t *wres, const uint64_t *m64g, int L,
-                                            int nw, int lane) {
-  uint64_t m[3][3];
-  if (nw > 1) load_rows(m, m64g, lane);
-  uint64_t a0 = wres[0], a1 = wres[1], a2 = wres[2];
-  for (int w = 1; w < nw; w++) {
-    gf2_matvec(m, a0, a1, a2);
-    a0 ^= wres[3 * w];
-    a1 ^= wres[3 * w + 1];
-    a2 ^= wres[3 * w + 2];
-  }
-  const uint64_t acc[3] = {a0, a1, a2};
-  if (lane < P / 8) frame[L + lane] = get_byte192(acc, P - 8 - 8 * lane);
-}
-
-// fused mode: the map phases' LDS (cell indices at SM_BLK, index pairs after them, the codeword
-// words beyond the FEC carve and the indices)
-__host__ __device__ inline int fec_map_idx_bytes(int cs) { return (cs + 15) & ~15; }
-__host__ __device__ inline int fec_map_cww_off(int cs) {
-  const int a = SM_BLK + fec_map_idx_bytes(cs), b = (FEC_SMEM + 15) & ~15;
-  return a > b ? a : b;
-}
-__host__ __device__ inline int fec_map_smem(int cs, int nldpc) {
-  const int cw = fec_map_cww_off(cs) + ((nldpc / 8 + 4 + 15) & ~15);
-  const int st = SM_BLK + fec_map_idx_bytes(cs) + ((2 * cs + 15) & ~15);
-  return cw > st ? cw : st;
-}
-
-template <int NT> __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, int tid);
-template <int NT, int CQ = MAP_CQ>
-__device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
-                                uint16_t *stage, int blk, int tid, bool alias = false);
 
 // LDPC parity rows: row a, word w of p[a][c] = XOR over the row's entries (g, b) of the window
 // d_g[(c - b) mod 360], c = 32 w; 12 words per row at rowA
@@ -419,8 +257,7 @@ __device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, con
 }
 
 template <int MODE>
-__global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io, MapDev md,
-                                                                        uint16_t *out_pairs, int64_t frame_stride) {
+__global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int L = d.kbch >> 3;           // BBFRAME bytes
@@ -433,41 +270,24 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
   uint8_t *const phase = smem + cv.phase;   // raw TS bytes (NM), then the LDPC groups and rows
   uint8_t *hcrc8 = smem + SM_HCRC;
   uint8_t *syncv = smem + SM_SYNC;
-#if FEC_BTAB_GLOBAL
-  const uint64_t *btab = d.bch_tab;
-#else
   uint64_t *btab = (uint64_t *)(smem + SM_BTAB);
-#endif
   uint32_t *D = (uint32_t *)phase;
   uint32_t *Wv = (uint32_t *)(smem + SM_W);
   uint32_t *ents = (uint32_t *)(smem + SM_ENT);
-  uint64_t *wres = (uint64_t *)(smem + SM_SYNC);   // BCH wave remainders (SM_SYNC + SM_W, free then)
 
   // ---- constant tables into LDS, once: the workgroup then loops over FEC blocks
-  if (!FEC_BTAB_GLOBAL)
-    for (int i = tid; i < 768; i += FEC_THREADS) ((uint64_t *)(smem + SM_BTAB))[i] = d.bch_tab[i];
+  for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
   for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
   if (MODE != FEC_BITS_TO_BITS)
     for (int i = tid; i < 72; i += FEC_THREADS) hcrc8[i] = d.hcrc_bits[i];
   __syncthreads();
 
-  // blocks of this workgroup: a stride over the launch, or (fused mode, grid a multiple of 8) a
-  // stride within the eighth of the launch that its XCD covers, so that the FEC blocks of a time-
-  // interleaver block, whose index pairs interleave in 10-byte runs, are stored through one L2
-  int bstart = blockIdx.x, bstep = gridDim.x, bend = io.nblocks;
-  if (MODE == FEC_TS_TO_PAIRS && (gridDim.x & 7) == 0) {
-    const int q = (io.nblocks + 7) >> 3, x = blockIdx.x & 7;
-    bstart = x * q + (blockIdx.x >> 3);
-    bstep = gridDim.x >> 3;
-    bend = min((x + 1) * q, io.nblocks);
-  }
-  for (int bi = bstart; bi < bend; bi += bstep) {
+  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
   // stream-major multi-stream batch: launch block bi is block bi % bps of stream bi / bps, whose TS
   // slice (same ts_base / ts_len layout for every stream) starts at in + stream * ts_stride
   const int sidx = io.blocks_per_stream ? bi / io.blocks_per_stream : 0;
   const int64_t B = io.first_block + (bi - sidx * io.blocks_per_stream);
   const uint8_t *tin = io.in + (int64_t)sidx * io.ts_stride;
-  FEC_PHASE(0);
   do {   // one FEC block; `break` ends it early (block-API modes)
   if (MODE == FEC_BITS_TO_BITS) {
     // pack nbch unpacked info bits
@@ -494,12 +314,9 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
     int count0;   // TS packet position of the next input byte at block start
     if (d.hem) count0 = J0 == 0 ? 0 : (int)((payload_pos(J0 - 1, 1) + 1) % 188);
     else count0 = (int)(pos0 % 188);
-    FEC_PHASE(1);
-    // ---- CRC-8 of each packet whose sync slot falls in this block (NM only):
-    //      8 lanes per packet, 24-byte chunks combined with zero-extension tables
-    // NM: stage the raw stream bytes [pos0 - 188, pos0 + npay) once (independent dword loads;
-    // raw byte i = stream byte rs + i lives at LDS byte cv.phase + delta + i); the CRC-8 chains and
-    // the payload words then read LDS
+    // NM: stage the raw stream bytes [pos0 - 188, pos0 + npay) once with 16-byte loads from a
+    // 16-byte aligned start (raw byte i = stream byte rs + i lives at LDS byte cv.phase + delta + i);
+    // the CRC-8 chains and the payload words then read LDS
     const int64_t rs = pos0 - 188;
     int delta = 0, first_slot = 0;
     const uint32_t *raww = (const uint32_t *)phase;
@@ -507,47 +324,26 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
       const int64_t rel = rs - io.ts_base;                 // >= -188
       for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)crc8)[i] = ((const uint32_t *)d.crc8_tab)[i];
       for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)crcsh)[i] = ((const uint32_t *)d.crc8_shift)[i];
-      if (FEC_STAGE16) {
-        // 16-byte loads from a 16-byte aligned start (delta < 16)
-        const int64_t w0 = (rel >= 0 ? rel : rel - 15) / 16;   // floor
-        delta = (int)(rel - 16 * w0);
-        const int nq = (delta + npay + 188 + 15) >> 4;
-        uint4 *rawq = (uint4 *)phase;
-        const bool aligned = (((uintptr_t)tin) & 15) == 0;
-        for (int i = tid; i < nq; i += FEC_THREADS) {
-          const int64_t b = 16 * (w0 + i);
-          uint4 v = make_uint4(0u, 0u, 0u, 0u);
-          if (aligned && b >= 0 && b + 16 <= io.ts_len) {
-            v = *(const uint4 *)(tin + b);
-          } else {
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
-            for (int e = 0; e < 16; e++)
-              if (b + e >= 0 && b + e < io.ts_len) w[e >> 2] |= (uint32_t)tin[b + e] << (8 * (e & 3));
-            v = make_uint4(w[0], w[1], w[2], w[3]);
-          }
-          rawq[i] = v;
+      const int64_t w0 = (rel >= 0 ? rel : rel - 15) / 16;   // floor
+      delta = (int)(rel - 16 * w0);
+      const int nq = (delta + npay + 188 + 15) >> 4;
+      uint4 *rawq = (uint4 *)phase;
+      const bool aligned = (((uintptr_t)tin) & 15) == 0;
+      for (int i = tid; i < nq; i += FEC_THREADS) {
+        const int64_t b = 16 * (w0 + i);
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (aligned && b >= 0 && b + 16 <= io.ts_len) {
+          v = *(const uint4 *)(tin + b);
+        } else {   // misaligned buffer or stream edge: byte loads
+          uint32_t w[4] = {0u, 0u, 0u, 0u};
+          for (int e = 0; e < 16; e++)
+            if (b + e >= 0 && b + e < io.ts_len) w[e >> 2] |= (uint32_t)tin[b + e] << (8 * (e & 3));
+          v = make_uint4(w[0], w[1], w[2], w[3]);
         }
-      } else {
-        const int64_t w0 = (rel >= 0 ? rel : rel - 3) / 4;   // floor
-        delta = (int)(rel - 4 * w0);
-        const int nw = (delta + npay + 188 + 3) >> 2;
-        uint32_t *rawst = (uint32_t *)phase;
-        const bool aligned = (((uintptr_t)tin) & 3) == 0;
-        for (int i = tid; i < nw; i += FEC_THREADS) {
-          const int64_t b = 4 * (w0 + i);
-          uint32_t v = 0;
-          if (aligned && b >= 0 && b + 4 <= io.ts_len) {
-            v = *(const uint32_t *)(tin + b);
-          } else {
-            for (int e = 0; e < 4; e++)
-              if (b + e >= 0 && b + e < io.ts_len) v |= (uint32_t)tin[b + e] << (8 * e);
-          }
-          rawst[i] = v;
-        }
+        rawq[i] = v;
       }
       const uint8_t *raw = phase + delta;
       __syncthreads();
-      FEC_PHASE(2);
       first_slot = (188 - count0) % 188;
       const int nslots = first_slot < npay ? (npay - 1 - first_slot) / 188 + 1 : 0;
       // CRC-8 of each packet whose sync slot falls in this block: 8 lanes per packet, 24-byte
@@ -581,7 +377,6 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
         }
       }
       __syncthreads();
-      FEC_PHASE(3);
     }
     if (d.hem && io.sync_err) {
       // HEM drops each packet's sync byte; the one of packet p is consumed just before payload
@@ -650,42 +445,22 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
       }
     }
     __syncthreads();
-    FEC_PHASE(4);
-#if !(FEC_VARIANT & 2)
-    FEC_PHASE(5);
-#endif
 
-    // ---- BCH: waves 0 .. bch_waves - 1 divide 64 chunks each and Horner-combine them
-    //      (bch_wave_part); wave 0 then combines the wave remainders and writes the parity.  The
-    //      other waves meanwhile (chain mode) lay out the LDPC info groups that hold no BCH parity.
+    // ---- BCH on wave 0 (raised issue priority: it is the block's critical path); waves 1..3
+    //      meanwhile (chain mode) lay out the LDPC info groups that hold no BCH parity
     const int ngroups = d.nbch / 360;
-    const int nbw = d.bch_waves, nchunks = 64 * nbw;
-#if FEC_BCH_PRIO
-    if (wave < nbw) __builtin_amdgcn_s_setprio(FEC_BCH_PRIO);   // the BCH is the block's critical path
-#endif
-    if (wave < nbw) {
+    if (wave == 0) {
+      __builtin_amdgcn_s_setprio(1);
       uint64_t a[3];
       switch (P) {   // compile-time register geometry per BCH parity length (t = 12, 10, 8; short 12)
-        case 192: bch_wave_part<192>(frame, btab, d.bch_m1, d.bch_ctab, L, d.chunk, nchunks, tid, lane, a); break;
-        case 168: bch_wave_part<168>(frame, btab, d.bch_m1, d.bch_ctab, L, d.chunk, nchunks, tid, lane, a); break;
-        case 160: bch_wave_part<160>(frame, btab, d.bch_m1, d.bch_ctab, L, d.chunk, nchunks, tid, lane, a); break;
-        default: bch_wave_part<128>(frame, btab, d.bch_m1, d.bch_ctab, L, d.chunk, nchunks, tid, lane, a); break;
+        case 192: bch_wave<192>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
+        case 168: bch_wave<168>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
+        case 160: bch_wave<160>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
+        default: bch_wave<128>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
       }
-      if (lane < 3) wres[3 * wave + lane] = lane == 0 ? a[0] : lane == 1 ? a[1] : a[2];
-    }
-    if (nbw > 1) __syncthreads();     // uniform: every wave remainder is in LDS
-    if (wave == 0) {
-      // same wave as the remainder writes when nbw == 1: its LDS accesses complete in order
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      switch (P) {
-        case 192: bch_combine<192>(frame, wres, d.bch_m64, L, nbw, lane); break;
-        case 168: bch_combine<168>(frame, wres, d.bch_m64, L, nbw, lane); break;
-        case 160: bch_combine<160>(frame, wres, d.bch_m64, L, nbw, lane); break;
-        default: bch_combine<128>(frame, wres, d.bch_m64, L, nbw, lane); break;
-      }
-      if (MODE == FEC_TS_TO_TEMPU || MODE == FEC_TS_TO_PAIRS) {
+      // parity MSB (x^(P-1)) first as frame[L..L + P/8) (bbheader:504-531)
+      if (lane < P / 8) frame[L + lane] = get_byte192(a, P - 8 - 8 * lane);
+      if (MODE == FEC_TS_TO_TEMPU) {
         // the last info group holds the BCH parity (P < 360): lay it out here, after the parity
         // bytes (same wave; LDS accesses of one wave complete in order)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -693,19 +468,14 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (lane < FEC_DW) ldpc_group_word(D, frame, ngroups - 1, lane);
       }
-    } else if (MODE == FEC_TS_TO_TEMPU || MODE == FEC_TS_TO_PAIRS) {
-      // waves 1..3 (after their BCH share, if any) lay out the info groups without parity
+      __builtin_amdgcn_s_setprio(0);
+    } else if (MODE == FEC_TS_TO_TEMPU) {
       for (int it = tid - 64; it < (ngroups - 1) * FEC_DW; it += FEC_THREADS - 64) {
         const int g = it / FEC_DW;
         ldpc_group_word(D, frame, g, it - g * FEC_DW);
       }
     }
-#if FEC_BCH_PRIO
-    if (wave < nbw) __builtin_amdgcn_s_setprio(0);
-#endif
     __syncthreads();
-    FEC_PHASE(6);
-    FEC_PHASE(7);
     if (MODE == FEC_TS_TO_BITS) {
       uint8_t *dst = io.out + (int64_t)bi * d.nbch;
       for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
@@ -722,32 +492,21 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
       ldpc_group_word(D, frame, g, it - g * FEC_DW);
     }
     __syncthreads();
-    FEC_PHASE(7);
   }
   // row a, word w of p[a][c] = XOR over entries (g, b) of d_g[(c - b) mod 360]
   const int q = d.q;
   uint32_t *rowA = D + ngroups * FEC_DW;
   ldpc_rows(D, rowA, ents, d.ldpc_rowptr, q, tid, FEC_THREADS);
   __syncthreads();
-  FEC_PHASE(8);
   // inclusive prefix XOR over rows a, in place: wave w scans word columns 3w..3w+2, 64 rows
-  // per wave-level shuffle scan plus the carry of the previous 64
+  // per DPP wave scan plus the carry of the previous 64
   uint32_t *cur = rowA;
   for (int col = 3 * wave; col < 3 * wave + 3; col++) {
     uint32_t carry = 0;
     for (int a0 = 0; a0 < q; a0 += 64) {
       const int a = a0 + lane;
       uint32_t v = a < q ? cur[a * 12 + col] : 0u;
-#if FEC_DPP_SCAN
-      v = wave_prefix_xor(v);
-#else
-#pragma unroll
-      for (int dd = 1; dd < 64; dd <<= 1) {
-        uint32_t t = __shfl_up(v, dd);
-        if (lane >= dd) v ^= t;
-      }
-#endif
-      v ^= carry;
+      v = wave_prefix_xor(v) ^ carry;
       if (a < q) cur[a * 12 + col] = v;
       carry = rd_lane_u32(v, 63);
     }
@@ -770,7 +529,6 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
   __syncthreads();
   for (int it = tid; it < q * 12; it += FEC_THREADS) cur[it] ^= Wv[it % 12];
   __syncthreads();
-  FEC_PHASE(9);
   // parity bit of row a (interleaved position 360 a + c) / natural index a + q c
   auto pbit = [&](int a, int c) -> uint32_t { return (cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1; };
 
@@ -798,30 +556,6 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
   };
   uint32_t *dstw = (uint32_t *)(io.out + (int64_t)bi * io.cw_stride);
   const uint32_t *framew = (const uint32_t *)frame;
-  if (MODE == FEC_TS_TO_PAIRS) {
-    // the codeword as the map phases read it (big-endian words, one word of slack), in LDS
-    const int cs = md.cs, ib = fec_map_idx_bytes(cs);
-    uint32_t *cww = (uint32_t *)(smem + fec_map_cww_off(cs));
-    for (int i = tid; i <= (cwb + 3) >> 2; i += FEC_THREADS) {
-      uint32_t v = 0;
-      if (4 * i + 4 <= NB) {
-        v = framew[i];
-      } else if (4 * i < cwb) {
-        for (int e = 0; e < 4; e++) {
-          const int bidx = 4 * i + e;
-          const uint32_t by = bidx < NB ? (uint32_t)frame[bidx] : bidx < cwb ? parity_byte(bidx - NB) : 0u;
-          v |= by << (8 * e);
-        }
-      }
-      cww[i] = __builtin_bswap32(v);
-    }
-    __syncthreads();
-    uint8_t *idx = smem + SM_BLK;
-    map_cells<FEC_THREADS>(md, cww, idx, tid);
-    __syncthreads();
-    map_store_pairs<FEC_THREADS>(md, out_pairs, frame_stride, idx, (uint16_t *)(smem + SM_BLK + ib), bi, tid);
-    break;
-  }
   auto out_word = [&](int i) -> uint32_t {
     if (4 * i + 4 <= NB) return framew[i];
     uint32_t v = 0;
@@ -834,14 +568,6 @@ __global__ __launch_bounds__(FEC_THREADS, MODE == FEC_TS_TO_PAIRS ? 4 : FEC_WG_P
   };
   // (16-byte stores of four words measured +0.8 % kernel time: 4-byte stores stay)
   for (int i = tid; i < (cwb + 3) >> 2; i += FEC_THREADS) dstw[i] = out_word(i);
-#if FEC_VARIANT & 1
-  __syncthreads();
-  FEC_PHASE(10);
-  if (tid == 0) {
-    dstw[0] = (uint32_t)g_fec_ts[0];
-    for (int i = 1; i < 11; i++) dstw[i] = (uint32_t)(g_fec_ts[i] - g_fec_ts[0]);
-  }
-#endif
   } while (0);
   __syncthreads();   // frame / phase regions are reused by the next block
   }
@@ -861,10 +587,9 @@ static int fec_grid(int nblocks, int per_cu) {
 }
 
 static bool fec_plan_fits(const FecDev &d) {
-  // the LDS carve is sized for the standard codes: refuse anything larger
+  // the LDS carve is sized for the standard codes, the BCH wave for 64 chunks: refuse anything else
   return !(d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 52 * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
-           (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.bch_waves < 1 || d.bch_waves > 4 ||
-           d.chunk * 64 * d.bch_waves < d.kbch / 8);
+           (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.chunk * 64 < d.kbch / 8);
 }
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {
@@ -874,49 +599,19 @@ hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s)
   int per_cu = (160 * 1024) / lds;
   per_cu = per_cu < 1 ? 1 : per_cu > FEC_WG_PER_CU ? FEC_WG_PER_CU : per_cu;
   dim3 grid(fec_grid(io.nblocks, per_cu)), block(FEC_THREADS);
-  const MapDev md{};
   switch (mode) {
-    case FEC_TS_TO_TEMPU:
-      hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, lds, s, d, io, md, nullptr, (int64_t)0);
-      break;
-    case FEC_TS_TO_BITS:
-      hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_BITS>, grid, block, lds, s, d, io, md, nullptr, (int64_t)0);
-      break;
-    default:
-      hipLaunchKernelGGL(fec_kernel<FEC_BITS_TO_BITS>, grid, block, lds, s, d, io, md, nullptr, (int64_t)0);
-      break;
+    case FEC_TS_TO_TEMPU: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, lds, s, d, io); break;
+    case FEC_TS_TO_BITS: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_BITS>, grid, block, lds, s, d, io); break;
+    default: hipLaunchKernelGGL(fec_kernel<FEC_BITS_TO_BITS>, grid, block, lds, s, d, io); break;
   }
   return hipGetLastError();
 }
 
-int fec_map_lds(int cs, int nldpc) {
-  const int b = fec_map_smem(cs, nldpc);
-  return b <= 160 * 1024 ? b : 0;
-}
-
-hipError_t launch_fec_map(const FecDev &d, const FecIO &io, const MapDev &md, uint16_t *out_pairs,
-                          int64_t frame_stride, hipStream_t s) {
-  if (io.nblocks <= 0) return hipSuccess;
-  const int lds = fec_map_lds(md.cs, d.nldpc);
-  if (!fec_plan_fits(d) || !lds || md.F < 1) return hipErrorInvalidValue;
-  hipError_t e = lds_limit((const void *)fec_kernel<FEC_TS_TO_PAIRS>, lds);
-  if (e != hipSuccess) return e;
-  int per_cu = (160 * 1024) / lds;
-  per_cu = per_cu < 1 ? 1 : per_cu > FEC_WG_PER_CU ? FEC_WG_PER_CU : per_cu;
-  dim3 grid(fec_grid(io.nblocks, per_cu)), block(FEC_THREADS);
-  hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_PAIRS>, grid, block, lds, s, d, io, md, out_pairs, frame_stride);
-  return hipGetLastError();
-}
-
 // ============================================================================ map kernel
-#ifndef MAP_MB
-#define MAP_MB 8   // cells per thread per batched load round (CI and TI loops)
-#endif
-#ifndef MAP_THREADS_EXP
-#define MAP_THREADS_EXP 256
-#endif
-constexpr int MAP_THREADS = MAP_THREADS_EXP;
-constexpr int MAP_LDS_MAX = 160 * 1024 - 256;   // leaves room for static LDS of experiment builds
+constexpr int MAP_THREADS = 256;
+constexpr int MAP_MB = 8;                    // cells per thread per batched load round (CI and TI loops)
+constexpr int MAP_CQ = 8;                    // quads per thread staged in registers by the compact layout
+constexpr int MAP_LDS_MAX = 160 * 1024 - 256;
 // LDS: [LUT 2 KB][cell indices, cs bytes][codeword bytes | cell-interleaved index pairs (2 cs)]
 // (<= 99 KB for QPSK normal, 26 KB for 256-QAM normal)
 __host__ __device__ inline int map_idx_bytes(int cs) { return (cs + 15) & ~15; }
@@ -924,14 +619,11 @@ __host__ __device__ inline int map_idx_bytes(int cs) { return (cs + 15) & ~15; }
 // in 2 idx-bytes, the cell-interleaved pairs (2 cs bytes) overlaying both once the indices are in
 // registers (map_store_pairs alias mode); no LUT (the chain's constellation lookup is in the OFDM
 // kernel).  16 KB instead of 26 KB for 256-QAM normal: 8 workgroups per CU instead of 6.
-#ifndef MAP_COMPACT
-#define MAP_COMPACT 1
-#endif
-// register staging per thread of the compact layout: MAP_CQ quads (cs <= 8192: eight workgroups per
-// CU at 64 VGPRs) or 2 MAP_CQ (cs <= 16384, e.g. 64-QAM and 16-QAM normal: a second kernel
-// instantiation with a 96-VGPR budget, five to seven workgroups per CU by LDS); 0: not compact
+// Register staging per thread: MAP_CQ quads (cs <= 8192: eight workgroups per CU at 64 VGPRs) or
+// 2 MAP_CQ (cs <= 16384, e.g. 64-QAM and 16-QAM normal: a second kernel instantiation with a
+// 96-VGPR budget, five to seven workgroups per CU by LDS); 0: not compact
 __host__ __device__ inline int map_compact_cq(int cs, int cw_bytes, int apply_ci) {
-  if (!MAP_COMPACT || !apply_ci || cw_bytes > map_idx_bytes(cs)) return 0;
+  if (!apply_ci || cw_bytes > map_idx_bytes(cs)) return 0;
   const int nq = (cs + 3) / 4;
   return nq <= MAP_CQ * MAP_THREADS ? MAP_CQ : nq <= 2 * MAP_CQ * MAP_THREADS ? 2 * MAP_CQ : 0;
 }
@@ -952,31 +644,13 @@ __device__ __forceinline__ int xcd_major(int i, int n) {
   return i < (q << 3) ? (i & 7) * q + (i >> 3) : i;
 }
 
-// experiment switch (product builds: 0): bit 0 = phase timestamps of each chain block written
-// over its first three cell-interleaved cells (wrong output; tools/map_phases.py decodes them)
-#ifndef MAP_VARIANT
-#define MAP_VARIANT 0
-#endif
-#ifndef MAP_SKIP
-#define MAP_SKIP 0     // experiment switch (wrong output): bit 0 = no TI store, 1 = no cell interleave, 2 = no demux
-#endif
-#ifndef MAP_QUADS
-#define MAP_QUADS 1    // 1: TI store with quad loads of the partition deltas (see map_store_pairs)
-#endif
-#if MAP_VARIANT & 1
-__shared__ uint64_t g_map_ts[8];
-#define MAP_PHASE(i) do { if (threadIdx.x == 0) g_map_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define MAP_PHASE(i) do { } while (0)
-#endif
-
 // column twist + demux of one FEC block: interleaver-input bits (big-endian words cww, one word of
 // slack past the end) -> cell indices idx (one byte per cell)
 template <int NT>
 __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, int tid) {
   const int cs = d.cs;
   // ---- cell indices: column-twist write / row read / demux (interleavermod:351-403, 440-500,
-  //      529-598, 626-677).  One thread per 32 rows: each column's 32 bits are one (twisted,
+  //      529-598, 626-677).  One thread per 8 rows: each column's 8 bits are one (twisted,
   //      wrapping) window of the codeword, the W windows are ordered by demuxed bit position and
   //      transposed as a bit matrix, giving each row's demuxed word directly.
   if (d.mode == 0) {
@@ -1060,14 +734,27 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   }
   const int rows = cs / 5, cols = 5 * nb;
   const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
-  // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell
-  // (loops batched by 8 so each thread keeps 8 independent global loads in flight)
-  constexpr int MB = MAP_MB;
+  const int nq = (cs + 3) >> 2;
+  const uint32_t *idxw = (const uint32_t *)idx;
+  // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell, four
+  // consecutive cells per thread (one 8-byte load of their permutation entries and one 4-byte LDS
+  // read of their indices, plus the previous cell's byte for the rotation)
+  auto ci_quad = [&](int q, uint2 pq, uint32_t w, uint32_t prev) {
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int j = 4 * q + e;
+      const uint32_t lo = (w >> (8 * e)) & 0xFFu, hi = d.rotation ? prev : lo;
+      prev = lo;
+      if (j < cs) {
+        int tt = (int)(int16_t)(((e < 2 ? pq.x : pq.y) >> (16 * (e & 1))) & 0xFFFFu) + shift;
+        tt = tt >= cs ? tt - cs : tt;
+        stage[tt] = (uint16_t)(lo | (hi << 8));
+      }
+    }
+  };
   if (alias) {
     // compact LDS (map_compact): stage overlays the cell indices, so every thread first takes its
-    // (at most MAP_CQ) quads of indices and permutation entries into registers, then all write
-    const int nq = (cs + 3) >> 2;
-    const uint32_t *idxw = (const uint32_t *)idx;
+    // (at most CQ) quads of indices and permutation entries into registers, then all write
     uint2 pq[CQ];
     uint32_t wv[CQ], pv[CQ];
 #pragma unroll
@@ -1081,84 +768,34 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
 #pragma unroll
     for (int k = 0; k < CQ; k++) {
       const int q = tid + k * NT;
-      if (q < nq && !(MAP_SKIP & 2)) {
-        uint32_t prev = pv[k];
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-          const int j = 4 * q + e;
-          const uint32_t lo = (wv[k] >> (8 * e)) & 0xFFu, hi = d.rotation ? prev : lo;
-          prev = lo;
-          if (j < cs) {
-            int tt = (int)(int16_t)(((e < 2 ? pq[k].x : pq[k].y) >> (16 * (e & 1))) & 0xFFFFu) + shift;
-            tt = tt >= cs ? tt - cs : tt;
-            stage[tt] = (uint16_t)(lo | (hi << 8));
-          }
-        }
-      }
+      if (q < nq) ci_quad(q, pq[k], wv[k], pv[k]);
     }
-  } else if (MAP_QUADS) {
-    // four consecutive cells per thread: one 8-byte load of their permutation entries and one
-    // 4-byte LDS read of their indices (plus the previous cell's byte for the rotation)
-    constexpr int MQ = MB / 2;
-    const int nq = (cs + 3) >> 2;
-    const uint32_t *idxw = (const uint32_t *)idx;
-    for (int q0 = tid; q0 < ((MAP_SKIP & 2) ? 0 : nq); q0 += MQ * NT) {
+  } else {
+    constexpr int MQ = MAP_MB / 2;
+    for (int q0 = tid; q0 < nq; q0 += MQ * NT) {
       uint2 pq[MQ];
 #pragma unroll
       for (int u = 0; u < MQ; u++) pq[u] = ld_off((const uint2 *)d.ci_perm, (uint32_t)min(q0 + u * NT, nq - 1) * 8u);
 #pragma unroll
       for (int u = 0; u < MQ; u++) {
         const int q = q0 + u * NT;
-        if (q < nq) {
-          const uint32_t w = idxw[q];
-          uint32_t prev = idx[q == 0 ? cs - 1 : 4 * q - 1];
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const int j = 4 * q + k;
-            const uint32_t lo = (w >> (8 * k)) & 0xFFu, hi = d.rotation ? prev : lo;
-            prev = lo;
-            if (j < cs) {
-              int tt = (int)(int16_t)(((k < 2 ? pq[u].x : pq[u].y) >> (16 * (k & 1))) & 0xFFFFu) + shift;
-              tt = tt >= cs ? tt - cs : tt;
-              stage[tt] = (uint16_t)(lo | (hi << 8));
-            }
-          }
-        }
-      }
-    }
-  } else
-  for (int j0 = tid; j0 < ((MAP_SKIP & 2) ? 0 : cs); j0 += MB * NT) {
-    int t[MB];
-#pragma unroll
-    for (int u = 0; u < MB; u++) {
-      const int j = min(j0 + u * NT, cs - 1);
-      t[u] = d.ci_perm[j] + shift;
-    }
-#pragma unroll
-    for (int u = 0; u < MB; u++) {
-      const int j = j0 + u * NT;
-      if (j < cs) {
-        const int tt = t[u] >= cs ? t[u] - cs : t[u];
-        const uint32_t lo = idx[j], hi = d.rotation ? idx[j == 0 ? cs - 1 : j - 1] : lo;
-        stage[tt] = (uint16_t)(lo | (hi << 8));
+        if (q < nq) ci_quad(q, pq[u], idxw[q], idx[q == 0 ? cs - 1 : 4 * q - 1]);
       }
     }
   }
   __syncthreads();
-  MAP_PHASE(3);
   // time-interleaver store of the index pairs: row-major over (row, e), 5 consecutive cells
   // (10 B) per TI row (32K: through the half partition); the constellation lookup (QAM +
   // rotated-constellation Q delay) is fused into the OFDM kernel's bin scatter
   const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
   // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
   const int16_t *pr = d.part ? d.part + (int64_t)r * d.part_stride : nullptr;   // block-major int16 table
-  if (MAP_QUADS && pr) {
+  if (pr) {
     // four consecutive TI-store indices per thread: one 8-byte load of their partition deltas
     // instead of four 2-byte loads (the memory instruction count, not the bytes, sets this loop's
     // rate; the pair stores stay 2 bytes per cell)
-    constexpr int MQ = MB / 2;
-    const int nq = (cs + 3) >> 2;
-    for (int q0 = tid; q0 < ((MAP_SKIP & 1) ? 0 : nq); q0 += MQ * NT) {
+    constexpr int MQ = MAP_MB / 2;
+    for (int q0 = tid; q0 < nq; q0 += MQ * NT) {
       uint2 pq[MQ];
 #pragma unroll
       for (int u = 0; u < MQ; u++) pq[u] = ld_off((const uint2 *)pr, (uint32_t)min(q0 + u * NT, nq - 1) * 8u);
@@ -1182,27 +819,14 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
     }
     return;
   }
-  for (int j0 = tid; j0 < ((MAP_SKIP & 1) ? 0 : cs); j0 += MB * NT) {
-    uint32_t dsl[MB];
-    int tt[MB];
-#pragma unroll
-    for (int u = 0; u < MB; u++) {
-      const int j = min(j0 + u * NT, cs - 1);
-      int o;
-      if (d.ti_on) {
-        const int row = j / 5, e = j - 5 * row;
-        tt[u] = e * rows + row;
-        o = row * cols + e;
-      } else {
-        tt[u] = j;
-        o = j;
-      }
-      dsl[u] = (uint32_t)fbase + (uint32_t)o + (uint32_t)(pr ? (int)pr[j] : 0);
+  for (int j = tid; j < cs; j += NT) {
+    int tt = j, o = j;
+    if (d.ti_on) {
+      const int row = j / 5, e = j - 5 * row;
+      tt = e * rows + row;
+      o = row * cols + e;
     }
-#pragma unroll
-    for (int u = 0; u < MB; u++) {
-      if (j0 + u * NT < cs) st_off(dst, dsl[u] * 2u, stage[tt[u]]);
-    }
+    st_off(dst, ((uint32_t)fbase + (uint32_t)o) * 2u, stage[tt]);
   }
 }
 
@@ -1358,11 +982,9 @@ hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s) {
 // The chain's launches prepend ceil8(L1 frames) workgroups that generate the frames' L1-post cells
 // (they run beside the map workgroups instead of as a launch of their own; a multiple of 8 keeps
 // each map workgroup's XCD)
-#ifndef MAP_MINWG
-#define MAP_MINWG 8    // resident workgroups per CU the register allocation must allow (compact LDS: 8 fit)
-#endif
+static_assert(MAP_THREADS == L1_NT, "the map launch's L1-post workgroups run l1post_frame at L1_NT threads");
 template <int CQ>
-__global__ __launch_bounds__(MAP_THREADS, CQ <= MAP_CQ ? MAP_MINWG : 5) void map_kernel(MapDev d, MapIO io, L1Dev l1d, L1IO l1io) {
+__global__ __launch_bounds__(MAP_THREADS, CQ <= MAP_CQ ? 8 : 5) void map_kernel(MapDev d, MapIO io, L1Dev l1d, L1IO l1io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int nl1 = (l1io.nframes + 7) & ~7;
@@ -1378,7 +1000,6 @@ __global__ __launch_bounds__(MAP_THREADS, CQ <= MAP_CQ ? MAP_MINWG : 5) void map
   // chain: (idx[j], idx[j-1]) at cell-interleaved position t
   uint16_t *stage = compact ? (uint16_t *)smem : (uint16_t *)cw;
   const int cs = d.cs, nl = d.nldpc;
-  MAP_PHASE(0);
   if (!io.apply_ci)
     for (int i = tid; i < 256; i += MAP_THREADS) lut[i] = d.lut[i];
   // ---- interleaver input bits (tempu) into LDS as big-endian words: bit i of the codeword is
@@ -1387,7 +1008,7 @@ __global__ __launch_bounds__(MAP_THREADS, CQ <= MAP_CQ ? MAP_MINWG : 5) void map
   const int nlw = (nl + 31) >> 5;
   if (io.packed_in) {
     const uint32_t *src = (const uint32_t *)(io.in + (int64_t)blk * io.cw_stride);
-    if (MAP_CW16 && (((uintptr_t)src) & 15) == 0 && 4 * ((nlw + 3) & ~3) <= (int)io.cw_stride &&
+    if ((((uintptr_t)src) & 15) == 0 && 4 * ((nlw + 3) & ~3) <= (int)io.cw_stride &&
         4 * ((nlw + 3) & ~3) <= (compact ? map_idx_bytes(cs) : 1 << 30)) {
       // 16-byte loads (the codeword stride and the LDS area hold the rounded-up word count)
       for (int k = tid; k < (nlw + 3) >> 2; k += MAP_THREADS) {
@@ -1416,10 +1037,8 @@ __global__ __launch_bounds__(MAP_THREADS, CQ <= MAP_CQ ? MAP_MINWG : 5) void map
     }
   }
   __syncthreads();
-  MAP_PHASE(1);
-  if (!(MAP_SKIP & 4)) map_cells<MAP_THREADS>(d, cww, idx, tid);
+  map_cells<MAP_THREADS>(d, cww, idx, tid);
   __syncthreads();
-  MAP_PHASE(2);
   // ---- constellation + cyclic Q delay; chain: cell interleaver (framemapper:1973-1998) on the
   //      cell indices in LDS, then QAM fused into the time-interleaver (framemapper:1999-2028)
   //      store pattern: FEC block r of its TI block fills columns 5(r-r0)..+4 of a rows x 5nb
@@ -1461,15 +1080,7 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1D
 }
 
 // ============================================================================ OFDM kernels
-#ifndef OFDM_SKIP
-#define OFDM_SKIP 0   // experiment switch (wrong output): bit 0 = no data-slot scatter, 1 = no direct aux entries
-#endif
-#ifndef O32_OCT
-#define O32_OCT 1   // 1: the 32K scatter loads its data slots as aligned octets (16-byte loads)
-#endif
-#ifndef OFDM_SQ16
-#define OFDM_SQ16 8   // data-slot quads per thread per scatter round (N <= 16K)
-#endif
+constexpr int OFDM_SQ16 = 8;   // data-slot quads per thread per scatter round (N <= 16K)
 // exp(+2 pi i k / 32): exact at multiples of pi/2
 __device__ constexpr float kCos32[32] = {
     1.0f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f, 0.70710678118654757f,
@@ -1645,19 +1256,6 @@ template <> struct FftPlan<4096, 16> { static constexpr int RL = 16, PS = 4; usi
 template <> struct FftPlan<8192, 16> { static constexpr int RL = 2, PS = 4; using Tail = StockhamTail<8192, 512, 4, 16, 16, 16, 2>; };
 template <> struct FftPlan<16384, 16> { static constexpr int RL = 4, PS = 4; using Tail = StockhamTail<16384, 1024, 4, 16, 16, 16, 4>; };
 
-// experiment switch (product builds: 0): bit 3 = phase timestamps (s_memrealtime, 100 MHz) of
-// each workgroup written over the first samples of its symbol's guard interval (wrong output;
-// tools/ofdm_phases.py decodes them)
-#ifndef OFDM_VARIANT
-#define OFDM_VARIANT 0
-#endif
-#if OFDM_VARIANT & 8
-__shared__ uint64_t g_phase_ts[16];
-#define OFDM_PHASE(i) do { if (threadIdx.x == 0) g_phase_ts[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define OFDM_PHASE(i) do { } while (0)
-#endif
-
 // Where a transform's inputs come from.  Gather (pilotgen block: cells in carrier order, so per-bin
 // loads are near unit-stride): bin k reads map[k].  Scatter (fused chain: cells in TI output order,
 // randomly placed by the frequency interleaver): aux bins (map < 0) are filled from the aux
@@ -1689,7 +1287,7 @@ template <int NT, int SQ>
 __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src, int g, uint32_t r0, uint32_t rn,
                                               uint32_t dummy, int tid) {
   const int4 gr = src.agrp[g];
-  for (uint32_t q = (uint32_t)tid; q < ((OFDM_SKIP & 2) ? 0u : (uint32_t)gr.y >> 2); q += NT) {
+  for (uint32_t q = (uint32_t)tid; q < ((uint32_t)gr.y >> 2); q += NT) {
     const uint32_t e0 = (uint32_t)gr.x + 4u * q;
     const uint2 b = ld_off((const uint2 *)src.abin, e0 * 2u);
     const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
@@ -1704,7 +1302,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
     const uint32_t e = src.aind[(uint32_t)gr.z + i];
     lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
   }
-  if (O32_OCT && SQ == 4 && !(OFDM_SKIP & 1)) {
+  if (SQ == 4) {
     // 32K kernel: slots in aligned octets, one 16-byte load of bins and one of index pairs per
     // octet (half the load instructions of quads; the pair rows are padded to a multiple of 8)
     const uint32_t o0 = r0 & ~7u, no = (r0 + rn - o0 + 7u) >> 3;
@@ -1734,7 +1332,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
     }
     return;
   }
-  const uint32_t q0 = r0 & ~3u, nq = (OFDM_SKIP & 1) ? 0u : (r0 + rn - q0 + 3u) >> 2;
+  const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
   const uint32_t lastq = nq - 1u;
   for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
     uint2 b[SQ], c[SQ];
@@ -1774,11 +1372,9 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     }
     stage.store((unsigned char *)lds, true, tid);
     __syncthreads();
-    OFDM_PHASE(1);
     const uint32_t dummy = (uint32_t)(NSUB + (NSUB >> PS)) + (uint32_t)(tid & 63);
     scatter_group<NT, OFDM_SQ16>(lds, src, 0, src.d0, src.dn, dummy, tid);
     __syncthreads();
-    OFDM_PHASE(2);
     StockhamPass<NSUB, NT, V, 1, PS>::load_lds(v, lds, tid);
     __syncthreads();
   } else {
@@ -1823,10 +1419,6 @@ struct OfdmShape {
   static constexpr int LDS_BYTES = QAM_OFF + 256 * 8;                // + constellation re[256], im[256]
 };
 
-// experiment switch: 0 = one sample per IQ store (o32_store and the plain loop of ofdm_kernel)
-#ifndef O32_STORE_X2
-#define O32_STORE_X2 1
-#endif
 // value of lane l ^ 1 (DPP quad_perm [1,0,3,2])
 __device__ __forceinline__ float swap_adjacent_lane(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
@@ -1969,10 +1561,8 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const IqOut<FMT> o{(char *)io.out + ((int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + G)) * SB, d.gain};
   const float nrm = d.norm;
   float2 v[V];
-  OFDM_PHASE(0);
   sub_ifft<N, V>(v, lds, src, d.isinc, twl, tid, tabs);
-  OFDM_PHASE(3);
-  if (O32_STORE_X2 && ((((uintptr_t)o.base + (uint32_t)G * SB) & (2u * SB - 1u)) == 0)) {
+  if ((((uintptr_t)o.base + (uint32_t)G * SB) & (2u * SB - 1u)) == 0) {
     // two consecutive samples per lane and store: lanes t, t ^ 1 swap half of their values
     // (as o32_store_pairs), so the even lane stores (t, t + 1) of every even m and the odd lane
     // those of every odd m, m = uu + UL r
@@ -2002,16 +1592,6 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
         if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
       }
   }
-#if OFDM_VARIANT & 8
-  __syncthreads();
-  OFDM_PHASE(8);
-  if (tid == 0) {
-    uint32_t *w = (uint32_t *)o.base;
-    w[0] = (uint32_t)(g_phase_ts[0] & 0xFFFFFFFFu);
-    for (int i = 1; i < 9; i++) w[i] = (uint32_t)(g_phase_ts[i] - g_phase_ts[0]);
-    w[9] = __smid();
-  }
-#endif
 }
 
 // ---------------------------------------------------------------- 32K symbols
@@ -2046,10 +1626,7 @@ static_assert((16384 + 2 * 32) * 8 <= O32_DATA, "exchange slots fit the data are
 __device__ __forceinline__ uint32_t o32_bin(uint32_t k) { return k + (k >> O32_PS); }
 // exchange slots: two pad slots per 512 (stride-512 lane patterns spread over the banks, and even
 // slots stay 16-byte aligned so exchange 1 reads its value pairs as ds_read_b128)
-#ifndef O32_X2PAD
-#define O32_X2PAD 1   // experiment switch: 0 = one pad slot per 512 and 8-byte exchange-1 reads
-#endif
-__device__ __forceinline__ uint32_t o32_x(uint32_t e) { return e + (O32_X2PAD ? 2u : 1u) * (e >> 9); }
+__device__ __forceinline__ uint32_t o32_x(uint32_t e) { return e + 2u * (e >> 9); }
 
 // v[r] *= w^(e r) for r = 1..31 from the seven table values w^(e k) (k = 1, 2, 3, 4, 8, 12, 16):
 // r = 16 t + 4 h + l -> top^t hi[h] lo[l]
@@ -2073,20 +1650,11 @@ __device__ __forceinline__ void o32_twiddle(float2 *v, const Lookup &tw) {
 // n2 = r) and reads (m0 = a, m1 = r, n2 = b) at (m1 & 15) + 16 (m0 & 15) + 256 (m1 >> 4) + 512 n2;
 // exchange 2 (SPLIT 9) writes (n2 = b, m0 = a, n1 = r) and reads (n2 = b, m0 = r, n1 = a) at
 // (n2 & 15) + 16 (n1 & 15) + 256 (n1 >> 4) + 512 m0
-#ifndef O32_EXCH_EXP
-#define O32_EXCH_EXP 0   // experiment switch (wrong output): 1 = barriers only, 2 = LDS traffic only, 3 = neither
-#endif
 template <int SPLIT>
 __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t tid, uint32_t a, uint32_t b) {
-#if O32_EXCH_EXP == 1
-  __syncthreads(); __syncthreads(); __syncthreads(); __syncthreads();
-  return;
-#elif O32_EXCH_EXP == 3
-  return;
-#endif
 #pragma unroll
   for (uint32_t h = 0; h < 2; h++) {
-    if (O32_EXCH_EXP != 2) __syncthreads();
+    __syncthreads();
     const bool mine = ((tid >> SPLIT) & 1u) == h;
     if (mine) {
 #pragma unroll
@@ -2096,9 +1664,9 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
         lds[o32_x(e)] = v[r];
       }
     }
-    if (O32_EXCH_EXP != 2) __syncthreads();
+    __syncthreads();
     if (mine) {
-      if (SPLIT == 8 && O32_X2PAD) {
+      if (SPLIT == 8) {
         // values r, r + 1 are adjacent, 16-byte aligned slots: one ds_read_b128 per pair (lanes
         // b = 0..15 at a stride of 514 slots cover the 64 banks; the compiler would otherwise pair
         // the 8-byte reads into ds_read2_b64, at half the LDS rate)
@@ -2112,8 +1680,7 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
       } else {
 #pragma unroll
         for (uint32_t r = 0; r < 32; r++) {
-          const uint32_t e = SPLIT == 8 ? (r & 15u) + 16u * (a & 15u) + 256u * (r >> 4) + 512u * b
-                                        : (b & 15u) + 16u * (a & 15u) + 256u * (a >> 4) + 512u * r;
+          const uint32_t e = (b & 15u) + 16u * (a & 15u) + 256u * (a >> 4) + 512u * r;
           v[r] = lds[o32_x(e)];
         }
       }
@@ -2121,80 +1688,9 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
   }
 }
 
-// Exchange with 16-byte LDS slots (O32_XCHG128, the default).  Thread t <-> a = t4 | t3 << 1 |
-// t[6..7] << 2 | t8 << 4, b = t5 | t[0..2] << 1 | t9 << 4 (o32_ta / o32_tb), so b's bit 0 pairs lanes
-// l, l ^ 32 and a's bit 0 lanes l, l ^ 16.  Before exchange 1 the lanes b, b ^ 1 swap v[r + 1] of the
-// lower lane with v[r] of the upper one (v_permlane32_swap): each lane then holds, per even r, the
-// two values (m1 = 2p, 2p + 1) of one n2 = r + b0, which is the pair the reader wants in adjacent
-// registers.  Exchange 2 does the same on a's bit 0 (v_permlane16_swap, pairs m0 = 2p, 2p + 1 of one
-// n1).  Both sides then move 16 bytes per lane (ds_write_b128 / ds_read_b128), half the LDS
-// instructions of 8-byte slots, and the wide stores reach their rate with few waves per SIMD.
-// A half holds 512 rows x 16 slots of 16 bytes (128 KB, no padding): row = (kept coordinate & 15)
-// + 16 * (the coordinate that travels with r), column = pair index ^ g, g = ((n2 >> 1) & 7) |
-// (bit 1 of the remaining coordinate) << 3, which puts every lane group of ds_write_b128 (8 lanes,
-// t0..t2) and of ds_read_b128 (16 lanes over t0..t4) on distinct banks (MI355X_MICROARCH.md LDS).
-#ifndef O32_XCHG128
-#define O32_XCHG128 0   // experiment switch (measured: +3 % OFDM time, dropped): 1 = 16-byte slots and the lane
-                       // mapping above; 0 = 8-byte slots, lanes b = t[0..3]
-#endif
-__device__ __forceinline__ uint32_t o32_ta(uint32_t t) {
-  if (O32_XCHG128) return ((t >> 4) & 1u) | (((t >> 3) & 1u) << 1) | (((t >> 6) & 3u) << 2) | (((t >> 8) & 1u) << 4);
-  return ((t >> 4) & 15u) | (((t >> 8) & 1u) << 4);
-}
-__device__ __forceinline__ uint32_t o32_tb(uint32_t t) {
-  if (O32_XCHG128) return ((t >> 5) & 1u) | ((t & 7u) << 1) | (((t >> 9) & 1u) << 4);
-  return (t & 15u) | (((t >> 9) & 1u) << 4);
-}
-// swap the upper lanes' lo with the lower lanes' hi across lane bit 5 (W = 32) or 4 (W = 16)
-template <int W>
-__device__ __forceinline__ void lane_pair_swap(float2 &lo, float2 &hi) {
-  uint32_t x0 = __float_as_uint(lo.x), x1 = __float_as_uint(hi.x), y0 = __float_as_uint(lo.y), y1 = __float_as_uint(hi.y);
-  if (W == 32) {
-    const auto sx = __builtin_amdgcn_permlane32_swap(x0, x1, false, false);
-    const auto sy = __builtin_amdgcn_permlane32_swap(y0, y1, false, false);
-    x0 = sx[0]; x1 = sx[1]; y0 = sy[0]; y1 = sy[1];
-  } else {
-    const auto sx = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
-    const auto sy = __builtin_amdgcn_permlane16_swap(y0, y1, false, false);
-    x0 = sx[0]; x1 = sx[1]; y0 = sy[0]; y1 = sy[1];
-  }
-  lo = make_float2(__uint_as_float(x0), __uint_as_float(y0));
-  hi = make_float2(__uint_as_float(x1), __uint_as_float(y1));
-}
-template <int SPLIT>
-__device__ __forceinline__ void o32_exchange128(float2 *v, float2 *lds, uint32_t tid, uint32_t a, uint32_t b) {
-#pragma unroll
-  for (int r = 0; r < 32; r += 2) lane_pair_swap<SPLIT == 8 ? 32 : 16>(v[r], v[r + 1]);
-  float4 *x = (float4 *)lds;
-  const uint32_t lo = SPLIT == 8 ? (b & 1u) : (a & 1u);
-  const uint32_t a1 = (a >> 1) & 1u;
-  const uint32_t rbase = 16u * (SPLIT == 8 ? (a & 15u) + 16u * b : (b & 15u) + 16u * a);
-  const uint32_t rg = ((b >> 1) & 7u) | (a1 << 3);
-#pragma unroll
-  for (uint32_t h = 0; h < 2; h++) {
-    __syncthreads();
-    const bool mine = ((tid >> SPLIT) & 1u) == h;
-    if (mine) {
-#pragma unroll
-      for (uint32_t r = 0; r < 32; r += 2) {
-        const uint32_t n = r + lo;
-        const uint32_t row = (SPLIT == 8 ? (a & 15u) : (b & 15u)) + 16u * n;
-        const uint32_t g = SPLIT == 8 ? (((n >> 1) & 7u) | (a1 << 3)) : (((b >> 1) & 7u) | (((n >> 1) & 1u) << 3));
-        const uint32_t col = ((SPLIT == 8 ? b : a) >> 1) ^ g;
-        x[16u * row + col] = make_float4(v[r].x, v[r].y, v[r + 1].x, v[r + 1].y);
-      }
-    }
-    __syncthreads();
-    if (mine) {
-#pragma unroll
-      for (uint32_t q = 0; q < 16; q++) {
-        const float4 f = x[rbase + (q ^ rg)];
-        v[2 * q] = make_float2(f.x, f.y);
-        v[2 * q + 1] = make_float2(f.z, f.w);
-      }
-    }
-  }
-}
+// thread t <-> a = t[4..7] | t8 << 4, b = t[0..3] | t9 << 4
+__device__ __forceinline__ uint32_t o32_ta(uint32_t t) { return ((t >> 4) & 15u) | (((t >> 8) & 1u) << 4); }
+__device__ __forceinline__ uint32_t o32_tb(uint32_t t) { return (t & 15u) | (((t >> 9) & 1u) << 4); }
 
 // stages A, B, C with the two exchanges: v[r] = bin kin + 1024 r on entry (kin = a + 32 b), sample
 // b + 32 a + 1024 r on exit.  Every thread is past its last LDS access of the symbol on return.
@@ -2208,20 +1704,15 @@ __device__ __forceinline__ void o32_fft(float2 *v, float2 *lds, const float2 *tw
     const uint32_t i = kin * (uint32_t)k;   // < 16384
     return cmulf(tw2[128 + (i >> 7)], tw2[i & 127u]);
   });
-  OFDM_PHASE(3);
-  if (O32_XCHG128) o32_exchange128<8>(v, lds, tid, ta, tb); else o32_exchange<8>(v, lds, tid, ta, tb);
-  OFDM_PHASE(4);
+  o32_exchange<8>(v, lds, tid, ta, tb);
   // stage B: DFT over m1, twiddle w_1024^(m0 n1) = w_1024^(a r)
   __builtin_amdgcn_sched_barrier(0);
   Dft<32>::run(v);
   o32_twiddle(v, [&](int k) { return tw1k[(ta * (uint32_t)k) & 1023u]; });
-  OFDM_PHASE(5);
-  if (O32_XCHG128) o32_exchange128<9>(v, lds, tid, ta, tb); else o32_exchange<9>(v, lds, tid, ta, tb);
-  OFDM_PHASE(6);
+  o32_exchange<9>(v, lds, tid, ta, tb);
   // stage C: DFT over m0 -> x[b + 32 a + 1024 r]
   __builtin_amdgcn_sched_barrier(0);
   Dft<32>::run(v);
-  OFDM_PHASE(7);
 }
 
 // normalisation, guard interval and IQ store of samples b + 32 a + 1024 r, r in [R0, R1)
@@ -2248,19 +1739,6 @@ __device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT
   constexpr uint32_t N = 32768;
   const bool odd = nout & 1u;
   const uint32_t n0 = nout & ~1u;
-  if (O32_XCHG128) {
-    // b's bit 0 is lane bit 5: after the swap the lower lane holds samples (b, b + 1) of r = 2k and
-    // the upper lane those of r = 2k + 1, with no select
-#pragma unroll
-    for (uint32_t k = 0; k < 16; k++) {
-      float2 e = cscale(cscale(v[2 * k], nrm), o.gain), d = cscale(cscale(v[2 * k + 1], nrm), o.gain);
-      lane_pair_swap<32>(e, d);
-      const uint32_t n = n0 + 1024u * (2u * k + (odd ? 1u : 0u));
-      o.put2((uint32_t)G + n, e, d);
-      if (n >= N - (uint32_t)G) o.put2(n - (N - (uint32_t)G), e, d);
-    }
-    return;
-  }
 #pragma unroll
   for (uint32_t k = 0; k < 16; k++) {
     const float2 e = cscale(cscale(v[2 * k], nrm), o.gain), d = cscale(cscale(v[2 * k + 1], nrm), o.gain);
@@ -2311,7 +1789,6 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     const IqOut<FMT> p{(char *)io.out + (int64_t)f * io.out_stride * SB, d.gain};
     for (int i = tid; i < 2048; i += NT) p.put((uint32_t)i, d.p1[i]);
   }
-  OFDM_PHASE(0);
   // twiddle tables: loaded here, stored to LDS once the scatter inputs are in flight
   const float2 t1k = d.twiddle1k[tid];
   const float2 t2 = tid < 384 ? d.twiddle[tid] : make_float2(0.f, 0.f);
@@ -2342,7 +1819,6 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
       const uint32_t r0 = src.d0 + (h ? src.dn0 : 0u), rn = h ? src.dn - src.dn0 : src.dn0;
       scatter_group<NT, 4>(lds, src, h, r0, rn, dummy, tid);
       __syncthreads();
-      if (h == 0) OFDM_PHASE(1);
 #pragma unroll
       for (uint32_t r = 0; r < 16; r++) v[16 * h + r] = lds[o32_bin(kin + 1024u * r)];
     }
@@ -2370,23 +1846,12 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
       v[r].y *= sc;
     }
   }
-  OFDM_PHASE(2);
   o32_fft(v, lds, tw1k, tw2, (uint32_t)tid, ta, tb);   // its first barrier publishes the tables
   const IqOut<FMT> o{(char *)io.out + ((int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + d.G)) * SB, d.gain};
-  if (O32_STORE_X2 && ((((uintptr_t)o.base + (uint32_t)d.G * SB) & (2u * SB - 1u)) == 0))
+  if ((((uintptr_t)o.base + (uint32_t)d.G * SB) & (2u * SB - 1u)) == 0)
     o32_store_pairs<FMT>(v, o, tb + 32u * ta, d.norm, d.G);
   else
     o32_store<FMT, 0, 32>(v, o, tb + 32u * ta, d.norm, d.G);
-#if OFDM_VARIANT & 8
-  __syncthreads();
-  OFDM_PHASE(8);
-  if (tid == 0) {
-    uint32_t *ww = (uint32_t *)o.base;
-    ww[0] = (uint32_t)(g_phase_ts[0] & 0xFFFFFFFFu);
-    for (int i = 1; i < 9; i++) ww[i] = (uint32_t)(g_phase_ts[i] - g_phase_ts[0]);
-    ww[9] = __smid();
-  }
-#endif
 }
 
 template <int N, int FMT>

@@ -68,23 +68,6 @@ Poly192 bch_generator(bool normal, int P) {
   return g;
 }
 
-// rows of the GF(2) matrix of v -> v * x^K mod g, lane-friendly layout: row r = 3 words
-std::vector<uint64_t> shift_matrix(const Poly192 &g, int P, long K) {
-  Poly192 c;
-  c.set(0);
-  for (long i = 0; i < K; i++) c = times_x(c, g, P);
-  std::vector<Poly192> cols(P);
-  for (int i = 0; i < P; i++) {
-    cols[i] = c;
-    c = times_x(c, g, P);
-  }
-  std::vector<uint64_t> rows(192 * 3, 0);
-  for (int r = 0; r < P; r++)
-    for (int i = 0; i < P; i++)
-      if (cols[i].bit(r)) rows[r * 3 + (i >> 6)] |= 1ull << (i & 63);
-  return rows;
-}
-
 const t2_ldpc_code_t *find_code(int normal, int rate) {
   for (int i = 0; i < T2_LDPC_NCODES; i++)
     if (T2_LDPC_CODES[i].framesize_normal == normal && T2_LDPC_CODES[i].rate == rate) return &T2_LDPC_CODES[i];
@@ -138,7 +121,7 @@ static bool fec_numbers(int normal, int rate, int *kbch, int *nbch, int *q, int 
   return true;
 }
 
-int build_fec(int framesize, int rate, int constellation, FecPlan &fp, int bch_waves) {
+int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
   int normal = framesize == 1;
   if (framesize != 0 && framesize != 1) return -1;
   if (!fec_numbers(normal, rate, &fp.kbch, &fp.nbch, &fp.q, &fp.nparity)) return -1;
@@ -159,14 +142,9 @@ int build_fec(int framesize, int rate, int constellation, FecPlan &fp, int bch_w
     for (int k = 0; k < 3; k++) fp.bch_tab[d * 3 + k] = v.w[k];
   }
   const int L = fp.kbch / 8;
-  // 64 chunks per BCH wave: each wave combines its 64 chunk remainders with M1 = x^(8 chunk), wave
-  // 0 the wave results with M64
-  if (bch_waves < 1 || bch_waves > 4) return -1;
-  fp.bch_waves = bch_waves;
-  fp.bch_chunk = (L + 64 * bch_waves - 1) / (64 * bch_waves);
-  fp.bch_m1 = shift_matrix(g, P, 8L * fp.bch_chunk);
-  fp.bch_m64 = shift_matrix(g, P, 8L * 64 * fp.bch_chunk);
-  // the chunk remainder of lane l moves to the end of its wave's 64 chunks: r_l x^(8 chunk (63 - l))
+  // the BBFRAME in 64 chunks, one per lane of the BCH wave (the chunks end at L)
+  fp.bch_chunk = (L + 63) / 64;
+  // the chunk remainder of lane l moves to the end of the message: r_l x^(8 chunk (63 - l))
   // mod g, as the XOR of P/4 nibble-table entries (one lookup per 4-bit digit of r_l)
   {
     const int NJ = P / 4;

@@ -28,11 +28,8 @@ struct FecPlan {
   int normal = 0, rate = 0;
   int kbch = 0, nbch = 0, nparity = 0, nldpc = 0, q = 0, pbits = 0;
   bool parity_interleave = true;      // tempu carries parity in [a][c] (interleaved) order
-  int bch_waves = 1;                  // waves sharing the BCH division (64 chunks each)
-  int bch_chunk = 0;                  // message bytes per lane chunk (64 * bch_waves lanes)
+  int bch_chunk = 0;                  // message bytes per lane chunk (64 lanes of one wave)
   std::vector<uint64_t> bch_tab;      // 256 x 3 words: d(x) * x^P mod g(x)
-  std::vector<uint64_t> bch_m1;       // 192 rows x 3 words: v -> v * x^(8*chunk) mod g
-  std::vector<uint64_t> bch_m64;      // 192 rows x 3 words: v -> v * x^(8*64*chunk) mod g
   // per-lane chunk shift as nibble tables: entry [j][v][lane] (4 words, the 4th zero) =
   // v x^(4 j) x^(8 chunk (63 - lane)) mod g for nibble j < P/4, value v < 16, lane < 64
   std::vector<uint64_t> bch_ctab;
@@ -43,9 +40,7 @@ struct FecPlan {
   std::vector<uint8_t> crc8_shift;    // 8 x 256: crc after appending k zero bytes (packet CRC combine)
   std::vector<uint8_t> hcrc_bits;     // 72: BBHEADER CRC-8 contribution of each header bit
 };
-// bch_waves: waves of the FEC kernel that share the BCH division (64 chunks each; 1 = the fewest
-// instructions, more = a shorter per-block critical path for more Horner work)
-int build_fec(int framesize, int rate, int constellation, FecPlan &fp, int bch_waves = 1);
+int build_fec(int framesize, int rate, int constellation, FecPlan &fp);
 
 // ----------------------------------------------------------------------------- bit interleave + map
 enum MapMode { MAP_PAIRS = 0, MAP_TWIST2 = 1, MAP_TWIST1 = 2 };

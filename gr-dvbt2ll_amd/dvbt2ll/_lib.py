@@ -50,7 +50,7 @@ class _ChainInfo(ctypes.Structure):
                 ("ts_bytes_per_frame", ctypes.c_int64), ("iq_samples_per_frame", ctypes.c_int64),
                 ("cell_size", ctypes.c_int), ("stream_items", ctypes.c_int), ("mapped_items", ctypes.c_int),
                 ("num_symbols", ctypes.c_int), ("fft_size", ctypes.c_int), ("guard_interval", ctypes.c_int),
-                ("cw_stride_bytes", ctypes.c_int64), ("fused_fec_map", ctypes.c_int)]
+                ("cw_stride_bytes", ctypes.c_int64)]
 
 
 BLOCKS = ("bbheaderbch", "ldpc", "interleavermod", "framemapperfint", "pilotgenp1insert")

@@ -27,12 +27,17 @@ def gather_frames(local, total_frames, per_frame, group=None, dst=0):
     sends its shard point-to-point (one grouped batch of isend / irecv, ncclGroupStart/End under the
     nccl backend) straight into its place in dst's output.  dst receives world - 1 shards, the
     other ranks receive nothing.  Returns the [total_frames * per_frame, ...] tensor on dst, None
-    elsewhere; empty shards (more ranks than frames) send nothing."""
+    elsewhere; empty shards (more ranks than frames) send nothing (verified under gloo; the RCCL
+    empty-shard case has not run on a multi-GPU node)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     counts = [frame_range(total_frames, r, world)[1] for r in range(world)]
     firsts = [frame_range(total_frames, r, world)[0] for r in range(world)]
     assert local.shape[0] == counts[rank] * per_frame, "shard size mismatch"
+    # every rank joins one collective first: under RCCL a grouped send/recv that is the group's
+    # first operation and leaves some ranks out (empty shards) is undefined
+    sync = torch.zeros(1, dtype=torch.int32, device=local.device)
+    dist.all_reduce(sync, group=group)
 
     def peer(r):
         return dist.get_global_rank(group, r) if group is not None else r

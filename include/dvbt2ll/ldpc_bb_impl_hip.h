@@ -17,7 +17,7 @@ namespace dvbt2ll {
 
 class ldpc_bb : virtual public gr::block {
  public:
-  typedef std::shared_ptr<ldpc_bb> sptr;
+  typedef boost::shared_ptr<ldpc_bb> sptr;   // GNU Radio 3.7 block pointers
   static sptr make(dvbt2_framesize_t framesize, dvbt2_code_rate_t rate);
 };
 

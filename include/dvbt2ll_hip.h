@@ -159,8 +159,6 @@ typedef struct {
   int64_t iq_samples_per_frame;
   int cell_size, stream_items, mapped_items, num_symbols, fft_size, guard_interval;
   int64_t cw_stride_bytes;     /* packed codeword stride in the internal buffer */
-  int fused_fec_map;           /* 1: FEC and bit interleave / map run as one kernel (codewords stay in
-                                  LDS; timing stage 1 is then empty); default 0 */
 } dvbt2ll_chain_info;
 int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, dvbt2ll_chain **out);
 int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info);
@@ -213,14 +211,13 @@ int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, in
 #define DVBT2LL_IQ_SC16 1
 int dvbt2ll_chain_set_output(dvbt2ll_chain *h, float gain, int format);
 /* per-stage kernel timing with HIP events on the launch stream: enable, then read the
- * accumulated milliseconds and launch counts of stages {0: fec (+ map when fused), 1: map, 2: ofdm,
- * 3: l1post}; nstages <= 4.  The frames' L1-post signalling is generated on the GPU every run: by
- * extra workgroups of the map launch (counted in stage 1; stage 3 then times an empty interval), or,
- * with the fused FEC + map kernel, by a launch of its own (stage 3). */
+ * accumulated milliseconds and launch counts of stages {0: fec, 1: map, 2: ofdm, 3: reserved (0)};
+ * nstages <= 4.  The frames' L1-post signalling is generated on the GPU every run by extra
+ * workgroups of the map launch (counted in stage 1). */
 int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable);
 int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages);
 /* test hooks (host outputs, synchronous), last run's frame 0: packed codewords (tempu
- * order; only without the fused FEC + map kernel, else DVBT2LL_EINVAL); the frame data region in the slot order the OFDM kernel reads, as stored
+ * order); the frame data region in the slot order the OFDM kernel reads, as stored
  * (uint16 constellation index pairs: lo = the cell's index, hi = the index whose Q part
  * it carries, i.e. the previous cell's under rotation) and as complex64 cells */
 int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes);

@@ -1,4 +1,4 @@
-// Test-only stand-in for GNU Radio 3.7's gr::block: the members the dvbt2ll HIP adapters use
+// Test-only stand-in for GNU Radio 3.7's gr::block (GNU Radio is not installed in this image): the members the dvbt2ll HIP adapters use
 // (io signatures, set_output_multiple, forecast, general_work, consume_each, d_logger) plus two
 // accessors the test scheduler (tests/adapter/gr_flowgraph.cpp) reads after each call.
 #pragma once
@@ -8,6 +8,7 @@
 #include <string>
 #include <vector>
 
+#include <boost/shared_ptr.hpp>
 #include <gnuradio/io_signature.h>
 
 typedef std::vector<int> gr_vector_int;
@@ -20,7 +21,7 @@ struct logger {
   std::string name;
   int warnings = 0;
 };
-typedef std::shared_ptr<logger> logger_ptr;
+typedef boost::shared_ptr<logger> logger_ptr;
 
 class block {
  public:
@@ -68,7 +69,7 @@ class block {
 
 namespace gnuradio {
 template <class T>
-std::shared_ptr<T> get_initial_sptr(T *p) {
-  return std::shared_ptr<T>(p);
+boost::shared_ptr<T> get_initial_sptr(T *p) {
+  return boost::shared_ptr<T>(p);
 }
 }  // namespace gnuradio

@@ -1,12 +1,12 @@
 // Test-only stand-in for GNU Radio's gr::io_signature (just enough for the dvbt2ll HIP adapters;
 // GNU Radio is not installed in this image).  Not used by the product.
 #pragma once
-#include <memory>
+#include <boost/shared_ptr.hpp>
 
 namespace gr {
 class io_signature {
  public:
-  typedef std::shared_ptr<io_signature> sptr;
+  typedef boost::shared_ptr<io_signature> sptr;
   static sptr make(int min_streams, int max_streams, int sizeof_stream_item) {
     return sptr(new io_signature(min_streams, max_streams, sizeof_stream_item));
   }

@@ -11,7 +11,7 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
-LIB_PATH = ROOT / "oracle" / "_build" / "libdvbt2_oracle.so"
+LIB_PATH = ROOT / "oracle" / "_build" / ("asan/" if os.environ.get("DVBT2LL_SANITIZED") == "1" else "") / "libdvbt2_oracle.so"
 
 _lib = None
 

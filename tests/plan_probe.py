@@ -4,6 +4,7 @@ It exposes the product's configuration-time gather maps so CPU tests can check t
 the oracle for the whole parameter space; the GPU kernels that consume them are checked by
 the -m gpu tests."""
 import ctypes
+import os
 import subprocess
 from pathlib import Path
 
@@ -11,7 +12,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "gr-dvbt2ll_amd" / "csrc"
-LIB = CSRC / "_obj" / "libt2plan_probe.so"
+LIB = CSRC / "_obj" / ("asan/" if os.environ.get("DVBT2LL_SANITIZED") == "1" else "") / "libt2plan_probe.so"
 _L = None
 
 
@@ -132,7 +133,7 @@ def ti_dest(plan, r, t):
     small, big, ns = plan["ti_small"], plan["ti_big"], plan["ti_nsmall"]
     r = np.asarray(r)
     in_small = r < ns * small
-    r0 = np.where(in_small, (r // small) * small, ns * small + ((r - ns * small) // big) * big)
+    r0 = np.where(in_small, (r // max(small, 1)) * small, ns * small + ((r - ns * small) // big) * big)
     nb = np.where(in_small, small, big)
     rows = cs // 5
     return r0 * cs + (t % rows) * (5 * nb) + 5 * (r - r0) + t // rows

@@ -1,0 +1,49 @@
+"""bench.py's multi-rank path on CPU: `--gpus N` without an external launcher spawns
+N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set before any GPU use), checks
+the world size, shards frames with frame_range, times steps between barriers with the max over
+ranks (all_reduce), gathers the frames in order to rank 0 and relays rank 0's one JSON line.
+--dry-run replaces the HIP chain by placeholder frames on gloo."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _bench(*args, env=None):
+    e = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True,
+                          timeout=240, env=e)
+
+
+@pytest.mark.parametrize("n,frames", [(2, 4), (3, 5)])
+def test_bench_spawns_n_ranks(n, frames):
+    r = _bench("--gpus", str(n), "--dry-run", "--frames", str(frames), "--steps", "3", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout               # exactly one JSON line, from rank 0
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["world_size_verified"] and d["launcher"] == "bench.py spawn"
+    assert d["gather_in_order"]
+    # contiguous shards covering every frame once (frame_range)
+    seen = [f for first, cnt in d["shards"] for f in range(first, first + cnt)]
+    assert seen == list(range(n * frames))
+
+
+def test_bench_single_rank_unchanged():
+    r = _bench("--gpus", "1", "--dry-run", "--steps", "2", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and d["launcher"] == "single process"
+
+
+def test_bench_rejects_world_mismatch():
+    """under an external launcher WORLD_SIZE must equal --gpus"""
+    r = _bench("--gpus", "2", "--dry-run", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

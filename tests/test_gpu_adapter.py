@@ -1,6 +1,6 @@
 """GPU: the header-only GNU Radio adapters (include/dvbt2ll/*_impl_hip.h) compiled into a
-GR-style scheduler (tests/adapter/gr_flowgraph.cpp, against the stand-in GR headers in
-tests/gr_stub): make() -> set_output_multiple -> forecast -> general_work with random multiples of
+GR-style scheduler (tests/adapter/gr_flowgraph.cpp, against gr-dvbt2ll's own public headers plus
+stand-ins for the GNU Radio / Boost headers in tests/gr_stub; built in the build container): make() -> set_output_multiple -> forecast -> general_work with random multiples of
 the output multiple and random-size TS chunks -> consume_each, over several T2 frames.  The IQ it
 writes equals the oracle chain (IQ bounds of SURVEY 8(c)) and, bit for bit, the fused chain."""
 import subprocess
