@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Condense one GPU session directory (tools/gpu_r2_session.sh -> gpurun_out/<tag>) into
+"""Condense one GPU session directory (tools/gpu_session.sh -> gpurun_out/<tag>) into
 profiles/<round>_<tag>_summary.md (+ the bench JSON line) for the judge:
 
     python tools/prof_summary.py r2a r2
