@@ -87,8 +87,18 @@ struct DeviceCtx {
 // ---------------------------------------------------------------- FEC tables on device
 struct FecTables {
   FecPlan plan;
-  DevBuf hcrc, tab, ctab, rowptr, ent, prbs, crc8, crcsh;
+  DevBuf hcrc, tab, ctab, rowptr, ent, prbs, crc8, crcsh, bmf;
   FecDev dev{};
+  // the fused chain's BCH pass on the matrix cores: the generator matrix as fp4 B fragments
+  int init_chain() {
+    if (build_bch_mfma(plan)) return DVBT2LL_EINVAL;
+    int r = upload(bmf, plan.bch_mfma);
+    if (r) return r;
+    dev.bch_mfma = bmf.as<uint4>();
+    dev.bch_nq = plan.bch_nq;
+    dev.bch_nt = plan.bch_nt;
+    return 0;
+  }
   int init(int framesize, int rate, int constellation, int mode, int inband, int fecblocks, int tsrate) {
     if (build_fec(framesize, rate, constellation, plan)) return DVBT2LL_EINVAL;
     int r;
@@ -546,15 +556,17 @@ extern "C" int dvbt2ll_pilotgenp1insert_debug_carriers(dvbt2ll_pilotgenp1insert 
 extern "C" void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h) { delete h; }
 
 // ============================================================================ chain
-// one instantiated hipGraph of the chain's three kernels (fec -> map -> ofdm), per (nframes,
-// IQ format): captured once from the ordinary launch path, then every call rewrites the three
-// kernel nodes' arguments (hipGraphExecKernelNodeSetParams) and launches the graph
+// one instantiated hipGraph of the chain's five kernels (FEC BB pass -> BCH matrix-core pass ->
+// LDPC pass -> map -> ofdm), per (nframes, IQ format, slot): captured once from the ordinary launch
+// path, then every call rewrites the kernel nodes' arguments (hipGraphExecKernelNodeSetParams) and
+// launches the graph
 struct ChainGraph {
   int nframes = 0, fmt = -1, slot = -1;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
-  hipGraphNode_t node[4] = {};
-  hipKernelNodeParams base[4] = {};
+  static constexpr int NK = 5;
+  hipGraphNode_t node[NK] = {};
+  hipKernelNodeParams base[NK] = {};
   ~ChainGraph() {
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -576,6 +588,8 @@ struct dvbt2ll_chain {
   // calls issued on different streams overlap; a slot reused on another stream first waits for
   // its previous run (slot_done) -- see dvbt2ll_chain_set_slots
   DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], pairs[DVBT2LL_CHAIN_MAX_SLOTS];
+  // BCH partial parities of the matrix-core pass (FecIO::bch_part): 8 K slices x blocks x 8 words
+  DevBuf bpart[DVBT2LL_CHAIN_MAX_SLOTS];
   // per-frame L1-post cells of a run (l1post_kernel -> the OFDM kernel's indirect aux entries)
   L1Tables l1;
   DevBuf l1buf[DVBT2LL_CHAIN_MAX_SLOTS];
@@ -635,8 +649,8 @@ struct dvbt2ll_chain {
     evused = 0;
     return st;
   }
-  // the chain's kernels on stream s: FEC, map (its extra workgroups generate the frames' L1-post
-  // cells), OFDM.  ev1, ev2 (timing): recorded after the FEC and the map kernel
+  // the chain's kernels on stream s: FEC (three passes), map (its extra workgroups generate the
+  // frames' L1-post cells), OFDM.  ev1, ev2 (timing): recorded after the FEC passes and the map kernel
   hipError_t launch_chain(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, hipStream_t s,
                           hipEvent_t ev1, hipEvent_t ev2) {
     hipError_t e = launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, s);
@@ -653,7 +667,7 @@ struct dvbt2ll_chain {
   // under it; with several slots the calls still overlap on the device
   int graph_launch(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, int slot,
                    hipStream_t s) {
-    const int nk = 3;   // fec, map (+ L1-post), ofdm
+    const int nk = ChainGraph::NK;   // fec BB, BCH, LDPC passes (FecDev, FecIO), map (+ L1-post), ofdm
     ChainGraph *g = nullptr;
     for (auto &c : graphs)
       if (c->nframes == nframes && c->fmt == ofdm.dev.fmt && c->slot == slot) g = c.get();
@@ -720,7 +734,7 @@ struct dvbt2ll_chain {
     MapIO mi = mio;
     OfdmIO oi = oio;
     void *a0[2] = {&fd, &fi}, *a1[4] = {&md, &mi, &ld, &li}, *a2[2] = {&od, &oi};
-    void **args[3] = {a0, a1, a2};
+    void **args[ChainGraph::NK] = {a0, a0, a0, a1, a2};
     for (int k = 0; k < nk; k++) {
       hipKernelNodeParams p = g->base[k];
       p.kernelParams = args[k];
@@ -732,6 +746,7 @@ struct dvbt2ll_chain {
   }
   int alloc_slot(int k) {
     if (cw[k].ensure((size_t)frame.F * max_frames * cw_stride) ||
+        bpart[k].ensure((size_t)8 * frame.F * max_frames * 8 * sizeof(uint32_t)) ||
         pairs[k].ensure((size_t)pair_stride * max_frames * 2) || l1buf[k].ensure((size_t)l1_stride * max_frames * 8))
       return DVBT2LL_ENOMEM;
     if (!slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
@@ -764,6 +779,7 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if (r) return r;
   if ((r = h->fec.init(f.framesize, f.rate, f.constellation, f.inputmode, f.inband, f.fecblocks, p->tsrate)))
     return r;
+  if ((r = h->fec.init_chain())) return r;
   if ((r = h->map.init(f.framesize, f.rate, f.constellation, f.rotation, h->fec.plan))) return r;
   std::vector<int16_t> cip(h->frame.ci_perm.begin(), h->frame.ci_perm.end());
   cip.resize(((cip.size() + 3) & ~(size_t)3) + 4, 0);   // the map kernel reads aligned quads
@@ -927,6 +943,8 @@ extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, i
   fio.sync_err = h->sync_err.as<uint32_t>();
   fio.blocks_per_stream = nstreams > 1 ? F * nframes : 0;
   fio.ts_stride = nstreams > 1 ? ts_stride : 0;
+  fio.bch_part = h->bpart[slot].as<uint32_t>();
+  fio.bch_part_stride = (int64_t)F * h->max_frames;
   mio.in = cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
   mio.out_pairs = pairs.as<uint16_t>();
@@ -978,6 +996,7 @@ extern "C" int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots) {
   for (int k = nslots; k < DVBT2LL_CHAIN_MAX_SLOTS; k++) {
     h->cw[k].release();
     h->pairs[k].release();
+    h->bpart[k].release();
     h->slot_used[k] = false;
   }
   h->nslots = nslots;

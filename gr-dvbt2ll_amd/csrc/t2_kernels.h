@@ -7,7 +7,7 @@ namespace t2 {
 
 // ---------------------------------------------------------------- FEC (BB + BCH + LDPC)
 enum FecMode {
-  FEC_TS_TO_TEMPU = 0,   // chain: TS bytes -> packed interleaver-input codeword
+  FEC_TS_TO_TEMPU = 0,   // chain: TS bytes -> packed interleaver-input codeword (three passes)
   FEC_TS_TO_BITS = 1,    // bbheaderbch block: TS bytes -> unpacked nbch bits
   FEC_BITS_TO_BITS = 2,  // ldpc block: unpacked nbch bits -> unpacked nldpc bits (natural)
 };
@@ -21,6 +21,8 @@ struct FecDev {
   const uint8_t *crc8_tab;      // 256
   const uint8_t *crc8_shift;    // 8 x 256
   const uint8_t *hcrc_bits;     // 72: BBHEADER CRC-8 contribution of each header bit
+  const uint4 *bch_mfma;        // chain: fp4 B fragments of the BCH generator matrix (FecPlan::bch_mfma)
+  int bch_nq, bch_nt;           // chain: 32-byte message chunks, 32-parity tiles of bch_mfma
   int kbch, nbch, P, nldpc, q, nent, chunk, parity_il;   // chunk: BCH message bytes per lane (64 lanes)
   int hem, inband, fec_blocks, ts_rate;
 };
@@ -38,6 +40,10 @@ struct FecIO {
   // b / blocks_per_stream, whose TS bytes start at in + stream * ts_stride (same ts_base, ts_len)
   int blocks_per_stream;
   int64_t ts_stride;
+  // chain (FEC_TS_TO_TEMPU): BCH partial parities of the matrix-core pass, 8 words per (K slice,
+  // block) at (slice * bch_part_stride + block) * 8 (bch_part_stride >= nblocks)
+  uint32_t *bch_part;
+  int64_t bch_part_stride;
 };
 
 // ---------------------------------------------------------------- L1-post signalling (t2_plan.h L1PostPlan)

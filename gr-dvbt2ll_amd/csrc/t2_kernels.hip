@@ -93,39 +93,51 @@ static hipError_t lds_limit(const void *fn, int bytes) {
   return e;
 }
 
-// ============================================================================ FEC kernel
+// ============================================================================ FEC kernels
+// Block API (bbheaderbch / ldpc blocks): fec_kernel<MODE>, one fused pass per FEC block (BBFRAME,
+// BCH on one wave, LDPC).  The fused chain runs three passes instead (launch_fec FEC_TS_TO_TEMPU):
+//   fec_bb_kernel    TS -> BBFRAME bytes in the codeword row (header, CRC-8 sync replacement,
+//                    in-band field, BB scrambling)
+//   bch_gemm_kernel  BCH parity of every block as a GF(2) matrix product on the matrix cores
+//                    (blocks x message bits x parity bits, fp4 0/1 operands, exact f32 sums, parity
+//                    = sum & 1), K split over the eight XCDs into XOR-able partial parities
+//   fec_ldpc_kernel  info bytes + XOR of the partials -> LDPC parity -> interleaver-input codeword
 constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
 constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 233280 / 360)
 constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g || d_g[0..56)
-constexpr int FEC_WG_PER_CU = 7;        // most resident FEC workgroups per CU (72-VGPR budget; LDS may allow fewer)
+constexpr int FEC_WG_PER_CU = 7;        // fused kernel: resident workgroups per CU (72-VGPR budget)
+constexpr int FEC_PASS_WG_PER_CU = 8;   // chain BB / LDPC passes (64-VGPR budget, 32 waves per CU)
 constexpr int FEC_BCH_JB = 2;           // nibble-table lookups in flight per lane in the BCH combine
-// dynamic LDS carve (bytes): a persistent part (the workgroup loops over FEC blocks; tables are
-// staged once), then the per-block area, reused by phase:
-//   BB/CRC phase: [frame | raw TS bytes | CRC-8 table | CRC-8 zero-extension tables]
-//   LDPC: [frame | D: ngroups x 13 words | rows: q x 12 words], ngroups + q = nldpc / 360 (<= 180)
-constexpr int SM_BTAB = 0;                                   // 256*3*8 = 6144
-constexpr int SM_ENT = SM_BTAB + 6144;                       // 648*4
-constexpr int SM_HCRC = SM_ENT + FEC_MAX_ENT * 4;            // 72 (+8)
-constexpr int SM_SYNC = SM_HCRC + 80;                        // 48 (<= 36 sync slots)
-constexpr int SM_W = SM_SYNC + 48;                           // 12*4
-constexpr int SM_BLK = SM_W + 48;                            // per-block area
-constexpr int SM_FRAME = SM_BLK;
-constexpr int SM_PHASE = SM_FRAME + FEC_FRAME_BYTES;
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
-static_assert(SM_BTAB % 16 == 0 && SM_PHASE % 16 == 0 && SM_ENT % 16 == 0 && SM_BLK % 16 == 0, "LDS carve alignment");
-// the carve a plan actually needs (frame, raw TS and LDPC areas sized for its code): the launch
-// fits as many persistent workgroups per CU as it allows, up to FEC_WG_PER_CU (the register budget)
+constexpr int BCH_KS = 8;               // bch_gemm_kernel: K slices (one per XCD)
+constexpr int BCH_ROWS = 128;           // bch_gemm_kernel: FEC blocks per workgroup (4 waves x 32)
+constexpr int BCH_PART_WORDS = 8;       // partial parity words per (slice, block)
+
+// dynamic LDS carve (bytes) of each FEC kernel kind: persistent tables (staged once; the
+// workgroups loop over FEC blocks), then the per-block area, reused by phase:
+//   BB phase:   [frame | raw TS bytes | CRC-8 table | CRC-8 zero-extension tables]
+//   LDPC phase: [frame | D: ngroups x 13 words | rows: q x 12 words], ngroups + q = nldpc / 360 (<= 180)
+// sized for the plan's code, so a launch fits as many workgroups per CU as it allows
+enum FecCarveKind { CARVE_FUSED = 0, CARVE_BB = 1, CARVE_LDPC = 2 };
 struct FecCarve {
-  int phase, crc8, crcsh, total;
+  int btab, ents, hcrc, sync, w, frame, phase, crc8, crcsh, total;
 };
-__host__ __device__ inline FecCarve fec_carve(int kbch, int nbch, int q) {
-  FecCarve c;
-  c.phase = SM_FRAME + ((nbch / 8 + 15) & ~15);
+__host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int q) {
+  FecCarve c{};
+  const bool bch = kind == CARVE_FUSED, ldpc = kind != CARVE_BB, bb = kind != CARVE_LDPC;
+  int o = 0;
+  c.btab = o; o += bch ? 256 * 3 * 8 : 0;
+  c.ents = o; o += ldpc ? FEC_MAX_ENT * 4 : 0;
+  c.hcrc = o; o += bb ? 80 : 0;            // 72 header-bit CRC contributions
+  c.sync = o; o += bb ? 48 : 0;            // <= 36 sync-slot CRC-8s
+  c.w = o; o += ldpc ? 48 : 0;             // 12 column-parity words
+  c.frame = (o + 15) & ~15;
+  c.phase = c.frame + ((nbch / 8 + 15) & ~15);
   c.crc8 = c.phase + ((188 + (kbch - 80) / 8 + 32 + 15) & ~15);   // + slack: 16-byte staging start
   c.crcsh = c.crc8 + 256;
-  const int ldpc = 4 * (FEC_DW * (nbch / 360) + 12 * q);
-  c.total = c.crcsh + 2048 > c.phase + ldpc ? c.crcsh + 2048 : c.phase + ldpc;
+  const int bb_end = c.crcsh + 2048, ldpc_end = c.phase + 4 * (FEC_DW * (nbch / 360) + 12 * q);
+  c.total = kind == CARVE_BB ? bb_end : kind == CARVE_LDPC ? ldpc_end : (bb_end > ldpc_end ? bb_end : ldpc_end);
   return c;
 }
 
@@ -256,251 +268,16 @@ __device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, con
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int L = d.kbch >> 3;           // BBFRAME bytes
-  const int NB = d.nbch >> 3;          // info bytes (BBFRAME + BCH parity)
-  const int P = d.P;
-  uint8_t *frame = smem + SM_FRAME;
-  const FecCarve cv = fec_carve(d.kbch, d.nbch, d.q);
-  uint8_t *crc8 = smem + cv.crc8;
-  uint8_t *crcsh = smem + cv.crcsh;
-  uint8_t *const phase = smem + cv.phase;   // raw TS bytes (NM), then the LDPC groups and rows
-  uint8_t *hcrc8 = smem + SM_HCRC;
-  uint8_t *syncv = smem + SM_SYNC;
-  uint64_t *btab = (uint64_t *)(smem + SM_BTAB);
-  uint32_t *D = (uint32_t *)phase;
-  uint32_t *Wv = (uint32_t *)(smem + SM_W);
-  uint32_t *ents = (uint32_t *)(smem + SM_ENT);
-
-  // ---- constant tables into LDS, once: the workgroup then loops over FEC blocks
-  for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
-  for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
-  if (MODE != FEC_BITS_TO_BITS)
-    for (int i = tid; i < 72; i += FEC_THREADS) hcrc8[i] = d.hcrc_bits[i];
+// LDPC (ldpc_calculate, bbheader:625-646) of the info groups laid out in D: parity rows, the
+// accumulate as an inclusive prefix XOR over rows a (wave w scans word columns 3w..3w+2, 64 rows
+// per DPP wave scan plus the carry of the previous 64), then the exclusive bit-prefix of the column
+// parities along c.  Leaves p[a][c] at D + ngroups * FEC_DW (row a, 12 big-endian words).
+__device__ __forceinline__ uint32_t *fec_ldpc(const FecDev &d, uint32_t *D, int ngroups, const uint32_t *ents,
+                                              uint32_t *Wv, int tid) {
+  const int lane = tid & 63, wave = tid >> 6, q = d.q;
+  uint32_t *cur = D + ngroups * FEC_DW;
+  ldpc_rows(D, cur, ents, d.ldpc_rowptr, q, tid, FEC_THREADS);
   __syncthreads();
-
-  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
-  // stream-major multi-stream batch: launch block bi is block bi % bps of stream bi / bps, whose TS
-  // slice (same ts_base / ts_len layout for every stream) starts at in + stream * ts_stride
-  const int sidx = io.blocks_per_stream ? bi / io.blocks_per_stream : 0;
-  const int64_t B = io.first_block + (bi - sidx * io.blocks_per_stream);
-  const uint8_t *tin = io.in + (int64_t)sidx * io.ts_stride;
-  do {   // one FEC block; `break` ends it early (block-API modes)
-  if (MODE == FEC_BITS_TO_BITS) {
-    // pack nbch unpacked info bits
-    const uint8_t *src = tin + (int64_t)bi * d.nbch;
-    for (int k = tid; k < NB; k += FEC_THREADS) {
-      uint32_t v = 0;
-      for (int e = 0; e < 8; e++) v |= (uint32_t)(src[8 * k + e] & 1) << (7 - e);
-      frame[k] = (uint8_t)v;
-    }
-    __syncthreads();
-  } else {
-    // ---- block geometry (closed form in the absolute block index B; reference keeps
-    //      count / crc / fec_block as running state, bbheader:661-734)
-    const int pay_full = (d.kbch - 80) >> 3;
-    int64_t npad_before = 0;
-    int padding = 0;
-    if (d.inband) {
-      npad_before = (B + d.fec_blocks - 1) / d.fec_blocks;
-      padding = (B % d.fec_blocks) == 0 ? 104 : 0;
-    }
-    const int npay = (d.kbch - 80 - padding) >> 3;
-    const int64_t J0 = B * pay_full - 13 * npad_before;
-    const int64_t pos0 = payload_pos(J0, d.hem);
-    int count0;   // TS packet position of the next input byte at block start
-    if (d.hem) count0 = J0 == 0 ? 0 : (int)((payload_pos(J0 - 1, 1) + 1) % 188);
-    else count0 = (int)(pos0 % 188);
-    // NM: stage the raw stream bytes [pos0 - 188, pos0 + npay) once with 16-byte loads from a
-    // 16-byte aligned start (raw byte i = stream byte rs + i lives at LDS byte cv.phase + delta + i);
-    // the CRC-8 chains and the payload words then read LDS
-    const int64_t rs = pos0 - 188;
-    int delta = 0, first_slot = 0;
-    const uint32_t *raww = (const uint32_t *)phase;
-    if (!d.hem) {
-      const int64_t rel = rs - io.ts_base;                 // >= -188
-      for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)crc8)[i] = ((const uint32_t *)d.crc8_tab)[i];
-      for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)crcsh)[i] = ((const uint32_t *)d.crc8_shift)[i];
-      const int64_t w0 = (rel >= 0 ? rel : rel - 15) / 16;   // floor
-      delta = (int)(rel - 16 * w0);
-      const int nq = (delta + npay + 188 + 15) >> 4;
-      uint4 *rawq = (uint4 *)phase;
-      const bool aligned = (((uintptr_t)tin) & 15) == 0;
-      for (int i = tid; i < nq; i += FEC_THREADS) {
-        const int64_t b = 16 * (w0 + i);
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (aligned && b >= 0 && b + 16 <= io.ts_len) {
-          v = *(const uint4 *)(tin + b);
-        } else {   // misaligned buffer or stream edge: byte loads
-          uint32_t w[4] = {0u, 0u, 0u, 0u};
-          for (int e = 0; e < 16; e++)
-            if (b + e >= 0 && b + e < io.ts_len) w[e >> 2] |= (uint32_t)tin[b + e] << (8 * (e & 3));
-          v = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-        rawq[i] = v;
-      }
-      const uint8_t *raw = phase + delta;
-      __syncthreads();
-      first_slot = (188 - count0) % 188;
-      const int nslots = first_slot < npay ? (npay - 1 - first_slot) / 188 + 1 : 0;
-      // CRC-8 of each packet whose sync slot falls in this block: 8 lanes per packet, 24-byte
-      // chunks combined with zero-extension tables; up to 36 slots per block (5/6 normal), 32 per pass
-      for (int m0 = 0; m0 < nslots; m0 += FEC_THREADS / 8) {
-        const int m = m0 + (tid >> 3), k = tid & 7;
-        uint8_t part = 0;
-        int64_t p = pos0 + first_slot + 188 * (int64_t)m;   // sync position
-        bool active = m < nslots && p > 0;
-        if (active) {
-          const uint8_t *b0 = raw + (p - 187 + 24 * k - rs);
-          const int n = k == 7 ? 19 : 24;            // 187 = 7 x 24 + 19
-          uint8_t by[24];
-#pragma unroll
-          for (int i = 0; i < 24; i++) by[i] = i < n ? b0[i] : 0;
-          uint32_t c = 0;
-#pragma unroll
-          for (int i = 0; i < 24; i++)
-            if (i < n) c = crc8[by[i] ^ c];
-          part = crcsh[k * 256 + c];
-        }
-        // XOR of the 8 lanes' parts into lane k == 0: DPP quad_perm [1,0,3,2], [2,3,0,1], row_shl:4
-        uint32_t v = part;
-        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);
-        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);
-        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, true);
-        if (k == 0 && m < nslots) {
-          syncv[m] = active ? (uint8_t)v : 0;
-          // the reference warns on every consumed sync byte that is not 0x47 (bbheader:703-705)
-          if (io.sync_err && raw[p - rs] != 0x47) atomicAdd(io.sync_err, 1u);
-        }
-      }
-      __syncthreads();
-    }
-    if (d.hem && io.sync_err) {
-      // HEM drops each packet's sync byte; the one of packet p is consumed just before payload
-      // byte 187 p (bbheader:673-680, warning at :675-677)
-      const int64_t p0 = (J0 + 186) / 187;
-      for (int64_t pk = p0 + tid; 187 * pk < J0 + npay; pk += FEC_THREADS)
-        if (tin[188 * pk - io.ts_base] != 0x47) atomicAdd(io.sync_err, 1u);
-    }
-    // BBHEADER (bbheader:272-325), uniform across the workgroup: MATYPE-1 = TS, SIS, CCM, ISSYI 0,
-    // NPD 0, RO 0; ISI 0; bytes 0..7 big-endian in hw, byte 8 = SYNCD low, byte 9 = CRC-8
-    const uint32_t upl = d.hem ? 0u : 188u * 8u, dfl = (uint32_t)(d.kbch - 80 - padding);
-    const uint32_t syncb = d.hem ? 0u : 0x47u, syncd = count0 == 0 ? 0u : (uint32_t)(188 - count0) * 8u;
-    const uint64_t hw = (0xF0ull << 56) | ((uint64_t)upl << 32) | ((uint64_t)dfl << 16) | ((uint64_t)syncb << 8) |
-                        (uint64_t)(syncd >> 8);
-    // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270): XOR
-    // of the per-bit contributions (t2_plan hcrc_bits), lane n taking header bit n (and 64 + n),
-    // then an XOR reduction over the wave; only wave 0 writes the header word (bytes 8..11)
-    uint32_t hcrc = 0;
-    if (__builtin_amdgcn_readfirstlane(wave) == 0) {
-      uint32_t v = ((hw >> (63 - lane)) & 1u) ? (uint32_t)hcrc8[lane] : 0u;
-      if (lane < 8 && (((syncd & 0xFFu) >> (7 - lane)) & 1u)) v ^= hcrc8[64 + lane];
-      hcrc = rd_lane_u32(wave_prefix_xor(v), 63);   // XOR over the wave
-      if (d.hem) hcrc ^= 0x80u;
-    }
-    const uint32_t hcrc_rev = __builtin_bitreverse32(hcrc) >> 24;   // register LSB written first
-    auto slow_byte = [&](int pidx) -> uint32_t {   // BBFRAME byte pidx outside the bulk payload path
-      if (pidx < 8) return (uint32_t)(hw >> (56 - 8 * pidx)) & 0xFFu;
-      if (pidx == 8) return syncd & 0xFFu;
-      if (pidx == 9) return hcrc_rev;
-      const int j = pidx - 10;
-      if (j < npay) {
-        if (d.hem) return tin[payload_pos(J0 + j, 1) - io.ts_base];
-        const int r = (count0 + j) % 188;
-        return r == 0 ? (uint32_t)syncv[(j - first_slot) / 188] : (uint32_t)phase[delta + 188 + j];
-      }
-      const int k = j - npay;   // in-band type B (bbheader:327-355): 01, 65 zero bits, TS rate (27 bits), 10 zeros
-      if (!padding || k >= 13) return 0u;
-      uint32_t v = k == 0 ? 0x40u : 0u;
-      for (int e = 0; e < 8; e++) {
-        const int bit = 8 * k + e;
-        if (bit >= 67 && bit < 94 && ((d.ts_rate >> (26 - (bit - 67))) & 1)) v |= 1u << (7 - e);
-      }
-      return v;
-    };
-    // BBFRAME words = header | payload (each sync slot carries the CRC-8 of the previous packet,
-    // bbheader:701-719) | in-band field, BB-scrambled (:694-696, :724-726)
-    {
-      uint32_t *framew = (uint32_t *)frame;
-      const uint32_t *prbsw = (const uint32_t *)d.prbs;
-      for (int w = tid; w < (L + 3) >> 2; w += FEC_THREADS) {
-        const int p0 = 4 * w, j0 = p0 - 10;
-        uint32_t v;
-        if (!d.hem && j0 >= 0 && j0 + 4 <= npay) {
-          const int q = delta + 188 + j0;
-          v = __builtin_amdgcn_alignbyte(raww[(q >> 2) + 1], raww[q >> 2], (uint32_t)(q & 3));
-          const int r0 = (count0 + j0) % 188, e = r0 == 0 ? 0 : 188 - r0;
-          if (e < 4) {
-            const uint32_t sb = syncv[(j0 + e - first_slot) / 188];
-            v = (v & ~(0xFFu << (8 * e))) | (sb << (8 * e));
-          }
-        } else {
-          v = 0;
-          for (int e = 0; e < 4; e++) v |= slow_byte(p0 + e) << (8 * e);
-        }
-        framew[w] = v ^ prbsw[w];
-      }
-    }
-    __syncthreads();
-
-    // ---- BCH on wave 0 (raised issue priority: it is the block's critical path); waves 1..3
-    //      meanwhile (chain mode) lay out the LDPC info groups that hold no BCH parity
-    const int ngroups = d.nbch / 360;
-    if (wave == 0) {
-      __builtin_amdgcn_s_setprio(1);
-      uint64_t a[3];
-      switch (P) {   // compile-time register geometry per BCH parity length (t = 12, 10, 8; short 12)
-        case 192: bch_wave<192>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
-        case 168: bch_wave<168>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
-        case 160: bch_wave<160>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
-        default: bch_wave<128>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
-      }
-      // parity MSB (x^(P-1)) first as frame[L..L + P/8) (bbheader:504-531)
-      if (lane < P / 8) frame[L + lane] = get_byte192(a, P - 8 - 8 * lane);
-      if (MODE == FEC_TS_TO_TEMPU) {
-        // the last info group holds the BCH parity (P < 360): lay it out here, after the parity
-        // bytes (same wave; LDS accesses of one wave complete in order)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane < FEC_DW) ldpc_group_word(D, frame, ngroups - 1, lane);
-      }
-      __builtin_amdgcn_s_setprio(0);
-    } else if (MODE == FEC_TS_TO_TEMPU) {
-      for (int it = tid - 64; it < (ngroups - 1) * FEC_DW; it += FEC_THREADS - 64) {
-        const int g = it / FEC_DW;
-        ldpc_group_word(D, frame, g, it - g * FEC_DW);
-      }
-    }
-    __syncthreads();
-    if (MODE == FEC_TS_TO_BITS) {
-      uint8_t *dst = io.out + (int64_t)bi * d.nbch;
-      for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
-      break;
-    }
-  }
-
-  // ---- LDPC.  Extended info groups: D[g][k] = big-endian word k of d_g || d_g[0..56)
-  //      (chain mode: laid out above, overlapping the BCH)
-  const int ngroups = d.nbch / 360;
-  if (MODE == FEC_BITS_TO_BITS) {
-    for (int it = tid; it < ngroups * FEC_DW; it += FEC_THREADS) {
-      const int g = it / FEC_DW;
-      ldpc_group_word(D, frame, g, it - g * FEC_DW);
-    }
-    __syncthreads();
-  }
-  // row a, word w of p[a][c] = XOR over entries (g, b) of d_g[(c - b) mod 360]
-  const int q = d.q;
-  uint32_t *rowA = D + ngroups * FEC_DW;
-  ldpc_rows(D, rowA, ents, d.ldpc_rowptr, q, tid, FEC_THREADS);
-  __syncthreads();
-  // inclusive prefix XOR over rows a, in place: wave w scans word columns 3w..3w+2, 64 rows
-  // per DPP wave scan plus the carry of the previous 64
-  uint32_t *cur = rowA;
   for (int col = 3 * wave; col < 3 * wave + 3; col++) {
     uint32_t carry = 0;
     for (int a0 = 0; a0 < q; a0 += 64) {
@@ -512,7 +289,6 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     }
   }
   __syncthreads();
-  // exclusive bit-prefix XOR of the last row (the column parities) along c
   if (tid == 0) {
     uint32_t carry = 0;
     for (int w = 0; w < 12; w++) {
@@ -529,47 +305,435 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   __syncthreads();
   for (int it = tid; it < q * 12; it += FEC_THREADS) cur[it] ^= Wv[it % 12];
   __syncthreads();
-  // parity bit of row a (interleaved position 360 a + c) / natural index a + q c
-  auto pbit = [&](int a, int c) -> uint32_t { return (cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1; };
+  return cur;
+}
 
-  if (MODE == FEC_BITS_TO_BITS) {
-    uint8_t *dst = io.out + (int64_t)bi * d.nldpc;
-    for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
-    const int pbits = d.nldpc - d.nbch;
-    for (int j = tid; j < pbits; j += FEC_THREADS) dst[d.nbch + j] = (uint8_t)pbit(j % q, j / q);
-    break;
+// BBFRAME of FEC block B (absolute index; the reference keeps count / crc / fec_block as running
+// state, bbheader:661-734, here they are closed-form in B) into frame[0, L): raw TS staging, the
+// sync-slot CRC-8s, BBHEADER + its CRC-8, payload words, the in-band field, BB scrambling.  Ends
+// with a barrier.  crc_resident: the CRC-8 tables already sit at cv.crc8 / cv.crcsh (the BB pass
+// stages them once; the fused kernel's LDPC area overlays them, so it reloads them per block).
+template <bool CRC_RESIDENT>
+__device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv, unsigned char *smem, int64_t B,
+                            const uint8_t *tin, int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+  const int L = d.kbch >> 3;
+  uint8_t *frame = smem + cv.frame, *phase = smem + cv.phase;
+  uint8_t *crc8 = smem + cv.crc8, *crcsh = smem + cv.crcsh;
+  const uint8_t *hcrc8 = smem + cv.hcrc;
+  uint8_t *syncv = smem + cv.sync;
+  const int pay_full = (d.kbch - 80) >> 3;
+  int64_t npad_before = 0;
+  int padding = 0;
+  if (d.inband) {
+    npad_before = (B + d.fec_blocks - 1) / d.fec_blocks;
+    padding = (B % d.fec_blocks) == 0 ? 104 : 0;
   }
-  // FEC_TS_TO_TEMPU: interleaver input words = info bytes (frame) | parity bytes (rows; parity
-  // interleaved: byte m = byte m % 45 of row m / 45)
-  const int cwb = d.nldpc >> 3;
-  auto parity_byte = [&](int m) -> uint32_t {
-    if (d.parity_il) {
-      const int a = m / 45, k = m - 45 * a;
-      return (cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu;
+  const int npay = (d.kbch - 80 - padding) >> 3;
+  const int64_t J0 = B * pay_full - 13 * npad_before;
+  const int64_t pos0 = payload_pos(J0, d.hem);
+  int count0;   // TS packet position of the next input byte at block start
+  if (d.hem) count0 = J0 == 0 ? 0 : (int)((payload_pos(J0 - 1, 1) + 1) % 188);
+  else count0 = (int)(pos0 % 188);
+  // NM: stage the raw stream bytes [pos0 - 188, pos0 + npay) once with 16-byte loads from a
+  // 16-byte aligned start (raw byte i = stream byte rs + i lives at LDS byte cv.phase + delta + i);
+  // the CRC-8 chains and the payload words then read LDS
+  const int64_t rs = pos0 - 188;
+  int delta = 0, first_slot = 0;
+  const uint32_t *raww = (const uint32_t *)phase;
+  if (!d.hem) {
+    const int64_t rel = rs - io.ts_base;                 // >= -188
+    if (!CRC_RESIDENT) {
+      for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)crc8)[i] = ((const uint32_t *)d.crc8_tab)[i];
+      for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)crcsh)[i] = ((const uint32_t *)d.crc8_shift)[i];
     }
-    uint32_t v = 0;
+    const int64_t w0 = (rel >= 0 ? rel : rel - 15) / 16;   // floor
+    delta = (int)(rel - 16 * w0);
+    const int nq = (delta + npay + 188 + 15) >> 4;
+    uint4 *rawq = (uint4 *)phase;
+    const bool aligned = (((uintptr_t)tin) & 15) == 0;
+    for (int i = tid; i < nq; i += FEC_THREADS) {
+      const int64_t b = 16 * (w0 + i);
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (aligned && b >= 0 && b + 16 <= io.ts_len) {
+        v = *(const uint4 *)(tin + b);
+      } else {   // misaligned buffer or stream edge: byte loads
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int e = 0; e < 16; e++)
+          if (b + e >= 0 && b + e < io.ts_len) w[e >> 2] |= (uint32_t)tin[b + e] << (8 * (e & 3));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      rawq[i] = v;
+    }
+    const uint8_t *raw = phase + delta;
+    __syncthreads();
+    first_slot = (188 - count0) % 188;
+    const int nslots = first_slot < npay ? (npay - 1 - first_slot) / 188 + 1 : 0;
+    // CRC-8 of each packet whose sync slot falls in this block: 8 lanes per packet, 24-byte
+    // chunks combined with zero-extension tables; up to 36 slots per block (5/6 normal), 32 per pass
+    for (int m0 = 0; m0 < nslots; m0 += FEC_THREADS / 8) {
+      const int m = m0 + (tid >> 3), k = tid & 7;
+      uint8_t part = 0;
+      int64_t p = pos0 + first_slot + 188 * (int64_t)m;   // sync position
+      bool active = m < nslots && p > 0;
+      if (active) {
+        const uint8_t *b0 = raw + (p - 187 + 24 * k - rs);
+        const int n = k == 7 ? 19 : 24;            // 187 = 7 x 24 + 19
+        uint8_t by[24];
+#pragma unroll
+        for (int i = 0; i < 24; i++) by[i] = i < n ? b0[i] : 0;
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 24; i++)
+          if (i < n) c = crc8[by[i] ^ c];
+        part = crcsh[k * 256 + c];
+      }
+      // XOR of the 8 lanes' parts into lane k == 0: DPP quad_perm [1,0,3,2], [2,3,0,1], row_shl:4
+      uint32_t v = part;
+      v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);
+      v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);
+      v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xF, 0xF, true);
+      if (k == 0 && m < nslots) {
+        syncv[m] = active ? (uint8_t)v : 0;
+        // the reference warns on every consumed sync byte that is not 0x47 (bbheader:703-705)
+        if (io.sync_err && raw[p - rs] != 0x47) atomicAdd(io.sync_err, 1u);
+      }
+    }
+    __syncthreads();
+  }
+  if (d.hem && io.sync_err) {
+    // HEM drops each packet's sync byte; the one of packet p is consumed just before payload
+    // byte 187 p (bbheader:673-680, warning at :675-677)
+    const int64_t p0 = (J0 + 186) / 187;
+    for (int64_t pk = p0 + tid; 187 * pk < J0 + npay; pk += FEC_THREADS)
+      if (tin[188 * pk - io.ts_base] != 0x47) atomicAdd(io.sync_err, 1u);
+  }
+  // BBHEADER (bbheader:272-325), uniform across the workgroup: MATYPE-1 = TS, SIS, CCM, ISSYI 0,
+  // NPD 0, RO 0; ISI 0; bytes 0..7 big-endian in hw, byte 8 = SYNCD low, byte 9 = CRC-8
+  const uint32_t upl = d.hem ? 0u : 188u * 8u, dfl = (uint32_t)(d.kbch - 80 - padding);
+  const uint32_t syncb = d.hem ? 0u : 0x47u, syncd = count0 == 0 ? 0u : (uint32_t)(188 - count0) * 8u;
+  const uint64_t hw = (0xF0ull << 56) | ((uint64_t)upl << 32) | ((uint64_t)dfl << 16) | ((uint64_t)syncb << 8) |
+                      (uint64_t)(syncd >> 8);
+  // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270): XOR
+  // of the per-bit contributions (t2_plan hcrc_bits), lane n taking header bit n (and 64 + n),
+  // then an XOR reduction over the wave; only wave 0 writes the header word (bytes 8..11)
+  uint32_t hcrc = 0;
+  if (__builtin_amdgcn_readfirstlane(wave) == 0) {
+    uint32_t v = ((hw >> (63 - lane)) & 1u) ? (uint32_t)hcrc8[lane] : 0u;
+    if (lane < 8 && (((syncd & 0xFFu) >> (7 - lane)) & 1u)) v ^= hcrc8[64 + lane];
+    hcrc = rd_lane_u32(wave_prefix_xor(v), 63);   // XOR over the wave
+    if (d.hem) hcrc ^= 0x80u;
+  }
+  const uint32_t hcrc_rev = __builtin_bitreverse32(hcrc) >> 24;   // register LSB written first
+  auto slow_byte = [&](int pidx) -> uint32_t {   // BBFRAME byte pidx outside the bulk payload path
+    if (pidx < 8) return (uint32_t)(hw >> (56 - 8 * pidx)) & 0xFFu;
+    if (pidx == 8) return syncd & 0xFFu;
+    if (pidx == 9) return hcrc_rev;
+    const int j = pidx - 10;
+    if (j < npay) {
+      if (d.hem) return tin[payload_pos(J0 + j, 1) - io.ts_base];
+      const int r = (count0 + j) % 188;
+      return r == 0 ? (uint32_t)syncv[(j - first_slot) / 188] : (uint32_t)phase[delta + 188 + j];
+    }
+    const int k = j - npay;   // in-band type B (bbheader:327-355): 01, 65 zero bits, TS rate (27 bits), 10 zeros
+    if (!padding || k >= 13) return 0u;
+    uint32_t v = k == 0 ? 0x40u : 0u;
     for (int e = 0; e < 8; e++) {
-      const int j = 8 * m + e;
-      v |= pbit(j % q, j / q) << (7 - e);
+      const int bit = 8 * k + e;
+      if (bit >= 67 && bit < 94 && ((d.ts_rate >> (26 - (bit - 67))) & 1)) v |= 1u << (7 - e);
     }
     return v;
   };
-  uint32_t *dstw = (uint32_t *)(io.out + (int64_t)bi * io.cw_stride);
-  const uint32_t *framew = (const uint32_t *)frame;
-  auto out_word = [&](int i) -> uint32_t {
-    if (4 * i + 4 <= NB) return framew[i];
-    uint32_t v = 0;
-    for (int e = 0; e < 4; e++) {
-      const int bidx = 4 * i + e;
-      const uint32_t by = bidx < NB ? (uint32_t)frame[bidx] : bidx < cwb ? parity_byte(bidx - NB) : 0u;
-      v |= by << (8 * e);
+  // BBFRAME words = header | payload (each sync slot carries the CRC-8 of the previous packet,
+  // bbheader:701-719) | in-band field, BB-scrambled (:694-696, :724-726)
+  uint32_t *framew = (uint32_t *)frame;
+  const uint32_t *prbsw = (const uint32_t *)d.prbs;
+  for (int w = tid; w < (L + 3) >> 2; w += FEC_THREADS) {
+    const int p0 = 4 * w, j0 = p0 - 10;
+    uint32_t v;
+    if (!d.hem && j0 >= 0 && j0 + 4 <= npay) {
+      const int q = delta + 188 + j0;
+      v = __builtin_amdgcn_alignbyte(raww[(q >> 2) + 1], raww[q >> 2], (uint32_t)(q & 3));
+      const int r0 = (count0 + j0) % 188, e = r0 == 0 ? 0 : 188 - r0;
+      if (e < 4) {
+        const uint32_t sb = syncv[(j0 + e - first_slot) / 188];
+        v = (v & ~(0xFFu << (8 * e))) | (sb << (8 * e));
+      }
+    } else {
+      v = 0;
+      for (int e = 0; e < 4; e++) v |= slow_byte(p0 + e) << (8 * e);
     }
-    return v;
+    framew[w] = v ^ prbsw[w];
+  }
+  __syncthreads();
+}
+
+// launch block bi of a (multi-stream) batch: its absolute FEC block index and TS base.  Stream-major
+// batch: launch block bi is block bi % bps of stream bi / bps, whose TS slice (same ts_base / ts_len
+// layout for every stream) starts at in + stream * ts_stride
+__device__ __forceinline__ int64_t fec_block_of(const FecIO &io, int bi, const uint8_t *&tin) {
+  const int sidx = io.blocks_per_stream ? bi / io.blocks_per_stream : 0;
+  tin = io.in + (int64_t)sidx * io.ts_stride;
+  return io.first_block + (bi - sidx * io.blocks_per_stream);
+}
+
+// fused FEC for the block API: TS -> BBFRAME + BCH (unpacked nbch bits, the bbheaderbch block) or
+// unpacked nbch bits -> LDPC codeword (unpacked nldpc bits in natural order, the ldpc block)
+template <int MODE>
+__global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev d, FecIO io) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int L = d.kbch >> 3;           // BBFRAME bytes
+  const int NB = d.nbch >> 3;          // info bytes (BBFRAME + BCH parity)
+  const int P = d.P;
+  const FecCarve cv = fec_carve(CARVE_FUSED, d.kbch, d.nbch, d.q);
+  uint8_t *frame = smem + cv.frame;
+  uint64_t *btab = (uint64_t *)(smem + cv.btab);
+  uint32_t *ents = (uint32_t *)(smem + cv.ents);
+  uint32_t *D = (uint32_t *)(smem + cv.phase);
+  // ---- constant tables into LDS, once: the workgroup then loops over FEC blocks
+  if (MODE == FEC_TS_TO_BITS) {
+    for (int i = tid; i < 768; i += FEC_THREADS) btab[i] = d.bch_tab[i];
+    for (int i = tid; i < 72; i += FEC_THREADS) smem[cv.hcrc + i] = d.hcrc_bits[i];
+  } else {
+    for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
+  }
+  __syncthreads();
+  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
+    if (MODE == FEC_TS_TO_BITS) {
+      const uint8_t *tin;
+      const int64_t B = fec_block_of(io, bi, tin);
+      fec_bbframe<false>(d, io, cv, smem, B, tin, tid);
+      // BCH on wave 0 (raised issue priority: the block's critical path)
+      if (wave == 0) {
+        __builtin_amdgcn_s_setprio(1);
+        uint64_t a[3];
+        switch (P) {   // compile-time register geometry per BCH parity length (t = 12, 10, 8; short 12)
+          case 192: bch_wave<192>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
+          case 168: bch_wave<168>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
+          case 160: bch_wave<160>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
+          default: bch_wave<128>(frame, btab, d.bch_ctab, L, d.chunk, lane, a); break;
+        }
+        // parity MSB (x^(P-1)) first as frame[L..L + P/8) (bbheader:504-531)
+        if (lane < P / 8) frame[L + lane] = get_byte192(a, P - 8 - 8 * lane);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      __syncthreads();
+      uint8_t *dst = io.out + (int64_t)bi * d.nbch;
+      for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
+    } else {
+      // pack nbch unpacked info bits, lay out the info groups, LDPC, unpacked natural-order output
+      const uint8_t *src = io.in + (int64_t)bi * d.nbch;
+      for (int k = tid; k < NB; k += FEC_THREADS) {
+        uint32_t v = 0;
+        for (int e = 0; e < 8; e++) v |= (uint32_t)(src[8 * k + e] & 1) << (7 - e);
+        frame[k] = (uint8_t)v;
+      }
+      __syncthreads();
+      const int ngroups = d.nbch / 360;
+      for (int it = tid; it < ngroups * FEC_DW; it += FEC_THREADS) {
+        const int g = it / FEC_DW;
+        ldpc_group_word(D, frame, g, it - g * FEC_DW);
+      }
+      __syncthreads();
+      const uint32_t *cur = fec_ldpc(d, D, ngroups, ents, (uint32_t *)(smem + cv.w), tid);
+      const int q = d.q;
+      uint8_t *dst = io.out + (int64_t)bi * d.nldpc;
+      for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
+      const int pbits = d.nldpc - d.nbch;
+      for (int j = tid; j < pbits; j += FEC_THREADS) {   // parity bit of row a = j mod q, column c = j / q
+        const int a = j % q, c = j / q;
+        dst[d.nbch + j] = (uint8_t)((cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1);
+      }
+    }
+    __syncthreads();   // frame / phase regions are reused by the next block
+  }
+}
+
+// chain pass 1: the BBFRAME of every launch block into its codeword row (bytes [0, L); bytes past L
+// of the last 16-byte unit are don't-care: the BCH pass multiplies them by zero rows, the LDPC pass
+// rewrites them)
+__global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel(FecDev d, FecIO io) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int L = d.kbch >> 3;
+  const FecCarve cv = fec_carve(CARVE_BB, d.kbch, d.nbch, d.q);
+  for (int i = tid; i < 72; i += FEC_THREADS) smem[cv.hcrc + i] = d.hcrc_bits[i];
+  for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)(smem + cv.crc8))[i] = ((const uint32_t *)d.crc8_tab)[i];
+  for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)(smem + cv.crcsh))[i] = ((const uint32_t *)d.crc8_shift)[i];
+  __syncthreads();
+  const uint4 *framq = (const uint4 *)(smem + cv.frame);
+  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
+    const uint8_t *tin;
+    const int64_t B = fec_block_of(io, bi, tin);
+    fec_bbframe<true>(d, io, cv, smem, B, tin, tid);
+    uint4 *dst = (uint4 *)(io.out + (int64_t)bi * io.cw_stride);
+    for (int i = tid; i < (L + 15) >> 4; i += FEC_THREADS) dst[i] = framq[i];
+    __syncthreads();   // the frame is rebuilt by the next block
+  }
+}
+
+// ---- chain pass 2: BCH as a GF(2) matrix product on the matrix cores
+typedef int bch_v8i __attribute__((ext_vector_type(8)));
+typedef float bch_v16f __attribute__((ext_vector_type(16)));
+// message bits 0..7 of x -> fp4 (e2m1) nibbles 0..7, 0x2 (1.0) where set
+__device__ __forceinline__ uint32_t fp4_spread(uint32_t x) {
+  x &= 0xFFu;
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  x = (x | (x << 3)) & 0x11111111u;
+  return x << 1;
+}
+
+// Workgroup (tile, slice): 128 FEC blocks (wave w: blocks 32 w .. 32 w + 31 of the tile, one per
+// A row) x all bch_nt parity tiles, over the 32-byte message chunks q of K slice `slice` (slice =
+// blockIdx % 8, so each XCD's L2 holds one eighth of the generator table).  Per chunk: the B
+// fragments (t2_plan build_bch_mfma) are staged in LDS (double-buffered, one barrier per chunk),
+// each lane loads 16 message bytes of its block and spreads them into four A fragments, and each
+// wave issues 4 x NT v_mfma_scale_f32_32x32x64_f8f6f4 (fp4 A and B, unit E8M0 scales).  Sums are
+// exact small integers in f32; the partial parity of the slice is (int) sum & 1, packed by wave
+// ballots into 8 words per block (bytes in transmission order) at bch_part[(slice * stride + b) * 8].
+template <int NT>
+__global__ __launch_bounds__(FEC_THREADS, 3) void bch_gemm_kernel(FecDev d, FecIO io) {
+  extern __shared__ __attribute__((aligned(16))) uint4 bsm[];
+  constexpr int PER = 4 * NT * 64;                   // uint4 per chunk buffer
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int slice = (int)blockIdx.x % BCH_KS, tile = (int)blockIdx.x / BCH_KS;
+  const int q0 = slice * d.bch_nq / BCH_KS, q1 = (slice + 1) * d.bch_nq / BCH_KS;
+  const int row0 = tile * BCH_ROWS + wave * 32;
+  const int blk = row0 + (lane & 31);
+  const bool live = blk < io.nblocks;
+  const uint4 *msg = (const uint4 *)(io.out + (int64_t)(live ? blk : 0) * io.cw_stride) + (lane >> 5);
+  // chunk q's B fragments into LDS buffer buf by LDS-DMA (16 bytes per lane, no VGPR staging): each
+  // wave-instruction fills 1 KB at a wave-uniform base, lane l at + 16 l (the table is lane-linear)
+  auto stage = [&](int q, int buf) {
+#pragma unroll
+    for (int k = 0; k < NT; k++) {
+      const uint4 *src = d.bch_mfma + (size_t)q * PER + FEC_THREADS * k + tid;
+      uint4 *dst = bsm + buf * PER + FEC_THREADS * k + 64 * wave;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                       (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+    }
   };
-  // (16-byte stores of four words measured +0.8 % kernel time: 4-byte stores stay)
-  for (int i = tid; i < (cwb + 3) >> 2; i += FEC_THREADS) dstw[i] = out_word(i);
-  } while (0);
-  __syncthreads();   // frame / phase regions are reused by the next block
+  bch_v16f acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) acc[t] = bch_v16f{};
+  uint4 a = make_uint4(0u, 0u, 0u, 0u);
+  if (q0 < q1) {
+    stage(q0, 0);
+    if (live) a = msg[2 * q0];
+  }
+  __syncthreads();   // (its vmcnt(0) retires the DMA)
+  for (int q = q0; q < q1; q++) {
+    const int cur = (q - q0) & 1;
+    uint4 an = make_uint4(0u, 0u, 0u, 0u);
+    if (q + 1 < q1) {   // the other buffer was last read before the previous barrier
+      stage(q + 1, cur ^ 1);
+      if (live) an = msg[2 * (q + 1)];
+    }
+    const uint4 *bq = bsm + cur * PER;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t w = u == 0 ? a.x : u == 1 ? a.y : u == 2 ? a.z : a.w;
+      const bch_v8i A = {(int)fp4_spread(w), (int)fp4_spread(w >> 8), (int)fp4_spread(w >> 16),
+                         (int)fp4_spread(w >> 24), 0, 0, 0, 0};
+#pragma unroll
+      for (int t = 0; t < NT; t++) {
+        const uint4 b = bq[(u * NT + t) * 64 + lane];
+        const bch_v8i Bv = {(int)b.x, (int)b.y, (int)b.z, (int)b.w, 0, 0, 0, 0};
+        acc[t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, Bv, acc[t], 4, 4, 0, 127, 0, 127);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one K-step's B fragments in registers at a time
+    }
+    __syncthreads();
+    a = an;
+  }
+  // partial parities: accumulator register r of lane l is block row (r & 3) + 8 (r >> 2) + 4 (l >> 5),
+  // parity column l & 31 of its tile; one ballot per (tile, register) gives 32 parities of two rows,
+  // bit c -> byte c / 8, bit 7 - c % 8 of the row's tile word (bswap o bitreverse)
+  uint32_t *pw = (uint32_t *)bsm + wave * 32 * BCH_PART_WORDS;   // after the loop's last barrier
+#pragma unroll
+  for (int t = 0; t < NT; t++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(((int)acc[t][r] & 1) != 0);
+      const int row = (r & 3) + 8 * (r >> 2);
+      if (lane == 0) pw[row * BCH_PART_WORDS + t] = __builtin_bswap32(__builtin_bitreverse32((uint32_t)m));
+      if (lane == 1) pw[(row + 4) * BCH_PART_WORDS + t] = __builtin_bswap32(__builtin_bitreverse32((uint32_t)(m >> 32)));
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int i = lane; i < 32 * BCH_PART_WORDS; i += 64) {
+    const int row = i / BCH_PART_WORDS, t = i % BCH_PART_WORDS;
+    if (row0 + row < io.nblocks)
+      io.bch_part[((int64_t)slice * io.bch_part_stride + row0 + row) * BCH_PART_WORDS + t] = t < NT ? pw[i] : 0u;
+  }
+}
+
+// chain pass 3: info bytes [0, L) from the codeword row + the BCH parity (XOR of the BCH_KS partials),
+// the info groups laid out, LDPC, then the interleaver-input words from word L / 4 on (the BB pass
+// wrote the words before): BCH parity | LDPC parity (parity interleaved: byte m = byte m % 45 of row
+// m / 45, or natural order a + q c for QPSK without parity interleaving)
+__global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_ldpc_kernel(FecDev d, FecIO io) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int L = d.kbch >> 3, NB = d.nbch >> 3, PB = d.P >> 3;
+  const FecCarve cv = fec_carve(CARVE_LDPC, d.kbch, d.nbch, d.q);
+  uint8_t *frame = smem + cv.frame;
+  uint32_t *ents = (uint32_t *)(smem + cv.ents);
+  uint32_t *D = (uint32_t *)(smem + cv.phase);
+  uint32_t *Wv = (uint32_t *)(smem + cv.w);
+  for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
+  __syncthreads();
+  const int ngroups = d.nbch / 360, q = d.q, cwb = d.nldpc >> 3;
+  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
+    uint8_t *row = io.out + (int64_t)bi * io.cw_stride;
+    for (int i = tid; i < (L + 15) >> 4; i += FEC_THREADS) ((uint4 *)frame)[i] = ((const uint4 *)row)[i];
+    uint32_t par = 0;
+    if (tid < (PB + 3) >> 2) {
+#pragma unroll
+      for (int s = 0; s < BCH_KS; s++) par ^= io.bch_part[((int64_t)s * io.bch_part_stride + bi) * BCH_PART_WORDS + tid];
+    }
+    __syncthreads();   // the 16-byte loads past L land before the parity bytes overwrite them
+    if (tid < (PB + 3) >> 2)
+      for (int k = 0; k < 4 && 4 * tid + k < PB; k++) frame[L + 4 * tid + k] = (uint8_t)(par >> (8 * k));
+    __syncthreads();
+    for (int it = tid; it < ngroups * FEC_DW; it += FEC_THREADS) {
+      const int g = it / FEC_DW;
+      ldpc_group_word(D, frame, g, it - g * FEC_DW);
+    }
+    __syncthreads();
+    const uint32_t *cur = fec_ldpc(d, D, ngroups, ents, Wv, tid);
+    auto parity_byte = [&](int m) -> uint32_t {
+      if (d.parity_il) {
+        const int a = m / 45, k = m - 45 * a;
+        return (cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu;
+      }
+      uint32_t v = 0;
+      for (int e = 0; e < 8; e++) {
+        const int j = 8 * m + e, a = j % q, c = j / q;
+        v |= ((cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1u) << (7 - e);
+      }
+      return v;
+    };
+    const uint32_t *framew = (const uint32_t *)frame;
+    uint32_t *dstw = (uint32_t *)row;
+    for (int i = (L >> 2) + tid; i < (cwb + 3) >> 2; i += FEC_THREADS) {
+      uint32_t v;
+      if (4 * i + 4 <= NB) {
+        v = framew[i];
+      } else {
+        v = 0;
+        for (int e = 0; e < 4; e++) {
+          const int bidx = 4 * i + e;
+          const uint32_t by = bidx < NB ? (uint32_t)frame[bidx] : bidx < cwb ? parity_byte(bidx - NB) : 0u;
+          v |= by << (8 * e);
+        }
+      }
+      dstw[i] = v;
+    }
+    __syncthreads();   // frame / phase regions are reused by the next block
   }
 }
 
@@ -592,19 +756,47 @@ static bool fec_plan_fits(const FecDev &d) {
            (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.chunk * 64 < d.kbch / 8);
 }
 
+// persistent launch of one FEC kernel kind: as many workgroups per CU as its LDS carve allows, up
+// to cap
+static hipError_t fec_launch_persistent(const void *fn, int kind, int cap, const FecDev &d, const FecIO &io,
+                                        hipStream_t s) {
+  const int lds = fec_carve(kind, d.kbch, d.nbch, d.q).total;
+  int per_cu = (160 * 1024) / lds;
+  per_cu = per_cu < 1 ? 1 : per_cu > cap ? cap : per_cu;
+  void *args[2] = {(void *)&d, (void *)&io};
+  return hipLaunchKernel(fn, dim3(fec_grid(io.nblocks, per_cu)), dim3(FEC_THREADS), args, lds, s);
+}
+
+template <int NT>
+static hipError_t bch_launch(const FecDev &d, const FecIO &io, hipStream_t s) {
+  const int lds = 2 * 4 * NT * 64 * 16;
+  hipError_t e = lds_limit((const void *)bch_gemm_kernel<NT>, lds);
+  if (e != hipSuccess) return e;
+  const int tiles = (io.nblocks + BCH_ROWS - 1) / BCH_ROWS;
+  hipLaunchKernelGGL(bch_gemm_kernel<NT>, dim3(tiles * BCH_KS), dim3(FEC_THREADS), lds, s, d, io);
+  return hipGetLastError();
+}
+
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
   if (!fec_plan_fits(d)) return hipErrorInvalidValue;
-  const int lds = fec_carve(d.kbch, d.nbch, d.q).total;
-  int per_cu = (160 * 1024) / lds;
-  per_cu = per_cu < 1 ? 1 : per_cu > FEC_WG_PER_CU ? FEC_WG_PER_CU : per_cu;
-  dim3 grid(fec_grid(io.nblocks, per_cu)), block(FEC_THREADS);
+  hipError_t e;
   switch (mode) {
-    case FEC_TS_TO_TEMPU: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_TEMPU>, grid, block, lds, s, d, io); break;
-    case FEC_TS_TO_BITS: hipLaunchKernelGGL(fec_kernel<FEC_TS_TO_BITS>, grid, block, lds, s, d, io); break;
-    default: hipLaunchKernelGGL(fec_kernel<FEC_BITS_TO_BITS>, grid, block, lds, s, d, io); break;
+    case FEC_TS_TO_TEMPU:   // the fused chain: BB pass, BCH on the matrix cores, LDPC pass
+      if (!d.bch_mfma || !io.bch_part || io.bch_part_stride < io.nblocks || d.bch_nt < 4 || d.bch_nt > 6 ||
+          d.bch_nq < 1 || d.bch_nq * 32 > io.cw_stride)
+        return hipErrorInvalidValue;
+      e = fec_launch_persistent((const void *)fec_bb_kernel, CARVE_BB, FEC_PASS_WG_PER_CU, d, io, s);
+      if (e == hipSuccess)
+        e = d.bch_nt == 6 ? bch_launch<6>(d, io, s) : d.bch_nt == 5 ? bch_launch<5>(d, io, s) : bch_launch<4>(d, io, s);
+      if (e == hipSuccess)
+        e = fec_launch_persistent((const void *)fec_ldpc_kernel, CARVE_LDPC, FEC_PASS_WG_PER_CU, d, io, s);
+      return e;
+    case FEC_TS_TO_BITS:
+      return fec_launch_persistent((const void *)fec_kernel<FEC_TS_TO_BITS>, CARVE_FUSED, FEC_WG_PER_CU, d, io, s);
+    default:
+      return fec_launch_persistent((const void *)fec_kernel<FEC_BITS_TO_BITS>, CARVE_FUSED, FEC_WG_PER_CU, d, io, s);
   }
-  return hipGetLastError();
 }
 
 // ============================================================================ map kernel

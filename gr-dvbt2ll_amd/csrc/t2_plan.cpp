@@ -226,6 +226,42 @@ int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
   return 0;
 }
 
+int build_bch_mfma(FecPlan &fp) {
+  if (!fp.kbch) return -1;
+  const int P = fp.nparity, L = fp.kbch / 8;
+  Poly192 g = bch_generator(fp.normal, P);
+  // BCH as a GF(2) matrix product for the chain's MFMA pass (bch_gemm_kernel): parity bit p (p = 0
+  // the x^(P-1) coefficient, sent first) of message bit i is coefficient P-1-p of x^(kbch-1-i) x^P
+  // mod g.  fp4 (e2m1) B fragments of v_mfma_scale_f32_32x32x64_f8f6f4: 32-byte message chunk q,
+  // K-step u (its 4-byte word), parity tile t, lane l, dword d, nibble e <-> message byte
+  // b = 32 q + 16 (l >> 5) + 4 u + d, bit e (LSB first, i = 8 b + 7 - e), parity p = 32 t + (l & 31);
+  // nibble 0x2 (1.0) where G[i][p] = 1.  Bits past kbch and parities past P are zero.
+  fp.bch_nq = (L + 31) / 32;
+  fp.bch_nt = (P + 31) / 32;
+  std::vector<Poly192> col(fp.kbch);
+  Poly192 r;
+  r.set(0);
+  for (int i = 0; i < P; i++) r = times_x(r, g, P);   // x^P mod g: message bit kbch - 1
+  for (int i = fp.kbch - 1; i >= 0; i--) {
+    col[i] = r;
+    r = times_x(r, g, P);
+  }
+  fp.bch_mfma.assign((size_t)fp.bch_nq * 4 * fp.bch_nt * 64 * 4, 0);
+  for (int q = 0; q < fp.bch_nq; q++)
+    for (int u = 0; u < 4; u++)
+      for (int t = 0; t < fp.bch_nt; t++)
+        for (int l = 0; l < 64; l++) {
+          const int p = 32 * t + (l & 31);
+          uint32_t *e4 = &fp.bch_mfma[((((size_t)q * 4 + u) * fp.bch_nt + t) * 64 + l) * 4];
+          for (int d = 0; d < 4; d++)
+            for (int e = 0; e < 8; e++) {
+              const int b = 32 * q + 16 * (l >> 5) + 4 * u + d, i = 8 * b + 7 - e;
+              if (i < fp.kbch && p < P && col[i].bit(P - 1 - p)) e4[d] |= 2u << (4 * e);
+            }
+        }
+  return 0;
+}
+
 // ============================================================================ QAM / bit interleaver
 // complex<float> *= complex<float> as libstdc++ performs it (no contraction)
 static cf32 cmul(cf32 a, cf32 b) {

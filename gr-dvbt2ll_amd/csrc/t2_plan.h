@@ -33,6 +33,11 @@ struct FecPlan {
   // per-lane chunk shift as nibble tables: entry [j][v][lane] (4 words, the 4th zero) =
   // v x^(4 j) x^(8 chunk (63 - lane)) mod g for nibble j < P/4, value v < 16, lane < 64
   std::vector<uint64_t> bch_ctab;
+  // the chain's BCH as a GF(2) matrix product on the matrix cores (bch_gemm_kernel): fp4 B
+  // fragments [32-byte message chunk q < bch_nq][K-step u < 4][parity tile t < bch_nt][lane][4
+  // dwords] of the parity-generator matrix (layout: build_bch_mfma)
+  int bch_nq = 0, bch_nt = 0;
+  std::vector<uint32_t> bch_mfma;
   std::vector<uint16_t> ldpc_rowptr;  // q + 1
   std::vector<uint32_t> ldpc_ent;     // (group << 16) | rotation, grouped by parity row
   std::vector<uint8_t> prbs_bytes;    // BB scrambler, kbch/8 bytes
@@ -41,6 +46,8 @@ struct FecPlan {
   std::vector<uint8_t> hcrc_bits;     // 72: BBHEADER CRC-8 contribution of each header bit
 };
 int build_fec(int framesize, int rate, int constellation, FecPlan &fp);
+// fp.bch_nq / bch_nt / bch_mfma for a plan built by build_fec (the fused chain only)
+int build_bch_mfma(FecPlan &fp);
 
 // ----------------------------------------------------------------------------- bit interleave + map
 enum MapMode { MAP_PAIRS = 0, MAP_TWIST2 = 1, MAP_TWIST1 = 2 };

@@ -90,6 +90,15 @@ int t2probe_bch(int framesize, int rate, int *info, uint64_t *tab, uint64_t *cta
   return 0;
 }
 
+// the chain's BCH matrix-core table: info [nq, nt]; tab nq x 4 x nt x 64 x 4 words
+int t2probe_bch_mfma(int framesize, int rate, int *info, uint32_t *tab) {
+  FecPlan fp;
+  if (build_fec(framesize, rate, 3, fp) || build_bch_mfma(fp)) return -1;
+  info[0] = fp.bch_nq; info[1] = fp.bch_nt;
+  if (tab) memcpy(tab, fp.bch_mfma.data(), fp.bch_mfma.size() * 4);
+  return 0;
+}
+
 // fused-chain layout: cmap Nsym x N (stored row order), inv S, sym_d0/sym_n Nsym;
 // info [Nsym, N, S, split]
 int t2probe_chain(const int *p20, const int *pg3, int *info, int32_t *cmap, uint16_t *inv, int32_t *d0,

@@ -28,6 +28,7 @@ def lib():
         L.t2probe_map.argtypes = [ctypes.c_int] * 4 + [vp, vp]
         L.t2probe_fec.argtypes = [ctypes.c_int] * 3 + [vp, vp, vp]
         L.t2probe_bch.argtypes = [ctypes.c_int] * 2 + [vp, vp, vp]
+        L.t2probe_bch_mfma.argtypes = [ctypes.c_int] * 2 + [vp, vp]
         L.t2probe_chain.argtypes = [vp] * 9
         L.t2probe_counts.argtypes = [ctypes.c_int] * 6 + [vp]
         L.t2probe_aux_lists.argtypes = [vp] * 9
@@ -122,6 +123,16 @@ def bch_tables(framesize, rate):
     ctab = np.zeros((P // 4) * 16 * 64 * 4, np.uint64)
     assert lib().t2probe_bch(framesize, rate, _p(info), _p(tab), _p(ctab)) == 0
     return dict(P=P, chunk=chunk, L=L, tab=tab.reshape(256, 3), ctab=ctab.reshape(P // 4, 16, 64, 4))
+
+
+def bch_mfma_table(framesize, rate):
+    """the chain's BCH matrix-core table (t2_plan build_bch_mfma): uint32 [nq][4][nt][64][4]"""
+    info = np.zeros(2, np.int32)
+    assert lib().t2probe_bch_mfma(framesize, rate, _p(info), None) == 0
+    nq, nt = (int(x) for x in info)
+    tab = np.zeros(nq * 4 * nt * 64 * 4, np.uint32)
+    assert lib().t2probe_bch_mfma(framesize, rate, _p(info), _p(tab)) == 0
+    return tab.reshape(nq, 4, nt, 64, 4)
 
 
 def ti_dest(plan, r, t):

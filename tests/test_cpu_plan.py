@@ -337,3 +337,48 @@ def test_bch_lane_shift_tables(framesize, rate):
         assert total == divide(msg)
         m = int.from_bytes(msg.tobytes(), "big")
         assert _gf2_mod((m << P) | total, g) == 0
+
+
+@pytest.mark.parametrize("framesize,rate", [(1, r) for r in range(6)] + [(0, r) for r in range(8)])
+def test_bch_matrix_core_table(framesize, rate):
+    """The chain's BCH pass (t2_kernels.hip bch_gemm_kernel) computes every block's parity as a GF(2)
+    matrix product on the matrix cores: fp4 A fragments spread from the message bytes, fp4 B fragments
+    from the planner table (build_bch_mfma), exact sums, parity = sum & 1, K split into 8 slices whose
+    partial parities are XORed.  Replayed here with the kernel's operand pairing (lane half h, element
+    j = 8 d + e: message byte 32 q + 16 h + 4 u + d, bit e; column = lane & 31 of tile t) on random
+    messages whose bytes past the BBFRAME are garbage (the kernel reads them and must ignore them);
+    the parities must equal the byte-table division of the message (bbheaderbch:504-531)."""
+    t = PP.bch_tables(framesize, rate)
+    P, L = t["P"], t["L"]
+    tabb = [int(a) | int(b) << 64 | int(c) << 128 for a, b, c in t["tab"]]
+    mask = (1 << P) - 1
+
+    def divide(msg):
+        r = 0
+        for byte in msg:
+            r = ((r << 8) & mask) ^ tabb[((r >> (P - 8)) & 0xFF) ^ int(byte)]
+        return r
+
+    tab = PP.bch_mfma_table(framesize, rate)
+    nq, nt = tab.shape[0], tab.shape[2]
+    assert nq == (L + 31) // 32 and nt == (P + 31) // 32
+    nib = (tab[..., None] >> (4 * np.arange(8, dtype=np.uint32))) & 0xF    # (nq, 4, nt, 64, 4, 8)
+    assert set(np.unique(nib)) <= {0, 2}
+    tb = (nib == 2).astype(np.int64).reshape(nq, 4, nt, 2, 32, 4, 8)       # lane = 32 h + c
+    rng = np.random.default_rng(2000 + 10 * framesize + rate)
+    for _ in range(2):
+        msg = rng.integers(0, 256, 32 * nq, dtype=np.uint8)                # garbage past L
+        mb = msg.reshape(nq, 2, 4, 4)                                       # [q][h][u][d]
+        bits = (mb[..., None] >> np.arange(8)) & 1                          # [q][h][u][d][e]
+        bits = bits.transpose(0, 2, 1, 3, 4).astype(np.int64)               # [q][u][h][d][e]
+        acc = np.einsum("quhde,quthcde->qtc", bits, tb)
+        bounds = [s * nq // 8 for s in range(9)]
+        par = np.zeros((nt, 32), np.int64)
+        for s in range(8):                                                  # XOR of slice partials
+            par ^= acc[bounds[s]:bounds[s + 1]].sum(axis=0) & 1
+        ref = divide(msg[:L])
+        got = 0
+        for p in range(P):
+            got |= int(par[p // 32, p % 32]) << (P - 1 - p)
+        assert got == ref
+        assert not par.reshape(-1)[P:].any()

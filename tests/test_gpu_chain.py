@@ -308,3 +308,39 @@ def test_chain_streams_rejects_bad_args(gpu):
     for stride, S, B in ((len(ts), 5, 1), (len(ts), 2, 3), (len(ts) - 1, 2, 1), (len(ts), 0, 1)):
         with pytest.raises(dvbt2ll.DVBT2Error):
             ch.run_streams(d.data_ptr(), stride, S, base, len(ts), 0, B, iq.data_ptr())
+
+
+from dvbt2ll import enums as E  # noqa: E402
+from test_gpu_blocks import ALL_CODES, MODES  # noqa: E402
+
+
+CW_CASES = [(m, i, E.MOD_16QAM) for m, i in MODES] + [(E.INPUTMODE_NORMAL, E.INBAND_OFF, E.MOD_QPSK)]
+
+
+@pytest.mark.parametrize("framesize,rate", ALL_CODES)
+@pytest.mark.parametrize("mode,inband,const", CW_CASES, ids=["nm", "hem", "nm-inband", "nm-qpsk"])
+def test_chain_codewords_all_codes(gpu, framesize, rate, mode, inband, const):
+    """the chain's FEC passes (BB pass, BCH on the matrix cores, LDPC pass) for every code x input
+    mode: the packed interleaver-input codewords of two frames equal the oracle's bbheaderbch + ldpc
+    output (info bits, then the parity interleaved [row a][column c] where the constellation has it)"""
+    import plan_probe as PP
+    cfg = CONFIGS["cfg4"].with_(framesize=framesize, rate=rate, inputmode=mode, inband=inband, constellation=const,
+                                fecblocks=3)
+    nb = 2 * cfg.fecblocks
+    ch = dvbt2ll.Chain(cfg, max_frames=2)
+    ch.run(0, 2)
+    got = ch.debug_codewords(nb)
+    ts, base = ts_for_frames(cfg, 0, 2)
+    assert base == 0
+    bits, _ = O.BB(*cfg.bb_args()).work(ts, nb)
+    fp = PP.fec_plan(framesize, rate, cfg.constellation)
+    nbch, q = fp["nbch"], fp["q"]
+    nldpc = 64800 if framesize else 16200
+    cw = O.LDPC(framesize, rate).work(bits, nb).reshape(nb, nldpc)
+    if fp["parity_il"]:
+        t, s = np.divmod(np.arange(nldpc - nbch), 360)
+        cw = cw.copy()
+        cw[:, nbch:] = cw[:, nbch + q * s + t]
+    want = np.packbits(cw, axis=1)
+    bad = np.nonzero((got[:, :nldpc // 8] != want).any(axis=1))[0]
+    assert bad.size == 0, ("blocks", bad.tolist())
