@@ -464,7 +464,8 @@ static PgParams to_pg(const dvbt2ll_pilotgenp1insert_params &p) {
 struct OfdmTables {
   DevBuf map, tw, tw1k, isinc, p1;
   OfdmDev dev{};
-  // stored_map: per-symbol rows in the kernel's read order (ofdm_stored_rows: natural order)
+  // stored_map: per-symbol rows in the kernel's read order (the chain: ofdm_stored_rows; the pilotgen
+  // block's gather mode: natural order)
   int init(const PilotPlan &pp, const std::vector<int32_t> &stored_map, int aux_len, int t2frames) {
     int r;
     if ((r = upload(map, stored_map))) return r;
@@ -502,7 +503,7 @@ extern "C" int dvbt2ll_pilotgenp1insert_create(const dvbt2ll_pilotgenp1insert_pa
   if (r) return r;
   std::vector<cf32> aux(PG_AUX_PAD, cf32{0.f, 0.f});
   for (int i = 0; i < 12; i++) aux[AUX_PILOT0 + i] = h->plan.pilot_values[i];
-  if ((r = h->ofdm.init(h->plan, ofdm_stored_rows(h->plan.N, h->plan.Nsym, h->plan.bin_map), PG_AUX_PAD, 1))) return r;
+  if ((r = h->ofdm.init(h->plan, h->plan.bin_map, PG_AUX_PAD, 1))) return r;   // gather rows: natural order
   if (h->din.ensure((size_t)(PG_AUX_PAD + h->plan.active) * 8)) return DVBT2LL_ENOMEM;
   HIP_TRY(hipMemcpy(h->din.p, aux.data(), PG_AUX_PAD * 8, hipMemcpyHostToDevice));
   h->out_items = h->plan.Nsym * (h->plan.N + h->plan.G) + 2048;

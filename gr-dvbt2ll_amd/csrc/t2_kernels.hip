@@ -723,6 +723,17 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_ldpc_kern
       uint32_t v;
       if (4 * i + 4 <= NB) {
         v = framew[i];
+      } else if (d.parity_il && 4 * i >= NB && 4 * i + 4 <= cwb) {
+        // four parity bytes m .. m + 3 (byte k of row a = m / 45, rows of 12 big-endian words)
+        int a = (4 * i - NB) / 45, k = 4 * i - NB - 45 * a;
+        v = 0;
+        for (int e = 0; e < 4; e++) {
+          v |= ((cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu) << (8 * e);
+          if (++k == 45) {
+            k = 0;
+            a++;
+          }
+        }
       } else {
         v = 0;
         for (int e = 0; e < 4; e++) {
@@ -1475,9 +1486,14 @@ struct BinSource {
 //   of (uint16 bin, uint16 index pair) and looked up in the constellation (QAM + rotated-Q
 //   delay).  Slots outside the run (quad edges) and padding bins go to a per-lane dummy slot.
 // The zero run is written separately by the caller.
-template <int NT, int SQ>
+struct NoWork {
+  __device__ __forceinline__ void operator()() const {}
+};
+// mid (32K): register work independent of the LDS, run once by every thread while its first round
+// of data-slot loads is in flight (after the loop when the run has no slots)
+template <int NT, int SQ, class Mid = NoWork>
 __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src, int g, uint32_t r0, uint32_t rn,
-                                              uint32_t dummy, int tid) {
+                                              uint32_t dummy, int tid, const Mid &mid = Mid()) {
   const int4 gr = src.agrp[g];
   for (uint32_t q = (uint32_t)tid; q < ((uint32_t)gr.y >> 2); q += NT) {
     const uint32_t e0 = (uint32_t)gr.x + 4u * q;
@@ -1499,13 +1515,18 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
     // octet (half the load instructions of quads; the pair rows are padded to a multiple of 8)
     const uint32_t o0 = r0 & ~7u, no = (r0 + rn - o0 + 7u) >> 3;
     const uint32_t lasto = no - 1u;
-    for (uint32_t g0 = 0; g0 < no; g0 += 2u * NT) {
+    bool pending = true;
+    for (uint32_t g0 = 0; g0 < no; g0 += 2u * NT) {   // (no is uniform: every thread runs the same rounds)
       uint4 b[2], c[2];
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const uint32_t s = o0 + 8u * min(g0 + (uint32_t)(tid + NT * u), lasto);
         b[u] = ld_off((const uint4 *)src.inv, s * 2u);
         c[u] = ld_off((const uint4 *)src.pairs, (src.cbase + s) * 2u);
+      }
+      if (pending) {
+        mid();
+        pending = false;
       }
 #pragma unroll
       for (int u = 0; u < 2; u++) {
@@ -1522,6 +1543,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
         }
       }
     }
+    if (pending) mid();
     return;
   }
   const uint32_t q0 = r0 & ~3u, nq = (r0 + rn - q0 + 3u) >> 2;
@@ -1884,14 +1906,31 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
 __device__ __forceinline__ uint32_t o32_ta(uint32_t t) { return ((t >> 4) & 15u) | (((t >> 8) & 1u) << 4); }
 __device__ __forceinline__ uint32_t o32_tb(uint32_t t) { return (t & 15u) | (((t >> 9) & 1u) << 4); }
 
-// stages A, B, C with the two exchanges: v[r] = bin kin + 1024 r on entry (kin = a + 32 b), sample
-// b + 32 a + 1024 r on exit.  Every thread is past its last LDS access of the symbol on return.
+// the last radix-2 stage of Dft<32> (len 32) from the DFT-16s of the even (e) and odd (o) inputs: the
+// same operations, in the same order per output, as Dft<32>::run, whose first four stages are the two
+// DFT-16s (after the 5-bit reversal, positions 0..15 hold the even inputs in 4-bit reversed order)
+__device__ __forceinline__ void dft32_combine(float2 *v, const float2 *e, const float2 *o) {
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const float2 a = e[k], b = o[k];
+    if (k == 8) {                                   // * i
+      v[8] = cadd_i(a, b);
+      v[24] = csub_i(a, b);
+      continue;
+    }
+    const float2 t = k == 0 ? b : cmulf(b, make_float2(kCos32[k], kSin32[k]));
+    v[k] = cadd(a, t);
+    v[k + 16] = csub(a, t);
+  }
+}
+
+// stages A (twiddle onwards), B, C with the two exchanges: v[r] = the stage-A DFT over m2 of bins
+// kin + 1024 r on entry (kin = a + 32 b), sample b + 32 a + 1024 r on exit.  Every thread is past its
+// last LDS access of the symbol on return.
 __device__ __forceinline__ void o32_fft(float2 *v, float2 *lds, const float2 *tw1k, const float2 *tw2, uint32_t tid,
                                         uint32_t ta, uint32_t tb) {
   const uint32_t kin = ta + 32u * tb;
-  // stage A: DFT over m2, twiddle w^((m0 + 32 m1) n2) = w^(kin r)
-  __builtin_amdgcn_sched_barrier(0);
-  Dft<32>::run(v);
+  // stage A: (DFT over m2, by the caller) twiddle w^((m0 + 32 m1) n2) = w^(kin r)
   o32_twiddle(v, [&](int k) {
     const uint32_t i = kin * (uint32_t)k;   // < 16384
     return cmulf(tw2[128 + (i >> 7)], tw2[i & 127u]);
@@ -1985,8 +2024,20 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   const float2 t1k = d.twiddle1k[tid];
   const float2 t2 = tid < 384 ? d.twiddle[tid] : make_float2(0.f, 0.f);
   float2 v[32];
+  // EQ (inverse sinc) of the bins kin + 1024 (S r + h), r < R (before the stage-A DFT)
+  auto eq = [&](float2 *x, int R, uint32_t S, uint32_t h) {
+    if (d.isinc) {
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const float sc = d.isinc[(kin + 1024u * (S * (uint32_t)r + h) + N / 2) & (N - 1)];
+        x[r].x *= sc;
+        x[r].y *= sc;
+      }
+    }
+  };
   if (d.inv) {
-    // scatter mode, one half of the bins (m2 < 16, then m2 >= 16) at a time
+    // scatter mode, one stored half at a time: the bins of even m2, then of odd m2 (t2_plan.h
+    // ofdm_stored_index); the even half's DFT-16 runs while the odd half's first loads are in flight
     float *qre = (float *)(smem + O32_QAM), *qim = qre + 256;
     const float2 tq = tid < 256 ? d.qam[tid] : make_float2(0.f, 0.f);
     BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv, io.pairs, qre, qim, (uint32_t)d.sym_d0[j], (uint32_t)d.sym_n[j],
@@ -1994,26 +2045,40 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     const uint32_t dummy = (uint32_t)(O32_H + (O32_H >> O32_PS)) + (uint32_t)(tid & 63);
     // (measured and dropped: both halves' scatter inputs prefetched into registers before the
     // first half is written, in one batch or half 1 behind half 0's arrival: +11 % kernel time)
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      if (h) __syncthreads();                     // half 0 read back before half 1 overwrites it
-      const int2 zr = src.azr[h];
+    float2 ev[16], od[16];                        // stage-A inputs m2 = 2 r, 2 r + 1
+    {
+      const int2 zr = src.azr[0];
       for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
-      if (h == 0) {
-        if (tid < 256) {
-          qre[tid] = tq.x;
-          qim[tid] = tq.y;
-        }
-        tw1k[tid] = t1k;
-        if (tid < 384) tw2[tid] = t2;
-        __syncthreads();                          // constellation visible to the scatter
+      if (tid < 256) {
+        qre[tid] = tq.x;
+        qim[tid] = tq.y;
       }
-      const uint32_t r0 = src.d0 + (h ? src.dn0 : 0u), rn = h ? src.dn - src.dn0 : src.dn0;
-      scatter_group<NT, 4>(lds, src, h, r0, rn, dummy, tid);
+      tw1k[tid] = t1k;
+      if (tid < 384) tw2[tid] = t2;
+      __syncthreads();                            // constellation visible to the scatter
+      scatter_group<NT, 4>(lds, src, 0, src.d0, src.dn0, dummy, tid);
       __syncthreads();
 #pragma unroll
-      for (uint32_t r = 0; r < 16; r++) v[16 * h + r] = lds[o32_bin(kin + 1024u * r)];
+      for (uint32_t r = 0; r < 16; r++) ev[r] = lds[o32_bin(kin + 1024u * r)];
     }
+    __syncthreads();                              // half 0 read back before half 1 overwrites it
+    {
+      const int2 zr = src.azr[1];
+      for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
+      auto dft_even = [&]() {
+        eq(ev, 16, 2u, 0u);
+        __builtin_amdgcn_sched_barrier(0);
+        Dft<16>::run(ev);
+      };
+      scatter_group<NT, 4>(lds, src, 1, src.d0 + src.dn0, src.dn - src.dn0, dummy, tid, dft_even);
+      __syncthreads();
+#pragma unroll
+      for (uint32_t r = 0; r < 16; r++) od[r] = lds[o32_bin(kin + 1024u * r)];
+    }
+    eq(od, 16, 2u, 1u);
+    __builtin_amdgcn_sched_barrier(0);
+    Dft<16>::run(od);
+    dft32_combine(v, ev, od);
   } else {
   tw1k[tid] = t1k;
   if (tid < 384) tw2[tid] = t2;
@@ -2029,14 +2094,9 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     for (int uu = 0; uu < 8; uu++) v[c0 + uu] = ld_off(data, off[uu]);
     __builtin_amdgcn_sched_barrier(0);
   }
-  }
-  if (d.isinc) {
-#pragma unroll
-    for (uint32_t r = 0; r < 32; r++) {
-      const float sc = d.isinc[(kin + 1024u * r + N / 2) & (N - 1)];
-      v[r].x *= sc;
-      v[r].y *= sc;
-    }
+  eq(v, 32, 1u, 0u);
+  __builtin_amdgcn_sched_barrier(0);
+  Dft<32>::run(v);
   }
   o32_fft(v, lds, tw1k, tw2, (uint32_t)tid, ta, tb);   // its first barrier publishes the tables
   const IqOut<FMT> o{(char *)io.out + ((int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + d.G)) * SB, d.gain};

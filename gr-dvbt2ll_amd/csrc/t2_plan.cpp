@@ -1129,12 +1129,13 @@ int build_pilot(const PgParams &p, PilotPlan &pp) {
   return 0;
 }
 
-// the OFDM kernels read every symbol row in natural FFT-input order (the 32K kernel's two halves
-// are bins < N/2 and >= N/2)
+// every symbol row of the fused chain in stored order (ofdm_stored_index)
 std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t> &bin_map) {
-  (void)N;
-  (void)Nsym;
-  return bin_map;
+  if (!ofdm_split(N)) return bin_map;
+  std::vector<int32_t> out(bin_map.size());
+  for (int j = 0; j < Nsym; j++)
+    for (int k = 0; k < N; k++) out[(size_t)j * N + ofdm_stored_index(N, k)] = bin_map[(size_t)j * N + k];
+  return out;
 }
 
 int64_t ti_dest(const FramePlan &fp, int r, int t) {

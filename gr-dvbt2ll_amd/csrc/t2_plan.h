@@ -146,6 +146,14 @@ int fft_points(int fftsize);
 // The OFDM kernels read the per-symbol map rows in IFFT-input order k; for N > 16384 the 32K
 // kernel fills its bins one half (k < N/2, then k >= N/2) at a time.
 inline bool ofdm_split(int N) { return N > 16384; }
+// The fused chain's stored bin order.  32K: the two halves the kernel fills one at a time are the
+// bins of even and of odd m2 = k >> 10 (k: natural FFT-input index), so the half read back first
+// holds the even inputs of every stage-A DFT-32, whose DFT-16 then runs beside the second half's
+// scatter.  Stored index s = h N/2 + kr with h = (k >> 10) & 1, kr = (k & 1023) | (k >> 11) << 10;
+// N <= 16K: s = k.  (The pilotgen block's gather rows stay in natural order.)
+inline int ofdm_stored_index(int N, int k) {
+  return ofdm_split(N) ? ((k >> 10) & 1) * (N / 2) + ((k & 1023) | ((k >> 11) << 10)) : k;
+}
 std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t> &bin_map);
 
 // Fused chain layout.  The map kernel writes each FEC block's cells through the cell and time

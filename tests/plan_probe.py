@@ -203,7 +203,15 @@ def l1post(fm_args, frame_idx, plan=True):
     return out
 
 
+def stored_index(N, split):
+    """natural FFT-input index k -> the chain's stored index (t2_plan.h ofdm_stored_index): 32K halves
+    are the bins of even / odd k >> 10"""
+    k = np.arange(N)
+    if not split:
+        return k
+    return ((k >> 10) & 1) * (N // 2) + ((k & 1023) | ((k >> 11) << 10))
+
+
 def stored_to_natural(row, N, split):
-    """the kernels' stored row order is the natural FFT-input order (32K: halves = bins < N/2 and
-    >= N/2, t2_plan ofdm_stored_rows)"""
-    return row
+    """a symbol row in the chain's stored order -> natural FFT-input order"""
+    return np.asarray(row)[stored_index(N, split)]

@@ -134,7 +134,7 @@ def test_chain_cell_layout_matches_oracle(name, over):
         row = np.where(code < 0, aux[np.clip(-code - 1, 0, None)], 0).astype(np.complex64)
         sl = np.arange(lay["d0"][j], lay["d0"][j] + lay["n"][j])
         assert (code[lay["inv"][sl]] >= 0).all()
-        if lay["split"]:   # the first n0 slots feed the bins < N/2, the rest the upper half
+        if lay["split"]:   # the first n0 slots feed stored half 0 (even k >> 10), the rest half 1
             n0 = lay["n0"][j]
             assert (lay["inv"][sl[:n0]] < N // 2).all() and (lay["inv"][sl[n0:]] >= N // 2).all()
         row[lay["inv"][sl]] = data[sl]
