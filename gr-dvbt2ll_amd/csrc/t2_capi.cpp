@@ -589,7 +589,7 @@ struct dvbt2ll_chain {
   // calls issued on different streams overlap; a slot reused on another stream first waits for
   // its previous run (slot_done) -- see dvbt2ll_chain_set_slots
   DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], pairs[DVBT2LL_CHAIN_MAX_SLOTS];
-  // BCH partial parities of the matrix-core pass (FecIO::bch_part): 8 K slices x blocks x 8 words
+  // BCH parities of the matrix-core pass (FecIO::bch_part): blocks x BCH_PART_WORDS
   DevBuf bpart[DVBT2LL_CHAIN_MAX_SLOTS];
   // per-frame L1-post cells of a run (l1post_kernel -> the OFDM kernel's indirect aux entries)
   L1Tables l1;
@@ -747,7 +747,7 @@ struct dvbt2ll_chain {
   }
   int alloc_slot(int k) {
     if (cw[k].ensure((size_t)frame.F * max_frames * cw_stride) ||
-        bpart[k].ensure((size_t)8 * frame.F * max_frames * 8 * sizeof(uint32_t)) ||
+        bpart[k].ensure((size_t)frame.F * max_frames * BCH_PART_WORDS * sizeof(uint32_t)) ||
         pairs[k].ensure((size_t)pair_stride * max_frames * 2) || l1buf[k].ensure((size_t)l1_stride * max_frames * 8))
       return DVBT2LL_ENOMEM;
     if (!slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
@@ -945,7 +945,7 @@ extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, i
   fio.blocks_per_stream = nstreams > 1 ? F * nframes : 0;
   fio.ts_stride = nstreams > 1 ? ts_stride : 0;
   fio.bch_part = h->bpart[slot].as<uint32_t>();
-  fio.bch_part_stride = (int64_t)F * h->max_frames;
+  fio.bch_part_blocks = (int64_t)F * h->max_frames;
   mio.in = cw.as<uint8_t>();
   mio.cw_stride = h->cw_stride;
   mio.out_pairs = pairs.as<uint16_t>();

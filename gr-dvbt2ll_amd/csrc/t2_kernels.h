@@ -12,6 +12,11 @@ enum FecMode {
   FEC_BITS_TO_BITS = 2,  // ldpc block: unpacked nbch bits -> unpacked nldpc bits (natural)
 };
 
+// the chain's BCH pass (bch_gemm_kernel): K slices (one per XCD: slice = blockIdx % 8); parity words
+// per block (the slices XOR their partial parities into them)
+constexpr int BCH_KS = 8;
+constexpr int BCH_PART_WORDS = 8;
+
 struct FecDev {
   const uint64_t *bch_tab;      // 256 x 3
   const uint64_t *bch_ctab;     // [P/4][16][64] x 4: lane shift nibble tables (FecPlan::bch_ctab)
@@ -40,10 +45,11 @@ struct FecIO {
   // b / blocks_per_stream, whose TS bytes start at in + stream * ts_stride (same ts_base, ts_len)
   int blocks_per_stream;
   int64_t ts_stride;
-  // chain (FEC_TS_TO_TEMPU): BCH partial parities of the matrix-core pass, 8 words per (K slice,
-  // block) at (slice * bch_part_stride + block) * 8 (bch_part_stride >= nblocks)
+  // chain (FEC_TS_TO_TEMPU): BCH parity of launch block b at bch_part + b * BCH_PART_WORDS (zeroed by
+  // the BB pass, XOR-accumulated by the K slices of the matrix-core pass, read by the LDPC pass;
+  // room for bch_part_blocks >= nblocks)
   uint32_t *bch_part;
-  int64_t bch_part_stride;
+  int64_t bch_part_blocks;
 };
 
 // ---------------------------------------------------------------- L1-post signalling (t2_plan.h L1PostPlan)

@@ -100,7 +100,8 @@ static hipError_t lds_limit(const void *fn, int bytes) {
 //                    in-band field, BB scrambling)
 //   bch_gemm_kernel  BCH parity of every block as a GF(2) matrix product on the matrix cores
 //                    (blocks x message bits x parity bits, fp4 0/1 operands, exact f32 sums, parity
-//                    = sum & 1), K split over the eight XCDs into XOR-able partial parities
+//                    = sum & 1), K split into slices (each XCD's L2 holds its slices' share of
+//                    the generator table) whose partial parities are XORed by the LDPC pass
 //   fec_ldpc_kernel  info bytes + XOR of the partials -> LDPC parity -> interleaver-input codeword
 constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
@@ -110,9 +111,7 @@ constexpr int FEC_WG_PER_CU = 7;        // fused kernel: resident workgroups per
 constexpr int FEC_PASS_WG_PER_CU = 8;   // chain BB / LDPC passes (64-VGPR budget, 32 waves per CU)
 constexpr int FEC_BCH_JB = 2;           // nibble-table lookups in flight per lane in the BCH combine
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
-constexpr int BCH_KS = 8;               // bch_gemm_kernel: K slices (one per XCD)
 constexpr int BCH_ROWS = 128;           // bch_gemm_kernel: FEC blocks per workgroup (4 waves x 32)
-constexpr int BCH_PART_WORDS = 8;       // partial parity words per (slice, block)
 
 // dynamic LDS carve (bytes) of each FEC kernel kind: persistent tables (staged once; the
 // workgroups loop over FEC blocks), then the per-block area, reused by phase:
@@ -121,7 +120,7 @@ constexpr int BCH_PART_WORDS = 8;       // partial parity words per (slice, bloc
 // sized for the plan's code, so a launch fits as many workgroups per CU as it allows
 enum FecCarveKind { CARVE_FUSED = 0, CARVE_BB = 1, CARVE_LDPC = 2 };
 struct FecCarve {
-  int btab, ents, hcrc, sync, w, frame, phase, crc8, crcsh, total;
+  int btab, ents, hcrc, sync, w, rowp, frame, phase, crc8, crcsh, total;
 };
 __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int q) {
   FecCarve c{};
@@ -132,6 +131,7 @@ __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int 
   c.hcrc = o; o += bb ? 80 : 0;            // 72 header-bit CRC contributions
   c.sync = o; o += bb ? 48 : 0;            // <= 36 sync-slot CRC-8s
   c.w = o; o += ldpc ? 48 : 0;             // 12 column-parity words
+  c.rowp = o; o += ldpc ? 192 : 0;         // q + 1 <= 91 LDPC row pointers
   c.frame = (o + 15) & ~15;
   c.phase = c.frame + ((nbch / 8 + 15) & ~15);
   c.crc8 = c.phase + ((188 + (kbch - 80) / 8 + 32 + 15) & ~15);   // + slack: 16-byte staging start
@@ -248,23 +248,34 @@ __device__ __forceinline__ void bch_wave(const uint8_t *frame, const uint64_t *b
 }
 
 // LDPC parity rows: row a, word w of p[a][c] = XOR over the row's entries (g, b) of the window
-// d_g[(c - b) mod 360], c = 32 w; 12 words per row at rowA
+// d_g[(c - b) mod 360], c = 32 w; 12 words per row at rowA.  One item = (row, 4 words): each entry is
+// read once for its four windows (3 q items, one round of the workgroup for q <= 85)
+__device__ __forceinline__ uint32_t ldpc_window(const uint32_t *dg, int o) {   // d_g bits [o, o + 32)
+  const uint64_t win = ((uint64_t)dg[o >> 5] << 32) | dg[(o >> 5) + 1];
+  return (uint32_t)(win >> (32 - (o & 31)));
+}
 __device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, const uint32_t *ents, const uint16_t *rp,
                                           int q, int t0, int nt) {
-  for (int it = t0; it < q * 12; it += nt) {
-    const int a = it / 12, w = it - a * 12;
-    uint32_t acc = 0;
-    for (int e = rp[a]; e < rp[a + 1]; e++) {
+  for (int it = t0; it < q * 3; it += nt) {
+    const int a = it / 3, w0 = 4 * (it - 3 * a);
+    uint32_t acc[4] = {0u, 0u, 0u, 0u};
+    const int e1 = rp[a + 1];
+#pragma unroll 2
+    for (int e = rp[a]; e < e1; e++) {
       const uint32_t ent = ents[e];
-      const int g = ent >> 16, b = ent & 0xFFFF;
-      int o = 32 * w - b;            // window start (c - b) mod 360 for c = 32 w
+      const uint32_t *dg = D + (ent >> 16) * FEC_DW;
+      int o = 32 * w0 - (int)(ent & 0xFFFF);   // window start (c - b) mod 360 for c = 32 w0
       o += o < 0 ? 360 : 0;
-      const uint32_t *dg = D + g * FEC_DW + (o >> 5);
-      const uint64_t win = ((uint64_t)dg[0] << 32) | dg[1];
-      acc ^= (uint32_t)(win >> (32 - (o & 31)));
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        acc[k] ^= ldpc_window(dg, o);
+        o += 32;
+        o -= o >= 360 ? 360 : 0;
+      }
     }
-    if (w == 11) acc &= 0xFF000000u;
-    rowA[it] = acc;
+    if (w0 == 8) acc[3] &= 0xFF000000u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) rowA[12 * a + w0 + k] = acc[k];
   }
 }
 
@@ -273,10 +284,10 @@ __device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, con
 // per DPP wave scan plus the carry of the previous 64), then the exclusive bit-prefix of the column
 // parities along c.  Leaves p[a][c] at D + ngroups * FEC_DW (row a, 12 big-endian words).
 __device__ __forceinline__ uint32_t *fec_ldpc(const FecDev &d, uint32_t *D, int ngroups, const uint32_t *ents,
-                                              uint32_t *Wv, int tid) {
+                                              const uint16_t *rowp, uint32_t *Wv, int tid) {
   const int lane = tid & 63, wave = tid >> 6, q = d.q;
   uint32_t *cur = D + ngroups * FEC_DW;
-  ldpc_rows(D, cur, ents, d.ldpc_rowptr, q, tid, FEC_THREADS);
+  ldpc_rows(D, cur, ents, rowp, q, tid, FEC_THREADS);
   __syncthreads();
   for (int col = 3 * wave; col < 3 * wave + 3; col++) {
     uint32_t carry = 0;
@@ -289,18 +300,14 @@ __device__ __forceinline__ uint32_t *fec_ldpc(const FecDev &d, uint32_t *D, int 
     }
   }
   __syncthreads();
-  if (tid == 0) {
-    uint32_t carry = 0;
-    for (int w = 0; w < 12; w++) {
-      uint32_t x = cur[(q - 1) * 12 + w];
-      uint32_t y = x;
-      y ^= y >> 1; y ^= y >> 2; y ^= y >> 4; y ^= y >> 8; y ^= y >> 16;
-      uint32_t ex = y ^ x;
-      if (carry) ex = ~ex;
-      Wv[w] = ex;
-      carry ^= y & 1;
-    }
-    Wv[11] &= 0xFF000000u;
+  if (tid < 64) {   // word w of the last row by lane w < 12: in-word prefix, carry = parity of words < w
+    const uint32_t x = tid < 12 ? cur[(q - 1) * 12 + tid] : 0u;
+    uint32_t y = x;
+    y ^= y >> 1; y ^= y >> 2; y ^= y >> 4; y ^= y >> 8; y ^= y >> 16;
+    const uint32_t p = y & 1u, carry = wave_prefix_xor(p) ^ p;
+    uint32_t ex = y ^ x;
+    if (carry) ex = ~ex;
+    if (tid < 12) Wv[tid] = tid == 11 ? ex & 0xFF000000u : ex;
   }
   __syncthreads();
   for (int it = tid; it < q * 12; it += FEC_THREADS) cur[it] ^= Wv[it % 12];
@@ -313,57 +320,77 @@ __device__ __forceinline__ uint32_t *fec_ldpc(const FecDev &d, uint32_t *D, int 
 // sync-slot CRC-8s, BBHEADER + its CRC-8, payload words, the in-band field, BB scrambling.  Ends
 // with a barrier.  crc_resident: the CRC-8 tables already sit at cv.crc8 / cv.crcsh (the BB pass
 // stages them once; the fused kernel's LDPC area overlays them, so it reloads them per block).
-template <bool CRC_RESIDENT>
+// BBFRAME geometry of absolute FEC block B, closed form (the reference keeps count / crc / fec_block
+// as running state, bbheader:661-734).  NM: the raw stream bytes [pos0 - 188, pos0 + npay) are staged
+// as nq 16-byte units from the aligned stream offset 16 w0 (raw byte i = stream byte rs + i at LDS
+// byte phase + delta + i)
+struct BbGeom {
+  int64_t J0, pos0, w0;
+  int npay, padding, count0, delta, nq;
+};
+__device__ __forceinline__ BbGeom bb_geom(const FecDev &d, const FecIO &io, int64_t B) {
+  BbGeom g;
+  const int pay_full = (d.kbch - 80) >> 3;
+  int64_t npad_before = 0;
+  g.padding = 0;
+  if (d.inband) {
+    npad_before = (B + d.fec_blocks - 1) / d.fec_blocks;
+    g.padding = (B % d.fec_blocks) == 0 ? 104 : 0;
+  }
+  g.npay = (d.kbch - 80 - g.padding) >> 3;
+  g.J0 = B * pay_full - 13 * npad_before;
+  g.pos0 = payload_pos(g.J0, d.hem);
+  // TS packet position of the next input byte at block start
+  if (d.hem) g.count0 = g.J0 == 0 ? 0 : (int)((payload_pos(g.J0 - 1, 1) + 1) % 188);
+  else g.count0 = (int)(g.pos0 % 188);
+  const int64_t rel = g.pos0 - 188 - io.ts_base;        // >= -188
+  g.w0 = (rel >= 0 ? rel : rel - 15) / 16;              // floor
+  g.delta = (int)(rel - 16 * g.w0);
+  g.nq = (g.delta + g.npay + 188 + 15) >> 4;
+  return g;
+}
+// raw unit i (16 stream bytes at offset 16 (w0 + i) of the TS buffer): one 16-byte load, or byte
+// loads for a misaligned buffer or at the stream edges (zeros outside)
+__device__ __forceinline__ uint4 bb_raw_unit(const FecIO &io, const uint8_t *tin, int64_t w0, int i) {
+  const int64_t b = 16 * (w0 + i);
+  if ((((uintptr_t)tin) & 15) == 0 && b >= 0 && b + 16 <= io.ts_len) return *(const uint4 *)(tin + b);
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  for (int e = 0; e < 16; e++)
+    if (b + e >= 0 && b + e < io.ts_len) w[e >> 2] |= (uint32_t)tin[b + e] << (8 * (e & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+constexpr int FEC_PRE = 2;   // raw units per thread a BB pass workgroup prefetches for its next block (nq <= 512)
+
+template <bool CRC_RESIDENT, bool PRE>
 __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv, unsigned char *smem, int64_t B,
-                            const uint8_t *tin, int tid) {
+                            const uint8_t *tin, int tid, const uint4 *pre = nullptr) {
   const int lane = tid & 63, wave = tid >> 6;
   const int L = d.kbch >> 3;
   uint8_t *frame = smem + cv.frame, *phase = smem + cv.phase;
   uint8_t *crc8 = smem + cv.crc8, *crcsh = smem + cv.crcsh;
   const uint8_t *hcrc8 = smem + cv.hcrc;
   uint8_t *syncv = smem + cv.sync;
-  const int pay_full = (d.kbch - 80) >> 3;
-  int64_t npad_before = 0;
-  int padding = 0;
-  if (d.inband) {
-    npad_before = (B + d.fec_blocks - 1) / d.fec_blocks;
-    padding = (B % d.fec_blocks) == 0 ? 104 : 0;
-  }
-  const int npay = (d.kbch - 80 - padding) >> 3;
-  const int64_t J0 = B * pay_full - 13 * npad_before;
-  const int64_t pos0 = payload_pos(J0, d.hem);
-  int count0;   // TS packet position of the next input byte at block start
-  if (d.hem) count0 = J0 == 0 ? 0 : (int)((payload_pos(J0 - 1, 1) + 1) % 188);
-  else count0 = (int)(pos0 % 188);
-  // NM: stage the raw stream bytes [pos0 - 188, pos0 + npay) once with 16-byte loads from a
-  // 16-byte aligned start (raw byte i = stream byte rs + i lives at LDS byte cv.phase + delta + i);
-  // the CRC-8 chains and the payload words then read LDS
+  const BbGeom g = bb_geom(d, io, B);
+  const int npay = g.npay, padding = g.padding, count0 = g.count0;
+  const int64_t J0 = g.J0, pos0 = g.pos0;
+  // NM: stage the raw stream bytes once (PRE: the units this thread prefetched, unit tid + 256 k in
+  // pre[k]); the CRC-8 chains and the payload words then read LDS
   const int64_t rs = pos0 - 188;
   int delta = 0, first_slot = 0;
   const uint32_t *raww = (const uint32_t *)phase;
   if (!d.hem) {
-    const int64_t rel = rs - io.ts_base;                 // >= -188
     if (!CRC_RESIDENT) {
       for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)crc8)[i] = ((const uint32_t *)d.crc8_tab)[i];
       for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)crcsh)[i] = ((const uint32_t *)d.crc8_shift)[i];
     }
-    const int64_t w0 = (rel >= 0 ? rel : rel - 15) / 16;   // floor
-    delta = (int)(rel - 16 * w0);
-    const int nq = (delta + npay + 188 + 15) >> 4;
+    delta = g.delta;
     uint4 *rawq = (uint4 *)phase;
-    const bool aligned = (((uintptr_t)tin) & 15) == 0;
-    for (int i = tid; i < nq; i += FEC_THREADS) {
-      const int64_t b = 16 * (w0 + i);
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (aligned && b >= 0 && b + 16 <= io.ts_len) {
-        v = *(const uint4 *)(tin + b);
-      } else {   // misaligned buffer or stream edge: byte loads
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        for (int e = 0; e < 16; e++)
-          if (b + e >= 0 && b + e < io.ts_len) w[e >> 2] |= (uint32_t)tin[b + e] << (8 * (e & 3));
-        v = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-      rawq[i] = v;
+    if (PRE) {
+#pragma unroll
+      for (int k = 0; k < FEC_PRE; k++)
+        if (tid + FEC_THREADS * k < g.nq) rawq[tid + FEC_THREADS * k] = pre[k];
+    } else {
+      for (int i = tid; i < g.nq; i += FEC_THREADS) rawq[i] = bb_raw_unit(io, tin, g.w0, i);
     }
     const uint8_t *raw = phase + delta;
     __syncthreads();
@@ -497,13 +524,14 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
     for (int i = tid; i < 72; i += FEC_THREADS) smem[cv.hcrc + i] = d.hcrc_bits[i];
   } else {
     for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
+    for (int i = tid; i <= d.q; i += FEC_THREADS) ((uint16_t *)(smem + cv.rowp))[i] = d.ldpc_rowptr[i];
   }
   __syncthreads();
   for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
     if (MODE == FEC_TS_TO_BITS) {
       const uint8_t *tin;
       const int64_t B = fec_block_of(io, bi, tin);
-      fec_bbframe<false>(d, io, cv, smem, B, tin, tid);
+      fec_bbframe<false, false>(d, io, cv, smem, B, tin, tid);
       // BCH on wave 0 (raised issue priority: the block's critical path)
       if (wave == 0) {
         __builtin_amdgcn_s_setprio(1);
@@ -536,7 +564,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
         ldpc_group_word(D, frame, g, it - g * FEC_DW);
       }
       __syncthreads();
-      const uint32_t *cur = fec_ldpc(d, D, ngroups, ents, (uint32_t *)(smem + cv.w), tid);
+      const uint32_t *cur = fec_ldpc(d, D, ngroups, ents, (const uint16_t *)(smem + cv.rowp), (uint32_t *)(smem + cv.w), tid);
       const int q = d.q;
       uint8_t *dst = io.out + (int64_t)bi * d.nldpc;
       for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
@@ -563,12 +591,27 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel
   for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)(smem + cv.crcsh))[i] = ((const uint32_t *)d.crc8_shift)[i];
   __syncthreads();
   const uint4 *framq = (const uint4 *)(smem + cv.frame);
+  // NM: each block's raw TS units are requested one block ahead (in flight during the previous block)
+  uint4 pre[FEC_PRE];
+  auto prefetch = [&](int b) {
+    const uint8_t *tn;
+    const BbGeom gn = bb_geom(d, io, fec_block_of(io, b, tn));
+#pragma unroll
+    for (int k = 0; k < FEC_PRE; k++)
+      pre[k] = tid + FEC_THREADS * k < gn.nq ? bb_raw_unit(io, tn, gn.w0, tid + FEC_THREADS * k) : make_uint4(0u, 0u, 0u, 0u);
+  };
+  if (!d.hem && (int)blockIdx.x < io.nblocks) prefetch(blockIdx.x);
   for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
     const uint8_t *tin;
     const int64_t B = fec_block_of(io, bi, tin);
-    fec_bbframe<true>(d, io, cv, smem, B, tin, tid);
+    uint4 cur[FEC_PRE];
+#pragma unroll
+    for (int k = 0; k < FEC_PRE; k++) cur[k] = pre[k];
+    if (!d.hem && bi + (int)gridDim.x < io.nblocks) prefetch(bi + gridDim.x);
+    fec_bbframe<true, true>(d, io, cv, smem, B, tin, tid, cur);
     uint4 *dst = (uint4 *)(io.out + (int64_t)bi * io.cw_stride);
     for (int i = tid; i < (L + 15) >> 4; i += FEC_THREADS) dst[i] = framq[i];
+    if (tid < BCH_PART_WORDS) io.bch_part[(int64_t)bi * BCH_PART_WORDS + tid] = 0u;   // the BCH pass XORs into it
     __syncthreads();   // the frame is rebuilt by the next block
   }
 }
@@ -576,23 +619,16 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel
 // ---- chain pass 2: BCH as a GF(2) matrix product on the matrix cores
 typedef int bch_v8i __attribute__((ext_vector_type(8)));
 typedef float bch_v16f __attribute__((ext_vector_type(16)));
-// message bits 0..7 of x -> fp4 (e2m1) nibbles 0..7, 0x2 (1.0) where set
-__device__ __forceinline__ uint32_t fp4_spread(uint32_t x) {
-  x &= 0xFFu;
-  x = (x | (x << 12)) & 0x000F000Fu;
-  x = (x | (x << 6)) & 0x03030303u;
-  x = (x | (x << 3)) & 0x11111111u;
-  return x << 1;
-}
 
 // Workgroup (tile, slice): 128 FEC blocks (wave w: blocks 32 w .. 32 w + 31 of the tile, one per
 // A row) x all bch_nt parity tiles, over the 32-byte message chunks q of K slice `slice` (slice =
 // blockIdx % 8, so each XCD's L2 holds one eighth of the generator table).  Per chunk: the B
 // fragments (t2_plan build_bch_mfma) are staged in LDS (double-buffered, one barrier per chunk),
-// each lane loads 16 message bytes of its block and spreads them into four A fragments, and each
-// wave issues 4 x NT v_mfma_scale_f32_32x32x64_f8f6f4 (fp4 A and B, unit E8M0 scales).  Sums are
+// each lane loads 16 message bytes of its block (four K-steps of 32 bits) and masks each word into
+// an A fragment, and each wave issues 4 x NT v_mfma_scale_f32_32x32x64_f8f6f4 (fp4 A and B; E8M0
+// scales 2 for A, 1 for B).  Sums are
 // exact small integers in f32; the partial parity of the slice is (int) sum & 1, packed by wave
-// ballots into 8 words per block (bytes in transmission order) at bch_part[(slice * stride + b) * 8].
+// ballots into 8 words per block (bytes in transmission order), XORed into bch_part[b * 8].
 template <int NT>
 __global__ __launch_bounds__(FEC_THREADS, 3) void bch_gemm_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) uint4 bsm[];
@@ -632,18 +668,29 @@ __global__ __launch_bounds__(FEC_THREADS, 3) void bch_gemm_kernel(FecDev d, FecI
       if (live) an = msg[2 * (q + 1)];
     }
     const uint4 *bq = bsm + cur * PER;
+    // B fragments of K-step u + 1 requested before the MFMAs of step u (two steps' fragments live)
+    uint4 bc[NT], bx[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) bc[t] = bq[t * 64 + lane];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
+      if (u < 3) {
+#pragma unroll
+        for (int t = 0; t < NT; t++) bx[t] = bq[((u + 1) * NT + t) * 64 + lane];
+      }
+      // A fragment: dword d = bits d, d + 4, .. of the message word as fp4 nibbles 0x1 (0.5; the A
+      // scale 2^1 makes them 1.0): two VALU ops per dword
       const uint32_t w = u == 0 ? a.x : u == 1 ? a.y : u == 2 ? a.z : a.w;
-      const bch_v8i A = {(int)fp4_spread(w), (int)fp4_spread(w >> 8), (int)fp4_spread(w >> 16),
-                         (int)fp4_spread(w >> 24), 0, 0, 0, 0};
+      const bch_v8i A = {(int)(w & 0x11111111u), (int)((w >> 1) & 0x11111111u), (int)((w >> 2) & 0x11111111u),
+                         (int)((w >> 3) & 0x11111111u), 0, 0, 0, 0};
 #pragma unroll
       for (int t = 0; t < NT; t++) {
-        const uint4 b = bq[(u * NT + t) * 64 + lane];
-        const bch_v8i Bv = {(int)b.x, (int)b.y, (int)b.z, (int)b.w, 0, 0, 0, 0};
-        acc[t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, Bv, acc[t], 4, 4, 0, 127, 0, 127);
+        const bch_v8i Bv = {(int)bc[t].x, (int)bc[t].y, (int)bc[t].z, (int)bc[t].w, 0, 0, 0, 0};
+        acc[t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, Bv, acc[t], 4, 4, 0, 128, 0, 127);
       }
-      __builtin_amdgcn_sched_barrier(0);   // one K-step's B fragments in registers at a time
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < NT; t++) bc[t] = bx[t];
     }
     __syncthreads();
     a = an;
@@ -666,12 +713,11 @@ __global__ __launch_bounds__(FEC_THREADS, 3) void bch_gemm_kernel(FecDev d, FecI
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   for (int i = lane; i < 32 * BCH_PART_WORDS; i += 64) {
     const int row = i / BCH_PART_WORDS, t = i % BCH_PART_WORDS;
-    if (row0 + row < io.nblocks)
-      io.bch_part[((int64_t)slice * io.bch_part_stride + row0 + row) * BCH_PART_WORDS + t] = t < NT ? pw[i] : 0u;
+    if (t < NT && row0 + row < io.nblocks) atomicXor(&io.bch_part[(int64_t)(row0 + row) * BCH_PART_WORDS + t], pw[i]);
   }
 }
 
-// chain pass 3: info bytes [0, L) from the codeword row + the BCH parity (XOR of the BCH_KS partials),
+// chain pass 3: info bytes [0, L) from the codeword row + the BCH parity (the XOR of the K slices),
 // the info groups laid out, LDPC, then the interleaver-input words from word L / 4 on (the BB pass
 // wrote the words before): BCH parity | LDPC parity (parity interleaved: byte m = byte m % 45 of row
 // m / 45, or natural order a + q c for QPSK without parity interleaving)
@@ -684,18 +730,31 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_ldpc_kern
   uint32_t *ents = (uint32_t *)(smem + cv.ents);
   uint32_t *D = (uint32_t *)(smem + cv.phase);
   uint32_t *Wv = (uint32_t *)(smem + cv.w);
+  uint16_t *rowp = (uint16_t *)(smem + cv.rowp);
   for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
+  for (int i = tid; i <= d.q; i += FEC_THREADS) rowp[i] = d.ldpc_rowptr[i];
   __syncthreads();
-  const int ngroups = d.nbch / 360, q = d.q, cwb = d.nldpc >> 3;
+  const int ngroups = d.nbch / 360, q = d.q, cwb = d.nldpc >> 3, nqi = (L + 15) >> 4;
+  // each block's info units and BCH partials are requested one block ahead (in flight during the
+  // previous block)
+  uint4 pre[FEC_PRE];
+  uint32_t ppar = 0;
+  auto prefetch = [&](int b) {
+    const uint4 *rowq = (const uint4 *)(io.out + (int64_t)b * io.cw_stride);
+#pragma unroll
+    for (int k = 0; k < FEC_PRE; k++)
+      pre[k] = tid + FEC_THREADS * k < nqi ? rowq[tid + FEC_THREADS * k] : make_uint4(0u, 0u, 0u, 0u);
+    if (tid < (PB + 3) >> 2) ppar = io.bch_part[(int64_t)b * BCH_PART_WORDS + tid];
+  };
+  if ((int)blockIdx.x < io.nblocks) prefetch(blockIdx.x);
   for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
     uint8_t *row = io.out + (int64_t)bi * io.cw_stride;
-    for (int i = tid; i < (L + 15) >> 4; i += FEC_THREADS) ((uint4 *)frame)[i] = ((const uint4 *)row)[i];
-    uint32_t par = 0;
-    if (tid < (PB + 3) >> 2) {
 #pragma unroll
-      for (int s = 0; s < BCH_KS; s++) par ^= io.bch_part[((int64_t)s * io.bch_part_stride + bi) * BCH_PART_WORDS + tid];
-    }
-    __syncthreads();   // the 16-byte loads past L land before the parity bytes overwrite them
+    for (int k = 0; k < FEC_PRE; k++)
+      if (tid + FEC_THREADS * k < nqi) ((uint4 *)frame)[tid + FEC_THREADS * k] = pre[k];
+    const uint32_t par = ppar;
+    if (bi + (int)gridDim.x < io.nblocks) prefetch(bi + gridDim.x);
+    __syncthreads();   // the 16-byte units past L land before the parity bytes overwrite them
     if (tid < (PB + 3) >> 2)
       for (int k = 0; k < 4 && 4 * tid + k < PB; k++) frame[L + 4 * tid + k] = (uint8_t)(par >> (8 * k));
     __syncthreads();
@@ -704,7 +763,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_ldpc_kern
       ldpc_group_word(D, frame, g, it - g * FEC_DW);
     }
     __syncthreads();
-    const uint32_t *cur = fec_ldpc(d, D, ngroups, ents, Wv, tid);
+    const uint32_t *cur = fec_ldpc(d, D, ngroups, ents, rowp, Wv, tid);
     auto parity_byte = [&](int m) -> uint32_t {
       if (d.parity_il) {
         const int a = m / 45, k = m - 45 * a;
@@ -764,6 +823,7 @@ static int fec_grid(int nblocks, int per_cu) {
 static bool fec_plan_fits(const FecDev &d) {
   // the LDS carve is sized for the standard codes, the BCH wave for 64 chunks: refuse anything else
   return !(d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 52 * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
+           (d.kbch - 80) / 8 + 218 > 16 * FEC_PRE * FEC_THREADS || ((d.kbch >> 3) + 15) / 16 > FEC_PRE * FEC_THREADS ||
            (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.chunk * 64 < d.kbch / 8);
 }
 
@@ -794,7 +854,7 @@ hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s)
   hipError_t e;
   switch (mode) {
     case FEC_TS_TO_TEMPU:   // the fused chain: BB pass, BCH on the matrix cores, LDPC pass
-      if (!d.bch_mfma || !io.bch_part || io.bch_part_stride < io.nblocks || d.bch_nt < 4 || d.bch_nt > 6 ||
+      if (!d.bch_mfma || !io.bch_part || io.bch_part_blocks < io.nblocks || d.bch_nt < 4 || d.bch_nt > 6 ||
           d.bch_nq < 1 || d.bch_nq * 32 > io.cw_stride)
         return hipErrorInvalidValue;
       e = fec_launch_persistent((const void *)fec_bb_kernel, CARVE_BB, FEC_PASS_WG_PER_CU, d, io, s);

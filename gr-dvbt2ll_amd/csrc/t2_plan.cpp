@@ -233,9 +233,11 @@ int build_bch_mfma(FecPlan &fp) {
   // BCH as a GF(2) matrix product for the chain's MFMA pass (bch_gemm_kernel): parity bit p (p = 0
   // the x^(P-1) coefficient, sent first) of message bit i is coefficient P-1-p of x^(kbch-1-i) x^P
   // mod g.  fp4 (e2m1) B fragments of v_mfma_scale_f32_32x32x64_f8f6f4: 32-byte message chunk q,
-  // K-step u (its 4-byte word), parity tile t, lane l, dword d, nibble e <-> message byte
-  // b = 32 q + 16 (l >> 5) + 4 u + d, bit e (LSB first, i = 8 b + 7 - e), parity p = 32 t + (l & 31);
-  // nibble 0x2 (1.0) where G[i][p] = 1.  Bits past kbch and parities past P are zero.
+  // K-step u (the little-endian message word w of bytes 32 q + 16 (l >> 5) + 4 u .. + 3), parity tile
+  // t, lane l, dword d, nibble e <-> bit 4 e + d of w (the A fragment's dword d is (w >> d) & 0x11111111),
+  // i.e. message byte b = 32 q + 16 (l >> 5) + 4 u + (4 e + d) / 8, bit (4 e + d) % 8 (LSB first:
+  // i = 8 b + 7 - (4 e + d) % 8), parity p = 32 t + (l & 31); nibble 0x2 (1.0) where G[i][p] = 1.
+  // Bits past kbch and parities past P are zero.
   fp.bch_nq = (L + 31) / 32;
   fp.bch_nt = (P + 31) / 32;
   std::vector<Poly192> col(fp.kbch);
@@ -255,7 +257,7 @@ int build_bch_mfma(FecPlan &fp) {
           uint32_t *e4 = &fp.bch_mfma[((((size_t)q * 4 + u) * fp.bch_nt + t) * 64 + l) * 4];
           for (int d = 0; d < 4; d++)
             for (int e = 0; e < 8; e++) {
-              const int b = 32 * q + 16 * (l >> 5) + 4 * u + d, i = 8 * b + 7 - e;
+              const int wb = 4 * e + d, b = 32 * q + 16 * (l >> 5) + 4 * u + wb / 8, i = 8 * b + 7 - wb % 8;
               if (i < fp.kbch && p < P && col[i].bit(P - 1 - p)) e4[d] |= 2u << (4 * e);
             }
         }

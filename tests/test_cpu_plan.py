@@ -342,10 +342,11 @@ def test_bch_lane_shift_tables(framesize, rate):
 @pytest.mark.parametrize("framesize,rate", [(1, r) for r in range(6)] + [(0, r) for r in range(8)])
 def test_bch_matrix_core_table(framesize, rate):
     """The chain's BCH pass (t2_kernels.hip bch_gemm_kernel) computes every block's parity as a GF(2)
-    matrix product on the matrix cores: fp4 A fragments spread from the message bytes, fp4 B fragments
-    from the planner table (build_bch_mfma), exact sums, parity = sum & 1, K split into 8 slices whose
-    partial parities are XORed.  Replayed here with the kernel's operand pairing (lane half h, element
-    j = 8 d + e: message byte 32 q + 16 h + 4 u + d, bit e; column = lane & 31 of tile t) on random
+    matrix product on the matrix cores: fp4 A fragments masked from the message words, fp4 B fragments
+    from the planner table (build_bch_mfma), exact sums, parity = sum & 1, K split into slices whose
+    partial parities are XORed (BCH_KS = 8).  Replayed here with the kernel's operand pairing (lane half h,
+    K-step u, A dword d, nibble e: bit 4 e + d of the little-endian word of message bytes 32 q + 16 h + 4 u
+    .. + 3; column = lane & 31 of tile t) on random
     messages whose bytes past the BBFRAME are garbage (the kernel reads them and must ignore them);
     the parities must equal the byte-table division of the message (bbheaderbch:504-531)."""
     t = PP.bch_tables(framesize, rate)
@@ -368,9 +369,10 @@ def test_bch_matrix_core_table(framesize, rate):
     rng = np.random.default_rng(2000 + 10 * framesize + rate)
     for _ in range(2):
         msg = rng.integers(0, 256, 32 * nq, dtype=np.uint8)                # garbage past L
-        mb = msg.reshape(nq, 2, 4, 4)                                       # [q][h][u][d]
-        bits = (mb[..., None] >> np.arange(8)) & 1                          # [q][h][u][d][e]
-        bits = bits.transpose(0, 2, 1, 3, 4).astype(np.int64)               # [q][u][h][d][e]
+        words = msg.view("<u4").reshape(nq, 2, 4).astype(np.int64)         # [q][h][u] message words
+        sh = 4 * np.arange(8)[None, :] + np.arange(4)[:, None]              # [d][e] -> bit 4 e + d
+        bits = (words[..., None, None] >> sh) & 1                           # [q][h][u][d][e]
+        bits = bits.transpose(0, 2, 1, 3, 4)                                # [q][u][h][d][e]
         acc = np.einsum("quhde,quthcde->qtc", bits, tb)
         bounds = [s * nq // 8 for s in range(9)]
         par = np.zeros((nt, 32), np.int64)
