@@ -620,100 +620,108 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel
 typedef int bch_v8i __attribute__((ext_vector_type(8)));
 typedef float bch_v16f __attribute__((ext_vector_type(16)));
 
-// Workgroup (tile, slice): 128 FEC blocks (wave w: blocks 32 w .. 32 w + 31 of the tile, one per
-// A row) x all bch_nt parity tiles, over the 32-byte message chunks q of K slice `slice` (slice =
-// blockIdx % 8, so each XCD's L2 holds one eighth of the generator table).  Per chunk: the B
-// fragments (t2_plan build_bch_mfma) are staged in LDS (double-buffered, one barrier per chunk),
-// each lane loads 16 message bytes of its block (four K-steps of 32 bits) and masks each word into
-// an A fragment, and each wave issues 4 x NT v_mfma_scale_f32_32x32x64_f8f6f4 (fp4 A and B; E8M0
-// scales 2 for A, 1 for B).  Sums are
-// exact small integers in f32; the partial parity of the slice is (int) sum & 1, packed by wave
-// ballots into 8 words per block (bytes in transmission order), XORed into bch_part[b * 8].
+// Persistent workgroups, BCH_WG_PER_CU per CU.  Workgroup i serves K slice i % 8 (its XCD: that
+// XCD's L2 holds one eighth of the generator table) and a contiguous, equal share of the slice's
+// (tile, chunk) units, tile-major: a tile is 128 FEC blocks (wave w: blocks 32 w .. 32 w + 31, one per
+// A row) x all bch_nt parity tiles, a chunk 32 message bytes = four K-steps of 64 bits.  Per chunk
+// the B fragments (t2_plan build_bch_mfma) are staged in LDS (double-buffered LDS-DMA, one barrier per
+// chunk), each lane loads 16 message bytes of its block and masks each 32-bit word into an A
+// fragment, and each wave issues 4 x NT v_mfma_scale_f32_32x32x64_f8f6f4 (fp4 A and B; E8M0 scales 2
+// for A, 1 for B).  Sums are exact small integers in f32; at the end of each tile segment the partial
+// parity ((int) sum & 1) is packed by wave ballots into 8 words per block (bytes in transmission
+// order) and XORed into bch_part[b * 8] (zeroed by the BB pass).
+constexpr int BCH_WG_PER_CU = 3;
 template <int NT>
-__global__ __launch_bounds__(FEC_THREADS, 3) void bch_gemm_kernel(FecDev d, FecIO io) {
+__global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) uint4 bsm[];
   constexpr int PER = 4 * NT * 64;                   // uint4 per chunk buffer
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int slice = (int)blockIdx.x % BCH_KS, tile = (int)blockIdx.x / BCH_KS;
-  const int q0 = slice * d.bch_nq / BCH_KS, q1 = (slice + 1) * d.bch_nq / BCH_KS;
-  const int row0 = tile * BCH_ROWS + wave * 32;
-  const int blk = row0 + (lane & 31);
-  const bool live = blk < io.nblocks;
-  const uint4 *msg = (const uint4 *)(io.out + (int64_t)(live ? blk : 0) * io.cw_stride) + (lane >> 5);
+  const int slice = (int)blockIdx.x % BCH_KS, per_slice = (int)gridDim.x / BCH_KS, k = (int)blockIdx.x / BCH_KS;
+  const int qs0 = slice * d.bch_nq / BCH_KS, nc = (slice + 1) * d.bch_nq / BCH_KS - qs0;   // chunks per tile
+  const int64_t units = (int64_t)((io.nblocks + BCH_ROWS - 1) / BCH_ROWS) * nc;
+  const int64_t u1 = units * (k + 1) / per_slice;
   // chunk q's B fragments into LDS buffer buf by LDS-DMA (16 bytes per lane, no VGPR staging): each
   // wave-instruction fills 1 KB at a wave-uniform base, lane l at + 16 l (the table is lane-linear)
   auto stage = [&](int q, int buf) {
 #pragma unroll
-    for (int k = 0; k < NT; k++) {
-      const uint4 *src = d.bch_mfma + (size_t)q * PER + FEC_THREADS * k + tid;
-      uint4 *dst = bsm + buf * PER + FEC_THREADS * k + 64 * wave;
+    for (int j = 0; j < NT; j++) {
+      const uint4 *src = d.bch_mfma + (size_t)q * PER + FEC_THREADS * j + tid;
+      uint4 *dst = bsm + buf * PER + FEC_THREADS * j + 64 * wave;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                        (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
     }
   };
-  bch_v16f acc[NT];
+  for (int64_t u = units * k / per_slice; u < u1;) {
+    // one tile segment: chunks [q0, q1) of tile `tile`
+    const int tile = (int)(u / nc), q0 = qs0 + (int)(u % nc);
+    const int q1 = q0 + (int)min((int64_t)(qs0 + nc - q0), u1 - u);
+    u += q1 - q0;
+    const int row0 = tile * BCH_ROWS + wave * 32;
+    const int blk = row0 + (lane & 31);
+    const bool live = blk < io.nblocks;
+    const uint4 *msg = (const uint4 *)(io.out + (int64_t)(live ? blk : 0) * io.cw_stride) + (lane >> 5);
+    bch_v16f acc[NT];
 #pragma unroll
-  for (int t = 0; t < NT; t++) acc[t] = bch_v16f{};
-  uint4 a = make_uint4(0u, 0u, 0u, 0u);
-  if (q0 < q1) {
+    for (int t = 0; t < NT; t++) acc[t] = bch_v16f{};
+    __syncthreads();   // the previous segment's epilogue has read its parity words out of buffer 0
     stage(q0, 0);
-    if (live) a = msg[2 * q0];
-  }
-  __syncthreads();   // (its vmcnt(0) retires the DMA)
-  for (int q = q0; q < q1; q++) {
-    const int cur = (q - q0) & 1;
-    uint4 an = make_uint4(0u, 0u, 0u, 0u);
-    if (q + 1 < q1) {   // the other buffer was last read before the previous barrier
-      stage(q + 1, cur ^ 1);
-      if (live) an = msg[2 * (q + 1)];
-    }
-    const uint4 *bq = bsm + cur * PER;
-    // B fragments of K-step u + 1 requested before the MFMAs of step u (two steps' fragments live)
-    uint4 bc[NT], bx[NT];
-#pragma unroll
-    for (int t = 0; t < NT; t++) bc[t] = bq[t * 64 + lane];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      if (u < 3) {
-#pragma unroll
-        for (int t = 0; t < NT; t++) bx[t] = bq[((u + 1) * NT + t) * 64 + lane];
+    uint4 a = live ? msg[2 * q0] : make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();   // (its vmcnt(0) retires the DMA)
+    for (int q = q0; q < q1; q++) {
+      const int cur = (q - q0) & 1;
+      uint4 an = make_uint4(0u, 0u, 0u, 0u);
+      if (q + 1 < q1) {   // the other buffer was last read before the previous barrier
+        stage(q + 1, cur ^ 1);
+        if (live) an = msg[2 * (q + 1)];
       }
-      // A fragment: dword d = bits d, d + 4, .. of the message word as fp4 nibbles 0x1 (0.5; the A
-      // scale 2^1 makes them 1.0): two VALU ops per dword
-      const uint32_t w = u == 0 ? a.x : u == 1 ? a.y : u == 2 ? a.z : a.w;
-      const bch_v8i A = {(int)(w & 0x11111111u), (int)((w >> 1) & 0x11111111u), (int)((w >> 2) & 0x11111111u),
-                         (int)((w >> 3) & 0x11111111u), 0, 0, 0, 0};
+      const uint4 *bq = bsm + cur * PER;
+      // B fragments of K-step s + 1 requested before the MFMAs of step s (two steps' fragments live)
+      uint4 bc[NT], bx[NT];
 #pragma unroll
-      for (int t = 0; t < NT; t++) {
-        const bch_v8i Bv = {(int)bc[t].x, (int)bc[t].y, (int)bc[t].z, (int)bc[t].w, 0, 0, 0, 0};
-        acc[t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, Bv, acc[t], 4, 4, 0, 128, 0, 127);
+      for (int t = 0; t < NT; t++) bc[t] = bq[t * 64 + lane];
+#pragma unroll
+      for (int s = 0; s < 4; s++) {
+        if (s < 3) {
+#pragma unroll
+          for (int t = 0; t < NT; t++) bx[t] = bq[((s + 1) * NT + t) * 64 + lane];
+        }
+        // A fragment: dword e = bits e, e + 4, .. of the message word as fp4 nibbles 0x1 (0.5; the A
+        // scale 2^1 makes them 1.0): two VALU ops per dword
+        const uint32_t w = s == 0 ? a.x : s == 1 ? a.y : s == 2 ? a.z : a.w;
+        const bch_v8i A = {(int)(w & 0x11111111u), (int)((w >> 1) & 0x11111111u), (int)((w >> 2) & 0x11111111u),
+                           (int)((w >> 3) & 0x11111111u), 0, 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+          const bch_v8i Bv = {(int)bc[t].x, (int)bc[t].y, (int)bc[t].z, (int)bc[t].w, 0, 0, 0, 0};
+          acc[t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, Bv, acc[t], 4, 4, 0, 128, 0, 127);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < NT; t++) bc[t] = bx[t];
       }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < NT; t++) bc[t] = bx[t];
+      __syncthreads();
+      a = an;
     }
-    __syncthreads();
-    a = an;
-  }
-  // partial parities: accumulator register r of lane l is block row (r & 3) + 8 (r >> 2) + 4 (l >> 5),
-  // parity column l & 31 of its tile; one ballot per (tile, register) gives 32 parities of two rows,
-  // bit c -> byte c / 8, bit 7 - c % 8 of the row's tile word (bswap o bitreverse)
-  uint32_t *pw = (uint32_t *)bsm + wave * 32 * BCH_PART_WORDS;   // after the loop's last barrier
+    // partial parities: accumulator register r of lane l is block row (r & 3) + 8 (r >> 2) + 4 (l >> 5),
+    // parity column l & 31 of its tile; one ballot per (tile, register) gives 32 parities of two rows,
+    // bit c -> byte c / 8, bit 7 - c % 8 of the row's tile word (bswap o bitreverse)
+    uint32_t *pw = (uint32_t *)bsm + wave * 32 * BCH_PART_WORDS;   // after the loop's last barrier
 #pragma unroll
-  for (int t = 0; t < NT; t++)
+    for (int t = 0; t < NT; t++)
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      const uint64_t m = __builtin_amdgcn_ballot_w64(((int)acc[t][r] & 1) != 0);
-      const int row = (r & 3) + 8 * (r >> 2);
-      if (lane == 0) pw[row * BCH_PART_WORDS + t] = __builtin_bswap32(__builtin_bitreverse32((uint32_t)m));
-      if (lane == 1) pw[(row + 4) * BCH_PART_WORDS + t] = __builtin_bswap32(__builtin_bitreverse32((uint32_t)(m >> 32)));
+      for (int r = 0; r < 16; r++) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(((int)acc[t][r] & 1) != 0);
+        const int row = (r & 3) + 8 * (r >> 2);
+        if (lane == 0) pw[row * BCH_PART_WORDS + t] = __builtin_bswap32(__builtin_bitreverse32((uint32_t)m));
+        if (lane == 1) pw[(row + 4) * BCH_PART_WORDS + t] = __builtin_bswap32(__builtin_bitreverse32((uint32_t)(m >> 32)));
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int i = lane; i < 32 * BCH_PART_WORDS; i += 64) {
+      const int row = i / BCH_PART_WORDS, t = i % BCH_PART_WORDS;
+      if (t < NT && row0 + row < io.nblocks) atomicXor(&io.bch_part[(int64_t)(row0 + row) * BCH_PART_WORDS + t], pw[i]);
     }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (int i = lane; i < 32 * BCH_PART_WORDS; i += 64) {
-    const int row = i / BCH_PART_WORDS, t = i % BCH_PART_WORDS;
-    if (t < NT && row0 + row < io.nblocks) atomicXor(&io.bch_part[(int64_t)(row0 + row) * BCH_PART_WORDS + t], pw[i]);
   }
 }
 
@@ -843,8 +851,9 @@ static hipError_t bch_launch(const FecDev &d, const FecIO &io, hipStream_t s) {
   const int lds = 2 * 4 * NT * 64 * 16;
   hipError_t e = lds_limit((const void *)bch_gemm_kernel<NT>, lds);
   if (e != hipSuccess) return e;
-  const int tiles = (io.nblocks + BCH_ROWS - 1) / BCH_ROWS;
-  hipLaunchKernelGGL(bch_gemm_kernel<NT>, dim3(tiles * BCH_KS), dim3(FEC_THREADS), lds, s, d, io);
+  // persistent: BCH_WG_PER_CU workgroups per CU, a multiple of BCH_KS (one slice per XCD)
+  const int per_slice = (fec_grid(1 << 30, BCH_WG_PER_CU) + BCH_KS - 1) / BCH_KS;
+  hipLaunchKernelGGL(bch_gemm_kernel<NT>, dim3(per_slice * BCH_KS), dim3(FEC_THREADS), lds, s, d, io);
   return hipGetLastError();
 }
 
