@@ -166,11 +166,17 @@ __device__ __forceinline__ uint8_t get_byte192(const uint64_t w[3], int lowbit) 
 
 // word k of LDPC info group g laid out for 32-bit rotation windows: big-endian bytes
 // (4k .. 4k+3) mod 45 of the group's 45 frame bytes (d_g || d_g[0..56))
+// (words 0..10 and 12 are four consecutive frame bytes: two aligned word reads and a byte align;
+// word 11 wraps from byte 44 to bytes 0..2)
 __device__ __forceinline__ void ldpc_group_word(uint32_t *D, const uint8_t *frame, int g, int k) {
   const uint8_t *gb = frame + 45 * g;
-  const int b = 4 * k;
-  D[g * FEC_DW + k] = ((uint32_t)gb[b % 45] << 24) | ((uint32_t)gb[(b + 1) % 45] << 16) |
-                      ((uint32_t)gb[(b + 2) % 45] << 8) | (uint32_t)gb[(b + 3) % 45];
+  if (k == 11) {
+    D[g * FEC_DW + k] = ((uint32_t)gb[44] << 24) | ((uint32_t)gb[0] << 16) | ((uint32_t)gb[1] << 8) | (uint32_t)gb[2];
+    return;
+  }
+  const int o = 45 * g + (k == 12 ? 3 : 4 * k);   // frame is 4-byte aligned
+  const uint32_t *fw = (const uint32_t *)frame;
+  D[g * FEC_DW + k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(fw[(o >> 2) + 1], fw[o >> 2], (uint32_t)(o & 3)));
 }
 
 // byte-table division of frame[lo, hi) (lo clamped at 0) into the P-bit remainder r; the next message
@@ -791,14 +797,20 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_ldpc_kern
       if (4 * i + 4 <= NB) {
         v = framew[i];
       } else if (d.parity_il && 4 * i >= NB && 4 * i + 4 <= cwb) {
-        // four parity bytes m .. m + 3 (byte k of row a = m / 45, rows of 12 big-endian words)
+        // four parity bytes m .. m + 3 = bytes k .. k + 3 of row a (m = 45 a + k; rows of 12 big-endian
+        // words): one byte align of two row words, or bytewise where they cross into row a + 1
         int a = (4 * i - NB) / 45, k = 4 * i - NB - 45 * a;
-        v = 0;
-        for (int e = 0; e < 4; e++) {
-          v |= ((cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu) << (8 * e);
-          if (++k == 45) {
-            k = 0;
-            a++;
+        if (k <= 41) {
+          const uint32_t w0 = cur[a * 12 + (k >> 2)], w1 = cur[a * 12 + (k >> 2) + 1];
+          v = __builtin_bswap32((k & 3) ? __builtin_amdgcn_alignbyte(w0, w1, (uint32_t)(4 - (k & 3))) : w0);
+        } else {
+          v = 0;
+          for (int e = 0; e < 4; e++) {
+            v |= ((cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu) << (8 * e);
+            if (++k == 45) {
+              k = 0;
+              a++;
+            }
           }
         }
       } else {
