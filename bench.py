@@ -104,11 +104,13 @@ def minimal_bytes(cfg, info, iq_bytes=8):
 
 
 KERNELS = ("fec", "map", "ofdm")
+# the kernels each stage launches per step (the chain's FEC: BB pass, BCH matrix-core pass, LDPC pass)
+STAGE_KERNELS = {"fec": ("fec_bb", "bch_gemm", "fec_ldpc"), "map": ("map",), "ofdm": ("ofdm",)}
 # rocprofv3 FETCH_SIZE / WRITE_SIZE (KiB) -> bytes.  gfx950 tallies 128-B read requests at 64 B
 # (MI355X_MICROARCH.md, HBM): x2 on the read side, calibrated per access width by tools/fetch_calib
-# (profiles/r2_fetch_calib.json); the kernels' dominant access widths: fec 16-B TS staging loads and
-# 4-B codeword stores, map 16-B codeword loads and 2-B index-pair stores, ofdm 16-B data-slot loads
-# and 16-B IQ stores (two samples per lane)
+# (profiles/r2_fetch_calib.json); the kernels' dominant access widths: fec 16-B TS staging / codeword
+# loads and 16-B BBFRAME + 4-B parity stores, map 16-B codeword loads and 2-B index-pair stores, ofdm
+# 16-B data-slot loads and 16-B IQ stores (two samples per lane)
 LOAD_WIDTH = {"fec": 16, "map": 16, "ofdm": 16}
 STORE_WIDTH = {"fec": 4, "map": 2, "ofdm": 16}
 
@@ -149,11 +151,14 @@ def pmc_passes(args):
                 for row in csv.DictReader(fh):
                     kn = row.get("Kernel_Name", "")
                     names.add(kn[:60])
-                    m = re.search(r"\b(fec|map|ofdm)(32)?_kernel", kn)
+                    m = re.search(r"\b(fec_bb|bch_gemm|fec_ldpc|fec|map|ofdm)(32)?_kernel", kn)
                     if m and row.get("Counter_Name") in ctrs:
                         vals.setdefault((m.group(1), row["Counter_Name"]), []).append(float(row["Counter_Value"]))
-        for (k, c), v in vals.items():
-            res[k][c] = sum(v) / len(v)
+        # per-launch means; the chain's FEC stage is three kernels launched once each per step (BB pass,
+        # BCH on the matrix cores, LDPC pass): their means add up
+        for (kn, c), v in vals.items():
+            k = "fec" if kn in STAGE_KERNELS["fec"] else kn
+            res[k][c] = res[k].get(c, 0.0) + sum(v) / len(v)
         shutil.rmtree(d, ignore_errors=True)
     cal = _calibration()
     for k in KERNELS:
@@ -663,7 +668,8 @@ def main():
             t = avg_ms * 1e-3
             stages[name] = {"avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": ab[name] * B,
                             "achieved_GBs": ab[name] * B / t / 1e9 if t > 0 else None}
-            kname = "ofdm32_kernel" if name == "ofdm" and info["fft_size"] == 32768 else name + "_kernel"
+            kname = ("ofdm32_kernel" if name == "ofdm" and info["fft_size"] == 32768 else
+                     "fec_bb_kernel + bch_gemm_kernel + fec_ldpc_kernel" if name == "fec" else name + "_kernel")
             e = {"kernel": kname, "bound": "hbm", "avg_launch_ms": avg_ms, "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "min_bytes_per_launch": mb[name] * B,
                  "achieved": mb[name] * B / t / 1e9 if t > 0 else None,
@@ -684,8 +690,9 @@ def main():
             if name == "fec":
                 nb = info["fec_blocks_per_frame"] * B
                 e["fec_blocks_per_s"] = nb / t if t > 0 else None
-                e["note"] = ("integer BCH/LDPC codec: latency/issue-bound, not HBM-bound (SURVEY 8(d)); "
-                             "frac is its minimal HBM bytes / time / peak")
+                e["note"] = ("integer BB/BCH/LDPC codec (the BCH as a GF(2) product on the matrix cores): "
+                             "latency/issue-bound, not HBM-bound (SURVEY 8(d)); frac is its minimal HBM bytes / "
+                             "time / peak; traffic and instruction counts are the three pass kernels' sums")
                 if "SQ_INSTS_VALU" in pm and t > 0:
                     e["valu_wave_instr_per_block"] = pm["SQ_INSTS_VALU"] / nb
                     e["salu_wave_instr_per_block"] = pm.get("SQ_INSTS_SALU", 0) / nb

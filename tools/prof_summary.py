@@ -66,7 +66,7 @@ def main(tag, rnd):
                 "%.3f" % e["traffic_over_min"] if e.get("traffic_over_min") else "-"))
         fec = b.get("rooflines", {}).get("fec", {})
         if "valu_wave_instr_per_block" in fec:
-            lines += ["", "fec_kernel: %.3g FEC blocks/s, %.0f VALU + %.0f SALU wave-instructions per block, VALU issue "
+            lines += ["", "FEC passes: %.3g FEC blocks/s, %.0f VALU + %.0f SALU wave-instructions per block, VALU issue "
                           "%.2f of peak" % (fec["fec_blocks_per_s"], fec["valu_wave_instr_per_block"],
                                             fec["salu_wave_instr_per_block"], fec["valu_issue_frac"])]
         lines.append("")
@@ -84,6 +84,10 @@ def main(tag, rnd):
                 N, len(rs), max(r["rel_rms"] for r in rs), max(r["max_rel"] for r in rs),
                 max(r["f32_rel_rms"] for r in rs), max(r["rel_rms"] / r["f32_rel_rms"] for r in rs)))
         lines.append("")
+    sq = os.path.join(src, "pmc_sq.txt")
+    if os.path.exists(sq):
+        shutil.copy(sq, os.path.join("profiles", "%s_%s_pmc_sq.txt" % (rnd, tag)))
+        lines += ["SQ counters per launch (tools/gpu_pmc.sh): `profiles/%s_%s_pmc_sq.txt`" % (rnd, tag), ""]
     for f in ("pytest.log", "smoke.log"):
         p = os.path.join(src, f)
         if os.path.exists(p):
