@@ -1151,6 +1151,52 @@ int64_t ti_dest(const FramePlan &fp, int r, int t) {
   return (int64_t)r0 * cs + (int64_t)row * (5 * nb) + 5 * (r - r0) + e;
 }
 
+// LDS bank pair of a stored bin as the OFDM kernels' scatter writes it (8-byte slot within its half,
+// one pad slot per 2^ps: t2_kernels.h ofdm_padded_bin)
+static int scatter_bank(int N, int stored) {
+  const int nsub = ofdm_split(N) ? N / 2 : N, ps = ofdm_split(N) ? 5 : 4, k = stored % nsub;
+  return (k + (k >> ps)) & 15;
+}
+
+// Conflict-free scatter groups.  The OFDM kernels stream a run of scatter entries in units of U (8
+// data slots per lane per round for 32K, 4 for N <= 16K and for the aux quads); unit x (counted from
+// the run start rounded down to U, o0) goes to lane x mod 64, and element e of every lane's unit is
+// written by one ds_write_b64, whose 16-lane groups {16 g .. 16 g + 15} are bank-conflict-free when
+// their bank pairs differ.  So the entries of each window of 16 units (16 U positions, from o0) at the
+// same e should have distinct bank pairs.  seq holds the entries of positions [pos0, pos0 + n) in
+// position order; entries may move only within their segment (seg(k) equal for consecutive k): a
+// greedy first fit per position.
+template <class Bank, class Seg>
+static void bank_balance(std::vector<int32_t> &seq, int pos0, int U, const Bank &bank, const Seg &seg) {
+  const int n = (int)seq.size(), o0 = pos0 & ~(U - 1);
+  std::vector<uint16_t> used((size_t)((pos0 + n - o0) / (16 * U) + 1) * U, 0);
+  std::vector<int32_t> cand;
+  for (int k0 = 0; k0 < n;) {
+    int k1 = k0 + 1;
+    while (k1 < n && seg(seq[k1]) == seg(seq[k0])) k1++;
+    cand.assign(seq.begin() + k0, seq.begin() + k1);
+    int left[16] = {0};   // remaining candidates per bank pair
+    for (int c : cand) left[bank(c)]++;
+    for (int k = k0; k < k1; k++) {
+      const int p = pos0 + k, cls = ((p - o0) / (16 * U)) * U + (p - o0) % U;
+      // a candidate whose bank pair is still free in this class, the most plentiful such pair first
+      // (keeps the scarce ones for later positions); else the first candidate
+      size_t pick = 0;
+      int best = -1;
+      for (size_t i = 0; i < cand.size(); i++) {
+        const int b = bank(cand[i]);
+        if (!((used[cls] >> b) & 1) && left[b] > best) { best = left[b]; pick = i; }
+      }
+      const int b = bank(cand[pick]);
+      seq[k] = cand[pick];
+      used[cls] |= (uint16_t)(1u << b);
+      left[b]--;
+      cand.erase(cand.begin() + pick);
+    }
+    k0 = k1;
+  }
+}
+
 int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl) {
   if (pp.active != fp.M || pp.N > 32768) return -1;
   // bins -> frame data order (TI output) via the framemapper's composed map
@@ -1183,10 +1229,11 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
   for (int s = 0; s < fp.S; s++)
     if (!seen[s]) return -1;
   cl.sym_n0 = cl.sym_n;
-  // Slot order within each symbol (32K: within each half, bins < N/2 first): FEC-block-major, TI
-  // order within a block.  The OFDM kernels stream any order (inv follows it); this one gives the
-  // map kernel, which stores one FEC block per workgroup, one contiguous run per symbol (half)
-  // instead of 10-byte TI-row runs scattered over the symbol.
+  // Slot order within each symbol (32K: within each stored half): FEC-block-major, and within a
+  // block's run the order bank_balance picks for the OFDM scatter's write groups.  The OFDM kernels
+  // stream any order (inv follows it); block-major runs give the map kernel, which stores one FEC
+  // block per workgroup, one contiguous run per symbol (half) instead of 10-byte TI-row runs
+  // scattered over the symbol (its per-cell deltas take any order inside a run).
   std::vector<int32_t> blk_of(fp.S);
   for (int r = 0; r < fp.F; r++)
     for (int t = 0; t < fp.cs; t++) blk_of[ti_dest(fp, r, t)] = r;
@@ -1205,6 +1252,15 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
       const int hx = split && cl.inv[x] >= half, hy = split && cl.inv[y] >= half;
       return hx != hy ? hx < hy : blk_of[x] < blk_of[y];
     });
+    // within each FEC block's run, the order the OFDM scatter's write groups want (bank_balance)
+    const int nh = split ? n0 : n;
+    for (int h = 0; h < (split ? 2 : 1); h++) {
+      const int k0 = h ? nh : 0, k1 = h ? n : nh;
+      std::vector<int32_t> seq(order.begin() + k0, order.begin() + k1);
+      bank_balance(seq, d0 + k0, split ? 8 : 4, [&](int s) { return scatter_bank(pp.N, cl.inv[s]); },
+                   [&](int s) { return blk_of[s]; });
+      std::copy(seq.begin(), seq.end(), order.begin() + k0);
+    }
     for (int k = 0; k < n; k++) cl.part[order[k]] = d0 + k;
     cl.sym_n0[j] = split ? n0 : n;
   }
@@ -1282,6 +1338,22 @@ int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf
         if (code >= (1 << 17)) return -1;
         al.ind.push_back((uint32_t)k | ((uint32_t)code << 15));
       }
+    }
+    {   // the group's direct entries in the order the kernel's quad write groups want (bank_balance)
+      const int e0 = al.grp[4 * g + 0], ne = (int)al.dbin.size() - e0;
+      std::vector<int32_t> seq(ne);
+      for (int i = 0; i < ne; i++) seq[i] = e0 + i;
+      const int ps = split ? 5 : 4;
+      bank_balance(seq, 0, 4, [&](int i) { const int k = al.dbin[i]; return (k + (k >> ps)) & 15; },
+                   [](int) { return 0; });
+      std::vector<uint16_t> b2(ne);
+      std::vector<cf32> v2(ne);
+      for (int i = 0; i < ne; i++) {
+        b2[i] = al.dbin[seq[i]];
+        v2[i] = al.dval[seq[i]];
+      }
+      std::copy(b2.begin(), b2.end(), al.dbin.begin() + e0);
+      std::copy(v2.begin(), v2.end(), al.dval.begin() + e0);
     }
     while (al.dbin.size() & 3) {   // pad to a quad: bin 0xFFFF goes to the kernel's dummy slot
       al.dbin.push_back(0xFFFF);
