@@ -139,11 +139,12 @@ struct MapTables {
     dev.nldpc = plan.nldpc; dev.nbch = fec.nbch; dev.q = fec.q; dev.rotation = plan.rotation;
     dev.parity_il = fec.parity_interleave ? 1 : 0;
     dev.F = 1;
-    memcpy(dev.twist, plan.twist, 16);
-    memcpy(dev.mux, plan.mux, 16);
-    // column feeding bit b of the demuxed row word (b = W - 1 - mux[e]); 255 = none
-    memset(dev.colsel, 255, 16);
-    for (int e = 0; e < plan.W && plan.mode != 0; e++) dev.colsel[plan.W - 1 - plan.mux[e]] = (uint8_t)e;
+    // column feeding bit b of the demuxed row word (b = W - 1 - mux[e]): its start bit and twist
+    for (int b = 0; b < 16; b++) dev.colstart[b] = -1, dev.coltw[b] = 0;
+    for (int e = 0; e < plan.W && plan.mode != 0; e++) {
+      dev.colstart[plan.W - 1 - plan.mux[e]] = e * plan.R;
+      dev.coltw[plan.W - 1 - plan.mux[e]] = plan.twist[e];
+    }
     return 0;
   }
 };

@@ -85,8 +85,9 @@ struct MapDev {
   const int16_t *part;     // chain, 32K only: slot - TI position of (block r, TI-store index j), at
                            // r*part_stride + j (rows padded to a multiple of 4 for 8-byte quad loads)
   int part_stride;
-  uint8_t twist[16], mux[16];
-  uint8_t colsel[16];      // column e whose bit lands at position b of the row word (W-1-mux[e] = b), 255: none
+  // per demuxed bit b of the row word: the column e feeding it (W-1-mux[e] = b) as its first codeword
+  // bit e*R (-1: none) and its twist (int32: uniform scalar loads, no byte loads in the column loop)
+  int colstart[16], coltw[16];
 };
 struct MapIO {
   const uint8_t *in;   // packed tempu codewords (stride cw_stride) or unpacked natural bits

@@ -961,21 +961,21 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
       x ^= t ^ (t << 28);
       return x;
     };
-    // one thread per 8 rows: byte b of x = column colsel[b]'s 8 bits (row k at bit 7 - k); after
+    // one thread per 8 rows: byte b of x = the 8 bits of the column feeding bit b (row k at bit 7 - k); after
     // the transpose byte 7 - k holds row k's demuxed bits b
     for (int g = tid; g < (R + 7) >> 3; g += NT) {
       const int j0 = 8 * g;
       uint64_t x[2] = {0, 0};
 #pragma unroll
       for (int b = 0; b < 16; b++) {
-        const int e = d.colsel[b];
-        if (e == 255) continue;
-        int off = j0 - d.twist[e];
+        const int c0 = d.colstart[b];
+        if (c0 < 0) continue;
+        int off = j0 - d.coltw[b];
         off += off < 0 ? R : 0;
-        uint32_t win = window(e * R + off);
+        uint32_t win = window(c0 + off);
         if (off + 8 > R) {                       // the column wraps inside these 8 rows
           const int n1 = R - off;
-          win = (win & ~(0xFFFFFFFFu >> n1)) | (window(e * R) >> n1);
+          win = (win & ~(0xFFFFFFFFu >> n1)) | (window(c0) >> n1);
         }
         x[b >> 3] |= (uint64_t)(win >> 24) << (8 * (b & 7));
       }
@@ -1077,8 +1077,9 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   if (pr) {
     // four consecutive TI-store indices per thread: one 8-byte load of their partition deltas
     // instead of four 2-byte loads (the memory instruction count, not the bytes, sets this loop's
-    // rate; the pair stores stay 2 bytes per cell)
-    constexpr int MQ = MAP_MB / 2;
+    // rate; the pair stores stay 2 bytes per cell).  Eight quads per thread per round: cs <= 8192
+    // in one round, with no loop-head wait on a previous round's pair stores (map -3 %)
+    constexpr int MQ = MAP_MB;
     for (int q0 = tid; q0 < nq; q0 += MQ * NT) {
       uint2 pq[MQ];
 #pragma unroll
