@@ -961,26 +961,12 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
       x ^= t ^ (t << 28);
       return x;
     };
-    // one thread per 8 rows: byte b of x = the 8 bits of the column feeding bit b (row k at bit 7 - k); after
-    // the transpose byte 7 - k holds row k's demuxed bits b
-    for (int g = tid; g < (R + 7) >> 3; g += NT) {
+    // one thread per 16 rows (two 8-row groups g = 2 g2, 2 g2 + 1): byte b of xa / xb = the 8 bits of
+    // the column feeding bit b in rows 16 g2 .. + 7 / + 8 .. + 15 (row k at bit 7 - k), both cut from
+    // one 32-bit window; after the transpose byte 7 - k holds row k's demuxed bits b
+    uint32_t *idxw = (uint32_t *)idx;
+    auto emit = [&](int g, uint64_t lo, uint64_t hi) {
       const int j0 = 8 * g;
-      uint64_t x[2] = {0, 0};
-#pragma unroll
-      for (int b = 0; b < 16; b++) {
-        const int c0 = d.colstart[b];
-        if (c0 < 0) continue;
-        int off = j0 - d.coltw[b];
-        off += off < 0 ? R : 0;
-        uint32_t win = window(c0 + off);
-        if (off + 8 > R) {                       // the column wraps inside these 8 rows
-          const int n1 = R - off;
-          win = (win & ~(0xFFFFFFFFu >> n1)) | (window(c0) >> n1);
-        }
-        x[b >> 3] |= (uint64_t)(win >> 24) << (8 * (b & 7));
-      }
-      const uint64_t lo = tr8(x[0]), hi = d.W > 8 ? tr8(x[1]) : 0ull;
-      uint32_t *idxw = (uint32_t *)idx;
       if (d.mode == 1) {                         // two cells per row: pack >> mod, pack & (2^mod - 1)
         const uint32_t lo_mask = (1u << mod) - 1u;
 #pragma unroll
@@ -996,6 +982,26 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
         if (j0 < R) idxw[2 * g] = (uint32_t)rv;
         if (j0 + 4 < R) idxw[2 * g + 1] = (uint32_t)(rv >> 32);
       }
+    };
+    for (int g2 = tid; g2 < (R + 15) >> 4; g2 += NT) {
+      const int j0 = 16 * g2;
+      uint64_t xa[2] = {0, 0}, xb[2] = {0, 0};
+#pragma unroll
+      for (int b = 0; b < 16; b++) {
+        const int c0 = d.colstart[b];
+        if (c0 < 0) continue;
+        int off = j0 - d.coltw[b];
+        off += off < 0 ? R : 0;
+        uint32_t win = window(c0 + off);
+        if (off + 16 > R) {                      // the column wraps inside these 16 rows
+          const int n1 = R - off;
+          win = (win & ~(0xFFFFFFFFu >> n1)) | (window(c0) >> n1);
+        }
+        xa[b >> 3] |= (uint64_t)(win >> 24) << (8 * (b & 7));
+        xb[b >> 3] |= (uint64_t)((win >> 16) & 0xFFu) << (8 * (b & 7));
+      }
+      emit(2 * g2, tr8(xa[0]), d.W > 8 ? tr8(xa[1]) : 0ull);
+      emit(2 * g2 + 1, tr8(xb[0]), d.W > 8 ? tr8(xb[1]) : 0ull);
     }
   }
 }
