@@ -120,7 +120,7 @@ constexpr int BCH_ROWS = 128;           // bch_gemm_kernel: FEC blocks per workg
 // sized for the plan's code, so a launch fits as many workgroups per CU as it allows
 enum FecCarveKind { CARVE_FUSED = 0, CARVE_BB = 1, CARVE_LDPC = 2 };
 struct FecCarve {
-  int btab, ents, hcrc, sync, w, rowp, frame, phase, crc8, crcsh, total;
+  int btab, ents, hcrc, sync, w, rowp, frame, phase, crc8, crcsh, crcsl, total;
 };
 __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int q) {
   FecCarve c{};
@@ -136,7 +136,8 @@ __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int 
   c.phase = c.frame + ((nbch / 8 + 15) & ~15);
   c.crc8 = c.phase + ((188 + (kbch - 80) / 8 + 32 + 15) & ~15);   // + slack: 16-byte staging start
   c.crcsh = c.crc8 + 256;
-  const int bb_end = c.crcsh + 2048, ldpc_end = c.phase + 4 * (FEC_DW * (nbch / 360) + 12 * q);
+  c.crcsl = c.crcsh + 2048;                // BB pass: T^2, T^3, T^4 of the CRC-8 byte table (slicing by 4)
+  const int bb_end = c.crcsl + (kind == CARVE_BB ? 768 : 0), ldpc_end = c.phase + 4 * (FEC_DW * (nbch / 360) + 12 * q);
   c.total = kind == CARVE_BB ? bb_end : kind == CARVE_LDPC ? ldpc_end : (bb_end > ldpc_end ? bb_end : ldpc_end);
   return c;
 }
@@ -374,6 +375,7 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
   const int L = d.kbch >> 3;
   uint8_t *frame = smem + cv.frame, *phase = smem + cv.phase;
   uint8_t *crc8 = smem + cv.crc8, *crcsh = smem + cv.crcsh;
+  const uint8_t *crcsl = smem + cv.crcsl;   // BB pass (CRC_RESIDENT): T^2 | T^3 | T^4
   const uint8_t *hcrc8 = smem + cv.hcrc;
   uint8_t *syncv = smem + cv.sync;
   const BbGeom g = bb_geom(d, io, B);
@@ -410,15 +412,30 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
       int64_t p = pos0 + first_slot + 188 * (int64_t)m;   // sync position
       bool active = m < nslots && p > 0;
       if (active) {
-        const uint8_t *b0 = raw + (p - 187 + 24 * k - rs);
         const int n = k == 7 ? 19 : 24;            // 187 = 7 x 24 + 19
-        uint8_t by[24];
-#pragma unroll
-        for (int i = 0; i < 24; i++) by[i] = i < n ? b0[i] : 0;
         uint32_t c = 0;
+        if (CRC_RESIDENT) {
+          // slicing by 4 (the BB pass keeps T^2, T^3, T^4 in LDS; T is linear):
+          // c <- T^4[c ^ b0] ^ T^3[b1] ^ T^2[b2] ^ T[b3], six dependent lookups per 24 bytes instead of
+          // 24; the 19-byte last chunk is front-padded with zero bytes, which leave c = 0
+          const int pad = 24 - n;
+          const uint8_t *b0 = raw + (p - 187 + 24 * k - rs) - pad;
+          uint32_t by[24];
 #pragma unroll
-        for (int i = 0; i < 24; i++)
-          if (i < n) c = crc8[by[i] ^ c];
+          for (int i = 0; i < 24; i++) by[i] = i >= pad ? (uint32_t)b0[i] : 0u;
+#pragma unroll
+          for (int g = 0; g < 6; g++)
+            c = (uint32_t)crcsl[512 + (c ^ by[4 * g])] ^ (uint32_t)crcsl[256 + by[4 * g + 1]] ^
+                (uint32_t)crcsl[by[4 * g + 2]] ^ (uint32_t)crc8[by[4 * g + 3]];
+        } else {
+          const uint8_t *b0 = raw + (p - 187 + 24 * k - rs);
+          uint8_t by[24];
+#pragma unroll
+          for (int i = 0; i < 24; i++) by[i] = i < n ? b0[i] : 0;
+#pragma unroll
+          for (int i = 0; i < 24; i++)
+            if (i < n) c = crc8[by[i] ^ c];
+        }
         part = crcsh[k * 256 + c];
       }
       // XOR of the 8 lanes' parts into lane k == 0: DPP quad_perm [1,0,3,2], [2,3,0,1], row_shl:4
@@ -595,6 +612,17 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel
   for (int i = tid; i < 72; i += FEC_THREADS) smem[cv.hcrc + i] = d.hcrc_bits[i];
   for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)(smem + cv.crc8))[i] = ((const uint32_t *)d.crc8_tab)[i];
   for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)(smem + cv.crcsh))[i] = ((const uint32_t *)d.crc8_shift)[i];
+  __syncthreads();
+  {   // slicing-by-4 tables T^2, T^3, T^4 of the CRC-8 byte table T
+    const uint8_t *t1 = smem + cv.crc8;
+    uint8_t *sl = smem + cv.crcsl;
+    if (tid < 256) {
+      const uint8_t a2 = t1[t1[tid]], a3 = t1[a2], a4 = t1[a3];
+      sl[tid] = a2;
+      sl[256 + tid] = a3;
+      sl[512 + tid] = a4;
+    }
+  }
   __syncthreads();
   const uint4 *framq = (const uint4 *)(smem + cv.frame);
   // NM: each block's raw TS units are requested one block ahead (in flight during the previous block)
