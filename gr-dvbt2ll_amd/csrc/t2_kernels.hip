@@ -120,7 +120,7 @@ constexpr int BCH_ROWS = 128;           // bch_gemm_kernel: FEC blocks per workg
 // sized for the plan's code, so a launch fits as many workgroups per CU as it allows
 enum FecCarveKind { CARVE_FUSED = 0, CARVE_BB = 1, CARVE_LDPC = 2 };
 struct FecCarve {
-  int btab, ents, hcrc, sync, w, rowp, frame, phase, crc8, crcsh, crcsl, total;
+  int btab, ents, hcrc, sync, w, rowp, frame, phase, crc8, crcsh, crcsl, prbs, total;
 };
 __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int q) {
   FecCarve c{};
@@ -137,7 +137,8 @@ __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int 
   c.crc8 = c.phase + ((188 + (kbch - 80) / 8 + 32 + 15) & ~15);   // + slack: 16-byte staging start
   c.crcsh = c.crc8 + 256;
   c.crcsl = c.crcsh + 2048;                // BB pass: T^2, T^3, T^4 of the CRC-8 byte table (slicing by 4)
-  const int bb_end = c.crcsl + (kind == CARVE_BB ? 768 : 0), ldpc_end = c.phase + 4 * (FEC_DW * (nbch / 360) + 12 * q);
+  c.prbs = c.crcsl + (kind == CARVE_BB ? 768 : 0);   // BB pass: the BB-scrambler PRBS words
+  const int bb_end = c.prbs + (kind == CARVE_BB ? ((kbch / 8 + 15) & ~15) : 0), ldpc_end = c.phase + 4 * (FEC_DW * (nbch / 360) + 12 * q);
   c.total = kind == CARVE_BB ? bb_end : kind == CARVE_LDPC ? ldpc_end : (bb_end > ldpc_end ? bb_end : ldpc_end);
   return c;
 }
@@ -497,22 +498,28 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
   // BBFRAME words = header | payload (each sync slot carries the CRC-8 of the previous packet,
   // bbheader:701-719) | in-band field, BB-scrambled (:694-696, :724-726)
   uint32_t *framew = (uint32_t *)frame;
-  const uint32_t *prbsw = (const uint32_t *)d.prbs;
-  for (int w = tid; w < (L + 3) >> 2; w += FEC_THREADS) {
-    const int p0 = 4 * w, j0 = p0 - 10;
-    uint32_t v;
-    if (!d.hem && j0 >= 0 && j0 + 4 <= npay) {
-      const int q = delta + 188 + j0;
-      v = __builtin_amdgcn_alignbyte(raww[(q >> 2) + 1], raww[q >> 2], (uint32_t)(q & 3));
-      const int r0 = (count0 + j0) % 188, e = r0 == 0 ? 0 : 188 - r0;
-      if (e < 4) {
-        const uint32_t sb = syncv[(j0 + e - first_slot) / 188];
-        v = (v & ~(0xFFu << (8 * e))) | (sb << (8 * e));
-      }
-    } else {
-      v = 0;
-      for (int e = 0; e < 4; e++) v |= slow_byte(p0 + e) << (8 * e);
+  // (the BB pass keeps the PRBS in LDS: a global load per word here was waited for with vmcnt(0),
+  // which also waited for the next block's prefetched TS units)
+  const uint32_t *prbsw = CRC_RESIDENT ? (const uint32_t *)(smem + cv.prbs) : (const uint32_t *)d.prbs;
+  // bulk payload words (NM: bytes 10 + j, j in [0, npay), whole words w in [3, wf1)) from the staged
+  // stream; the few others (header, the edges, in-band field; every word in HEM) in a separate loop,
+  // so the bulk loop carries no global loads or their waits
+  const int nw = (L + 3) >> 2, wf1 = d.hem ? 3 : (npay + 10) >> 2;
+  for (int w = 3 + tid; w < wf1; w += FEC_THREADS) {
+    const int j0 = 4 * w - 10;
+    const int q = delta + 188 + j0;
+    uint32_t v = __builtin_amdgcn_alignbyte(raww[(q >> 2) + 1], raww[q >> 2], (uint32_t)(q & 3));
+    const int r0 = (count0 + j0) % 188, e = r0 == 0 ? 0 : 188 - r0;
+    if (e < 4) {
+      const uint32_t sb = syncv[(j0 + e - first_slot) / 188];
+      v = (v & ~(0xFFu << (8 * e))) | (sb << (8 * e));
     }
+    framew[w] = v ^ prbsw[w];
+  }
+  for (int i = tid; i < 3 + nw - wf1; i += FEC_THREADS) {
+    const int w = i < 3 ? i : wf1 + (i - 3);
+    uint32_t v = 0;
+    for (int e = 0; e < 4; e++) v |= slow_byte(4 * w + e) << (8 * e);
     framew[w] = v ^ prbsw[w];
   }
   __syncthreads();
@@ -613,6 +620,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel
   for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)(smem + cv.crc8))[i] = ((const uint32_t *)d.crc8_tab)[i];
   for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)(smem + cv.crcsh))[i] = ((const uint32_t *)d.crc8_shift)[i];
   __syncthreads();
+  for (int i = tid; i < (L + 3) >> 2; i += FEC_THREADS) ((uint32_t *)(smem + cv.prbs))[i] = ((const uint32_t *)d.prbs)[i];
   {   // slicing-by-4 tables T^2, T^3, T^4 of the CRC-8 byte table T
     const uint8_t *t1 = smem + cv.crc8;
     uint8_t *sl = smem + cv.crcsl;
