@@ -1005,18 +1005,30 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
       const int j0 = 8 * g;
       if (d.mode == 1) {                         // two cells per row: pack >> mod, pack & (2^mod - 1)
         const uint32_t lo_mask = (1u << mod) - 1u;
+        uint32_t wq[4];
 #pragma unroll
         for (int qd = 0; qd < 4; qd++) {
           const int k0 = 2 * qd;
           const uint32_t p0 = (uint32_t)((lo >> (8 * (7 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (7 - k0))) & 0xFFu) << 8);
           const uint32_t p1 = (uint32_t)((lo >> (8 * (6 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (6 - k0))) & 0xFFu) << 8);
-          if (j0 + k0 < R)
-            idxw[4 * g + qd] = (p0 >> mod) | ((p0 & lo_mask) << 8) | ((p1 >> mod) << 16) | ((p1 & lo_mask) << 24);
+          wq[qd] = (p0 >> mod) | ((p0 & lo_mask) << 8) | ((p1 >> mod) << 16) | ((p1 & lo_mask) << 24);
+        }
+        // one 16-byte LDS write of the group's four words (four b32 writes at a lane stride of 8 words
+        // were 8-way bank conflicts); the last group's rows past R bytewise-guarded
+        if (j0 + 6 < R) {
+          *(uint4 *)(idxw + 4 * g) = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+        } else {
+#pragma unroll
+          for (int qd = 0; qd < 4; qd++)
+            if (j0 + 2 * qd < R) idxw[4 * g + qd] = wq[qd];
         }
       } else {                                   // 256-QAM short: one cell per row (byte-reversed lo)
         const uint64_t rv = __builtin_bswap64(lo);
-        if (j0 < R) idxw[2 * g] = (uint32_t)rv;
-        if (j0 + 4 < R) idxw[2 * g + 1] = (uint32_t)(rv >> 32);
+        if (j0 + 4 < R) {
+          *(uint2 *)(idxw + 2 * g) = make_uint2((uint32_t)rv, (uint32_t)(rv >> 32));
+        } else if (j0 < R) {
+          idxw[2 * g] = (uint32_t)rv;
+        }
       }
     };
     for (int g2 = tid; g2 < (R + 15) >> 4; g2 += NT) {
