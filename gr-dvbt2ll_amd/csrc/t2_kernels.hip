@@ -106,11 +106,12 @@ static hipError_t lds_limit(const void *fn, int bytes) {
 constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
 constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 233280 / 360)
-constexpr int FEC_DW = 13;              // LDS words per LDPC info group: d_g || d_g[0..56)
+constexpr int FEC_DW = 13;              // LDS words per LDPC info group (fused kernel): d_g || d_g[0..56)
+constexpr int FEC_DW_PASS = 16;         // chain LDPC pass: d_g || d_g[0..152), four windows without wrap
 constexpr int FEC_WG_PER_CU = 7;        // fused kernel: resident workgroups per CU (72-VGPR budget)
 constexpr int FEC_PASS_WG_PER_CU = 8;   // chain BB / LDPC passes (64-VGPR budget, 32 waves per CU)
 constexpr int FEC_BCH_JB = 2;           // nibble-table lookups in flight per lane in the BCH combine
-constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW * 150 + 12 * 30); // max over codes of 52 ngroups + 48 q
+constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW_PASS * 150 + 12 * 30); // max over codes of 64 ngroups + 48 q
 constexpr int BCH_ROWS = 128;           // bch_gemm_kernel: FEC blocks per workgroup (4 waves x 32)
 
 // dynamic LDS carve (bytes) of each FEC kernel kind: persistent tables (staged once; the
@@ -138,7 +139,7 @@ __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int 
   c.crcsh = c.crc8 + 256;
   c.crcsl = c.crcsh + 2048;                // BB pass: T^2, T^3, T^4 of the CRC-8 byte table (slicing by 4)
   c.prbs = c.crcsl + (kind == CARVE_BB ? 768 : 0);   // BB pass: the BB-scrambler PRBS words
-  const int bb_end = c.prbs + (kind == CARVE_BB ? ((kbch / 8 + 15) & ~15) : 0), ldpc_end = c.phase + 4 * (FEC_DW * (nbch / 360) + 12 * q);
+  const int bb_end = c.prbs + (kind == CARVE_BB ? ((kbch / 8 + 15) & ~15) : 0), ldpc_end = c.phase + 4 * ((kind == CARVE_LDPC ? FEC_DW_PASS : FEC_DW) * (nbch / 360) + 12 * q);
   c.total = kind == CARVE_BB ? bb_end : kind == CARVE_LDPC ? ldpc_end : (bb_end > ldpc_end ? bb_end : ldpc_end);
   return c;
 }
@@ -166,19 +167,20 @@ __device__ __forceinline__ uint8_t get_byte192(const uint64_t w[3], int lowbit) 
   return (uint8_t)(w[lowbit >> 6] >> (lowbit & 63));
 }
 
-// word k of LDPC info group g laid out for 32-bit rotation windows: big-endian bytes
-// (4k .. 4k+3) mod 45 of the group's 45 frame bytes (d_g || d_g[0..56))
-// (words 0..10 and 12 are four consecutive frame bytes: two aligned word reads and a byte align;
+// word k < DW of LDPC info group g laid out for 32-bit rotation windows: big-endian bytes
+// (4k .. 4k+3) mod 45 of the group's 45 frame bytes (d_g || d_g[0..32 DW - 360))
+// (words other than 11 are four consecutive frame bytes: two aligned word reads and a byte align;
 // word 11 wraps from byte 44 to bytes 0..2)
+template <int DW>
 __device__ __forceinline__ void ldpc_group_word(uint32_t *D, const uint8_t *frame, int g, int k) {
   const uint8_t *gb = frame + 45 * g;
   if (k == 11) {
-    D[g * FEC_DW + k] = ((uint32_t)gb[44] << 24) | ((uint32_t)gb[0] << 16) | ((uint32_t)gb[1] << 8) | (uint32_t)gb[2];
+    D[g * DW + k] = ((uint32_t)gb[44] << 24) | ((uint32_t)gb[0] << 16) | ((uint32_t)gb[1] << 8) | (uint32_t)gb[2];
     return;
   }
-  const int o = 45 * g + (k == 12 ? 3 : 4 * k);   // frame is 4-byte aligned
+  const int o = 45 * g + (k >= 12 ? 4 * k - 45 : 4 * k);   // frame is 4-byte aligned
   const uint32_t *fw = (const uint32_t *)frame;
-  D[g * FEC_DW + k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(fw[(o >> 2) + 1], fw[o >> 2], (uint32_t)(o & 3)));
+  D[g * DW + k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(fw[(o >> 2) + 1], fw[o >> 2], (uint32_t)(o & 3)));
 }
 
 // byte-table division of frame[lo, hi) (lo clamped at 0) into the P-bit remainder r; the next message
@@ -262,6 +264,7 @@ __device__ __forceinline__ uint32_t ldpc_window(const uint32_t *dg, int o) {   /
   const uint64_t win = ((uint64_t)dg[o >> 5] << 32) | dg[(o >> 5) + 1];
   return (uint32_t)(win >> (32 - (o & 31)));
 }
+template <int DW>
 __device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, const uint32_t *ents, const uint16_t *rp,
                                           int q, int t0, int nt) {
   for (int it = t0; it < q * 3; it += nt) {
@@ -271,14 +274,26 @@ __device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, con
 #pragma unroll 2
     for (int e = rp[a]; e < e1; e++) {
       const uint32_t ent = ents[e];
-      const uint32_t *dg = D + (ent >> 16) * FEC_DW;
+      const uint32_t *dg = D + (ent >> 16) * DW;
       int o = 32 * w0 - (int)(ent & 0xFFFF);   // window start (c - b) mod 360 for c = 32 w0
       o += o < 0 ? 360 : 0;
+      if (DW >= 16) {
+        // d_g || d_g[0..152): the four windows o + 32 k end by bit o + 128 < 512, so they are five
+        // consecutive words with no wrap
+        const int wi = o >> 5;
+        const uint32_t sh = 32u - (uint32_t)(o & 31);
+        uint32_t x[5];
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        acc[k] ^= ldpc_window(dg, o);
-        o += 32;
-        o -= o >= 360 ? 360 : 0;
+        for (int k = 0; k < 5; k++) x[k] = dg[wi + k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc[k] ^= (uint32_t)((((uint64_t)x[k] << 32) | x[k + 1]) >> sh);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          acc[k] ^= ldpc_window(dg, o);
+          o += 32;
+          o -= o >= 360 ? 360 : 0;
+        }
       }
     }
     if (w0 == 8) acc[3] &= 0xFF000000u;
@@ -291,11 +306,12 @@ __device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, con
 // accumulate as an inclusive prefix XOR over rows a (wave w scans word columns 3w..3w+2, 64 rows
 // per DPP wave scan plus the carry of the previous 64), then the exclusive bit-prefix of the column
 // parities along c.  Leaves p[a][c] at D + ngroups * FEC_DW (row a, 12 big-endian words).
+template <int DW>
 __device__ __forceinline__ uint32_t *fec_ldpc(const FecDev &d, uint32_t *D, int ngroups, const uint32_t *ents,
                                               const uint16_t *rowp, uint32_t *Wv, int tid) {
   const int lane = tid & 63, wave = tid >> 6, q = d.q;
-  uint32_t *cur = D + ngroups * FEC_DW;
-  ldpc_rows(D, cur, ents, rowp, q, tid, FEC_THREADS);
+  uint32_t *cur = D + ngroups * DW;
+  ldpc_rows<DW>(D, cur, ents, rowp, q, tid, FEC_THREADS);
   __syncthreads();
   for (int col = 3 * wave; col < 3 * wave + 3; col++) {
     uint32_t carry = 0;
@@ -591,10 +607,10 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
       const int ngroups = d.nbch / 360;
       for (int it = tid; it < ngroups * FEC_DW; it += FEC_THREADS) {
         const int g = it / FEC_DW;
-        ldpc_group_word(D, frame, g, it - g * FEC_DW);
+        ldpc_group_word<FEC_DW>(D, frame, g, it - g * FEC_DW);
       }
       __syncthreads();
-      const uint32_t *cur = fec_ldpc(d, D, ngroups, ents, (const uint16_t *)(smem + cv.rowp), (uint32_t *)(smem + cv.w), tid);
+      const uint32_t *cur = fec_ldpc<FEC_DW>(d, D, ngroups, ents, (const uint16_t *)(smem + cv.rowp), (uint32_t *)(smem + cv.w), tid);
       const int q = d.q;
       uint8_t *dst = io.out + (int64_t)bi * d.nldpc;
       for (int i = tid; i < d.nbch; i += FEC_THREADS) dst[i] = (frame[i >> 3] >> (7 - (i & 7))) & 1;
@@ -808,12 +824,12 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_ldpc_kern
     if (tid < (PB + 3) >> 2)
       for (int k = 0; k < 4 && 4 * tid + k < PB; k++) frame[L + 4 * tid + k] = (uint8_t)(par >> (8 * k));
     __syncthreads();
-    for (int it = tid; it < ngroups * FEC_DW; it += FEC_THREADS) {
-      const int g = it / FEC_DW;
-      ldpc_group_word(D, frame, g, it - g * FEC_DW);
+    for (int it = tid; it < ngroups * FEC_DW_PASS; it += FEC_THREADS) {
+      const int g = it / FEC_DW_PASS;
+      ldpc_group_word<FEC_DW_PASS>(D, frame, g, it - g * FEC_DW_PASS);
     }
     __syncthreads();
-    const uint32_t *cur = fec_ldpc(d, D, ngroups, ents, rowp, Wv, tid);
+    const uint32_t *cur = fec_ldpc<FEC_DW_PASS>(d, D, ngroups, ents, rowp, Wv, tid);
     auto parity_byte = [&](int m) -> uint32_t {
       if (d.parity_il) {
         const int a = m / 45, k = m - 45 * a;
@@ -878,7 +894,7 @@ static int fec_grid(int nblocks, int per_cu) {
 
 static bool fec_plan_fits(const FecDev &d) {
   // the LDS carve is sized for the standard codes, the BCH wave for 64 chunks: refuse anything else
-  return !(d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 52 * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
+  return !(d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 4 * FEC_DW_PASS * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
            (d.kbch - 80) / 8 + 218 > 16 * FEC_PRE * FEC_THREADS || ((d.kbch >> 3) + 15) / 16 > FEC_PRE * FEC_THREADS ||
            (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.chunk * 64 < d.kbch / 8);
 }
