@@ -171,16 +171,16 @@ __device__ __forceinline__ uint8_t get_byte192(const uint64_t w[3], int lowbit) 
 // (4k .. 4k+3) mod 45 of the group's 45 frame bytes (d_g || d_g[0..32 DW - 360))
 // (words other than 11 are four consecutive frame bytes: two aligned word reads and a byte align;
 // word 11 wraps from byte 44 to bytes 0..2)
-template <int DW>
-__device__ __forceinline__ void ldpc_group_word(uint32_t *D, const uint8_t *frame, int g, int k) {
+__device__ __forceinline__ uint32_t ldpc_group_val(const uint8_t *frame, int g, int k) {
   const uint8_t *gb = frame + 45 * g;
-  if (k == 11) {
-    D[g * DW + k] = ((uint32_t)gb[44] << 24) | ((uint32_t)gb[0] << 16) | ((uint32_t)gb[1] << 8) | (uint32_t)gb[2];
-    return;
-  }
+  if (k == 11) return ((uint32_t)gb[44] << 24) | ((uint32_t)gb[0] << 16) | ((uint32_t)gb[1] << 8) | (uint32_t)gb[2];
   const int o = 45 * g + (k >= 12 ? 4 * k - 45 : 4 * k);   // frame is 4-byte aligned
   const uint32_t *fw = (const uint32_t *)frame;
-  D[g * DW + k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(fw[(o >> 2) + 1], fw[o >> 2], (uint32_t)(o & 3)));
+  return __builtin_bswap32(__builtin_amdgcn_alignbyte(fw[(o >> 2) + 1], fw[o >> 2], (uint32_t)(o & 3)));
+}
+template <int DW>
+__device__ __forceinline__ void ldpc_group_word(uint32_t *D, const uint8_t *frame, int g, int k) {
+  D[g * DW + k] = ldpc_group_val(frame, g, k);
 }
 
 // byte-table division of frame[lo, hi) (lo clamped at 0) into the P-bit remainder r; the next message
@@ -824,9 +824,12 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_ldpc_kern
     if (tid < (PB + 3) >> 2)
       for (int k = 0; k < 4 && 4 * tid + k < PB; k++) frame[L + 4 * tid + k] = (uint8_t)(par >> (8 * k));
     __syncthreads();
-    for (int it = tid; it < ngroups * FEC_DW_PASS; it += FEC_THREADS) {
-      const int g = it / FEC_DW_PASS;
-      ldpc_group_word<FEC_DW_PASS>(D, frame, g, it - g * FEC_DW_PASS);
+    // four words of a group per item, one 16-byte LDS write (the frame words shared by neighbouring
+    // output words are read once)
+    for (int it = tid; it < ngroups * (FEC_DW_PASS / 4); it += FEC_THREADS) {
+      const int g = it >> 2, k0 = 4 * (it & 3);
+      *(uint4 *)(D + g * FEC_DW_PASS + k0) = make_uint4(ldpc_group_val(frame, g, k0), ldpc_group_val(frame, g, k0 + 1),
+                                                        ldpc_group_val(frame, g, k0 + 2), ldpc_group_val(frame, g, k0 + 3));
     }
     __syncthreads();
     const uint32_t *cur = fec_ldpc<FEC_DW_PASS>(d, D, ngroups, ents, rowp, Wv, tid);
