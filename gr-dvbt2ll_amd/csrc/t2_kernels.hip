@@ -305,23 +305,38 @@ __device__ __forceinline__ void ldpc_rows(const uint32_t *D, uint32_t *rowA, con
 // LDPC (ldpc_calculate, bbheader:625-646) of the info groups laid out in D: parity rows, the
 // accumulate as an inclusive prefix XOR over rows a (wave w scans word columns 3w..3w+2, 64 rows
 // per DPP wave scan plus the carry of the previous 64), then the exclusive bit-prefix of the column
-// parities along c.  Leaves p[a][c] at D + ngroups * FEC_DW (row a, 12 big-endian words).
-template <int DW>
+// parities along c.  Leaves p[a][c] at D + ngroups * DW (row a, 12 big-endian words); !APPLY_W leaves the
+// rows without the column-parity correction, word w of every row to be XORed with Wv[w] by the reader.
+template <int DW, bool APPLY_W = true>
 __device__ __forceinline__ uint32_t *fec_ldpc(const FecDev &d, uint32_t *D, int ngroups, const uint32_t *ents,
                                               const uint16_t *rowp, uint32_t *Wv, int tid) {
   const int lane = tid & 63, wave = tid >> 6, q = d.q;
   uint32_t *cur = D + ngroups * DW;
   ldpc_rows<DW>(D, cur, ents, rowp, q, tid, FEC_THREADS);
   __syncthreads();
-  for (int col = 3 * wave; col < 3 * wave + 3; col++) {
-    uint32_t carry = 0;
-    for (int a0 = 0; a0 < q; a0 += 64) {
-      const int a = a0 + lane;
-      uint32_t v = a < q ? cur[a * 12 + col] : 0u;
-      v = wave_prefix_xor(v) ^ carry;
-      if (a < q) cur[a * 12 + col] = v;
-      carry = rd_lane_u32(v, 63);
+  {
+    // q <= 128 (two 64-row chunks): the wave's six column chunks are read before any is written (an LDS
+    // read cannot move past an LDS write it may alias: one round trip instead of six)
+    uint32_t v[3][2];
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int a = 64 * h + lane;
+        v[c][h] = a < q ? cur[a * 12 + 3 * wave + c] : 0u;
+      }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      v[c][0] = wave_prefix_xor(v[c][0]);
+      v[c][1] = wave_prefix_xor(v[c][1]) ^ rd_lane_u32(v[c][0], 63);
     }
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int a = 64 * h + lane;
+        if (a < q) cur[a * 12 + 3 * wave + c] = v[c][h];
+      }
   }
   __syncthreads();
   if (tid < 64) {   // word w of the last row by lane w < 12: in-word prefix, carry = parity of words < w
@@ -334,8 +349,23 @@ __device__ __forceinline__ uint32_t *fec_ldpc(const FecDev &d, uint32_t *D, int 
     if (tid < 12) Wv[tid] = tid == 11 ? ex & 0xFF000000u : ex;
   }
   __syncthreads();
-  for (int it = tid; it < q * 12; it += FEC_THREADS) cur[it] ^= Wv[it % 12];
-  __syncthreads();
+  if (APPLY_W) {
+    // read-modify-write of the rows in batches of four per thread (reads first, then writes)
+    for (int it0 = 0; it0 < q * 12; it0 += 4 * FEC_THREADS) {
+      uint32_t x[4];
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const int it = it0 + tid + h * FEC_THREADS;
+        x[h] = it < q * 12 ? cur[it] ^ Wv[it % 12] : 0u;
+      }
+#pragma unroll
+      for (int h = 0; h < 4; h++) {
+        const int it = it0 + tid + h * FEC_THREADS;
+        if (it < q * 12) cur[it] = x[h];
+      }
+    }
+    __syncthreads();
+  }
   return cur;
 }
 
@@ -897,7 +927,7 @@ static int fec_grid(int nblocks, int per_cu) {
 
 static bool fec_plan_fits(const FecDev &d) {
   // the LDS carve is sized for the standard codes, the BCH wave for 64 chunks: refuse anything else
-  return !(d.nent > FEC_MAX_ENT || d.nbch > 8 * FEC_FRAME_BYTES || 4 * FEC_DW_PASS * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
+  return !(d.nent > FEC_MAX_ENT || d.q > 128 || d.nbch > 8 * FEC_FRAME_BYTES || 4 * FEC_DW_PASS * (d.nbch / 360) + 48 * d.q > FEC_LDPC_BYTES ||
            (d.kbch - 80) / 8 + 218 > 16 * FEC_PRE * FEC_THREADS || ((d.kbch >> 3) + 15) / 16 > FEC_PRE * FEC_THREADS ||
            (d.P != 192 && d.P != 168 && d.P != 160 && d.P != 128) || d.chunk * 64 < d.kbch / 8);
 }
@@ -1686,15 +1716,22 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const uint32_t s = o0 + 8u * min(g0 + (uint32_t)(tid + NT * u), lasto);
+        // the octet's eight constellation lookups first, then its eight bin writes: in program order
+        // the compiler cannot move an LDS read past an LDS write it may alias, so lookup / write pairs
+        // would serialise into eight LDS round trips
+        float2 v[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const uint32_t cw = e < 2 ? c[u].x : e < 4 ? c[u].y : e < 6 ? c[u].z : c[u].w;
+          const uint32_t pr = cw >> (16 * (e & 1));
+          v[e] = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+        }
 #pragma unroll
         for (int e = 0; e < 8; e++) {
           const uint32_t bw = e < 2 ? b[u].x : e < 4 ? b[u].y : e < 6 ? b[u].z : b[u].w;
-          const uint32_t cw = e < 2 ? c[u].x : e < 4 ? c[u].y : e < 6 ? c[u].z : c[u].w;
           const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the group
-          const uint32_t pr = cw >> (16 * (e & 1));
           const bool in_run = s + (uint32_t)e - r0 < rn;
-          const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-          lds[in_run ? bin : dummy] = v;
+          lds[in_run ? bin : dummy] = v[e];
         }
       }
     }
@@ -1712,16 +1749,23 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
       c[u] = ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u);
     }
 #pragma unroll
-    for (int u = 0; u < SQ; u++) {
-      const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
+    for (int u = 0; u < SQ; u += 2) {
+      // two quads' lookups, then their writes (see the 32K path)
+      float2 v[8];
 #pragma unroll
-      for (int e = 0; e < 4; e++) {
-        const uint32_t bw = e < 2 ? b[u].x : b[u].y, cw = e < 2 ? c[u].x : c[u].y;
-        const uint32_t bin = (bw >> (16 * (e & 1))) & 0xFFFFu;   // padded, within the group
+      for (int e = 0; e < 8; e++) {
+        const uint32_t cw = (e & 2) ? c[u + (e >> 2)].y : c[u + (e >> 2)].x;
         const uint32_t pr = cw >> (16 * (e & 1));
-        const bool in_run = s + (uint32_t)e - r0 < rn;
-        const float2 v = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
-        lds[in_run ? bin : dummy] = v;
+        v[e] = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const int uu = u + (e >> 2), ee = e & 3;
+        const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * uu), lastq);
+        const uint32_t bw = (ee & 2) ? b[uu].y : b[uu].x;
+        const uint32_t bin = (bw >> (16 * (ee & 1))) & 0xFFFFu;   // padded, within the group
+        const bool in_run = s + (uint32_t)ee - r0 < rn;
+        lds[in_run ? bin : dummy] = v[e];
       }
     }
   }
