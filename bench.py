@@ -24,6 +24,7 @@ process touches the GPU), serial_1_stream (that pass's rate) and cpu_baseline (t
 restatement, single thread, bounded sample).
 """
 import argparse
+import datetime
 import glob
 import json
 import os
@@ -68,6 +69,11 @@ def parse():
                          "ordered gather path with placeholder frames (CPU tensors, gloo)")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default nccl = RCCL; gloo for "
                                                     "--dry-run)")
+    ap.add_argument("--rank-timeout", type=float, default=1500.0,
+                    help="spawned ranks: seconds before the parent ends a run that has not finished")
+    ap.add_argument("--init-timeout", type=float, default=600.0,
+                    help="seconds init_process_group and the first barrier may take")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)   # tests: this rank exits at init
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -424,18 +430,43 @@ def spawn_ranks(args):
         env0["DVBT2LL_BENCH_PMC_JSON"] = path
     port = _free_port()
     procs = []
+    outs = [tempfile.TemporaryFile(mode="w+") for _ in range(n)]
     for r in range(n):
         env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DVBT2LL_BENCH_SPAWNED="1")
         procs.append(subprocess.Popen([sys.executable, str(ROOT / "bench.py")] + sys.argv[1:], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
-    out0 = procs[0].communicate()[0]
-    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+                                      stdout=outs[r], text=True))
+    # poll every rank: the first one to exit non-zero ends the run (the survivors would otherwise sit
+    # in init_process_group or a barrier until the backend timeout); this parent never touches the GPU,
+    # so terminating its children is safe
+    deadline = time.monotonic() + args.rank_timeout
+    rcs = [None] * n
+    while any(c is None for c in rcs):
+        rcs = [p.poll() for p in procs]
+        failed = [c for c in rcs if c not in (None, 0)]
+        if failed or time.monotonic() > deadline:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            rcs = [p.returncode for p in procs]
+            if not failed:
+                sys.stderr.write("bench.py: ranks still running after %.0f s (--rank-timeout)\n" % args.rank_timeout)
+            break
+        time.sleep(0.1)
     if env0.get("DVBT2LL_BENCH_PMC_JSON"):
         os.unlink(env0["DVBT2LL_BENCH_PMC_JSON"])
-    if any(rcs):
+    outs[0].seek(0)
+    out0 = outs[0].read()
+    if any(rcs) or any(c is None for c in rcs):
         sys.stderr.write("bench.py: rank exit codes %s\n" % rcs)
-        return max(1, max(abs(c) for c in rcs))
+        sys.stderr.write(out0[-2000:])
+        return max([1] + [abs(c) for c in rcs if c])
     for line in out0.splitlines():        # rank 0's JSON line to stdout, its other output to stderr
         (sys.stdout if line.startswith("{") else sys.stderr).write(line + "\n")
     sys.stdout.flush()
@@ -449,8 +480,10 @@ def dry_run(args, rank, world):
     import torch
     import torch.distributed as dist
     from dvbt2ll.distributed import frame_range, gather_frames
+    if rank == args.fail_rank:
+        raise SystemExit("bench.py: rank %d made to fail at init (--fail-rank)" % rank)
     if world > 1:
-        dist.init_process_group(args.backend or "gloo")
+        dist.init_process_group(args.backend or "gloo", timeout=datetime.timedelta(seconds=args.init_timeout))
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     B, per = min(args.frames, 16), 1024
     first, count = frame_range(world * B, rank, world)
@@ -517,7 +550,10 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local_rank))
+        if rank == args.fail_rank:
+            raise SystemExit("bench.py: rank %d made to fail at init (--fail-rank)" % rank)
+        dist.init_process_group(args.backend or "nccl", device_id=torch.device("cuda", local_rank),
+                                timeout=datetime.timedelta(seconds=args.init_timeout))
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     B = args.frames
     chain = dvbt2ll.Chain(cfg, max_frames=B, device=local_rank)

@@ -719,6 +719,8 @@ typedef float bch_v16f __attribute__((ext_vector_type(16)));
 // parity ((int) sum & 1) is packed by wave ballots into 8 words per block (bytes in transmission
 // order) and XORed into bch_part[b * 8] (zeroed by the BB pass).
 constexpr int BCH_WG_PER_CU = 3;
+// s_waitcnt immediate for vmcnt(0) alone on gfx9: vmcnt [3:0] + [15:14] = 0, expcnt [6:4] = 7, lgkmcnt [11:8] = 15
+constexpr int BCH_WAIT_VMCNT0 = 0x0F70;
 template <int NT>
 __global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) uint4 bsm[];
@@ -754,7 +756,10 @@ __global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(Fe
     __syncthreads();   // the previous segment's epilogue has read its parity words out of buffer 0
     stage(q0, 0);
     uint4 a = live ? msg[2 * q0] : make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();   // (its vmcnt(0) retires the DMA)
+    // every wave retires its own LDS-DMA before the barrier, so after it all slices have landed (the
+    // workgroup-scope fence of __syncthreads does not promise a vmcnt(0) on gfx950)
+    __builtin_amdgcn_s_waitcnt(BCH_WAIT_VMCNT0);
+    __syncthreads();
     for (int q = q0; q < q1; q++) {
       const int cur = (q - q0) & 1;
       uint4 an = make_uint4(0u, 0u, 0u, 0u);
@@ -787,6 +792,7 @@ __global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(Fe
 #pragma unroll
         for (int t = 0; t < NT; t++) bc[t] = bx[t];
       }
+      __builtin_amdgcn_s_waitcnt(BCH_WAIT_VMCNT0);   // chunk q + 1's DMA, as above
       __syncthreads();
       a = an;
     }

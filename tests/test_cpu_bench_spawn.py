@@ -47,3 +47,16 @@ def test_bench_rejects_world_mismatch():
     """under an external launcher WORLD_SIZE must equal --gpus"""
     r = _bench("--gpus", "2", "--dry-run", env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_rank_failure_fails_fast():
+    """a rank that dies at init ends the whole run: the parent polls every rank, terminates the
+    survivors (blocked in init_process_group / the first barrier) and exits non-zero"""
+    import time
+    t0 = time.monotonic()
+    r = _bench("--gpus", "3", "--dry-run", "--fail-rank", "1", "--steps", "2", "--warmup", "1")
+    dt = time.monotonic() - t0
+    assert r.returncode != 0, r.stdout
+    assert "rank exit codes" in r.stderr and "--fail-rank" in r.stderr
+    assert dt < 30, dt
+    assert not r.stdout.strip()                    # no JSON line from a failed run
