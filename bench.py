@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--no-sc16", action="store_true", help="skip the secondary sc16-output timing")
     ap.add_argument("--no-latency", action="store_true", help="skip the one-frame latency calls")
     ap.add_argument("--no-blocks", action="store_true", help="skip the per-block general_work timing")
+    ap.add_argument("--no-mplp", action="store_true", help="skip the secondary multi-PLP (2-PLP 32K frame) timing")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--shard", choices=("frames", "streams"), default="frames",
                     help="frames: one TS stream, disjoint frame ranges per rank; streams: an independent "
@@ -399,6 +400,51 @@ def one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per):
     return latency
 
 
+def mplp_rate(frames, steps, warmup, name="mplp2_32k"):
+    """secondary (not `value`): a T2 frame carrying two Type-1 data PLPs of cfg3's
+    frame geometry -- 100 FEC blocks of 256-QAM 3/5 rotated + 70 of 64-QAM 2/3, each PLP its own TS --
+    through the fused chain (dvbt2ll_chain_run_plps), TS resident in HBM, K steps on one stream"""
+    import numpy as np
+    import torch
+    import dvbt2ll
+    from dvbt2ll.configs import MPLP_CONFIGS, ts_for_frames
+    m = MPLP_CONFIGS[name]
+    ch = dvbt2ll.Chain(m, max_frames=frames)
+    per = ch.iq_per_frame
+    bufs, bases, lens = [], [], []
+    for k, p in enumerate(m.plps):
+        ts, base = ts_for_frames(p, 0, frames, seed=k + 1)
+        bufs.append(torch.from_numpy(ts).cuda())
+        bases.append(base)
+        lens.append(len(ts))
+    iq = torch.empty((frames * per, 2), dtype=torch.float32, device="cuda")
+    st = torch.cuda.Stream()
+    ptrs = [b.data_ptr() for b in bufs]
+
+    def step():
+        ch.run_plps(ptrs, bases, lens, 0, frames, iq.data_ptr(), st.cuda_stream)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ch.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ms, n = ch.timing()
+    ch.set_timing(False)
+    fec = frames * sum(p.fecblocks for p in m.plps) * steps
+    return {"value": frames * per * steps / dt / 1e6, "unit": "Msamples/s", "ms_per_step": dt / steps * 1e3,
+            "fec_blocks_per_sec": fec / dt, "frames_per_step": frames, "plps": m.nplp,
+            "workload": m.name + ": %d T2 frames per step, PLPs %s" % (frames, [
+                "%d FEC blocks %s" % (p.fecblocks, ("QPSK", "16QAM", "64QAM", "256QAM")[p.constellation])
+                for p in m.plps]),
+            "stage_avg_launch_ms": {k: ms[i] / max(1, n[i]) for i, k in enumerate(("fec", "map", "ofdm"))},
+            "note": "secondary: multi-PLP frames (parity unpinned beyond one PLP: the reference carries one); "
+                    "one stream, no cross-step overlap; not `value`"}
+
+
 def metric_for(cfg_name):
     """BASELINE.json's metric string for cfg3 (the configuration it is quoted on); the same metric
     named by its configuration for the others"""
@@ -669,6 +715,9 @@ def main():
     if not args.no_blocks and world == 1 and rank == 0:
         blocks = per_block_rate(cfg)
         blocks["pinned"] = per_block_rate(cfg, pinned=True)
+    mplp = None
+    if not args.no_mplp and world == 1 and rank == 0 and args.config == "cfg3":
+        mplp = mplp_rate(B, args.steps, args.warmup)
     gathered = None
     if dist and args.shard == "frames" and NS == 1:
         # secondary (not `value`): each step followed by the ordered IQ gather to rank 0, the
@@ -775,6 +824,8 @@ def main():
             out["latency_1_frame"] = latency
         if gathered:
             out["gather_to_rank0"] = gathered
+        if mplp:
+            out["mplp_2plp_32k"] = mplp
         if blocks:
             out["per_block_general_work"] = blocks
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only (host cores are shared)

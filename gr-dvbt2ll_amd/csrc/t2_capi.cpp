@@ -122,6 +122,7 @@ struct FecTables {
     dev.inband = inband ? 1 : 0;
     dev.fec_blocks = fecblocks > 0 ? fecblocks : 1;
     dev.ts_rate = tsrate;
+    dev.matype = MATYPE_SIS;
     return 0;
   }
 };
@@ -291,6 +292,11 @@ extern "C" int dvbt2ll_bbheaderbch_general_work(dvbt2ll_bbheaderbch *h, int nout
 extern "C" int64_t dvbt2ll_bbheaderbch_sync_errors(const dvbt2ll_bbheaderbch *h) {
   return h ? (int64_t)h->sync_err_host : 0;
 }
+extern "C" int dvbt2ll_bbheaderbch_set_isi(dvbt2ll_bbheaderbch *h, int isi) {
+  if (!h || isi < 0 || isi > 255) return DVBT2LL_EINVAL;
+  h->fec.dev.matype = MATYPE_MIS | isi;   // bbheader:288-298
+  return DVBT2LL_OK;
+}
 extern "C" void dvbt2ll_bbheaderbch_destroy(dvbt2ll_bbheaderbch *h) { delete h; }
 
 // ============================================================================ ldpc
@@ -456,6 +462,79 @@ extern "C" int dvbt2ll_framemapperfint_general_work(dvbt2ll_framemapperfint *h, 
 }
 extern "C" void dvbt2ll_framemapperfint_destroy(dvbt2ll_framemapperfint *h) { delete h; }
 
+// ============================================================================ framemapper, multi-PLP
+static bool mplp_to_plan(const dvbt2ll_mplp_params &m, FmParams &fm, std::vector<PlpParams> &plps,
+                         std::vector<int> &tsrate);
+
+struct dvbt2ll_framemapper_mplp {
+  DeviceCtx ctx;
+  FramePlan plan;
+  L1Tables l1;
+  DevBuf map, aux, din, dout;   // din: one frame of every PLP's cells, PLP 0 first
+  int t2_frame_num = 0;
+};
+extern "C" int dvbt2ll_framemapper_mplp_create(const dvbt2ll_mplp_params *p, int device, dvbt2ll_framemapper_mplp **out) {
+  if (!p || !out) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  FmParams fm;
+  std::vector<PlpParams> plps;
+  std::vector<int> tsrate;
+  if (!mplp_to_plan(*p, fm, plps, tsrate)) return DVBT2LL_EINVAL;
+  std::unique_ptr<dvbt2ll_framemapper_mplp> h(new (std::nothrow) dvbt2ll_framemapper_mplp());
+  if (!h) return DVBT2LL_ENOMEM;
+  if (build_frame_mplp(fm, plps, h->plan)) return DVBT2LL_EINVAL;
+  int r = h->ctx.init(device);
+  if (r) return r;
+  if ((r = upload(h->map, h->plan.gather_in)) || (r = upload(h->aux, h->plan.aux)) || (r = h->l1.init(h->plan)))
+    return r;
+  *out = h.release();
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_framemapper_mplp_output_multiple(const dvbt2ll_framemapper_mplp *h) { return h ? h->plan.M : 0; }
+extern "C" int dvbt2ll_framemapper_mplp_stream_items(const dvbt2ll_framemapper_mplp *h, int plp) {
+  return h && plp >= 0 && plp < h->plan.nplp ? h->plan.plp[plp].S : 0;
+}
+extern "C" int dvbt2ll_framemapper_mplp_forecast(const dvbt2ll_framemapper_mplp *h, int nout, int *nin) {
+  if (!h || !nin) return DVBT2LL_EINVAL;
+  for (int k = 0; k < h->plan.nplp; k++) nin[k] = h->plan.plp[k].S * (nout / h->plan.M);   // framemapper:1942-1946
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_framemapper_mplp_general_work(dvbt2ll_framemapper_mplp *h, int nout, const int *nin,
+                                                     const void *const *in, void *out, int *consumed) {
+  if (!h || nout < 0 || (nout && (!in || !out || !nin))) return DVBT2LL_EINVAL;
+  const FramePlan &f = h->plan;
+  if (consumed)
+    for (int k = 0; k < f.nplp; k++) consumed[k] = 0;
+  if (nout < f.M) return 0;
+  for (int k = 0; k < f.nplp; k++)
+    if (!in[k] || nin[k] < f.plp[k].S) return DVBT2LL_ESHORT;
+  // one T2 frame per call, one frame of every port (framemapper:2147)
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  if (h->din.ensure((size_t)f.S * 8) || h->dout.ensure((size_t)f.M * 8)) return DVBT2LL_ENOMEM;
+  for (int k = 0; k < f.nplp; k++)
+    HIP_TRY(hipMemcpyAsync(h->din.as<float2>() + f.plp[k].start, in[k], (size_t)f.plp[k].S * 8, hipMemcpyHostToDevice,
+                           h->ctx.stream));
+  L1IO lio{};
+  lio.out = h->aux.as<float2>() + AUX_L1PRE + 1840;
+  lio.first_frame = h->t2_frame_num;
+  lio.nframes = 1;
+  HIP_TRY(launch_l1post(h->l1.dev, lio, h->ctx.stream));
+  GatherIO io{};
+  io.in = h->din.as<float2>();
+  io.out = h->dout.as<float2>();
+  io.map = h->map.as<int32_t>();
+  io.aux = h->aux.as<float2>();
+  io.M = f.M;
+  HIP_TRY(launch_gather(io, h->ctx.stream));
+  HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)f.M * 8, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  h->t2_frame_num = (h->t2_frame_num + 1) % f.t2frames;
+  if (consumed)
+    for (int k = 0; k < f.nplp; k++) consumed[k] = f.plp[k].S;
+  return f.M;
+}
+extern "C" void dvbt2ll_framemapper_mplp_destroy(dvbt2ll_framemapper_mplp *h) { delete h; }
+
 // ============================================================================ pilotgenp1insert
 static PgParams to_pg(const dvbt2ll_pilotgenp1insert_params &p) {
   return PgParams{p.carriermode, p.fftsize, p.pilotpattern, p.guardinterval, p.numdatasyms, p.paprmode, p.version,
@@ -558,40 +637,60 @@ extern "C" int dvbt2ll_pilotgenp1insert_debug_carriers(dvbt2ll_pilotgenp1insert 
 extern "C" void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h) { delete h; }
 
 // ============================================================================ chain
-// one instantiated hipGraph of the chain's five kernels (FEC BB pass -> BCH matrix-core pass ->
-// LDPC pass -> map -> ofdm), per (nframes, IQ format, slot): captured once from the ordinary launch
-// path, then every call rewrites the kernel nodes' arguments (hipGraphExecKernelNodeSetParams) and
-// launches the graph
+// One PLP of the fused chain: its FEC and map tables, the cell-interleaver / time-interleaver store
+// tables, and per buffer slot its packed codewords and BCH parities.  A single-PLP chain (the
+// reference's frame) has one.
+struct ChainPlp {
+  FecTables fec;
+  MapTables map;
+  DevBuf perm, shift, part;
+  DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], bpart[DVBT2LL_CHAIN_MAX_SLOTS];
+  int64_t cw_stride = 0;
+  int64_t ts_per_frame = 0;   // payload bytes per frame (NM positions; HEM: before sync-byte removal)
+  int pay = 0, F = 0, inputmode = 0, inband = 0;
+};
+
+// instantiated hipGraphs of the chain's kernels (per PLP: FEC BB pass, BCH matrix-core pass, LDPC pass;
+// per PLP: map (PLP 0's launch also generates the L1-post); OFDM) for one (nframes, IQ format, slot),
+// captured once from the ordinary launch path into a ring of instantiations.  A call takes the next
+// ring entry, waits for it only if it is still in flight, rewrites its kernel nodes' arguments
+// (hipGraphExecKernelNodeSetParams) and launches it.
 struct ChainGraph {
   int nframes = 0, fmt = -1, slot = -1;
   hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-  static constexpr int NK = 5;
-  hipGraphNode_t node[NK] = {};
-  hipKernelNodeParams base[NK] = {};
+  std::vector<hipGraphNode_t> node;            // kernel nodes in launch order
+  std::vector<hipKernelNodeParams> base;
+  hipGraphExec_t exec[DVBT2LL_CHAIN_GRAPH_RING] = {};
+  hipEvent_t done[DVBT2LL_CHAIN_GRAPH_RING] = {};
+  bool used[DVBT2LL_CHAIN_GRAPH_RING] = {};
+  int next = 0;
   ~ChainGraph() {
-    if (exec) (void)hipGraphExecDestroy(exec);
+    for (auto &e : exec)
+      if (e) (void)hipGraphExecDestroy(e);
+    for (auto &e : done)
+      if (e) (void)hipEventDestroy(e);
     if (graph) (void)hipGraphDestroy(graph);
   }
 };
 
 struct dvbt2ll_chain {
   DeviceCtx ctx;
-  dvbt2ll_chain_params p{};
-  FecTables fec;
-  MapTables map;
+  dvbt2ll_chain_params p{};   // single-PLP create parameters (PLP 0's for a multi-PLP chain)
+  int nplp = 1;
+  std::vector<std::unique_ptr<ChainPlp>> plps;
   FramePlan frame;
   PilotPlan pilot;
   OfdmTables ofdm;
-  DevBuf aux, perm, shift, inv, sym_d0, sym_n, sym_n0, part, ts_tmp, iq_tmp;
+  DevBuf aux, inv, sym_d0, sym_n, sym_n0, ts_tmp, iq_tmp;
   DevBuf abin, aval, aind, agrp, azr;   // non-data bins as compact lists (t2_plan.h AuxLists)
+  DevBuf plp_bnd, plp_qbase, qam_all;   // multi-PLP frames: slot ranges per PLP, the PLPs' constellations
+  std::vector<int32_t> plp_bnd_host;
+  std::vector<int> qbase_host;
   DevBuf sync_err;                      // TS sync bytes != 0x47 consumed by run calls (bbheader:675, 703)
-  // intermediate buffer slots (codewords, index pairs): run calls take them round-robin, so
-  // calls issued on different streams overlap; a slot reused on another stream first waits for
-  // its previous run (slot_done) -- see dvbt2ll_chain_set_slots
-  DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], pairs[DVBT2LL_CHAIN_MAX_SLOTS];
-  // BCH parities of the matrix-core pass (FecIO::bch_part): blocks x BCH_PART_WORDS
-  DevBuf bpart[DVBT2LL_CHAIN_MAX_SLOTS];
+  // intermediate buffer slots (index pairs, L1-post cells; the PLPs' codewords): run calls take them
+  // round-robin, so calls issued on different streams overlap; a slot reused on another stream first
+  // waits for its previous run (slot_done) -- see dvbt2ll_chain_set_slots
+  DevBuf pairs[DVBT2LL_CHAIN_MAX_SLOTS];
   // per-frame L1-post cells of a run (l1post_kernel -> the OFDM kernel's indirect aux entries)
   L1Tables l1;
   DevBuf l1buf[DVBT2LL_CHAIN_MAX_SLOTS];
@@ -606,10 +705,7 @@ struct dvbt2ll_chain {
   std::vector<std::unique_ptr<ChainGraph>> graphs;
   int max_frames = 0;
   int64_t pair_stride = 0;   // pairs buffer: frame k's slots at k * pair_stride (multiple of 8)
-  int64_t cw_stride = 0;
   int64_t iq_per_frame = 0;
-  int64_t ts_per_frame = 0;
-  int pay = 0;
   // stage timing: 4 events per run (start, after fec, after map + L1-post, after ofdm) recorded
   // on the launch stream without host synchronisation; folded into ms[] by get_timing()
   // (stages 0 fec, 1 map, 2 ofdm; stage 3 is reserved and stays 0)
@@ -651,25 +747,25 @@ struct dvbt2ll_chain {
     evused = 0;
     return st;
   }
-  // the chain's kernels on stream s: FEC (three passes), map (its extra workgroups generate the
-  // frames' L1-post cells), OFDM.  ev1, ev2 (timing): recorded after the FEC passes and the map kernel
-  hipError_t launch_chain(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, hipStream_t s,
+  // the chain's kernels on stream s: every PLP's FEC (three passes), every PLP's map (PLP 0's launch has
+  // the extra workgroups that generate the frames' L1-post cells), OFDM.  ev1, ev2 (timing): recorded
+  // after the FEC passes and the map kernels
+  hipError_t launch_chain(const L1IO &lio, const FecIO *fio, const MapIO *mio, const OfdmIO &oio, hipStream_t s,
                           hipEvent_t ev1, hipEvent_t ev2) {
-    hipError_t e = launch_fec(FEC_TS_TO_TEMPU, fec.dev, fio, s);
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < nplp && e == hipSuccess; k++) e = launch_fec(FEC_TS_TO_TEMPU, plps[k]->fec.dev, fio[k], s);
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, s);
-    if (e == hipSuccess) e = launch_map(map.dev, mio, s, &l1.dev, &lio);
+    for (int k = 0; k < nplp && e == hipSuccess; k++)
+      e = k == 0 ? launch_map(plps[k]->map.dev, mio[k], s, &l1.dev, &lio) : launch_map(plps[k]->map.dev, mio[k], s);
     if (e == hipSuccess && ev2) e = hipEventRecord(ev2, s);
     if (e == hipSuccess) e = launch_ofdm(ofdm.dev, oio, s);
     return e;
   }
-  // capture the launches once per (nframes, format, slot) on a private stream, then per call
-  // rewrite the kernel nodes' arguments and launch the instantiated graph on s.  An exec is only
-  // re-armed after its previous launch has completed (host wait on the slot's completion event,
-  // recorded after every run on the slot), so no in-flight launch ever sees arguments rewritten
-  // under it; with several slots the calls still overlap on the device
-  int graph_launch(const L1IO &lio, const FecIO &fio, const MapIO &mio, const OfdmIO &oio, int nframes, int slot,
+  // kernel nodes per run: 3 FEC passes and a map per PLP, one OFDM
+  int graph_nodes() const { return 4 * nplp + 1; }
+  int graph_launch(const L1IO &lio, const FecIO *fio, const MapIO *mio, const OfdmIO &oio, int nframes, int slot,
                    hipStream_t s) {
-    const int nk = ChainGraph::NK;   // fec BB, BCH, LDPC passes (FecDev, FecIO), map (+ L1-post), ofdm
+    const int nk = graph_nodes();
     ChainGraph *g = nullptr;
     for (auto &c : graphs)
       if (c->nframes == nframes && c->fmt == ofdm.dev.fmt && c->slot == slot) g = c.get();
@@ -697,16 +793,14 @@ struct dvbt2ll_chain {
         if (t == hipGraphNodeTypeKernel) kn.push_back(nd);
       }
       if ((int)kn.size() != nk) return DVBT2LL_EDEVICE;
-      auto ndeps = [&](hipGraphNode_t nd, size_t &k) -> int {
-        HIP_TRY(hipGraphNodeGetDependencies(nd, nullptr, &k));
-        return 0;
-      };
+      c->node.assign(nk, nullptr);
+      c->base.assign(nk, hipKernelNodeParams{});
       // order: the root (no dependencies), then the node depending on it, and so on
       hipGraphNode_t prev = nullptr;
       for (int k = 0; k < nk; k++) {
         for (auto nd : kn) {
           size_t nd_n = 0;
-          if (ndeps(nd, nd_n)) return DVBT2LL_EDEVICE;
+          HIP_TRY(hipGraphNodeGetDependencies(nd, nullptr, &nd_n));
           bool ok = false;
           if (k == 0) {
             ok = nd_n == 0;
@@ -722,34 +816,52 @@ struct dvbt2ll_chain {
         prev = c->node[k];
         HIP_TRY(hipGraphKernelNodeGetParams(c->node[k], &c->base[k]));
       }
-      HIP_TRY(hipGraphInstantiate(&c->exec, c->graph, nullptr, nullptr, 0));
+      for (int r = 0; r < DVBT2LL_CHAIN_GRAPH_RING; r++) {
+        HIP_TRY(hipGraphInstantiate(&c->exec[r], c->graph, nullptr, nullptr, 0));
+        HIP_TRY(hipEventCreateWithFlags(&c->done[r], hipEventDisableTiming));
+      }
       g = c.get();
       graphs.push_back(std::move(c));
     }
-    if (slot_used[slot]) HIP_TRY(hipEventSynchronize(slot_done[slot]));
-    L1Dev ld = l1.dev;
-    FecDev fd = fec.dev;
-    MapDev md = map.dev;
+    // the ring's next instantiation; the host waits only if it is still in flight (every entry of
+    // the ring is), so consecutive calls never wait for each other below that depth
+    const int r = g->next;
+    g->next = (r + 1) % DVBT2LL_CHAIN_GRAPH_RING;
+    if (g->used[r]) HIP_TRY(hipEventSynchronize(g->done[r]));
+    L1Dev ld = l1.dev, ld0{};   // PLP 0's map launch generates the L1-post, the others carry none
+    L1IO li = lio, li0{};
     OfdmDev od = ofdm.dev;
-    L1IO li = lio;
-    FecIO fi = fio;
-    MapIO mi = mio;
     OfdmIO oi = oio;
-    void *a0[2] = {&fd, &fi}, *a1[4] = {&md, &mi, &ld, &li}, *a2[2] = {&od, &oi};
-    void **args[ChainGraph::NK] = {a0, a0, a0, a1, a2};
+    std::vector<FecDev> fd(nplp);
+    std::vector<FecIO> fi(fio, fio + nplp);
+    std::vector<MapDev> md(nplp);
+    std::vector<MapIO> mi(mio, mio + nplp);
+    std::vector<std::vector<void *>> args;
+    for (int k = 0; k < nplp; k++) {
+      fd[k] = plps[k]->fec.dev;
+      md[k] = plps[k]->map.dev;
+    }
+    for (int k = 0; k < nplp; k++)
+      for (int pass = 0; pass < 3; pass++) args.push_back({&fd[k], &fi[k]});
+    for (int k = 0; k < nplp; k++) args.push_back({&md[k], &mi[k], k ? &ld0 : &ld, k ? &li0 : &li});
+    args.push_back({&od, &oi});
     for (int k = 0; k < nk; k++) {
       hipKernelNodeParams p = g->base[k];
-      p.kernelParams = args[k];
+      p.kernelParams = args[k].data();
       p.extra = nullptr;
-      HIP_TRY(hipGraphExecKernelNodeSetParams(g->exec, g->node[k], &p));
+      HIP_TRY(hipGraphExecKernelNodeSetParams(g->exec[r], g->node[k], &p));
     }
-    HIP_TRY(hipGraphLaunch(g->exec, s));
+    HIP_TRY(hipGraphLaunch(g->exec[r], s));
+    HIP_TRY(hipEventRecord(g->done[r], s));
+    g->used[r] = true;
     return 0;
   }
   int alloc_slot(int k) {
-    if (cw[k].ensure((size_t)frame.F * max_frames * cw_stride) ||
-        bpart[k].ensure((size_t)frame.F * max_frames * BCH_PART_WORDS * sizeof(uint32_t)) ||
-        pairs[k].ensure((size_t)pair_stride * max_frames * 2) || l1buf[k].ensure((size_t)l1_stride * max_frames * 8))
+    for (auto &pl : plps)
+      if (pl->cw[k].ensure((size_t)pl->F * max_frames * pl->cw_stride) ||
+          pl->bpart[k].ensure((size_t)pl->F * max_frames * BCH_PART_WORDS * sizeof(uint32_t)))
+        return DVBT2LL_ENOMEM;
+    if (pairs[k].ensure((size_t)pair_stride * max_frames * 2) || l1buf[k].ensure((size_t)l1_stride * max_frames * 8))
       return DVBT2LL_ENOMEM;
     if (!slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
     return 0;
@@ -764,74 +876,92 @@ struct dvbt2ll_chain {
   }
 };
 
-extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, dvbt2ll_chain **out) {
-  if (!p || !out || p->max_frames < 1) return DVBT2LL_EINVAL;
-  *out = nullptr;
-  const dvbt2ll_framemapperfint_params &f = p->fm;
-  std::unique_ptr<dvbt2ll_chain> h(new (std::nothrow) dvbt2ll_chain());
-  if (!h) return DVBT2LL_ENOMEM;
-  h->p = *p;
-  h->max_frames = p->max_frames;
-  FmParams fm = to_fm(f);
-  PgParams pg{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
-              f.preamble, p->misogroup, p->equalization, p->bandwidth, fft_points(f.fftsize)};
-  if (build_frame(fm, h->frame) || build_pilot(pg, h->pilot)) return DVBT2LL_EINVAL;
+// the common construction of single- and multi-PLP chains: fm's common fields with plps' PLPs
+static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<PlpParams> &plps,
+                       const std::vector<int> &tsrate, int misogroup, int equalization, int bandwidth, int device) {
+  PgParams pg{fm.carriermode, fm.fftsize, fm.pilotpattern, fm.guardinterval, fm.numdatasyms, fm.paprmode, fm.version,
+              fm.preamble, misogroup, equalization, bandwidth, fft_points(fm.fftsize)};
+  if (build_frame_mplp(fm, plps, h->frame) || build_pilot(pg, h->pilot)) return DVBT2LL_EINVAL;
   if (h->pilot.active != h->frame.M) return DVBT2LL_EINVAL;
+  const FramePlan &fp = h->frame;
+  h->nplp = fp.nplp;
   int r = h->ctx.init(device);
   if (r) return r;
-  if ((r = h->fec.init(f.framesize, f.rate, f.constellation, f.inputmode, f.inband, f.fecblocks, p->tsrate)))
-    return r;
-  if ((r = h->fec.init_chain())) return r;
-  if ((r = h->map.init(f.framesize, f.rate, f.constellation, f.rotation, h->fec.plan))) return r;
-  std::vector<int16_t> cip(h->frame.ci_perm.begin(), h->frame.ci_perm.end());
-  cip.resize(((cip.size() + 3) & ~(size_t)3) + 4, 0);   // the map kernel reads aligned quads
-  if ((r = upload(h->perm, cip)) || (r = upload(h->shift, h->frame.ci_shift))) return r;
-  h->map.dev.ci_perm = h->perm.as<int16_t>();
-  h->map.dev.ci_shift = h->shift.as<int32_t>();
-  h->map.dev.F = h->frame.F;
-  h->map.dev.ti_on = h->frame.ti_on;
-  h->map.dev.ti_small = h->frame.ti_small;
-  h->map.dev.ti_big = h->frame.ti_big;
-  h->map.dev.ti_nsmall = h->frame.ti_nsmall;
   // OFDM side: aux bins from cmap, data cells streamed per symbol and scattered through inv
   ChainLayout layout;
-  if (build_chain_layout(h->frame, h->pilot, layout)) return DVBT2LL_EINVAL;
+  if (build_chain_layout(fp, h->pilot, layout)) return DVBT2LL_EINVAL;
+  int nq = 0;   // the PLPs' constellation tables back to back (multi-PLP); 256 entries for one PLP
+  std::vector<cf32> qall;
+  for (int k = 0; k < h->nplp; k++) {
+    const PlpParams &q = plps[k];
+    std::unique_ptr<ChainPlp> pl(new (std::nothrow) ChainPlp());
+    if (!pl) return DVBT2LL_ENOMEM;
+    const PlpPlan &pp = fp.plp[k];
+    if ((r = pl->fec.init(q.framesize, q.rate, q.constellation, q.inputmode, q.inband, q.fecblocks, tsrate[k])))
+      return r;
+    // one PLP of several: multiple input streams, ISI = the PLP_ID (bbheader:288-298)
+    if (h->nplp > 1) pl->fec.dev.matype = MATYPE_MIS | k;
+    if ((r = pl->fec.init_chain())) return r;
+    if ((r = pl->map.init(q.framesize, q.rate, q.constellation, q.rotation, pl->fec.plan))) return r;
+    std::vector<int16_t> cip(pp.ci_perm.begin(), pp.ci_perm.end());
+    cip.resize(((cip.size() + 3) & ~(size_t)3) + 4, 0);   // the map kernel reads aligned quads
+    if ((r = upload(pl->perm, cip)) || (r = upload(pl->shift, pp.ci_shift))) return r;
+    MapDev &md = pl->map.dev;
+    md.ci_perm = pl->perm.as<int16_t>();
+    md.ci_shift = pl->shift.as<int32_t>();
+    md.F = pp.F;
+    md.ti_on = pp.ti_on;
+    md.ti_small = pp.ti_small;
+    md.ti_big = pp.ti_big;
+    md.ti_nsmall = pp.ti_nsmall;
+    md.data_off = pp.start;
+    // the map kernel's TI store through the symbol partition (layout.part), reordered to its store
+    // order (block r, index jj = 5 row + e with TI, else t) as int16 deltas from the TI position
+    // (a cell only moves within its symbol); the PLP's TI positions start at PLP_START
+    const int csp = (pp.cs + 3) & ~3;   // rows padded for the kernel's aligned quad loads
+    std::vector<int16_t> pb((size_t)pp.F * csp + 4, 0);
+    for (int rr = 0; rr < pp.F; rr++)
+      for (int jj = 0; jj < pp.cs; jj++) {
+        const int t = pp.ti_on ? (jj % 5) * (pp.cs / 5) + jj / 5 : jj;
+        const int64_t sd = ti_dest(fp, k, rr, t), delta = layout.part[sd] - sd;
+        if (delta < INT16_MIN || delta > INT16_MAX) return DVBT2LL_EINVAL;
+        pb[(size_t)rr * csp + jj] = (int16_t)delta;
+      }
+    if ((r = upload(pl->part, pb))) return r;
+    md.part = pl->part.as<int16_t>();
+    md.part_stride = csp;
+    pl->F = pp.F;
+    pl->inputmode = q.inputmode;
+    pl->inband = q.inband;
+    pl->cw_stride = ((pl->fec.plan.nldpc / 8) + 255) / 256 * 256;
+    pl->pay = (pl->fec.plan.kbch - 80) / 8;
+    // payload bytes per frame: in-band type B takes 13 bytes of the first BBFRAME of each frame
+    // (bbheader:327-355, fec_block == 0)
+    pl->ts_per_frame = (int64_t)pp.F * pl->pay - (q.inband ? 13 : 0);
+    h->qbase_host.push_back(nq);
+    const int entries = 1 << pl->map.plan.mod;
+    for (int i = 0; i < entries; i++) qall.push_back(pl->map.plan.lut[i]);
+    nq += entries;
+    h->plps.push_back(std::move(pl));
+  }
   // stored bins -> padded LDS slots within their half (the kernel writes them as they are)
   const int nsub_h = ofdm_split(h->pilot.N) ? h->pilot.N / 2 : h->pilot.N;
   std::vector<uint16_t> inv_pad(layout.inv.size());
-  for (size_t s = 0; s < layout.inv.size(); s++)
-    inv_pad[s] = (uint16_t)ofdm_padded_bin(h->pilot.N, layout.inv[s] % nsub_h);
+  for (size_t si = 0; si < layout.inv.size(); si++)
+    inv_pad[si] = (uint16_t)ofdm_padded_bin(h->pilot.N, layout.inv[si] % nsub_h);
   inv_pad.resize(((layout.inv.size() + 7) & ~(size_t)7) + 8, 0);   // the kernel reads aligned quads
   if ((r = upload(h->inv, inv_pad)) || (r = upload(h->sym_d0, layout.sym_d0)) ||
       (r = upload(h->sym_n, layout.sym_n)) || (r = upload(h->sym_n0, layout.sym_n0)))
     return r;
-  if (!layout.part.empty()) {
-    // reorder to the map kernel's store order: block r, index j = 5 row + e (TI on) or t
-    const FramePlan &fp = h->frame;
-    // stored as int16 deltas from the TI position (a cell only moves within its symbol)
-    const int csp = (fp.cs + 3) & ~3;   // rows padded for the kernel's aligned quad loads
-    std::vector<int16_t> pb((size_t)fp.F * csp + 4, 0);
-    for (int rr = 0; rr < fp.F; rr++)
-      for (int jj = 0; jj < fp.cs; jj++) {
-        const int t = fp.ti_on ? (jj % 5) * (fp.cs / 5) + jj / 5 : jj;
-        const int64_t s = ti_dest(fp, rr, t), delta = layout.part[s] - s;
-        if (delta < INT16_MIN || delta > INT16_MAX) return DVBT2LL_EINVAL;
-        pb[(size_t)rr * csp + jj] = (int16_t)delta;
-      }
-    if ((r = upload(h->part, pb))) return r;
-    h->map.dev.part = h->part.as<int16_t>();
-    h->map.dev.part_stride = csp;
-  }
   const PilotPlan &pp = h->pilot;
   // one aux row (pilot values, L1-pre, dummy cells): the L1-post cells come per frame from the GPU
-  std::vector<cf32> auxv = h->frame.aux;
+  std::vector<cf32> auxv = fp.aux;
   for (int i = 0; i < 12; i++) auxv[AUX_PILOT0 + i] = pp.pilot_values[i];
-  if ((r = h->ofdm.init(pp, layout.cmap, h->frame.aux_len, 1))) return r;
+  if ((r = h->ofdm.init(pp, layout.cmap, fp.aux_len, 1))) return r;
   AuxLists al;
-  if (build_aux_lists(layout, pp.N, pp.Nsym, auxv, h->frame.aux_len, 1, al, AUX_L1PRE + 1840, h->frame.Lp))
-    return DVBT2LL_EINVAL;
-  if ((r = h->l1.init(h->frame))) return r;
-  h->l1_stride = (uint32_t)((h->frame.Lp + 3) & ~3);
+  if (build_aux_lists(layout, pp.N, pp.Nsym, auxv, fp.aux_len, 1, al, AUX_L1PRE + 1840, fp.Lp)) return DVBT2LL_EINVAL;
+  if ((r = h->l1.init(fp))) return r;
+  h->l1_stride = (uint32_t)((fp.Lp + 3) & ~3);
   for (auto &b : al.dbin)
     if (b != 0xFFFF) b = (uint16_t)ofdm_padded_bin(pp.N, b);
   for (auto &e : al.ind) e = ofdm_padded_bin(pp.N, e & 0x7FFFu) | (e & ~0x7FFFu);
@@ -847,23 +977,33 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if ((r = upload(h->abin, al.dbin)) || (r = upload(h->aval, al.dval)) || (r = upload(h->aind, al.ind)) ||
       (r = upload(h->agrp, al.grp)) || (r = upload(h->azr, zr)))
     return r;
-  h->ofdm.dev.abin = h->abin.as<uint16_t>();
-  h->ofdm.dev.aval = h->aval.as<float2>();
-  h->ofdm.dev.aind = h->aind.as<uint32_t>();
-  h->ofdm.dev.agrp = h->agrp.as<int4>();
-  h->ofdm.dev.azr = h->azr.as<int2>();
-  h->ofdm.dev.inv = h->inv.as<uint16_t>();
-  h->ofdm.dev.sym_d0 = h->sym_d0.as<int32_t>();
-  h->ofdm.dev.sym_n = h->sym_n.as<int32_t>();
-  h->ofdm.dev.sym_n0 = h->sym_n0.as<int32_t>();
-  h->ofdm.dev.qam = h->map.dev.lut;
-  h->pair_stride = ((int64_t)h->frame.S + 7) / 8 * 8;
-  h->cw_stride = ((h->fec.plan.nldpc / 8) + 255) / 256 * 256;
+  OfdmDev &od = h->ofdm.dev;
+  od.abin = h->abin.as<uint16_t>();
+  od.aval = h->aval.as<float2>();
+  od.aind = h->aind.as<uint32_t>();
+  od.agrp = h->agrp.as<int4>();
+  od.azr = h->azr.as<int2>();
+  od.inv = h->inv.as<uint16_t>();
+  od.sym_d0 = h->sym_d0.as<int32_t>();
+  od.sym_n = h->sym_n.as<int32_t>();
+  od.sym_n0 = h->sym_n0.as<int32_t>();
+  od.nplp = h->nplp;
+  if (h->nplp == 1) {
+    od.qam = h->plps[0]->map.dev.lut;   // the 256-entry table (entries past the constellation are zero)
+    od.nq = 256;
+  } else {
+    if (nq > OFDM_MAX_QAM) return DVBT2LL_EINVAL;
+    h->plp_bnd_host = layout.plp_bnd;
+    std::vector<int32_t> qb(h->qbase_host.begin(), h->qbase_host.end());
+    if ((r = upload(h->qam_all, qall)) || (r = upload(h->plp_bnd, layout.plp_bnd)) || (r = upload(h->plp_qbase, qb)))
+      return r;
+    od.qam = h->qam_all.as<float2>();
+    od.nq = nq;
+    od.plp_bnd = h->plp_bnd.as<int32_t>();
+    od.plp_qbase = h->plp_qbase.as<int32_t>();
+  }
+  h->pair_stride = ((int64_t)fp.S + 7) / 8 * 8;
   h->iq_per_frame = (int64_t)pp.Nsym * (pp.N + pp.G) + 2048;
-  h->pay = (h->fec.plan.kbch - 80) / 8;
-  // payload bytes per frame: in-band type B takes 13 bytes of the first BBFRAME of each frame
-  // (bbheader:327-355, fec_block == 0)
-  h->ts_per_frame = (int64_t)h->frame.F * h->pay - (f.inband ? 13 : 0);
   // the OFDM kernel addresses index pairs and aux cells with 32-bit byte offsets
   if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32) ||
       (uint64_t)h->l1_stride * h->max_frames * 8 >= (1ull << 32))
@@ -872,23 +1012,92 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
   if ((r = upload(h->aux, auxv))) return r;
   if (h->sync_err.ensure(4)) return DVBT2LL_ENOMEM;
   HIP_TRY(hipMemset(h->sync_err.p, 0, 4));
+  return 0;
+}
+
+extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, dvbt2ll_chain **out) {
+  if (!p || !out || p->max_frames < 1) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  const dvbt2ll_framemapperfint_params &f = p->fm;
+  std::unique_ptr<dvbt2ll_chain> h(new (std::nothrow) dvbt2ll_chain());
+  if (!h) return DVBT2LL_ENOMEM;
+  h->p = *p;
+  h->max_frames = p->max_frames;
+  const PlpParams one{f.framesize, f.rate, f.constellation, f.rotation, f.fecblocks, f.tiblocks, f.inputmode, f.inband};
+  int r = chain_build(h.get(), to_fm(f), {one}, {p->tsrate}, p->misogroup, p->equalization, p->bandwidth, device);
+  if (r) return r;
   *out = h.release();
   return DVBT2LL_OK;
 }
 
-extern "C" int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info) {
-  if (!h || !info) return DVBT2LL_EINVAL;
-  info->fec_blocks_per_frame = h->frame.F;
-  info->payload_bytes_per_block = h->pay;
-  info->ts_bytes_per_frame = h->p.fm.inputmode ? (h->ts_per_frame * 188 + 186) / 187 : h->ts_per_frame;
+static bool mplp_to_plan(const dvbt2ll_mplp_params &m, FmParams &fm, std::vector<PlpParams> &plps,
+                         std::vector<int> &tsrate) {
+  if (m.nplp < 1 || m.nplp > DVBT2LL_MAX_PLP) return false;
+  const dvbt2ll_plp_params &q0 = m.plp[0];
+  fm = FmParams{q0.framesize, q0.rate, q0.constellation, q0.rotation, q0.fecblocks, q0.tiblocks, m.carriermode,
+                m.fftsize, m.guardinterval, m.l1constellation, m.pilotpattern, m.t2frames, m.numdatasyms, m.paprmode,
+                m.version, m.preamble, q0.inputmode, m.reservedbiasbits, m.l1scrambled, q0.inband};
+  plps.clear();
+  tsrate.clear();
+  for (int k = 0; k < m.nplp; k++) {
+    const dvbt2ll_plp_params &q = m.plp[k];
+    plps.push_back(PlpParams{q.framesize, q.rate, q.constellation, q.rotation, q.fecblocks, q.tiblocks, q.inputmode,
+                             q.inband});
+    tsrate.push_back(q.tsrate);
+  }
+  return true;
+}
+
+extern "C" int dvbt2ll_chain_create_mplp(const dvbt2ll_mplp_chain_params *p, int device, dvbt2ll_chain **out) {
+  if (!p || !out || p->max_frames < 1) return DVBT2LL_EINVAL;
+  *out = nullptr;
+  FmParams fm;
+  std::vector<PlpParams> plps;
+  std::vector<int> tsrate;
+  if (!mplp_to_plan(p->fm, fm, plps, tsrate)) return DVBT2LL_EINVAL;
+  std::unique_ptr<dvbt2ll_chain> h(new (std::nothrow) dvbt2ll_chain());
+  if (!h) return DVBT2LL_ENOMEM;
+  h->max_frames = p->max_frames;
+  const dvbt2ll_plp_params &q0 = p->fm.plp[0];
+  h->p.fm = dvbt2ll_framemapperfint_params{q0.framesize, q0.rate, q0.constellation, q0.rotation, q0.fecblocks,
+                                           q0.tiblocks, fm.carriermode, fm.fftsize, fm.guardinterval,
+                                           fm.l1constellation, fm.pilotpattern, fm.t2frames, fm.numdatasyms,
+                                           fm.paprmode, fm.version, fm.preamble, q0.inputmode, fm.reservedbiasbits,
+                                           fm.l1scrambled, q0.inband};
+  h->p.misogroup = p->misogroup;
+  h->p.equalization = p->equalization;
+  h->p.bandwidth = p->bandwidth;
+  h->p.max_frames = p->max_frames;
+  h->p.tsrate = q0.tsrate;
+  int r = chain_build(h.get(), fm, plps, tsrate, p->misogroup, p->equalization, p->bandwidth, device);
+  if (r) return r;
+  *out = h.release();
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_num_plps(const dvbt2ll_chain *h) { return h ? h->nplp : 0; }
+
+extern "C" int dvbt2ll_chain_get_plp_info(const dvbt2ll_chain *h, int plp, dvbt2ll_chain_info *info) {
+  if (!h || !info || plp < 0 || plp >= h->nplp) return DVBT2LL_EINVAL;
+  const ChainPlp &pl = *h->plps[plp];
+  info->fec_blocks_per_frame = pl.F;
+  info->payload_bytes_per_block = pl.pay;
+  info->ts_bytes_per_frame = pl.inputmode ? (pl.ts_per_frame * 188 + 186) / 187 : pl.ts_per_frame;
   info->iq_samples_per_frame = h->iq_per_frame;
-  info->cell_size = h->frame.cs;
-  info->stream_items = h->frame.S;
+  info->cell_size = h->frame.plp[plp].cs;
+  info->stream_items = h->frame.plp[plp].S;
   info->mapped_items = h->frame.M;
   info->num_symbols = h->pilot.Nsym;
   info->fft_size = h->pilot.N;
   info->guard_interval = h->pilot.G;
-  info->cw_stride_bytes = h->cw_stride;
+  info->cw_stride_bytes = pl.cw_stride;
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info) {
+  int r = dvbt2ll_chain_get_plp_info(h, 0, info);
+  if (r) return r;
+  info->stream_items = h->frame.S;   // the frame's data cells (every PLP)
   return DVBT2LL_OK;
 }
 
@@ -897,28 +1106,32 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   return dvbt2ll_chain_run_streams(h, ts_dev, 0, 1, ts_base, ts_len, first_frame, nframes, iq_dev, stream);
 }
 
-extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_stride, int nstreams,
-                                         int64_t ts_base, int64_t ts_len, int64_t first_frame, int nframes,
-                                         void *iq_dev, void *stream) {
-  if (!h || !ts_dev || !iq_dev || nframes < 1 || nstreams < 1 || (int64_t)nframes * nstreams > h->max_frames ||
-      first_frame < 0 || ts_base < 0 || ts_base % 188 != 0 || (nstreams > 1 && ts_stride < ts_len))
+// one run over nstreams independent single-PLP streams (nplp == 1) or over one frame sequence of
+// every PLP (nstreams == 1): ts[k], base[k], len[k] per PLP (stream s of a batch at ts[0] + s * ts_stride)
+static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *base, const int64_t *len,
+                     int64_t ts_stride, int nstreams, int64_t first_frame, int nframes, void *iq_dev, void *stream) {
+  if (!h || !ts || !iq_dev || nframes < 1 || nstreams < 1 || (int64_t)nframes * nstreams > h->max_frames ||
+      first_frame < 0 || (nstreams > 1 && (h->nplp > 1 || ts_stride < len[0])))
     return DVBT2LL_EINVAL;
   const int nf = nframes * nstreams;   // frames of the launch, stream-major
   hipStream_t s = stream ? (hipStream_t)stream : h->ctx.stream;
-  const int F = h->frame.F;
-  // the TS slice must cover every byte the frames consume plus the packet before the
-  // first one touched (its CRC-8 replaces the next sync byte, bbheader:701-713)
-  int64_t start = first_frame * h->ts_per_frame, end = (first_frame + nframes) * h->ts_per_frame;
-  if (h->p.fm.inputmode) {
-    start = 188 * (start / 187) + (start % 187);
-    end = 188 * (end / 187) + (end % 187) + 1;
+  for (int k = 0; k < h->nplp; k++) {
+    const ChainPlp &pl = *h->plps[k];
+    if (!ts[k] || base[k] < 0 || base[k] % 188 != 0) return DVBT2LL_EINVAL;
+    // the TS slice must cover every byte the frames consume plus the packet before the
+    // first one touched (its CRC-8 replaces the next sync byte, bbheader:701-713)
+    int64_t start = first_frame * pl.ts_per_frame, end = (first_frame + nframes) * pl.ts_per_frame;
+    if (pl.inputmode) {
+      start = 188 * (start / 187) + (start % 187);
+      end = 188 * (end / 187) + (end % 187) + 1;
+    }
+    int64_t lo = start >= 188 ? (start / 188) * 188 - 188 : 0;
+    if (base[k] > lo || base[k] + len[k] < end) return DVBT2LL_EINVAL;
   }
-  int64_t lo = start >= 188 ? (start / 188) * 188 - 188 : 0;
-  if (ts_base > lo || ts_base + ts_len < end) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
   const int slot = h->next_slot;
   if (h->slot_used[slot] && h->slot_stream[slot] != s) HIP_TRY(hipStreamWaitEvent(s, h->slot_done[slot], 0));
-  DevBuf &cw = h->cw[slot], &pairs = h->pairs[slot];
+  DevBuf &pairs = h->pairs[slot];
   hipEvent_t ev[dvbt2ll_chain::NEV] = {};
   if (h->timing && !h->use_graph) {   // per-stage events only on the direct launch path
     if (h->evused + dvbt2ll_chain::NEV > 4096 && h->fold_timing()) return DVBT2LL_EDEVICE;
@@ -927,33 +1140,37 @@ extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, i
     HIP_TRY(hipEventRecord(ev[0], s));
   }
   L1IO lio{};
-  FecIO fio{};
-  MapIO mio{};
+  FecIO fio[DVBT2LL_MAX_PLP] = {};
+  MapIO mio[DVBT2LL_MAX_PLP] = {};
   OfdmIO oio{};
   lio.out = h->l1buf[slot].as<float2>();
   lio.out_stride = h->l1_stride;
   lio.first_frame = first_frame;
   lio.nframes = nf;
   lio.frames_per_stream = nstreams > 1 ? nframes : 0;
-  fio.in = (const uint8_t *)ts_dev;
-  fio.ts_base = ts_base;
-  fio.ts_len = ts_len;
-  fio.first_block = first_frame * F;
-  fio.out = cw.as<uint8_t>();
-  fio.cw_stride = h->cw_stride;
-  fio.nblocks = F * nf;
-  fio.sync_err = h->sync_err.as<uint32_t>();
-  fio.blocks_per_stream = nstreams > 1 ? F * nframes : 0;
-  fio.ts_stride = nstreams > 1 ? ts_stride : 0;
-  fio.bch_part = h->bpart[slot].as<uint32_t>();
-  fio.bch_part_blocks = (int64_t)F * h->max_frames;
-  mio.in = cw.as<uint8_t>();
-  mio.cw_stride = h->cw_stride;
-  mio.out_pairs = pairs.as<uint16_t>();
-  mio.frame_stride = h->pair_stride;
-  mio.nblocks = F * nf;
-  mio.packed_in = 1;
-  mio.apply_ci = 1;
+  for (int k = 0; k < h->nplp; k++) {
+    ChainPlp &pl = *h->plps[k];
+    DevBuf &cw = pl.cw[slot];
+    fio[k].in = (const uint8_t *)ts[k];
+    fio[k].ts_base = base[k];
+    fio[k].ts_len = len[k];
+    fio[k].first_block = first_frame * pl.F;
+    fio[k].out = cw.as<uint8_t>();
+    fio[k].cw_stride = pl.cw_stride;
+    fio[k].nblocks = pl.F * nf;
+    fio[k].sync_err = h->sync_err.as<uint32_t>();
+    fio[k].blocks_per_stream = nstreams > 1 ? pl.F * nframes : 0;
+    fio[k].ts_stride = nstreams > 1 ? ts_stride : 0;
+    fio[k].bch_part = pl.bpart[slot].as<uint32_t>();
+    fio[k].bch_part_blocks = (int64_t)pl.F * h->max_frames;
+    mio[k].in = cw.as<uint8_t>();
+    mio[k].cw_stride = pl.cw_stride;
+    mio[k].out_pairs = pairs.as<uint16_t>();
+    mio[k].frame_stride = h->pair_stride;
+    mio[k].nblocks = pl.F * nf;
+    mio[k].packed_in = 1;
+    mio[k].apply_ci = 1;
+  }
   oio.data = h->aux.as<float2>();
   oio.aux_off = 0;
   oio.cell_off = 0;
@@ -981,6 +1198,21 @@ extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, i
   return DVBT2LL_OK;
 }
 
+extern "C" int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_stride, int nstreams,
+                                         int64_t ts_base, int64_t ts_len, int64_t first_frame, int nframes,
+                                         void *iq_dev, void *stream) {
+  if (!h || h->nplp != 1) return DVBT2LL_EINVAL;
+  const void *ts[1] = {ts_dev};
+  return chain_run(h, ts, &ts_base, &ts_len, ts_stride, nstreams, first_frame, nframes, iq_dev, stream);
+}
+
+extern "C" int dvbt2ll_chain_run_plps(dvbt2ll_chain *h, const void *const *ts_dev, const int64_t *ts_base,
+                                      const int64_t *ts_len, int64_t first_frame, int nframes, void *iq_dev,
+                                      void *stream) {
+  if (!h || !ts_dev || !ts_base || !ts_len) return DVBT2LL_EINVAL;
+  return chain_run(h, ts_dev, ts_base, ts_len, 0, 1, first_frame, nframes, iq_dev, stream);
+}
+
 extern "C" int dvbt2ll_chain_set_graph(dvbt2ll_chain *h, int enable) {
   if (!h) return DVBT2LL_EINVAL;
   h->use_graph = enable != 0;
@@ -996,9 +1228,12 @@ extern "C" int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots) {
     if (r) return r;
   }
   for (int k = nslots; k < DVBT2LL_CHAIN_MAX_SLOTS; k++) {
-    h->cw[k].release();
+    for (auto &pl : h->plps) {
+      pl->cw[k].release();
+      pl->bpart[k].release();
+    }
     h->pairs[k].release();
-    h->bpart[k].release();
+    h->l1buf[k].release();
     h->slot_used[k] = false;
   }
   h->nslots = nslots;
@@ -1009,7 +1244,7 @@ extern "C" int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots) {
 
 extern "C" int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                                       int64_t first_frame, int nframes, void *iq) {
-  if (!h || !ts || !iq || nframes < 1 || nframes > h->max_frames) return DVBT2LL_EINVAL;
+  if (!h || !ts || !iq || nframes < 1 || nframes > h->max_frames || h->nplp != 1) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
   size_t iq_bytes = (size_t)nframes * h->iq_per_frame * (h->ofdm.dev.fmt == DVBT2LL_IQ_SC16 ? 4 : 8);
   if (h->ts_tmp.ensure((size_t)ts_len + 16) || h->iq_tmp.ensure(iq_bytes)) return DVBT2LL_ENOMEM;
@@ -1044,13 +1279,17 @@ extern "C" int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *l
   }
   return DVBT2LL_OK;
 }
-extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes) {
-  if (!h || !out || bytes < 0 || (size_t)bytes > h->cw[h->last_slot].n) return DVBT2LL_EINVAL;
-  const DevBuf &cw = h->cw[h->last_slot];
+extern "C" int dvbt2ll_chain_debug_plp_codewords(dvbt2ll_chain *h, int plp, void *out, int64_t bytes) {
+  if (!h || !out || bytes < 0 || plp < 0 || plp >= h->nplp) return DVBT2LL_EINVAL;
+  const DevBuf &cw = h->plps[plp]->cw[h->last_slot];
+  if ((size_t)bytes > cw.n) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, cw.p, (size_t)bytes, hipMemcpyDeviceToHost));
   return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes) {
+  return dvbt2ll_chain_debug_plp_codewords(h, 0, out, bytes);
 }
 extern "C" int dvbt2ll_chain_debug_cell_pairs(dvbt2ll_chain *h, void *out, int64_t cells) {
   if (!h || !out || cells < 0 || (size_t)cells * 2 > h->pairs[h->last_slot].n) return DVBT2LL_EINVAL;
@@ -1061,14 +1300,24 @@ extern "C" int dvbt2ll_chain_debug_cell_pairs(dvbt2ll_chain *h, void *out, int64
 }
 extern "C" int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells) {
   // frame 0's data cells: index pairs expanded through the constellation exactly as the OFDM
-  // kernel does, (lut[lo].re, lut[hi].im)
+  // kernel does, (lut[lo].re, lut[hi].im) with the table of the slot's PLP
   if (!h || !out || cells < 0 || (size_t)cells * 2 > h->pairs[h->last_slot].n) return DVBT2LL_EINVAL;
   std::vector<uint16_t> pr((size_t)cells);
   int r = dvbt2ll_chain_debug_cell_pairs(h, pr.data(), cells);
   if (r) return r;
   cf32 *o = (cf32 *)out;
-  const cf32 *lut = h->map.plan.lut;
-  for (int64_t i = 0; i < cells; i++) o[i] = cf32{lut[pr[i] & 0xFF].re, lut[pr[i] >> 8].im};
+  std::vector<int> plp_of((size_t)cells, 0);
+  if (h->nplp > 1) {
+    const int P = h->nplp;
+    for (size_t g = 0; g + 1 <= h->plp_bnd_host.size() / (P + 1); g++)
+      for (int k = 0; k < P; k++)
+        for (int32_t s = h->plp_bnd_host[g * (P + 1) + k]; s < h->plp_bnd_host[g * (P + 1) + k + 1]; s++)
+          if (s < cells) plp_of[s] = k;
+  }
+  for (int64_t i = 0; i < cells; i++) {
+    const cf32 *lut = h->plps[plp_of[i]]->map.plan.lut;
+    o[i] = cf32{lut[pr[i] & 0xFF].re, lut[pr[i] >> 8].im};
+  }
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_sync_errors(dvbt2ll_chain *h, int64_t *count) {

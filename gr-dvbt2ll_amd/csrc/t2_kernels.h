@@ -30,7 +30,11 @@ struct FecDev {
   int bch_nq, bch_nt;           // chain: 32-byte message chunks, 32-parity tiles of bch_mfma
   int kbch, nbch, P, nldpc, q, nent, chunk, parity_il;   // chunk: BCH message bytes per lane (64 lanes)
   int hem, inband, fec_blocks, ts_rate;
+  // BBHEADER MATYPE-1 << 8 | MATYPE-2: 0xF000 = TS, SIS, CCM, ISSYI 0, NPD 0, RO 0, ISI 0 (the reference's
+  // ctor, bbheader:168-182); 0xD000 | ISI = multiple input streams (one PLP of a multi-PLP frame, :288-298)
+  int matype;
 };
+constexpr int MATYPE_SIS = 0xF000, MATYPE_MIS = 0xD000;
 
 struct FecIO {
   const uint8_t *in;       // TS bytes (ts modes) or unpacked bits
@@ -82,6 +86,7 @@ struct MapDev {
   const int32_t *ci_shift; // F  (chain only)
   int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
+  int data_off;            // chain: the PLP's first data cell (PLP_START) within the frame data region
   const int16_t *part;     // chain, 32K only: slot - TI position of (block r, TI-store index j), at
                            // r*part_stride + j (rows padded to a multiple of 4 for 8-byte quad loads)
   int part_stride;
@@ -110,6 +115,7 @@ __host__ __device__ inline int ofdm_pad_shift(int N) { return N > 16384 ? OFDM_P
 __host__ __device__ inline uint32_t ofdm_padded_bin(int N, uint32_t k) {   // k: bin within its half
   return k + (k >> ofdm_pad_shift(N));
 }
+constexpr int OFDM_MAX_QAM = 1024;   // constellation entries the OFDM kernels hold in LDS (all PLPs' tables)
 struct OfdmDev {
   const int32_t *bin_map;   // Nsym x N (natural FFT-input order): >= 0 cell index, < 0 aux entry
   // chain (scatter) mode: symbol j's cells are the slots [sym_d0[j], +sym_n[j]), slot s goes to
@@ -120,7 +126,14 @@ struct OfdmDev {
   const float2 *twiddle1k;  // 1024: w_1024^m (PilotPlan::twiddle1k; 32K kernel)
   const float *isinc;       // N or null
   const float2 *p1;         // 2048
-  const float2 *qam;        // scatter mode: 256-entry constellation; cell = (qam[lo].x, qam[hi].y)
+  const float2 *qam;        // scatter mode: nq-entry constellation table(s); cell = (qam[b + lo].x, qam[b + hi].y),
+                            // b = the cell's PLP's table base plp_qbase[p] (0 with one PLP)
+  int nq;                   // entries of qam: 256 for one PLP, <= OFDM_MAX_QAM (the PLPs' tables back to back)
+  // multi-PLP frames (nplp > 1): the PLP of data slot s in group g (2 j + h) is the p with
+  // plp_bnd[g (nplp + 1) + p] <= s < plp_bnd[g (nplp + 1) + p + 1] (t2_plan ChainLayout::plp_bnd)
+  int nplp;
+  const int32_t *plp_bnd;
+  const int32_t *plp_qbase;   // nplp: PLP p's table starts at entry plp_qbase[p] of qam
   // scatter mode: non-data bins as compact lists per (symbol, half) group 2 j + h (t2_plan.h
   // AuxLists): agrp[g] = {direct offset, direct count, indirect offset, indirect count}
   const uint16_t *abin;     // direct padded bins, quads (0xFFFF = padding)

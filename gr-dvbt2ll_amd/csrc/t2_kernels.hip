@@ -505,11 +505,11 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
     for (int64_t pk = p0 + tid; 187 * pk < J0 + npay; pk += FEC_THREADS)
       if (tin[188 * pk - io.ts_base] != 0x47) atomicAdd(io.sync_err, 1u);
   }
-  // BBHEADER (bbheader:272-325), uniform across the workgroup: MATYPE-1 = TS, SIS, CCM, ISSYI 0,
-  // NPD 0, RO 0; ISI 0; bytes 0..7 big-endian in hw, byte 8 = SYNCD low, byte 9 = CRC-8
+  // BBHEADER (bbheader:272-325), uniform across the workgroup: MATYPE (FecDev::matype: TS, SIS or MIS
+  // with ISI, CCM, ISSYI 0, NPD 0, RO 0); bytes 0..7 big-endian in hw, byte 8 = SYNCD low, byte 9 = CRC-8
   const uint32_t upl = d.hem ? 0u : 188u * 8u, dfl = (uint32_t)(d.kbch - 80 - padding);
   const uint32_t syncb = d.hem ? 0u : 0x47u, syncd = count0 == 0 ? 0u : (uint32_t)(188 - count0) * 8u;
-  const uint64_t hw = (0xF0ull << 56) | ((uint64_t)upl << 32) | ((uint64_t)dfl << 16) | ((uint64_t)syncb << 8) |
+  const uint64_t hw = ((uint64_t)(uint32_t)d.matype << 48) | ((uint64_t)upl << 32) | ((uint64_t)dfl << 16) | ((uint64_t)syncb << 8) |
                       (uint64_t)(syncd >> 8);
   // CRC-8 over the 72 header bits, LSB-first register with 0xAB (add_crc8_bits :247-270): XOR
   // of the per-bit contributions (t2_plan hcrc_bits), lane n taking header bit n (and 64 + n),
@@ -1180,7 +1180,7 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   // time-interleaver store of the index pairs: row-major over (row, e), 5 consecutive cells
   // (10 B) per TI row (32K: through the half partition); the constellation lookup (QAM +
   // rotated-constellation Q delay) is fused into the OFDM kernel's bin scatter
-  const int64_t fbase = d.ti_on ? base : (int64_t)r * cs;
+  const int64_t fbase = (d.ti_on ? base : (int64_t)r * cs) + d.data_off;   // + PLP_START
   // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
   const int16_t *pr = d.part ? d.part + (int64_t)r * d.part_stride : nullptr;   // block-major int16 table
   if (pr) {
@@ -1229,7 +1229,7 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
 // (framemapper:1536-1910) from the t2_plan L1PostPlan.  The codeword lives in LDS as 16200 bits
 // packed MSB first: information bits 0..7031 (shortened positions zero), BCH parity 7032..7199,
 // LDPC parity 7200..16199 (word-aligned at word 225).
-constexpr int L1_NT = 256, L1_CW_WORDS = (16200 + 31) / 32, L1_SIG_WORDS = 16;
+constexpr int L1_NT = 256, L1_CW_WORDS = (16200 + 31) / 32, L1_SIG_WORDS = 64;   // <= 2048 signal bits
 
 __device__ __forceinline__ uint32_t l1_bit(const uint32_t *w, int i) { return (w[i >> 5] >> (31 - (i & 31))) & 1u; }
 
@@ -1668,6 +1668,11 @@ struct BinSource {
   const uint32_t *aind;
   const int4 *agrp;            // this symbol's groups (halves)
   const int2 *azr;             // this symbol's zero runs (padded LDS slot ranges)
+  // multi-PLP frames: this symbol's PLP boundaries (OfdmDev::plp_bnd + 2 j (nplp + 1)) and the PLPs'
+  // constellation table bases in qre / qim
+  int nplp;
+  const int32_t *bnd;
+  const int32_t *qbase;
 };
 
 // Scatter-mode fill of one group (a whole symbol, or one half of a split 32K symbol) into LDS,
@@ -1682,7 +1687,13 @@ struct NoWork {
 };
 // mid (32K): register work independent of the LDS, run once by every thread while its first round
 // of data-slot loads is in flight (after the loop when the run has no slots)
-template <int NT, int SQ, class Mid = NoWork>
+template <int NT, int SQ, class Mid>
+__device__ __forceinline__ void scatter_slots(float2 *lds, const BinSource &src, uint32_t r0, uint32_t rn,
+                                              uint32_t dummy, int tid, const Mid &mid, uint32_t lb);
+// MULTI (a kernel instantiation of its own, so the one-PLP kernels keep their register allocation):
+// the data slots of a multi-PLP frame, streamed PLP by PLP (a group's slots are PLP-major), each
+// PLP's run looked up in its own constellation table
+template <int NT, int SQ, bool MULTI = false, class Mid = NoWork>
 __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src, int g, uint32_t r0, uint32_t rn,
                                               uint32_t dummy, int tid, const Mid &mid = Mid()) {
   const int4 gr = src.agrp[g];
@@ -1701,6 +1712,23 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
     const uint32_t e = src.aind[(uint32_t)gr.z + i];
     lds[e & 0x7FFFu] = ld_off(src.data, (src.abase + (e >> 15)) * 8u);
   }
+  if (MULTI) {
+    mid();
+    const int P = src.nplp;
+    for (int p = 0; p < P; p++) {   // (uniform)
+      const uint32_t a = (uint32_t)src.bnd[g * (P + 1) + p], b = (uint32_t)src.bnd[g * (P + 1) + p + 1];
+      if (b > a) scatter_slots<NT, SQ>(lds, src, a, b - a, dummy, tid, NoWork(), (uint32_t)src.qbase[p]);
+    }
+  } else {
+    scatter_slots<NT, SQ>(lds, src, r0, rn, dummy, tid, mid, 0u);
+  }
+}
+
+// the data slots [r0, r0 + rn): streamed as aligned octets (32K) or quads, looked up in the constellation
+// table at lb of qre / qim (QAM + rotated-Q delay) and written to their bins
+template <int NT, int SQ, class Mid>
+__device__ __forceinline__ void scatter_slots(float2 *lds, const BinSource &src, uint32_t r0, uint32_t rn,
+                                              uint32_t dummy, int tid, const Mid &mid, uint32_t lb) {
   if (SQ == 4) {
     // 32K kernel: slots in aligned octets, one 16-byte load of bins and one of index pairs per
     // octet (half the load instructions of quads; the pair rows are padded to a multiple of 8)
@@ -1730,7 +1758,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
         for (int e = 0; e < 8; e++) {
           const uint32_t cw = e < 2 ? c[u].x : e < 4 ? c[u].y : e < 6 ? c[u].z : c[u].w;
           const uint32_t pr = cw >> (16 * (e & 1));
-          v[e] = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+          v[e] = make_float2(src.qre[lb + (pr & 0xFFu)], src.qim[lb + ((pr >> 8) & 0xFFu)]);
         }
 #pragma unroll
         for (int e = 0; e < 8; e++) {
@@ -1762,7 +1790,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
       for (int e = 0; e < 8; e++) {
         const uint32_t cw = (e & 2) ? c[u + (e >> 2)].y : c[u + (e >> 2)].x;
         const uint32_t pr = cw >> (16 * (e & 1));
-        v[e] = make_float2(src.qre[pr & 0xFFu], src.qim[(pr >> 8) & 0xFFu]);
+        v[e] = make_float2(src.qre[lb + (pr & 0xFFu)], src.qim[lb + ((pr >> 8) & 0xFFu)]);
       }
 #pragma unroll
       for (int e = 0; e < 8; e++) {
@@ -1779,7 +1807,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
 
 // One NSUB-point transform (N <= 16K) by NT = NSUB/V threads, ending with
 // v[u*RL + r] = y[t + NT*(u + (V/RL)*r)].  Also stores the kernel's constant tables (`stage`) to LDS.
-template <int NSUB, int V, class Stage>
+template <int NSUB, int V, bool MULTI, class Stage>
 __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource &src, const float *isinc,
                                          const float2 *tw, int tid, const Stage &stage) {
   constexpr int NT = NSUB / V, N = NSUB;
@@ -1792,7 +1820,7 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
     stage.store((unsigned char *)lds, true, tid);
     __syncthreads();
     const uint32_t dummy = (uint32_t)(NSUB + (NSUB >> PS)) + (uint32_t)(tid & 63);
-    scatter_group<NT, OFDM_SQ16>(lds, src, 0, src.d0, src.dn, dummy, tid);
+    scatter_group<NT, OFDM_SQ16, MULTI>(lds, src, 0, src.d0, src.dn, dummy, tid);
     __syncthreads();
     StockhamPass<NSUB, NT, V, 1, PS>::load_lds(v, lds, tid);
     __syncthreads();
@@ -1836,6 +1864,8 @@ struct OfdmShape {
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
   static constexpr int QAM_OFF = FFT_LDS + TW_ENTRIES * 8;
   static constexpr int LDS_BYTES = QAM_OFF + 256 * 8;                // + constellation re[256], im[256]
+  // with the constellation tables of nq entries (multi-PLP frames: every PLP's table, re[nq] then im[nq])
+  static constexpr int lds_bytes(int nq) { return QAM_OFF + nq * 8; }
 };
 
 // value of lane l ^ 1 (DPP quad_perm [1,0,3,2])
@@ -1886,7 +1916,11 @@ struct TableStage {
   using Sh = OfdmShape<N>;
   static constexpr int NT = Sh::NT, TWK = (Sh::TW_ENTRIES + NT - 1) / NT, QK = (256 + NT - 1) / NT;
   float2 tw[TWK], q[QK];
+  int nq = 256;
+  const float2 *qam = nullptr;
   __device__ __forceinline__ void load(const OfdmDev &d, int tid) {
+    nq = d.nq;
+    qam = d.qam;
 #pragma unroll
     for (int k = 0; k < TWK; k++) {
       const int i = tid + k * NT;
@@ -1908,7 +1942,7 @@ struct TableStage {
       if (i < Sh::TW_ENTRIES) twl[i] = tw[k];
     }
     if (chain) {
-      float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + 256;
+      float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + nq;
 #pragma unroll
       for (int k = 0; k < QK; k++) {
         const int i = tid + k * NT;
@@ -1917,13 +1951,18 @@ struct TableStage {
           qim[i] = q[k].y;
         }
       }
+      for (int i = 256 + tid; i < nq; i += NT) {   // the further PLPs' tables (multi-PLP frames)
+        const float2 t = qam[i];
+        qre[i] = t.x;
+        qim[i] = t.y;
+      }
     }
   }
 };
 
 // OFDM symbols of N <= 16K points: one workgroup of N / 16 threads per (symbol, frame), the
 // symbol's bins in LDS, radix-16 Stockham passes, normalisation, GI copy, IQ store
-template <int N, int FMT>
+template <int N, int FMT, bool MULTI>
 __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmIO io) {
   using Sh = OfdmShape<N>;
   constexpr int NT = Sh::NT, V = Sh::V, RL = FftPlan<N, V>::RL, UL = V / RL;
@@ -1931,7 +1970,7 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   float2 *lds = (float2 *)smem;
   float2 *twl = (float2 *)(smem + Sh::FFT_LDS);
   const int tid = threadIdx.x;
-  float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + 256;
+  float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + d.nq;
   // constant tables: loaded into registers here, stored to LDS after the zero fill
   TableStage<N> tabs;
   tabs.load(d, tid);
@@ -1946,7 +1985,7 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const uint32_t abase = io.aux_off + (uint32_t)(frame % d.t2frames) * (uint32_t)d.aux_len - 1u;
   const int32_t *map = d.bin_map + (int64_t)j * N;
   BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u, d.abin, d.aval, d.aind, nullptr,
-                nullptr};
+                nullptr, 1, nullptr, nullptr};
   if (d.inv) {
     src.data = io.l1;                              // indirect entries: this frame's L1-post cells
     src.abase = (uint32_t)f * io.l1_stride - 1u;
@@ -1955,6 +1994,9 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
     src.dn0 = (uint32_t)d.sym_n0[j];
     src.agrp = d.agrp + 2 * j;
     src.azr = d.azr + 2 * j;
+    src.nplp = d.nplp;
+    src.bnd = d.plp_bnd ? d.plp_bnd + 2 * j * (d.nplp + 1) : nullptr;
+    src.qbase = d.plp_qbase;
   }
   if (io.carriers_only) {                          // test hook (gather mode): bins in natural order
     if (d.inv) return;
@@ -1980,7 +2022,7 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const IqOut<FMT> o{(char *)io.out + ((int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + G)) * SB, d.gain};
   const float nrm = d.norm;
   float2 v[V];
-  sub_ifft<N, V>(v, lds, src, d.isinc, twl, tid, tabs);
+  sub_ifft<N, V, MULTI>(v, lds, src, d.isinc, twl, tid, tabs);
   if ((((uintptr_t)o.base + (uint32_t)G * SB) & (2u * SB - 1u)) == 0) {
     // two consecutive samples per lane and store: lanes t, t ^ 1 swap half of their values
     // (as o32_store_pairs), so the even lane stores (t, t + 1) of every even m and the odd lane
@@ -2036,9 +2078,9 @@ constexpr int O32_NT = 1024, O32_H = 16384, O32_PS = OFDM_PAD_SHIFT_32K;
 constexpr int O32_DATA = (O32_H + (O32_H >> O32_PS) + 64) * 8;   // padded half + 64 dummy slots
 constexpr int O32_TW1K = O32_DATA;                                // w_1024^m, m < 1024
 constexpr int O32_TW2 = O32_TW1K + 1024 * 8;                      // two-level table, 128 + 256
-constexpr int O32_QAM = O32_TW2 + 384 * 8;                        // constellation re[256], im[256]
-constexpr int O32_LDS = O32_QAM + 256 * 8;
-static_assert(O32_LDS <= 160 * 1024, "32K OFDM LDS");
+constexpr int O32_QAM = O32_TW2 + 384 * 8;                        // constellation re[nq], im[nq]
+constexpr int o32_lds_bytes(int nq) { return O32_QAM + nq * 8; }
+static_assert(o32_lds_bytes(OFDM_MAX_QAM) <= 160 * 1024, "32K OFDM LDS");
 static_assert((16384 + 2 * 32) * 8 <= O32_DATA, "exchange slots fit the data area");
 
 // bins within a half as the scatter stores them (one pad slot per 32, t2_kernels.h)
@@ -2189,7 +2231,7 @@ __device__ __forceinline__ void o32_store_pairs(const float2 *v, const IqOut<FMT
 
 // 32K symbols, one workgroup per (symbol, frame): scatter mode (the fused chain), gather mode (the
 // pilotgen block: cells already in carrier order) and the carriers-only test hook
-template <int FMT>
+template <int FMT, bool MULTI>
 __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   constexpr int N = 32768, NT = O32_NT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2243,10 +2285,11 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
   if (d.inv) {
     // scatter mode, one stored half at a time: the bins of even m2, then of odd m2 (t2_plan.h
     // ofdm_stored_index); the even half's DFT-16 runs while the odd half's first loads are in flight
-    float *qre = (float *)(smem + O32_QAM), *qim = qre + 256;
-    const float2 tq = tid < 256 ? d.qam[tid] : make_float2(0.f, 0.f);
+    float *qre = (float *)(smem + O32_QAM), *qim = qre + d.nq;
+    const float2 tq = tid < d.nq ? d.qam[tid] : make_float2(0.f, 0.f);   // nq <= OFDM_MAX_QAM = O32_NT
     BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv, io.pairs, qre, qim, (uint32_t)d.sym_d0[j], (uint32_t)d.sym_n[j],
-                  (uint32_t)d.sym_n0[j], d.abin, d.aval, d.aind, d.agrp + 2 * j, d.azr + 2 * j};
+                  (uint32_t)d.sym_n0[j], d.abin, d.aval, d.aind, d.agrp + 2 * j, d.azr + 2 * j, d.nplp,
+                  d.plp_bnd ? d.plp_bnd + 2 * j * (d.nplp + 1) : nullptr, d.plp_qbase};
     const uint32_t dummy = (uint32_t)(O32_H + (O32_H >> O32_PS)) + (uint32_t)(tid & 63);
     // (measured and dropped: both halves' scatter inputs prefetched into registers before the
     // first half is written, in one batch or half 1 behind half 0's arrival: +11 % kernel time)
@@ -2254,14 +2297,14 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     {
       const int2 zr = src.azr[0];
       for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
-      if (tid < 256) {
+      if (tid < d.nq) {
         qre[tid] = tq.x;
         qim[tid] = tq.y;
       }
       tw1k[tid] = t1k;
       if (tid < 384) tw2[tid] = t2;
       __syncthreads();                            // constellation visible to the scatter
-      scatter_group<NT, 4>(lds, src, 0, src.d0, src.dn0, dummy, tid);
+      scatter_group<NT, 4, MULTI>(lds, src, 0, src.d0, src.dn0, dummy, tid);
       __syncthreads();
 #pragma unroll
       for (uint32_t r = 0; r < 16; r++) ev[r] = lds[o32_bin(kin + 1024u * r)];
@@ -2275,7 +2318,7 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
         __builtin_amdgcn_sched_barrier(0);
         Dft<16>::run(ev);
       };
-      scatter_group<NT, 4>(lds, src, 1, src.d0 + src.dn0, src.dn - src.dn0, dummy, tid, dft_even);
+      scatter_group<NT, 4, MULTI>(lds, src, 1, src.d0 + src.dn0, src.dn - src.dn0, dummy, tid, dft_even);
       __syncthreads();
 #pragma unroll
       for (uint32_t r = 0; r < 16; r++) od[r] = lds[o32_bin(kin + 1024u * r)];
@@ -2311,29 +2354,38 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     o32_store<FMT, 0, 32>(v, o, tb + 32u * ta, d.norm, d.G);
 }
 
-template <int N, int FMT>
+template <int N, int FMT, bool MULTI>
 static hipError_t launch_ofdm_f(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
   if (N == 32768) {
-    hipError_t e = lds_limit((const void *)ofdm32_kernel<FMT>, O32_LDS);
+    const void *fn = (const void *)ofdm32_kernel<FMT, MULTI>;
+    const int lds = o32_lds_bytes(d.inv ? d.nq : 256);
+    hipError_t e = lds_limit(fn, o32_lds_bytes(OFDM_MAX_QAM));   // the largest launch
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((ofdm32_kernel<FMT>), dim3(d.Nsym * io.nframes), dim3(O32_NT), O32_LDS, s, d, io);
+    hipLaunchKernelGGL((ofdm32_kernel<FMT, MULTI>), dim3(d.Nsym * io.nframes), dim3(O32_NT), lds, s, d, io);
     return hipGetLastError();
   }
   constexpr int NN = N > 16384 ? 16384 : N;
   using Sh = OfdmShape<NN>;
-  hipError_t e = lds_limit((const void *)ofdm_kernel<NN, FMT>, Sh::LDS_BYTES);
+  const int lds = Sh::lds_bytes(d.inv ? d.nq : 256);
+  hipError_t e = lds_limit((const void *)ofdm_kernel<NN, FMT, MULTI>, Sh::lds_bytes(OFDM_MAX_QAM));   // the largest launch
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((ofdm_kernel<NN, FMT>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), Sh::LDS_BYTES, s, d, io);
+  hipLaunchKernelGGL((ofdm_kernel<NN, FMT, MULTI>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), lds, s, d, io);
   return hipGetLastError();
+}
+template <int N, int FMT>
+static hipError_t launch_ofdm_m(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
+  return d.inv && d.nplp > 1 ? launch_ofdm_f<N, FMT, true>(d, io, s) : launch_ofdm_f<N, FMT, false>(d, io, s);
 }
 template <int N>
 static hipError_t launch_ofdm_t(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
-  if (d.fmt == 1 && !io.carriers_only) return launch_ofdm_f<N, 1>(d, io, s);
-  return d.fmt == 0 || io.carriers_only ? launch_ofdm_f<N, 0>(d, io, s) : hipErrorInvalidValue;
+  if (d.fmt == 1 && !io.carriers_only) return launch_ofdm_m<N, 1>(d, io, s);
+  return d.fmt == 0 || io.carriers_only ? launch_ofdm_m<N, 0>(d, io, s) : hipErrorInvalidValue;
 }
 
 hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
   if (io.nframes <= 0) return hipSuccess;
+  if (d.inv && (d.nq < 1 || d.nq > OFDM_MAX_QAM || d.nplp < 1 || d.nplp > 8 || (d.nplp > 1 && (!d.plp_bnd || !d.plp_qbase))))
+    return hipErrorInvalidValue;
   switch (d.N) {
     case 1024: return launch_ofdm_t<1024>(d, io, s);
     case 2048: return launch_ofdm_t<2048>(d, io, s);

@@ -502,87 +502,108 @@ void l1_encode(std::vector<uint8_t> &cw, int k, int nbch, int rate_id) {
 }  // namespace
 
 int build_frame(const FmParams &p, FramePlan &fp, bool host_l1post) {
-  int normal = p.framesize == 1;
-  fp.cs = cell_size_of(normal, p.constellation);
-  if (!fp.cs || p.fecblocks < 1 || p.t2frames < 1 || p.t2frames > 255 || p.numdatasyms < 1) return -1;
-  // tiblocks > fecblocks is accepted like the reference (framemapper:1114-1119): the surplus TI
-  // blocks are "small" ones of floor(fecblocks / tiblocks) = 0 FEC blocks, which carry no cells
-  if (p.tiblocks < 0 || p.tiblocks > 255) return -1;
+  const PlpParams one{p.framesize, p.rate, p.constellation, p.rotation, p.fecblocks, p.tiblocks, p.inputmode, p.inband};
+  return build_frame_mplp(p, std::vector<PlpParams>{one}, fp, host_l1post);
+}
+
+// L1-post signalling bits incl. CRC-32 for nplp PLPs: KSIG_POST = 350 for one (framemapperfint_cc_impl.h:32),
+// plus 89 configurable (:1577-1639) and 48 dynamic (:1672-1687) bits per further PLP
+static int ksig_post(int nplp) { return 350 + (nplp - 1) * (89 + 48); }
+
+int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, FramePlan &fp, bool host_l1post) {
+  const int nplp = (int)plps.size();
+  if (nplp < 1 || nplp > MAX_PLP) return -1;
+  if (p.t2frames < 1 || p.t2frames > 255 || p.numdatasyms < 1) return -1;
+  fp.nplp = nplp;
+  fp.plp_in = plps;
+  fp.plp.assign(nplp, PlpPlan());
   int N = fft_points(p.fftsize);
   Counts c;
   if (!active_counts(p.fftsize, p.carriermode, p.pilotpattern, p.paprmode, p.guardinterval, p.preamble, c))
     return -1;
   if (!c.c_data || (c.n_fc && p.numdatasyms < 2)) return -1;
   fp.N_P2 = c.n_p2; fp.C_P2 = c.c_p2; fp.C_DATA = c.c_data; fp.N_FC = c.n_fc; fp.C_FC = c.c_fc;
-  fp.F = p.fecblocks;
   fp.t2frames = p.t2frames;
   static const int eta_of[4] = {1, 2, 4, 6};
   if (p.l1constellation < 0 || p.l1constellation > 3) return -1;
   fp.eta = eta_of[p.l1constellation];
-  // L1-post size (framemapper:978-987)
-  const int KSIG_POST = 350, KBCH12 = 7032, KBCH14 = 3072, NBCH14 = 3240;
+  // L1-post size (framemapper:978-987) with K_sig = the L1-post signalling bits
+  const int KSIG_POST = ksig_post(nplp), KBCH12 = 7032, KBCH14 = 3072, NBCH14 = 3240;
+  if (KSIG_POST > KBCH12) return -1;
   int npunc_t = (6 * (KBCH12 - KSIG_POST)) / 5;
   int npost_t = KSIG_POST + 168 + 9000 - npunc_t;
   if (fp.N_P2 == 1) fp.N_post = (int)std::ceil((float)npost_t / (2 * (float)fp.eta)) * 2 * fp.eta;
   else fp.N_post = (int)std::ceil((float)npost_t / ((float)fp.eta * (float)fp.N_P2)) * fp.eta * fp.N_P2;
   fp.N_punc = npunc_t - (fp.N_post - npost_t);
   fp.Lp = fp.N_post / fp.eta;
-  fp.S = fp.cs * fp.F;
+
+  // ---- per PLP: cell interleaver (framemapper:1973-1998: per-TI-block running n, skip shifts >= cs) and
+  //      time interleaver geometry (:1108-1119); PLP p's cells are data cells [start, start + S)
+  fp.S = 0;
+  for (int k = 0; k < nplp; k++) {
+    const PlpParams &q = plps[k];
+    PlpPlan &pl = fp.plp[k];
+    pl.cs = cell_size_of(q.framesize == 1, q.constellation);
+    if (!pl.cs || q.fecblocks < 1 || (q.framesize != 0 && q.framesize != 1)) return -1;
+    // tiblocks > fecblocks is accepted like the reference (framemapper:1114-1119): the surplus TI
+    // blocks are "small" ones of floor(fecblocks / tiblocks) = 0 FEC blocks, which carry no cells
+    if (q.tiblocks < 0 || q.tiblocks > 255) return -1;
+    pl.F = q.fecblocks;
+    pl.S = pl.cs * pl.F;
+    pl.start = fp.S;
+    fp.S += pl.S;
+    int deg;
+    ci_permutation(pl.cs, pl.ci_perm, &deg);
+    int small_fec, big_fec, n_big, n_small;
+    if (q.tiblocks == 0) { small_fec = big_fec = 1; n_big = 0; n_small = q.fecblocks; }
+    else {
+      small_fec = (int)std::floor((float)q.fecblocks / (float)q.tiblocks);
+      big_fec = (int)std::ceil((float)q.fecblocks / (float)q.tiblocks);
+      n_big = q.fecblocks % q.tiblocks;
+      n_small = q.tiblocks - n_big;
+    }
+    pl.ti_on = q.tiblocks != 0;
+    pl.ti_small = small_fec;
+    pl.ti_big = big_fec;
+    pl.ti_nsmall = n_small;
+    for (int sb = 0; sb < n_small + n_big; sb++) {
+      const int nb = sb < n_small ? small_fec : big_fec;
+      unsigned n = 0;
+      for (int r = 0; r < nb; r++) {
+        int shift;
+        do {
+          unsigned rev = 0;
+          for (int b = 0; b < deg; b++) rev |= ((n >> b) & 1u) << (deg - 1 - b);
+          shift = (int)(rev << 1);
+          n++;
+        } while (shift >= pl.cs);
+        pl.ci_shift.push_back(shift);
+      }
+    }
+  }
+  {
+    const PlpPlan &p0 = fp.plp[0];
+    fp.cs = p0.cs; fp.F = p0.F; fp.ci_perm = p0.ci_perm; fp.ci_shift = p0.ci_shift;
+    fp.ti_on = p0.ti_on; fp.ti_small = p0.ti_small; fp.ti_big = p0.ti_big; fp.ti_nsmall = p0.ti_nsmall;
+  }
   fp.num_data_symbols = fp.N_FC ? p.numdatasyms - 1 : p.numdatasyms;
   fp.M = fp.N_P2 * fp.C_P2 + fp.num_data_symbols * fp.C_DATA + fp.N_FC;
   int fixed = fp.S + 1840 + fp.Lp + (fp.N_FC - fp.C_FC);
   if (fp.M < fixed) return -1;   // reference: "too many FEC blocks in T2 frame"
   fp.D = fp.M - fixed;
-
-  // ---- cell interleaver (framemapper:1973-1998): per-TI-block running n, skip shifts >= cs
-  int deg;
-  ci_permutation(fp.cs, fp.ci_perm, &deg);
-  int small_fec, big_fec, n_big, n_small;
-  if (p.tiblocks == 0) { small_fec = big_fec = 1; n_big = 0; n_small = p.fecblocks; }
-  else {
-    small_fec = (int)std::floor((float)p.fecblocks / (float)p.tiblocks);
-    big_fec = (int)std::ceil((float)p.fecblocks / (float)p.tiblocks);
-    n_big = p.fecblocks % p.tiblocks;
-    n_small = p.tiblocks - n_big;
+  // data cell (TI output order) -> framemapper input index: the inverse time interleave
+  // (framemapper:1999-2028) and cell interleave of its PLP; the input holds the PLPs' frames back to back
+  std::vector<int> data_in(fp.S);
+  for (int k = 0; k < nplp; k++) {
+    const PlpPlan &pl = fp.plp[k];
+    std::vector<int> perm_inv(pl.cs);
+    for (int w = 0; w < pl.cs; w++) perm_inv[pl.ci_perm[w]] = w;
+    for (int r = 0; r < pl.F; r++)
+      for (int t = 0; t < pl.cs; t++) {
+        const int w = perm_inv[((t - pl.ci_shift[r]) % pl.cs + pl.cs) % pl.cs];
+        data_in[ti_dest(fp, k, r, t)] = pl.start + r * pl.cs + w;
+      }
   }
-  fp.ti_on = p.tiblocks != 0;
-  fp.ti_small = small_fec;
-  fp.ti_big = big_fec;
-  fp.ti_nsmall = n_small;
-  fp.ci_shift.clear();
-  std::vector<int> ti_first, ti_count;           // FEC blocks per TI block
-  for (int s = 0, r0 = 0; s < n_small + n_big; s++) {
-    int nb = s < n_small ? small_fec : big_fec;
-    ti_first.push_back(r0);
-    ti_count.push_back(nb);
-    r0 += nb;
-    unsigned n = 0;
-    for (int r = 0; r < nb; r++) {
-      int shift;
-      do {
-        unsigned rev = 0;
-        for (int b = 0; b < deg; b++) rev |= ((n >> b) & 1u) << (deg - 1 - b);
-        shift = (int)(rev << 1);
-        n++;
-      } while (shift >= fp.cs);
-      fp.ci_shift.push_back(shift);
-    }
-  }
-  // ---- time interleaver (framemapper:1999-2028): stream position -> TI input position
-  std::vector<int> ti_src(fp.S);
-  if (p.tiblocks != 0) {
-    int s_out = 0;
-    for (size_t b = 0; b < ti_first.size(); b++) {
-      int cols = 5 * ti_count[b], rows = fp.cs / 5, base = ti_first[b] * fp.cs;
-      for (int k = 0; k < rows; k++)
-        for (int w = 0; w < cols; w++) ti_src[s_out++] = base + rows * w + k;
-    }
-  } else {
-    for (int s = 0; s < fp.S; s++) ti_src[s] = s;
-  }
-  // inverse cell interleave: TI input position t -> framemapper input index
-  std::vector<int> perm_inv(fp.cs);
-  for (int w = 0; w < fp.cs; w++) perm_inv[fp.ci_perm[w]] = w;
 
   // ---- frame vector [L1pre | L1post | data | dummy | zeros] and the P2 zig-zag
   //      (framemapper:2029-2103): frame_out index -> frame-vector index
@@ -616,11 +637,8 @@ int build_frame(const FmParams &p, FramePlan &fp, bool host_l1post) {
     if (v < 1840) code_d = code_in = -(AUX_L1PRE + v) - 1;
     else if (v < 1840 + Lp) code_d = code_in = -(AUX_L1PRE + v) - 1;
     else if (v < 1840 + Lp + fp.S) {
-      int t = ti_src[v - 1840 - Lp];
-      int r = t / fp.cs, pos = t % fp.cs;
-      int w = perm_inv[((pos - fp.ci_shift[r]) % fp.cs + fp.cs) % fp.cs];
       code_d = v - 1840 - Lp;
-      code_in = r * fp.cs + w;
+      code_in = data_in[code_d];
     } else if (v < 1840 + Lp + fp.S + fp.D) code_d = code_in = -(aux_dummy + (v - 1840 - Lp - fp.S)) - 1;
     else code_d = code_in = -AUX_ZERO - 1;
     fp.gather_d[o] = code_d;
@@ -689,22 +707,30 @@ int build_frame(const FmParams &p, FramePlan &fp, bool host_l1post) {
 }
 
 namespace {
-// L1-post signalling bits before the CRC-32 (framemapper:1560-1830, single PLP, no auxiliary
-// streams): FRAME_IDX (8 bits at *fidx_pos) = frame_idx
-std::vector<uint8_t> l1post_signal(const FmParams &p, int frame_idx, int *fidx_pos) {
+// L1-post signalling bits before the CRC-32 (framemapper:1553-1691, no auxiliary streams), the
+// configurable (:1577-1639) and dynamic (:1672-1687) PLP loops over the frame's PLPs (the reference's
+// one PLP: PLP_ID 0, PLP_START 0): FRAME_IDX (8 bits at *fidx_pos) = frame_idx
+std::vector<uint8_t> l1post_signal(const FmParams &p, const FramePlan &fp, int frame_idx, int *fidx_pos) {
   const bool v131 = p.version == 2, resv = p.reservedbiasbits && v131;
   Bits b;
-  b.put(1, 15); b.put(1, 8); b.put(0, 4); b.put(0, 8); b.put(0, 3); b.put(729833333u, 32);
-  b.put(0, 8); b.put(1, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3); b.put(0, 8); b.put(1, 8);
-  b.put(p.rate, 3); b.put(p.constellation, 3); b.put(p.rotation, 1); b.put(p.framesize, 2);
-  b.put(p.fecblocks, 10); b.put(1, 8); b.put(p.tiblocks, 8); b.put(0, 1); b.put(0, 1);
-  b.put((p.inband && v131) ? 1 : 0, 1); b.put(resv ? 0x7ff : 0, 11);
-  b.put(p.version == 0 ? 0 : p.inputmode + 1, 2); b.put(0, 1); b.put(0, 1); b.put(0, 2);
-  b.put(resv ? 0x3fffffff : 0, 30);
+  b.put(1, 15); b.put((uint64_t)fp.nplp, 8); b.put(0, 4); b.put(0, 8); b.put(0, 3); b.put(729833333u, 32);
+  for (int k = 0; k < fp.nplp; k++) {
+    const PlpParams &q = fp.plp_in[k];
+    b.put((uint64_t)k, 8); b.put(1, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3); b.put(0, 8); b.put(1, 8);
+    b.put(q.rate, 3); b.put(q.constellation, 3); b.put(q.rotation, 1); b.put(q.framesize, 2);
+    b.put(q.fecblocks, 10); b.put(1, 8); b.put(q.tiblocks, 8); b.put(0, 1); b.put(0, 1);
+    b.put((q.inband && v131) ? 1 : 0, 1); b.put(resv ? 0x7ff : 0, 11);
+    b.put(p.version == 0 ? 0 : q.inputmode + 1, 2); b.put(0, 1); b.put(0, 1);
+  }
+  b.put(0, 2); b.put(resv ? 0x3fffffff : 0, 30);
   if (fidx_pos) *fidx_pos = (int)b.b.size();
   b.put((uint64_t)frame_idx, 8); b.put(0, 22); b.put(0, 22); b.put(0, 8);
-  b.put(0, 3); b.put(resv ? 0xff : 0, 8); b.put(0, 8); b.put(0, 22); b.put(p.fecblocks, 10);
-  b.put(resv ? 0xff : 0, 8); b.put(resv ? 0xff : 0, 8);
+  b.put(0, 3); b.put(resv ? 0xff : 0, 8);
+  for (int k = 0; k < fp.nplp; k++) {
+    b.put((uint64_t)k, 8); b.put((uint64_t)fp.plp[k].start, 22); b.put(fp.plp[k].F, 10);
+    b.put(resv ? 0xff : 0, 8);
+  }
+  b.put(resv ? 0xff : 0, 8);
   return b.b;
 }
 
@@ -744,10 +770,10 @@ int build_l1post_plan(const FmParams &p, FramePlan &fp) {
   L1PostPlan &l = fp.l1;
   l = L1PostPlan();
   const bool v131 = p.version == 2;
-  std::vector<uint8_t> sig = l1post_signal(p, 0, &l.fidx_pos);
+  std::vector<uint8_t> sig = l1post_signal(p, fp, 0, &l.fidx_pos);
   const int L = (int)sig.size();           // CRC-covered bits
   l.nsig = L + 32;
-  if (l.nsig > 512 || l.fidx_pos + 8 > L) return -1;
+  if (l.nsig > L1_MAX_SIG || l.nsig != ksig_post(fp.nplp) || l.fidx_pos + 8 > L) return -1;
   const int nw = (l.nsig + 31) / 32;
   l.tmpl.assign(nw, 0);
   for (int i = 0; i < L; i++)
@@ -828,7 +854,7 @@ int build_l1post_plan(const FmParams &p, FramePlan &fp) {
 // operations, one bit at a time (framemapper:1536-1910)
 int l1post_host(const FmParams &p, const FramePlan &fp, int frame_idx, cf32 *dst) {
   const bool v131 = p.version == 2;
-  std::vector<uint8_t> bits = l1post_signal(p, frame_idx, nullptr);
+  std::vector<uint8_t> bits = l1post_signal(p, fp, frame_idx, nullptr);
   const uint32_t crc = crc32_mpeg2(bits);
   for (int i = 31; i >= 0; i--) bits.push_back((crc >> i) & 1);
   const int nsig = (int)bits.size();
@@ -1140,15 +1166,16 @@ std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t
   return out;
 }
 
-int64_t ti_dest(const FramePlan &fp, int r, int t) {
-  const int cs = fp.cs;
-  if (!fp.ti_on) return (int64_t)r * cs + t;
-  const int ns = fp.ti_nsmall * fp.ti_small;
+int64_t ti_dest(const FramePlan &fp, int plp, int r, int t) {
+  const PlpPlan &pl = fp.plp[plp];
+  const int cs = pl.cs;
+  if (!pl.ti_on) return pl.start + (int64_t)r * cs + t;
+  const int ns = pl.ti_nsmall * pl.ti_small;
   int r0, nb;
-  if (r < ns) { r0 = r - r % fp.ti_small; nb = fp.ti_small; }
-  else { r0 = r - (r - ns) % fp.ti_big; nb = fp.ti_big; }
+  if (r < ns) { r0 = r - r % pl.ti_small; nb = pl.ti_small; }
+  else { r0 = r - (r - ns) % pl.ti_big; nb = pl.ti_big; }
   const int rows = cs / 5, e = t / rows, row = t - e * rows;
-  return (int64_t)r0 * cs + (int64_t)row * (5 * nb) + 5 * (r - r0) + e;
+  return pl.start + (int64_t)r0 * cs + (int64_t)row * (5 * nb) + 5 * (r - r0) + e;
 }
 
 // LDS bank pair of a stored bin as the OFDM kernels' scatter writes it (8-byte slot within its half,
@@ -1234,9 +1261,15 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
   // stream any order (inv follows it); block-major runs give the map kernel, which stores one FEC
   // block per workgroup, one contiguous run per symbol (half) instead of 10-byte TI-row runs
   // scattered over the symbol (its per-cell deltas take any order inside a run).
-  std::vector<int32_t> blk_of(fp.S);
-  for (int r = 0; r < fp.F; r++)
-    for (int t = 0; t < fp.cs; t++) blk_of[ti_dest(fp, r, t)] = r;
+  // (blocks numbered PLP-major: PLP k's block r is g0_k + r, so each symbol half's slots are PLP-major too)
+  std::vector<int32_t> blk_of(fp.S), plp_of_blk;
+  for (int k = 0, g0 = 0; k < fp.nplp; g0 += fp.plp[k].F, k++)
+    for (int r = 0; r < fp.plp[k].F; r++) {
+      plp_of_blk.push_back(k);
+      for (int t = 0; t < fp.plp[k].cs; t++) blk_of[ti_dest(fp, k, r, t)] = g0 + r;
+    }
+  const int P = fp.nplp;
+  cl.plp_bnd.assign((size_t)2 * pp.Nsym * (P + 1), 0);
   const bool split = ofdm_split(pp.N);
   const int half = pp.N / 2;
   cl.part.assign(fp.S, 0);
@@ -1263,6 +1296,18 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
     }
     for (int k = 0; k < n; k++) cl.part[order[k]] = d0 + k;
     cl.sym_n0[j] = split ? n0 : n;
+    // PLP boundaries of each group's (PLP-major) slot range
+    for (int h = 0; h < 2; h++) {
+      const int k0 = h ? (split ? nh : n) : 0, k1 = h ? n : nh;
+      int32_t *bnd = &cl.plp_bnd[(size_t)(2 * j + h) * (P + 1)];
+      for (int q = 0, k = k0; q <= P; q++) {
+        while (k < k1 && plp_of_blk[blk_of[order[k]]] < q) k++;
+        bnd[q] = d0 + k;
+      }
+      bnd[P] = d0 + k1;
+      for (int k = k0; k + 1 < k1; k++)
+        if (plp_of_blk[blk_of[order[k]]] > plp_of_blk[blk_of[order[k + 1]]]) return -1;
+    }
   }
   std::vector<uint16_t> inv2(fp.S);
   for (int s = 0; s < fp.S; s++) inv2[cl.part[s]] = cl.inv[s];

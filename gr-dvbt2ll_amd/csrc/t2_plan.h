@@ -66,6 +66,22 @@ struct FmParams {
       guardinterval, l1constellation, pilotpattern, t2frames, numdatasyms, paprmode, version,
       preamble, inputmode, reservedbiasbits, l1scrambled, inband;
 };
+// One Type-1 data PLP of a multi-PLP frame (EN 302 755 8.3.6.3).  The reference carries exactly one
+// PLP (framemapper:152-250: num_plp 1, plp_type 1, time_il_type 0, frame_interval 1); a frame here
+// carries nplp of them, PLP_ID = index, each with its own FEC, constellation, cell and time
+// interleaver, its TI output occupying data cells [start, start + S) after the L1 signalling, PLPs
+// back to back in PLP_ID order.  TI type 0 with P_I = 1 keeps every T2 frame independent.
+struct PlpParams {
+  int framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband;
+};
+struct PlpPlan {
+  int cs = 0, F = 0, S = 0, start = 0;
+  int ti_on = 0, ti_small = 1, ti_big = 1, ti_nsmall = 0;
+  std::vector<int16_t> ci_perm;          // cs
+  std::vector<int32_t> ci_shift;         // F
+};
+constexpr int MAX_PLP = 8;
+
 // aux table (per t2_frame_num variant): [0] zero, [1..12] pilot values, then L1-pre,
 // L1-post, dummy cells.  Gather codes: >= 0 cell index, < 0 -> aux index (-code - 1).
 constexpr int AUX_ZERO = 0;
@@ -78,6 +94,7 @@ constexpr int AUX_L1PRE = 13;
 // groups :2190-2233), BCH(168) as the XOR of per-position remainders x^(168 + 7031 - p) mod g(x)
 // (:1269-1312), the LDPC 1/2 (16K) accumulate over its address table (:1314-1364), puncturing,
 // and the L1 constellation with the 16/64QAM bit interleaver + demux (:1832-1908).
+constexpr int L1_MAX_SIG = 2048;   // signalling bits the GPU L1-post generator holds (t2_kernels L1_SIG_WORDS)
 struct L1PostPlan {
   int nsig = 0;                    // signalling bits including the CRC-32
   int fidx_pos = 0;                // bit position of FRAME_IDX (8 bits, MSB first)
@@ -99,7 +116,11 @@ struct L1PostPlan {
   cf32 lut[64] = {};
 };
 
+// The single-PLP fields (cs, F, ci_perm, ci_shift, ti_*) are PLP 0's; S is the total over the PLPs.
 struct FramePlan {
+  int nplp = 1;
+  std::vector<PlpParams> plp_in;         // the PLPs' parameters
+  std::vector<PlpPlan> plp;
   int cs = 0, F = 0, S = 0, M = 0, N_P2 = 0, C_P2 = 0, C_DATA = 0, N_FC = 0, C_FC = 0;
   int eta = 0, N_post = 0, N_punc = 0, Lp = 0, D = 0, num_data_symbols = 0, t2frames = 0;
   int aux_len = 0;                       // entries per variant
@@ -107,7 +128,8 @@ struct FramePlan {
   std::vector<int32_t> ci_shift;         // F (per FEC block of a frame)
   std::vector<int32_t> gather_d;         // M: mapped cell -> frame data-region index (TI output order) | aux
   int ti_on = 0, ti_small = 1, ti_big = 1, ti_nsmall = 0;   // TI blocks: ti_nsmall of ti_small FEC blocks, then ti_big
-  std::vector<int32_t> gather_in;        // M: mapped cell -> framemapper input index | aux
+  std::vector<int32_t> gather_in;        // M: mapped cell -> framemapper input index | aux (input: one frame of
+                                         //   every PLP's cells, PLP 0 first)
   // host_l1post: t2frames x aux_len with every variant's L1-post cells (the CPU tests' cross-check);
   // else one variant whose L1-post cells [AUX_L1PRE + 1840, + Lp) are left zero for the GPU
   std::vector<cf32> aux;
@@ -117,6 +139,8 @@ struct FramePlan {
 // host_l1post: also encode every t2_frame_num variant's L1-post on the host (tests only; the
 // product generates L1-post per frame on the GPU from fp.l1)
 int build_frame(const FmParams &p, FramePlan &fp, bool host_l1post = false);
+// nplp PLPs; the per-PLP fields of p (framesize .. fecblocks, tiblocks, inputmode, inband) are ignored
+int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, FramePlan &fp, bool host_l1post = false);
 // fp.l1 from the parameters and fp's L1 geometry (called by build_frame)
 int build_l1post_plan(const FmParams &p, FramePlan &fp);
 // one FRAME_IDX variant's Lp L1-post cells, encoded bit by bit on the host (tests only)
@@ -169,6 +193,10 @@ struct ChainLayout {
   std::vector<uint16_t> inv;     // S: data slot -> stored bin index within its symbol's row
   std::vector<int32_t> sym_d0, sym_n, sym_n0;   // Nsym: run start, length, cells of the first half
   std::vector<int32_t> part;     // S: TI output index -> data slot (split only)
+  // per (symbol, half) group g = 2 j + h (h = 0 when N is not split): the first data slot of each PLP in
+  // the group's slot range, plp_bnd[g * (nplp + 1) + p], p = 0..nplp (the last = the range's end); a
+  // group's slots are PLP-major, so slot s of the group belongs to the PLP p with bnd[p] <= s < bnd[p + 1]
+  std::vector<int32_t> plp_bnd;
 };
 int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl);
 
@@ -194,8 +222,9 @@ struct AuxLists {
 // l1post kernel writes); l1_len = 0: indirect codes are aux index + 1 into the frame's variant
 int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf32> &auxv, int aux_len,
                     int t2frames, AuxLists &al, int l1_lo = 0, int l1_len = 0);
-// time-interleaver output index (frame data order) of cell-interleaved cell t of FEC block r
-int64_t ti_dest(const FramePlan &fp, int r, int t);
+// time-interleaver output index (frame data order) of cell-interleaved cell t of FEC block r of PLP plp
+int64_t ti_dest(const FramePlan &fp, int plp, int r, int t);
+inline int64_t ti_dest(const FramePlan &fp, int r, int t) { return ti_dest(fp, 0, r, t); }
 
 // framemapper cell counts {N_P2, C_P2, C_DATA, N_FC, C_FC} (framemapper:290-356, 425-915); -1 if invalid
 int frame_cell_counts(int fftsize, int carriermode, int pp, int papr, int gi, int preamble, int out[5]);

@@ -8,7 +8,77 @@
 
 using namespace t2;
 
+// multi-PLP parameters as laid out by include/dvbt2ll_hip.h dvbt2ll_mplp_params (ints): 12 common fields
+// {carriermode, fftsize, guardinterval, l1constellation, pilotpattern, t2frames, numdatasyms, paprmode,
+// version, preamble, reservedbiasbits, l1scrambled}, nplp, then MAX_PLP x 9 per-PLP fields {framesize,
+// rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, tsrate}
+static bool parse_mplp(const int *a, FmParams &f, std::vector<PlpParams> &plps) {
+  const int n = a[12];
+  if (n < 1 || n > MAX_PLP) return false;
+  const int *q0 = a + 13;
+  f = FmParams{q0[0], q0[1], q0[2], q0[3], q0[4], q0[5], a[0], a[1], a[2], a[3], a[4], a[5], a[6], a[7], a[8],
+               a[9], q0[6], a[10], a[11], q0[7]};
+  plps.clear();
+  for (int k = 0; k < n; k++) {
+    const int *q = a + 13 + 9 * k;
+    plps.push_back(PlpParams{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]});
+  }
+  return true;
+}
+
 extern "C" {
+
+// multi-PLP frame plan: info [M, S, aux_len, t2frames, Lp, D, nplp, starts[8], cs[8], F[8]]
+int t2probe_frame_mplp(const int *mp, int *info, int32_t *gather_in, int32_t *gather_d, float *aux) {
+  FmParams p;
+  std::vector<PlpParams> plps;
+  FramePlan fp;
+  if (!parse_mplp(mp, p, plps) || build_frame_mplp(p, plps, fp, true)) return -1;
+  int v[7] = {fp.M, fp.S, fp.aux_len, fp.t2frames, fp.Lp, fp.D, fp.nplp};
+  memcpy(info, v, sizeof(v));
+  for (int k = 0; k < 8; k++) {
+    info[7 + k] = k < fp.nplp ? fp.plp[k].start : 0;
+    info[15 + k] = k < fp.nplp ? fp.plp[k].cs : 0;
+    info[23 + k] = k < fp.nplp ? fp.plp[k].F : 0;
+  }
+  if (gather_in) memcpy(gather_in, fp.gather_in.data(), fp.gather_in.size() * 4);
+  if (gather_d) memcpy(gather_d, fp.gather_d.data(), fp.gather_d.size() * 4);
+  if (aux) memcpy(aux, fp.aux.data(), fp.aux.size() * 8);
+  return 0;
+}
+
+// multi-PLP chain layout: as t2probe_chain, plus plp_bnd (2 Nsym x (nplp + 1)); info [Nsym, N, S, split, nplp]
+int t2probe_chain_mplp(const int *mp, const int *pg3, int *info, int32_t *cmap, uint16_t *inv, int32_t *d0,
+                       int32_t *dn, int32_t *dn0, int32_t *part, int32_t *bnd) {
+  FmParams f;
+  std::vector<PlpParams> plps;
+  if (!parse_mplp(mp, f, plps)) return -1;
+  PgParams g{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
+             f.preamble, pg3[0], pg3[1], pg3[2], fft_points(f.fftsize)};
+  FramePlan fp;
+  PilotPlan pp;
+  ChainLayout cl;
+  if (build_frame_mplp(f, plps, fp) || build_pilot(g, pp) || build_chain_layout(fp, pp, cl)) return -1;
+  info[0] = pp.Nsym; info[1] = pp.N; info[2] = fp.S; info[3] = ofdm_split(pp.N) ? 1 : 0; info[4] = fp.nplp;
+  if (cmap) memcpy(cmap, cl.cmap.data(), cl.cmap.size() * 4);
+  if (inv) memcpy(inv, cl.inv.data(), cl.inv.size() * 2);
+  if (d0) memcpy(d0, cl.sym_d0.data(), cl.sym_d0.size() * 4);
+  if (dn) memcpy(dn, cl.sym_n.data(), cl.sym_n.size() * 4);
+  if (dn0) memcpy(dn0, cl.sym_n0.data(), cl.sym_n0.size() * 4);
+  if (part) memcpy(part, cl.part.data(), cl.part.size() * 4);
+  if (bnd) memcpy(bnd, cl.plp_bnd.data(), cl.plp_bnd.size() * 4);
+  return 0;
+}
+
+// multi-PLP L1-post of one FRAME_IDX from the bit-by-bit host encoder; out Lp complex; info [nsig, npost, Lp]
+int t2probe_l1post_mplp(const int *mp, int frame_idx, float *out, int *info) {
+  FmParams p;
+  std::vector<PlpParams> plps;
+  FramePlan fp;
+  if (!parse_mplp(mp, p, plps) || build_frame_mplp(p, plps, fp)) return -1;
+  if (info) { info[0] = fp.l1.nsig; info[1] = fp.l1.npost; info[2] = fp.l1.lp; }
+  return out ? l1post_host(p, fp, frame_idx, (cf32 *)out) : 0;
+}
 
 // info: [M, S, aux_len, t2frames, cs, F, N_P2, C_P2, C_DATA, N_FC, C_FC, Lp, D,
 //        ti_on, ti_small, ti_big, ti_nsmall]

@@ -7,6 +7,8 @@ HIP/gfx950 library libdvbt2ll_hip.so through its C ABI (include/dvbt2ll_hip.h).
 """
 from .enums import *  # noqa: F401,F403
 from .blocks import bbheaderbch_bb, ldpc_bb, interleavermod_bc, framemapperfint_cc, pilotgenp1insert_cc  # noqa: F401
+from .blocks import framemapper_mplp_cc  # noqa: F401
 from .chain import Chain, IQ_CF32, IQ_SC16  # noqa: F401
 from .configs import CONFIGS, T2Config, ts_packets, ts_for_frames  # noqa: F401
+from .configs import MPLP_CONFIGS, MplpConfig, PlpConfig  # noqa: F401
 from ._lib import lib, LIB_PATH, EXPORTS, DVBT2Error  # noqa: F401

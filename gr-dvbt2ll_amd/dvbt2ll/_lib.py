@@ -45,6 +45,34 @@ class _ChainParams(ctypes.Structure):
                 ("bandwidth", ctypes.c_int), ("max_frames", ctypes.c_int), ("tsrate", ctypes.c_int)]
 
 
+MAX_PLP = 8   # DVBT2LL_MAX_PLP
+
+
+class _PlpParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "framesize", "rate", "constellation", "rotation", "fecblocks", "tiblocks", "inputmode", "inband", "tsrate")]
+
+
+class _MplpParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "carriermode", "fftsize", "guardinterval", "l1constellation", "pilotpattern", "t2frames", "numdatasyms",
+        "paprmode", "version", "preamble", "reservedbiasbits", "l1scrambled", "nplp")] + [("plp", _PlpParams * MAX_PLP)]
+
+    @classmethod
+    def from_config(cls, mcfg):
+        """dvbt2ll_mplp_params of a dvbt2ll.configs.MplpConfig"""
+        a = mcfg.mplp_array()
+        p = cls(*a[:13])
+        for k in range(MAX_PLP):
+            p.plp[k] = _PlpParams(*a[13 + 9 * k:22 + 9 * k])
+        return p
+
+
+class _MplpChainParams(ctypes.Structure):
+    _fields_ = [("fm", _MplpParams), ("misogroup", ctypes.c_int), ("equalization", ctypes.c_int),
+                ("bandwidth", ctypes.c_int), ("max_frames", ctypes.c_int)]
+
+
 class _ChainInfo(ctypes.Structure):
     _fields_ = [("fec_blocks_per_frame", ctypes.c_int), ("payload_bytes_per_block", ctypes.c_int),
                 ("ts_bytes_per_frame", ctypes.c_int64), ("iq_samples_per_frame", ctypes.c_int64),
@@ -64,6 +92,11 @@ for _b in BLOCKS:
                 ("create", "output_multiple", "forecast", "general_work", "destroy")]
 EXPORTS += ["dvbt2ll_framemapperfint_stream_items", "dvbt2ll_pilotgenp1insert_active_items",
             "dvbt2ll_pilotgenp1insert_debug_carriers", "dvbt2ll_bbheaderbch_sync_errors"]
+EXPORTS += ["dvbt2ll_bbheaderbch_set_isi"]
+EXPORTS += ["dvbt2ll_framemapper_mplp_" + f for f in ("create", "output_multiple", "stream_items", "forecast",
+                                                      "general_work", "destroy")]
+EXPORTS += ["dvbt2ll_chain_" + f for f in ("create_mplp", "num_plps", "get_plp_info", "run_plps",
+                                           "debug_plp_codewords")]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_streams", "run_host", "set_output", "set_slots", "set_graph", "set_timing",
                                            "get_timing", "debug_codewords", "debug_cell_pairs", "debug_cells",
                                            "synchronize", "sync_errors",
@@ -109,6 +142,21 @@ def lib():
     L.dvbt2ll_chain_sync_errors.argtypes = [vp, ctypes.POINTER(i64)]
     L.dvbt2ll_bbheaderbch_sync_errors.argtypes = [vp]
     L.dvbt2ll_bbheaderbch_sync_errors.restype = i64
+    L.dvbt2ll_bbheaderbch_set_isi.argtypes = [vp, ci]
+    L.dvbt2ll_framemapper_mplp_create.argtypes = [ctypes.POINTER(_MplpParams), ci, ctypes.POINTER(vp)]
+    L.dvbt2ll_framemapper_mplp_output_multiple.argtypes = [vp]
+    L.dvbt2ll_framemapper_mplp_stream_items.argtypes = [vp, ci]
+    L.dvbt2ll_framemapper_mplp_forecast.argtypes = [vp, ci, ctypes.POINTER(ci)]
+    L.dvbt2ll_framemapper_mplp_general_work.argtypes = [vp, ci, ctypes.POINTER(ci), ctypes.POINTER(vp), vp,
+                                                        ctypes.POINTER(ci)]
+    L.dvbt2ll_framemapper_mplp_destroy.argtypes = [vp]
+    L.dvbt2ll_framemapper_mplp_destroy.restype = None
+    L.dvbt2ll_chain_create_mplp.argtypes = [ctypes.POINTER(_MplpChainParams), ci, ctypes.POINTER(vp)]
+    L.dvbt2ll_chain_num_plps.argtypes = [vp]
+    L.dvbt2ll_chain_get_plp_info.argtypes = [vp, ci, ctypes.POINTER(_ChainInfo)]
+    L.dvbt2ll_chain_run_plps.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i64), ctypes.POINTER(i64), i64, ci,
+                                         vp, vp]
+    L.dvbt2ll_chain_debug_plp_codewords.argtypes = [vp, ci, vp, i64]
     L.dvbt2ll_chain_destroy.argtypes = [vp]
     L.dvbt2ll_chain_destroy.restype = None
     _lib = L

@@ -10,7 +10,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import lib, check, _BbParams, _LdpcParams, _ImParams, _FmParams, _PgParams
+from ._lib import lib, check, _BbParams, _LdpcParams, _ImParams, _FmParams, _PgParams, _MplpParams
 
 
 class _Block:
@@ -71,6 +71,11 @@ class bbheaderbch_bb(_Block):
         """TS sync bytes != 0x47 consumed so far (reference: a GR_LOG_WARN each, :675, :703)"""
         return lib().dvbt2ll_bbheaderbch_sync_errors(self._h)
 
+    def set_isi(self, isi):
+        """one PLP of a multi-PLP frame: BBHEADER MATYPE multiple input streams, ISI = the PLP_ID
+        (the reference add_bbheader's MIS branch, lib/bbheaderbch_bb_impl.cc:288-298)"""
+        check(lib().dvbt2ll_bbheaderbch_set_isi(self._h, int(isi)), "set_isi")
+
 
 class ldpc_bb(_Block):
     """gr-dtv dvb_ldpc_bb(DVBT2, framesize, rate, MOD_OTHER) replacement used between
@@ -113,3 +118,58 @@ class pilotgenp1insert_cc(_Block):
         check(lib().dvbt2ll_pilotgenp1insert_debug_carriers(self._h, cells.ctypes.data_as(ctypes.c_void_p),
                                                              out.ctypes.data_as(ctypes.c_void_p)), "carriers")
         return out
+
+
+class framemapper_mplp_cc:
+    """framemapperfint_cc with one input port per Type-1 data PLP (the reference
+    carries one PLP, lib/framemapperfint_cc_impl.cc:152-250): make(MplpConfig); one T2 frame per
+    general_work call, consuming stream_items(k) cells from every port k"""
+    in_dtype = np.complex64
+    out_dtype = np.complex64
+
+    def __init__(self, mcfg, device=0):
+        self._h = None
+        self.nplp = mcfg.nplp
+        p = _MplpParams.from_config(mcfg)
+        h = ctypes.c_void_p()
+        check(lib().dvbt2ll_framemapper_mplp_create(ctypes.byref(p), int(device), ctypes.byref(h)),
+              "framemapper_mplp make")
+        self._h = h
+        self.nitems_consumed = [0] * self.nplp
+
+    @classmethod
+    def make(cls, *args, **kw):
+        return cls(*args, **kw)
+
+    def output_multiple(self):
+        return lib().dvbt2ll_framemapper_mplp_output_multiple(self._h)
+
+    def stream_items(self, plp):
+        return lib().dvbt2ll_framemapper_mplp_stream_items(self._h, int(plp))
+
+    def forecast(self, noutput_items):
+        n = (ctypes.c_int * self.nplp)()
+        check(lib().dvbt2ll_framemapper_mplp_forecast(self._h, int(noutput_items), n), "forecast")
+        return list(n)
+
+    def general_work(self, input_items, output_items, noutput_items=None):
+        assert len(input_items) == self.nplp
+        ins = [np.ascontiguousarray(x, np.complex64) for x in input_items]
+        out = output_items[0]
+        assert out.dtype == self.out_dtype and out.flags.c_contiguous
+        nout = len(out) if noutput_items is None else int(noutput_items)
+        nin = (ctypes.c_int * self.nplp)(*[len(x) for x in ins])
+        ptrs = (ctypes.c_void_p * self.nplp)(*[x.ctypes.data for x in ins])
+        cons = (ctypes.c_int * self.nplp)()
+        r = lib().dvbt2ll_framemapper_mplp_general_work(self._h, nout, nin, ptrs, out.ctypes.data_as(ctypes.c_void_p),
+                                                         cons)
+        check(r, "framemapper_mplp general_work")
+        for k in range(self.nplp):
+            self.nitems_consumed[k] += cons[k]
+        self.last_consumed = list(cons)
+        return r
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().dvbt2ll_framemapper_mplp_destroy(self._h)
+            self._h = None

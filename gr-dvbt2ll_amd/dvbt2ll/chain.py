@@ -9,8 +9,8 @@ import ctypes
 
 import numpy as np
 
-from ._lib import lib, check, _ChainParams, _ChainInfo, _FmParams
-from .configs import ts_for_frames
+from ._lib import lib, check, _ChainParams, _ChainInfo, _FmParams, _MplpParams, _MplpChainParams
+from .configs import ts_for_frames, MplpConfig
 
 IQ_CF32 = 0   # DVBT2LL_IQ_CF32
 IQ_SC16 = 1   # DVBT2LL_IQ_SC16
@@ -18,18 +18,30 @@ IQ_SC16 = 1   # DVBT2LL_IQ_SC16
 
 class Chain:
     def __init__(self, cfg, max_frames=1, device=0):
+        """cfg: a T2Config (the reference's single-PLP frame) or an MplpConfig (several Type-1 data PLPs,
+        dvbt2ll_chain_create_mplp)"""
         self.cfg = cfg
-        fm = _FmParams(*[int(v) for v in cfg.fm_args()])
-        p = _ChainParams(fm, int(cfg.misogroup), int(cfg.equalization), int(cfg.bandwidth), int(max_frames),
-                         int(cfg.tsrate))
         h = ctypes.c_void_p()
         self._h = None
-        check(lib().dvbt2ll_chain_create(ctypes.byref(p), int(device), ctypes.byref(h)), "chain create")
+        if isinstance(cfg, MplpConfig):
+            p = _MplpChainParams(_MplpParams.from_config(cfg), int(cfg.misogroup), int(cfg.equalization),
+                                 int(cfg.bandwidth), int(max_frames))
+            check(lib().dvbt2ll_chain_create_mplp(ctypes.byref(p), int(device), ctypes.byref(h)), "chain create")
+        else:
+            fm = _FmParams(*[int(v) for v in cfg.fm_args()])
+            p = _ChainParams(fm, int(cfg.misogroup), int(cfg.equalization), int(cfg.bandwidth), int(max_frames),
+                             int(cfg.tsrate))
+            check(lib().dvbt2ll_chain_create(ctypes.byref(p), int(device), ctypes.byref(h)), "chain create")
         self._h = h
         self.max_frames = max_frames
+        self.nplp = lib().dvbt2ll_chain_num_plps(self._h)
         info = _ChainInfo()
         check(lib().dvbt2ll_chain_get_info(self._h, ctypes.byref(info)), "chain info")
         self.info = {f: getattr(info, f) for f, _ in _ChainInfo._fields_}
+        self.plp_info = []
+        for k in range(self.nplp):
+            check(lib().dvbt2ll_chain_get_plp_info(self._h, k, ctypes.byref(info)), "plp info")
+            self.plp_info.append({f: getattr(info, f) for f, _ in _ChainInfo._fields_})
         self.iq_format = IQ_CF32
         self.nslots = 1
 
@@ -70,6 +82,24 @@ class Chain:
                                               int(ts_base), int(ts_len), int(first_frame), int(nframes),
                                               ctypes.c_void_p(iq_ptr), ctypes.c_void_p(stream or None)),
               "chain run streams")
+
+    def run_plps(self, ts_ptrs, ts_bases, ts_lens, first_frame, nframes, iq_ptr, stream=0):
+        """multi-PLP frames: PLP k's TS at device pointer ts_ptrs[k] (absolute offset ts_bases[k], ts_lens[k]
+        bytes) -> IQ of frames [first_frame, first_frame + nframes) (dvbt2ll_chain_run_plps)"""
+        n = self.nplp
+        assert len(ts_ptrs) == len(ts_bases) == len(ts_lens) == n
+        check(lib().dvbt2ll_chain_run_plps(self._h, (ctypes.c_void_p * n)(*ts_ptrs),
+                                           (ctypes.c_int64 * n)(*[int(x) for x in ts_bases]),
+                                           (ctypes.c_int64 * n)(*[int(x) for x in ts_lens]), int(first_frame),
+                                           int(nframes), ctypes.c_void_p(iq_ptr), ctypes.c_void_p(stream or None)),
+              "chain run plps")
+
+    def debug_plp_codewords(self, plp, nblocks):
+        stride = self.plp_info[plp]["cw_stride_bytes"]
+        out = np.zeros(nblocks * stride, np.uint8)
+        check(lib().dvbt2ll_chain_debug_plp_codewords(self._h, int(plp), out.ctypes.data_as(ctypes.c_void_p),
+                                                      len(out)), "cw")
+        return out.reshape(nblocks, stride)
 
     def run(self, first_frame, nframes, ts=None, ts_base=None, seed=1):
         """host convenience: synthetic TS (or the given buffer) -> IQ numpy array"""

@@ -88,6 +88,102 @@ CONFIGS = {
                       2, 3, E.CARRIERS_NORMAL, E.FFTSIZE_4K, E.GI_1_32, E.L1_MOD_64QAM, E.PILOT_PP7, 2, 3),
 }
 
+MAX_PLP = 8   # DVBT2LL_MAX_PLP
+
+
+@dataclass(frozen=True)
+class PlpConfig:
+    """one Type-1 data PLP of a multi-PLP T2 frame (EN 302 755 8.3.6.3; the reference carries one,
+    lib/framemapperfint_cc_impl.cc:152-250): its FEC, constellation, time interleaver and input stream.
+    Quacks like T2Config for ts_for_frames / the per-PLP blocks."""
+    framesize: int
+    rate: int
+    constellation: int
+    rotation: int
+    fecblocks: int
+    tiblocks: int
+    inputmode: int = E.INPUTMODE_NORMAL
+    inband: int = E.INBAND_OFF
+    tsrate: int = 4000000
+
+    def bb_args(self):
+        return (self.framesize, self.rate, self.inputmode, self.inband, self.fecblocks, self.tsrate)
+
+    def im_args(self):
+        return (self.framesize, self.rate, self.constellation, self.rotation)
+
+    def plp_args(self):
+        return (self.framesize, self.rate, self.constellation, self.rotation, self.fecblocks, self.tiblocks,
+                self.inputmode, self.inband, self.tsrate)
+
+
+@dataclass(frozen=True)
+class MplpConfig:
+    """a T2 frame carrying len(plps) Type-1 data PLPs (PLP_ID = index, PLP 0's TS seed 1, PLP k's k + 1)
+    with the common (frame / L1 / OFDM) parameters"""
+    name: str
+    plps: tuple
+    carriermode: int
+    fftsize: int
+    guardinterval: int
+    l1constellation: int
+    pilotpattern: int
+    t2frames: int
+    numdatasyms: int
+    paprmode: int = E.PAPR_OFF
+    version: int = E.VERSION_111
+    preamble: int = E.PREAMBLE_T2_SISO
+    reservedbiasbits: int = E.RESERVED_OFF
+    l1scrambled: int = E.L1_SCRAMBLED_OFF
+    misogroup: int = E.MISO_TX1
+    equalization: int = E.EQUALIZATION_OFF
+    bandwidth: int = E.BANDWIDTH_8_0_MHZ
+
+    @property
+    def nplp(self):
+        return len(self.plps)
+
+    @property
+    def vlength(self):
+        return FFT_POINTS[self.fftsize]
+
+    def common_args(self):
+        return (self.carriermode, self.fftsize, self.guardinterval, self.l1constellation, self.pilotpattern,
+                self.t2frames, self.numdatasyms, self.paprmode, self.version, self.preamble, self.reservedbiasbits,
+                self.l1scrambled)
+
+    def mplp_array(self):
+        """the dvbt2ll_mplp_params layout (include/dvbt2ll_hip.h) as ints"""
+        assert 1 <= self.nplp <= MAX_PLP
+        a = list(self.common_args()) + [self.nplp]
+        for k in range(MAX_PLP):
+            a += list(self.plps[k].plp_args()) if k < self.nplp else [0] * 9
+        return a
+
+    def pg_args(self):
+        return (self.carriermode, self.fftsize, self.pilotpattern, self.guardinterval, self.numdatasyms,
+                self.paprmode, self.version, self.preamble, self.misogroup, self.equalization, self.bandwidth,
+                self.vlength)
+
+    def with_(self, **kw):
+        return replace(self, **kw)
+
+
+def _plp(cfg, **kw):
+    d = dict(framesize=cfg.framesize, rate=cfg.rate, constellation=cfg.constellation, rotation=cfg.rotation,
+             fecblocks=cfg.fecblocks, tiblocks=cfg.tiblocks, inputmode=cfg.inputmode, inband=cfg.inband,
+             tsrate=cfg.tsrate)
+    d.update(kw)
+    return PlpConfig(**d)
+
+
+def mplp_from(cfg, name, plps):
+    """a multi-PLP frame with cfg's common parameters"""
+    return MplpConfig(name, tuple(plps), cfg.carriermode, cfg.fftsize, cfg.guardinterval, cfg.l1constellation,
+                      cfg.pilotpattern, cfg.t2frames, cfg.numdatasyms, cfg.paprmode, cfg.version, cfg.preamble,
+                      cfg.reservedbiasbits, cfg.l1scrambled, cfg.misogroup, cfg.equalization, cfg.bandwidth)
+
+
 KBCH = {(1, 0): 32208, (1, 1): 38688, (1, 2): 43040, (1, 3): 48408, (1, 4): 51648, (1, 5): 53840,
         (0, 6): 5232, (0, 7): 6312, (0, 0): 7032, (0, 1): 9552, (0, 2): 10632, (0, 3): 11712,
         (0, 4): 12432, (0, 5): 13152}
@@ -138,3 +234,35 @@ def ts_for_frames(cfg, first_frame, nframes, seed=1):
     p0 = max(0, start // 188 - 1)
     p1 = (end + 187) // 188
     return ts_packets(p0, p1 - p0, seed), p0 * 188
+
+
+def _mplp_configs():
+    c3, c1, c4 = CONFIGS["cfg3"], CONFIGS["cfg1"], CONFIGS["cfg4"]
+    return {
+        # cfg3's frame split between a 256-QAM 3/5 rotated PLP and a 64-QAM 2/3 PLP (the bench's 2-PLP line)
+        "mplp2_32k": mplp_from(c3, "mplp2-32kext-256qam3/5rot+64qam2/3", [
+            _plp(c3, fecblocks=100), _plp(c3, rate=E.C2_3, constellation=E.MOD_64QAM, rotation=E.ROTATION_OFF,
+                                          fecblocks=70, tiblocks=2)]),
+        # three PLPs filling the GRC's 4K short frame exactly (no dummy cells): 256-QAM 4/5 rotated, QPSK 1/2,
+        # 16-QAM 3/5 HEM in two TI blocks (one of them empty)
+        "mplp3_4k": mplp_from(c1, "mplp3-4k-short", [
+            _plp(c1, fecblocks=2, tiblocks=1),
+            _plp(c1, rate=E.C1_2, constellation=E.MOD_QPSK, rotation=E.ROTATION_OFF, fecblocks=1, tiblocks=0),
+            _plp(c1, rate=E.C3_5, constellation=E.MOD_16QAM, fecblocks=1, tiblocks=2,
+                 inputmode=E.INPUTMODE_HIEFF)]),
+        # two 8K PLPs, normal + short FECFRAME
+        "mplp2_8k": mplp_from(c4, "mplp2-8k-16qam1/2+short-256qam", [
+            _plp(c4, fecblocks=12),
+            _plp(c4, framesize=E.FECFRAME_SHORT, rate=E.C2_3, constellation=E.MOD_256QAM, rotation=E.ROTATION_ON,
+                 fecblocks=10, tiblocks=1)]),
+        # three 32K PLPs (one in-band type B, v1.3.1 L1 scrambling)
+        "mplp3_32k": mplp_from(CONFIGS["cfg5"], "mplp3-32k-v131", [
+            _plp(CONFIGS["cfg5"], fecblocks=60, tiblocks=1),
+            _plp(CONFIGS["cfg5"], rate=E.C1_2, constellation=E.MOD_16QAM, rotation=E.ROTATION_ON, fecblocks=30,
+                 tiblocks=2, inband=E.INBAND_ON, tsrate=7654321),
+            _plp(CONFIGS["cfg5"], rate=E.C3_4, constellation=E.MOD_QPSK, fecblocks=15, tiblocks=0)]).with_(
+                version=E.VERSION_131, l1scrambled=E.L1_SCRAMBLED_ON, l1constellation=E.L1_MOD_16QAM),
+    }
+
+
+MPLP_CONFIGS = _mplp_configs()

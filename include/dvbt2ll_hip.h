@@ -190,13 +190,15 @@ int dvbt2ll_chain_run_streams(dvbt2ll_chain *h, const void *ts_dev, int64_t ts_s
  * general_work per block at a time): the pipelined form of the same calls. */
 #define DVBT2LL_CHAIN_MAX_SLOTS 4
 int dvbt2ll_chain_set_slots(dvbt2ll_chain *h, int nslots);
-/* hipGraph launch mode: run_device issues the three kernels as one instantiated hipGraph,
- * captured on first use for each (nframes, IQ format) and re-armed per call by rewriting the
- * kernel nodes' arguments (hipGraphExecKernelNodeSetParams), then one hipGraphLaunch.  For
- * small per-call batches (one T2 frame per call, as GNU Radio's scheduler calls a block);
- * output identical to the direct launches.  One instantiated graph per buffer slot; re-arming it
- * first waits (host side) for the slot's previous run to complete.  Per-stage timing events are skipped in this mode.
- * Default off. */
+/* hipGraph launch mode: run calls issue the chain's kernels as one instantiated hipGraph, captured
+ * on first use for each (nframes, IQ format, buffer slot) into a ring of DVBT2LL_CHAIN_GRAPH_RING
+ * instantiations; a call re-arms the next idle instantiation of the ring (its kernel nodes'
+ * arguments, hipGraphExecKernelNodeSetParams) and launches it, so back-to-back calls on one slot do
+ * not wait for each other on the host (the host only waits when every instantiation of the ring is
+ * still in flight).  For small per-call batches (one T2 frame per call, as GNU Radio's scheduler
+ * calls a block); output identical to the direct launches.  Per-stage timing events are skipped in
+ * this mode.  Default off. */
+#define DVBT2LL_CHAIN_GRAPH_RING 4
 int dvbt2ll_chain_set_graph(dvbt2ll_chain *h, int enable);
 /* host buffers, synchronous */
 int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
@@ -228,6 +230,65 @@ int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells);
 int dvbt2ll_chain_sync_errors(dvbt2ll_chain *h, int64_t *count);
 int dvbt2ll_chain_synchronize(dvbt2ll_chain *h);
 void dvbt2ll_chain_destroy(dvbt2ll_chain *h);
+
+/* ---------------------------------------------------------------------------
+ * Multi-PLP frames (EN 302 755 8.3.6.3): nplp Type-1 data PLPs in one T2
+ * frame, PLP_ID = index, each with its own TS stream, FEC, constellation, cell interleaver and time
+ * interleaver (TIME_IL_TYPE 0, FRAME_INTERVAL 1, so T2 frames stay independent), its cells placed
+ * back to back after the L1 signalling in PLP_ID order (PLP_START = the cells before it); the
+ * L1-post carries the PLP loops.  The reference carries exactly one PLP
+ * (lib/framemapperfint_cc_impl.cc:152-250: num_plp = 1; L1-post serialised at :1553-1691): nplp = 1
+ * is its frame bit for bit, nplp > 1 is not pinned by it (PARITY UNPINNED).
+ * ------------------------------------------------------------------------- */
+#define DVBT2LL_MAX_PLP 8
+typedef struct {
+  int framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, tsrate;
+} dvbt2ll_plp_params;
+typedef struct {
+  /* the common (frame, L1, OFDM) fields of framemapperfint_cc::make */
+  int carriermode, fftsize, guardinterval, l1constellation, pilotpattern, t2frames, numdatasyms, paprmode,
+      version, preamble, reservedbiasbits, l1scrambled;
+  int nplp;                                  /* 1 .. DVBT2LL_MAX_PLP */
+  dvbt2ll_plp_params plp[DVBT2LL_MAX_PLP];   /* plp[k]: PLP_ID k */
+} dvbt2ll_mplp_params;
+
+/* one PLP of a multi-PLP frame: the BBHEADER of every later BBFRAME says MATYPE SIS/MIS = multiple
+ * input streams and MATYPE-2 (ISI) = isi (the PLP_ID), the MIS branch of the reference's add_bbheader
+ * (lib/bbheaderbch_bb_impl.cc:288-298) that its ctor never selects (:168) */
+int dvbt2ll_bbheaderbch_set_isi(dvbt2ll_bbheaderbch *h, int isi);
+
+/* framemapperfint_cc with one input port per PLP (the per-PLP bbheaderbch -> ldpc -> interleavermod
+ * chains feed port k with PLP k's cells): one T2 frame per general_work call, consuming
+ * stream_items(k) cells from every port (framemapper:1942-1946, 2147 per port) */
+typedef struct dvbt2ll_framemapper_mplp dvbt2ll_framemapper_mplp;
+int dvbt2ll_framemapper_mplp_create(const dvbt2ll_mplp_params *p, int device, dvbt2ll_framemapper_mplp **out);
+int dvbt2ll_framemapper_mplp_output_multiple(const dvbt2ll_framemapper_mplp *h);     /* mapped_items */
+int dvbt2ll_framemapper_mplp_stream_items(const dvbt2ll_framemapper_mplp *h, int plp);
+/* nin_required[k] for each of the nplp ports */
+int dvbt2ll_framemapper_mplp_forecast(const dvbt2ll_framemapper_mplp *h, int noutput_items, int *ninput_items_required);
+/* in[k], ninput_items[k]: port k's cells (host complex64); consumed[k] per port */
+int dvbt2ll_framemapper_mplp_general_work(dvbt2ll_framemapper_mplp *h, int noutput_items, const int *ninput_items,
+                                          const void *const *in, void *out, int *consumed);
+void dvbt2ll_framemapper_mplp_destroy(dvbt2ll_framemapper_mplp *h);
+
+/* fused chain of a multi-PLP frame: every PLP's TS -> BBFRAME/BCH/LDPC -> map, one frame's OFDM */
+typedef struct {
+  dvbt2ll_mplp_params fm;
+  int misogroup, equalization, bandwidth;
+  int max_frames;
+} dvbt2ll_mplp_chain_params;
+int dvbt2ll_chain_create_mplp(const dvbt2ll_mplp_chain_params *p, int device, dvbt2ll_chain **out);
+int dvbt2ll_chain_num_plps(const dvbt2ll_chain *h);
+/* PLP plp's FEC blocks, payload and TS bytes per frame, cell size, cells per frame (stream_items) and
+ * codeword stride; the frame-wide fields as dvbt2ll_chain_get_info (which reports PLP 0's) */
+int dvbt2ll_chain_get_plp_info(const dvbt2ll_chain *h, int plp, dvbt2ll_chain_info *info);
+/* ts_dev[k], ts_base[k], ts_len[k]: PLP k's TS, laid out as run_device's (host arrays of nplp entries);
+ * frames [first_frame, first_frame + nframes) into iq_dev.  Asynchronous on stream.  run_device on a
+ * one-PLP chain == run_plps with one entry. */
+int dvbt2ll_chain_run_plps(dvbt2ll_chain *h, const void *const *ts_dev, const int64_t *ts_base,
+                           const int64_t *ts_len, int64_t first_frame, int nframes, void *iq_dev, void *stream);
+/* test hook: PLP plp's packed codewords of the last run's frame 0 (as dvbt2ll_chain_debug_codewords) */
+int dvbt2ll_chain_debug_plp_codewords(dvbt2ll_chain *h, int plp, void *out, int64_t bytes);
 
 #ifdef __cplusplus
 }

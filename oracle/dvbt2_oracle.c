@@ -197,6 +197,7 @@ static void ldpc_encode(const t2_ldpc_code_t *c, int nbch, int nldpc, uint8_t *c
 /* ========================================================================= */
 struct orc_bb {
   int kbch, nbch, P, mode, inband, fec_blocks, fec_block, ts_rate;
+  int sis_mis, isi;                  /* MATYPE-1 SIS/MIS bit, MATYPE-2 (bbheader:168, 281, 288-298) */
   unsigned count;
   uint8_t crc;
   int extra;
@@ -244,6 +245,7 @@ orc_bb *orc_bb_create(int framesize, int rate, int mode, int inband, int fecbloc
   h->mode = mode; h->inband = inband; h->fec_blocks = fecblocks > 0 ? fecblocks : 1;
   h->ts_rate = tsrate;
   h->count = 0; h->crc = 0; h->fec_block = 0;
+  h->sis_mis = 1; h->isi = 0;                      /* SIS_MIS_SINGLE (bbheader:168) */
   h->extra = (((h->kbch - 80) / 8) / 187) + 1;    /* bbheader:194 */
   crc8_table(h->crc_tab);
   orc_bb_prbs(h->bb_randomise, FRAME_SIZE_NORMAL);
@@ -252,6 +254,10 @@ orc_bb *orc_bb_create(int framesize, int rate, int mode, int inband, int fecbloc
   bch_table(&g, h->P, h->tab);
   return h;
 }
+/* multiple input streams (one PLP of a multi-PLP frame): SIS/MIS = SIS_MIS_MULTIPLE, ISI = the PLP_ID.
+ * The reference's ctor always sets SIS (bbheader:168); its add_bbheader already carries the MIS
+ * branch (:288-298), which this enables.  Parity unpinned (the reference never takes the branch). */
+void orc_bb_set_isi(orc_bb *h, int isi) { h->sis_mis = 0; h->isi = isi & 0xFF; }
 int orc_bb_nbch(const orc_bb *h) { return h->nbch; }
 int orc_bb_kbch(const orc_bb *h) { return h->kbch; }
 void orc_bb_destroy(orc_bb *h) { free(h); }
@@ -278,15 +284,15 @@ static void put_bits(uint8_t *dst, int *off, unsigned v, int nbits) {
   for (int n = nbits - 1; n >= 0; n--) dst[(*off)++] = (v >> n) & 1;
 }
 
-/* add_bbheader (bbheader:272-325): TS, SIS, CCM, ISSYI=0, NPD=0, RO=0, ISI=0 */
+/* add_bbheader (bbheader:272-325): TS, SIS (or MIS with ISI, :288-298), CCM, ISSYI=0, NPD=0, RO=0 */
 static void add_bbheader(const orc_bb *h, uint8_t *f, unsigned count, int padding) {
   int o = 0;
   f[o++] = 1; f[o++] = 1;          /* TS_GS = 3 */
-  f[o++] = 1;                      /* SIS */
+  f[o++] = (uint8_t)h->sis_mis;    /* SIS_MIS_SINGLE 1 / SIS_MIS_MULTIPLE 0 */
   f[o++] = 1;                      /* CCM */
   f[o++] = 0; f[o++] = 0;          /* ISSYI, NPD */
   f[o++] = 0; f[o++] = 0;          /* RO */
-  put_bits(f, &o, 0, 8);           /* MATYPE-2 (ISI) */
+  put_bits(f, &o, h->sis_mis ? 0u : (unsigned)h->isi, 8);   /* MATYPE-2 (ISI) */
   put_bits(f, &o, h->mode == INPUTMODE_NORMAL ? 188 * 8 : 0, 16);    /* UPL */
   put_bits(f, &o, (unsigned)(h->kbch - 80 - padding), 16);           /* DFL */
   put_bits(f, &o, h->mode == INPUTMODE_NORMAL ? 0x47 : 0, 8);        /* SYNC */
@@ -538,21 +544,34 @@ int orc_im_work(orc_im *h, int nout, const uint8_t *in, float *out, int *consume
 #define KSIG_POST 350
 #define NBCH_PARITY 168
 
-struct orc_fm {
-  int cell_size, stream_items, mapped_items, l1_constellation, eta_mod, t2_frames, t2_frame_num;
-  int l1_scrambled, N_P2, C_P2, N_FC, C_FC, C_DATA, N_post, N_punc, num_data_symbols, pn_degree;
+/* One Type-1 data PLP of the frame.  The reference carries exactly one (framemapper:152-250:
+ * num_plp = 1, plp_type = 1, time_il_type = 0, frame_interval = 1); this restatement generalises its
+ * per-PLP state to nplp PLPs of EN 302 755 8.3.6.3 (PARITY UNPINNED beyond nplp = 1): PLP p has PLP_ID p,
+ * its own FEC / constellation / cell interleaver / time interleaver, and its TI output occupies the
+ * data cells [start, start + stream_items) after the L1 signalling, PLPs in PLP_ID order. */
+#define ORC_MAX_PLP 16
+typedef struct {
+  int cell_size, stream_items, start, pn_degree;
   int ti_blocks, fec_blocks, small_fec, big_fec, n_big, n_small;
+  int plp_cod, plp_mod, rotation, fec_type, inband_b, plp_mode;
+  int *permutations;
+  cf *time_interleave;
+} orc_plp;
+
+struct orc_fm {
+  int nplp, ksig_post;               /* ksig_post: L1-post signalling bits incl. CRC (KSIG_POST = 350 for one PLP) */
+  orc_plp plp[ORC_MAX_PLP];
+  int stream_items, mapped_items, l1_constellation, eta_mod, t2_frames, t2_frame_num;
+  int l1_scrambled, N_P2, C_P2, N_FC, C_FC, C_DATA, N_post, N_punc, num_data_symbols;
   /* L1 fields that are not constant (framemapper ctor :114-250) */
   int pre_fields[32];
-  int post_plp_cod, post_plp_mod, post_rotation, post_fec_type, post_num_blocks, post_ti_length;
-  int post_inband_b, post_reserved1, post_plp_mode, post_reserved2, post_reserved3, post_reserved4,
-      post_reserved5;
+  int post_reserved1, post_reserved2, post_reserved3, post_reserved4, post_reserved5;
   r192 bch_short_tab[256];
   cf l1pre_cache[1840];
   cf m_bpsk[2], m_qpsk[4], m_16qam[16], m_64qam[64];
   uint8_t l1_randomize[KBCH_1_2];
-  int *Heven, *Hodd, *HevenP2, *HoddP2, *HevenFC, *HoddFC, *permutations;
-  cf *time_interleave, *cell_out, *frame_out, *zigzag, *dummy;
+  int *Heven, *Hodd, *HevenP2, *HoddP2, *HevenFC, *HoddFC;
+  cf *cell_out, *frame_out, *zigzag, *dummy;
 };
 
 /* add_crc32_bits (framemapper:1205-1224) */
@@ -589,7 +608,7 @@ static void add_l1pre(orc_fm *h, cf *out) {
   put_bits(b, &o, 0, 2);                /* L1_COD */
   put_bits(b, &o, 0, 2);                /* L1_FEC_TYPE */
   put_bits(b, &o, (unsigned)f[7], 18);  /* L1_POST_SIZE */
-  put_bits(b, &o, KSIG_POST - 32, 18);  /* L1_POST_INFO_SIZE */
+  put_bits(b, &o, (unsigned)(h->ksig_post - 32), 18);  /* L1_POST_INFO_SIZE (KSIG_POST - 32, :125) */
   put_bits(b, &o, (unsigned)f[8], 4);   /* PILOT_PATTERN */
   put_bits(b, &o, 0, 8);                /* TX_ID_AVAILABILITY */
   put_bits(b, &o, 0, 16);               /* CELL_ID */
@@ -622,37 +641,41 @@ static void add_l1pre(orc_fm *h, cf *out) {
     if (b[w + NBCH_1_4] != 0x55) out[idx++] = h->m_bpsk[b[w + NBCH_1_4]];
 }
 
-/* add_l1post (framemapper:1536-1910) */
+/* add_l1post (framemapper:1536-1910); the PLP loops of the configurable (:1577-1639) and dynamic
+ * (:1672-1687) parts run over the frame's PLPs */
 static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
   uint8_t info[FRAME_SIZE_SHORT], t[FRAME_SIZE_SHORT], map[KBCH_1_2];
   int o = 0;
   put_bits(info, &o, 1, 15);                 /* SUB_SLICES_PER_FRAME */
-  put_bits(info, &o, 1, 8);                  /* NUM_PLP */
+  put_bits(info, &o, (unsigned)h->nplp, 8);  /* NUM_PLP */
   put_bits(info, &o, 0, 4);                  /* NUM_AUX */
   put_bits(info, &o, 0, 8);                  /* AUX_CONFIG_RFU */
   put_bits(info, &o, 0, 3);                  /* RF_IDX */
   put_bits(info, &o, 729833333u, 32);        /* FREQUENCY */
-  put_bits(info, &o, 0, 8);                  /* PLP_ID */
-  put_bits(info, &o, 1, 3);                  /* PLP_TYPE */
-  put_bits(info, &o, 3, 5);                  /* PLP_PAYLOAD_TYPE */
-  info[o++] = 0;                             /* FF_FLAG */
-  put_bits(info, &o, 0, 3);                  /* FIRST_RF_IDX */
-  put_bits(info, &o, 0, 8);                  /* FIRST_FRAME_IDX */
-  put_bits(info, &o, 1, 8);                  /* PLP_GROUP_ID */
-  put_bits(info, &o, (unsigned)h->post_plp_cod, 3);
-  put_bits(info, &o, (unsigned)h->post_plp_mod, 3);
-  info[o++] = (uint8_t)h->post_rotation;
-  put_bits(info, &o, (unsigned)h->post_fec_type, 2);
-  put_bits(info, &o, (unsigned)h->post_num_blocks, 10);   /* PLP_NUM_BLOCKS_MAX */
-  put_bits(info, &o, 1, 8);                  /* FRAME_INTERVAL */
-  put_bits(info, &o, (unsigned)h->post_ti_length, 8);
-  info[o++] = 0;                             /* TIME_IL_TYPE */
-  info[o++] = 0;                             /* IN_BAND_A_FLAG */
-  info[o++] = (uint8_t)h->post_inband_b;
-  put_bits(info, &o, (unsigned)h->post_reserved1, 11);
-  put_bits(info, &o, (unsigned)h->post_plp_mode, 2);
-  info[o++] = 0;                             /* STATIC_FLAG */
-  info[o++] = 0;                             /* STATIC_PADDING_FLAG */
+  for (int p = 0; p < h->nplp; p++) {
+    const orc_plp *q = &h->plp[p];
+    put_bits(info, &o, (unsigned)p, 8);      /* PLP_ID */
+    put_bits(info, &o, 1, 3);                /* PLP_TYPE: data type 1 */
+    put_bits(info, &o, 3, 5);                /* PLP_PAYLOAD_TYPE: TS */
+    info[o++] = 0;                           /* FF_FLAG */
+    put_bits(info, &o, 0, 3);                /* FIRST_RF_IDX */
+    put_bits(info, &o, 0, 8);                /* FIRST_FRAME_IDX */
+    put_bits(info, &o, 1, 8);                /* PLP_GROUP_ID */
+    put_bits(info, &o, (unsigned)q->plp_cod, 3);
+    put_bits(info, &o, (unsigned)q->plp_mod, 3);
+    info[o++] = (uint8_t)q->rotation;
+    put_bits(info, &o, (unsigned)q->fec_type, 2);
+    put_bits(info, &o, (unsigned)q->fec_blocks, 10);   /* PLP_NUM_BLOCKS_MAX */
+    put_bits(info, &o, 1, 8);                /* FRAME_INTERVAL */
+    put_bits(info, &o, (unsigned)q->ti_blocks, 8);     /* TIME_IL_LENGTH */
+    info[o++] = 0;                           /* TIME_IL_TYPE */
+    info[o++] = 0;                           /* IN_BAND_A_FLAG */
+    info[o++] = (uint8_t)q->inband_b;
+    put_bits(info, &o, (unsigned)h->post_reserved1, 11);
+    put_bits(info, &o, (unsigned)q->plp_mode, 2);
+    info[o++] = 0;                           /* STATIC_FLAG */
+    info[o++] = 0;                           /* STATIC_PADDING_FLAG */
+  }
   put_bits(info, &o, 0, 2);                  /* FEF_LENGTH_MSB */
   put_bits(info, &o, (unsigned)h->post_reserved2, 30);
   put_bits(info, &o, (unsigned)t2_frame_num, 8);         /* FRAME_IDX */
@@ -661,10 +684,13 @@ static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
   put_bits(info, &o, 0, 8);                  /* L1_CHANGE_COUNTER */
   put_bits(info, &o, 0, 3);                  /* START_RF_IDX */
   put_bits(info, &o, (unsigned)h->post_reserved3, 8);
-  put_bits(info, &o, 0, 8);                  /* PLP_ID (dynamic, never set: 0) */
-  put_bits(info, &o, 0, 22);                 /* PLP_START */
-  put_bits(info, &o, (unsigned)h->post_num_blocks, 10);   /* PLP_NUM_BLOCKS */
-  put_bits(info, &o, (unsigned)h->post_reserved4, 8);
+  for (int p = 0; p < h->nplp; p++) {
+    /* PLP_ID (dynamic): the reference's plp_id_dynamic is never set, i.e. 0 for its one PLP */
+    put_bits(info, &o, (unsigned)p, 8);
+    put_bits(info, &o, (unsigned)h->plp[p].start, 22);       /* PLP_START (cell address after L1) */
+    put_bits(info, &o, (unsigned)h->plp[p].fec_blocks, 10);  /* PLP_NUM_BLOCKS */
+    put_bits(info, &o, (unsigned)h->post_reserved4, 8);
+  }
   put_bits(info, &o, (unsigned)h->post_reserved5, 8);
   uint32_t crc = orc_crc32_bits(info, o);
   put_bits(info, &o, crc, 32);
@@ -776,19 +802,36 @@ static void active_counts(int fft, int carriermode, int pp, int papr, int gi, in
   }
 }
 
-orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, int fecblocks,
-                      int tiblocks, int carriermode, int fftsize, int guardinterval,
-                      int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
-                      int paprmode, int version, int preamble, int inputmode,
-                      int reservedbiasbits, int l1scrambled, int inband) {
-  int normal = framesize == FECFRAME_NORMAL;
+/* framemapperfint ctor (framemapper:41-1190) for nplp Type-1 PLPs; plp: nplp x 8 ints per PLP
+ * {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband} */
+orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int carriermode, int fftsize, int guardinterval,
+                           int l1constellation, int pilotpattern, int t2frames, int numdatasyms, int paprmode,
+                           int version, int preamble, int reservedbiasbits, int l1scrambled) {
   int fft = fft_points(fftsize);
-  if (!fft || fecblocks < 1 || t2frames < 1) return NULL;
+  if (!fft || t2frames < 1 || nplp < 1 || nplp > ORC_MAX_PLP) return NULL;
   orc_fm *h = (orc_fm *)calloc(1, sizeof(orc_fm));
-  static const int cs_n[4] = {32400, 16200, 10800, 8100}, cs_s[4] = {8100, 4050, 2700, 2025};
-  h->cell_size = normal ? cs_n[constellation] : cs_s[constellation];
   int siso = preamble == PREAMBLE_T2_SISO || preamble == PREAMBLE_T2_LITE_SISO;
   int v131 = version == VERSION_131, resv = reservedbiasbits && v131;
+  static const int cs_n[4] = {32400, 16200, 10800, 8100}, cs_s[4] = {8100, 4050, 2700, 2025};
+  h->nplp = nplp;
+  /* KSIG_POST = 350 bits for one PLP (framemapperfint_cc_impl.h:32); each further PLP adds its 89
+   * configurable (:1577-1639) and 48 dynamic (:1672-1687) bits */
+  h->ksig_post = KSIG_POST + (nplp - 1) * (89 + 48);
+  for (int p = 0; p < nplp; p++) {
+    const int *q = plp + 8 * p;
+    orc_plp *d = &h->plp[p];
+    if (q[4] < 1 || q[2] < 0 || q[2] > 3) { orc_fm_destroy(h); return NULL; }
+    d->cell_size = q[0] == FECFRAME_NORMAL ? cs_n[q[2]] : cs_s[q[2]];
+    d->fec_blocks = q[4];
+    d->ti_blocks = q[5];
+    /* L1-post fields of the PLP (framemapper:165-221) */
+    d->plp_cod = q[1];                         /* C1_2..C5_6 -> 0..5, C1_3 -> 6, C2_5 -> 7 (:165-193) */
+    d->plp_mod = q[2];
+    d->rotation = q[3];
+    d->fec_type = q[0];
+    d->inband_b = (q[7] && v131) ? 1 : 0;
+    d->plp_mode = version == VERSION_111 ? 0 : q[6] + 1;
+  }
   /* L1-pre fields (framemapper:114-150) */
   h->pre_fields[0] = 0;                        /* STREAMTYPE_TS */
   h->pre_fields[1] = carriermode;
@@ -803,17 +846,8 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
   h->pre_fields[11] = version;
   h->pre_fields[12] = v131 ? l1scrambled : 0;
   h->pre_fields[13] = resv ? 0xf : 0;
-  /* L1-post fields (framemapper:152-250) */
-  static const int cod[8] = {0, 1, 2, 3, 4, 5, 6, 7};
-  h->post_plp_cod = cod[rate];
-  h->post_plp_mod = constellation;
-  h->post_rotation = rotation;
-  h->post_fec_type = framesize;
-  h->post_num_blocks = fecblocks;
-  h->post_ti_length = tiblocks;
-  h->post_inband_b = (inband && v131) ? 1 : 0;
+  /* L1-post reserved fields (framemapper:208-250) */
   h->post_reserved1 = resv ? 0x7ff : 0;
-  h->post_plp_mode = version == VERSION_111 ? 0 : inputmode + 1;
   h->post_reserved2 = resv ? 0x3fffffff : 0;
   h->post_reserved3 = resv ? 0xff : 0;
   h->post_reserved4 = resv ? 0xff : 0;
@@ -880,9 +914,10 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
     for (int j = 0; j < qoP; j++) h->HevenP2[h->HoddP2[j]] = j;
     for (int j = 0; j < qoF; j++) h->HevenFC[h->HoddFC[j]] = j;
   }
-  /* L1-post size (framemapper:978-987) */
-  int n_punc_t = (6 * (KBCH_1_2 - KSIG_POST)) / 5;
-  int n_post_t = KSIG_POST + NBCH_PARITY + 9000 - n_punc_t;
+  /* L1-post size (framemapper:978-987), K_sig = ksig_post */
+  int n_punc_t = (6 * (KBCH_1_2 - h->ksig_post)) / 5;
+  int n_post_t = h->ksig_post + NBCH_PARITY + 9000 - n_punc_t;
+  if (h->ksig_post > KBCH_1_2) { orc_fm_destroy(h); return NULL; }   /* one L1-post FEC block only */
   if (h->N_P2 == 1) h->N_post = (int)ceil((float)n_post_t / (2 * (float)h->eta_mod)) * 2 * h->eta_mod;
   else h->N_post = (int)ceil((float)n_post_t / ((float)h->eta_mod * (float)h->N_P2)) * h->eta_mod * h->N_P2;
   h->N_punc = n_punc_t - (h->N_post - n_post_t);
@@ -892,51 +927,52 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
   h->t2_frame_num = 0;
   h->l1_scrambled = v131 ? l1scrambled : 0;
 
-  /* cell interleaver permutation (framemapper:998-1107) */
+  /* per PLP: cell interleaver permutation (framemapper:998-1107) and time interleaver split (:1108-1119) */
   static const int lg11[2] = {0, 3}, lg12[2] = {0, 2}, lg13[4] = {0, 1, 4, 6}, lg14[6] = {0, 1, 4, 5, 9, 11},
                    lg15[4] = {0, 1, 2, 12};
-  int cs = h->cell_size;
-  if (cs == 32400) { pn_degree = 15; logic = lg15; xor_size = 4; }
-  else if (cs == 16200 || cs == 10800) { pn_degree = 14; logic = lg14; xor_size = 6; }
-  else if (cs == 8100 && normal) { pn_degree = 13; logic = lg13; xor_size = 4; }
-  else if (cs == 8100) { pn_degree = 13; logic = lg13; xor_size = 4; }
-  else if (cs == 4050 || cs == 2700) { pn_degree = 12; logic = lg12; xor_size = 2; }
-  else { pn_degree = 11; logic = lg11; xor_size = 2; }
-  pn_mask = (1 << (pn_degree - 1)) - 1;
-  max_states = 1 << pn_degree;
-  h->pn_degree = pn_degree;
-  h->permutations = (int *)calloc(32768, sizeof(int));
-  int q = 0;
-  lfsr = 0;
-  for (int i = 0; i < max_states; i++) {
-    if (i == 0 || i == 1) lfsr = 0;
-    else if (i == 2) lfsr = 1;
-    else {
-      int r = 0;
-      for (int k = 0; k < xor_size; k++) r ^= (lfsr >> logic[k]) & 1;
-      lfsr &= pn_mask;
-      lfsr >>= 1;
-      lfsr |= r << (pn_degree - 2);
+  h->stream_items = 0;
+  for (int p = 0; p < nplp; p++) {
+    orc_plp *d = &h->plp[p];
+    int cs = d->cell_size, pn_degree, xor_size;
+    const int *logic;
+    if (cs == 32400) { pn_degree = 15; logic = lg15; xor_size = 4; }
+    else if (cs == 16200 || cs == 10800) { pn_degree = 14; logic = lg14; xor_size = 6; }
+    else if (cs == 8100) { pn_degree = 13; logic = lg13; xor_size = 4; }
+    else if (cs == 4050 || cs == 2700) { pn_degree = 12; logic = lg12; xor_size = 2; }
+    else { pn_degree = 11; logic = lg11; xor_size = 2; }
+    int pn_mask = (1 << (pn_degree - 1)) - 1, max_states = 1 << pn_degree;
+    d->pn_degree = pn_degree;
+    d->permutations = (int *)calloc(32768, sizeof(int));
+    int q = 0, lfsr = 0;
+    for (int i = 0; i < max_states; i++) {
+      if (i == 0 || i == 1) lfsr = 0;
+      else if (i == 2) lfsr = 1;
+      else {
+        int r = 0;
+        for (int k = 0; k < xor_size; k++) r ^= (lfsr >> logic[k]) & 1;
+        lfsr &= pn_mask;
+        lfsr >>= 1;
+        lfsr |= r << (pn_degree - 2);
+      }
+      lfsr |= (i % 2) << (pn_degree - 1);
+      if (lfsr < cs) d->permutations[q++] = lfsr;
     }
-    lfsr |= (i % 2) << (pn_degree - 1);
-    if (lfsr < cs) h->permutations[q++] = lfsr;
+    if (d->ti_blocks == 0) { d->small_fec = 1; d->big_fec = 1; d->n_big = 0; d->n_small = d->fec_blocks; }
+    else {
+      d->small_fec = (int)floor(((float)d->fec_blocks) / ((float)d->ti_blocks));
+      d->big_fec = (int)ceil(((float)d->fec_blocks) / ((float)d->ti_blocks));
+      d->n_big = d->fec_blocks % d->ti_blocks;
+      d->n_small = d->ti_blocks - d->n_big;
+    }
+    d->stream_items = cs * d->fec_blocks;
+    d->start = h->stream_items;                /* PLP_START: PLPs back to back after the L1 signalling */
+    h->stream_items += d->stream_items;
+    d->time_interleave = (cf *)calloc((size_t)d->stream_items, sizeof(cf));
   }
-  /* time interleaver split (framemapper:1108-1119) */
-  if (tiblocks == 0) { h->small_fec = 1; h->big_fec = 1; h->n_big = 0; h->n_small = fecblocks; }
-  else {
-    h->small_fec = (int)floor(((float)fecblocks) / ((float)tiblocks));
-    h->big_fec = (int)ceil(((float)fecblocks) / ((float)tiblocks));
-    h->n_big = fecblocks % tiblocks;
-    h->n_small = tiblocks - h->n_big;
-  }
-  h->ti_blocks = tiblocks;
-  h->fec_blocks = fecblocks;
-  h->stream_items = cs * fecblocks;
   if (h->N_FC == 0) { h->mapped_items = h->N_P2 * h->C_P2 + numdatasyms * h->C_DATA; h->num_data_symbols = numdatasyms; }
   else { h->mapped_items = h->N_P2 * h->C_P2 + (numdatasyms - 1) * h->C_DATA + h->N_FC; h->num_data_symbols = numdatasyms - 1; }
   int fixed = h->stream_items + 1840 + h->N_post / h->eta_mod + (h->N_FC - h->C_FC);
   if (h->mapped_items < fixed) { orc_fm_destroy(h); return NULL; }   /* reference warns + overflows */
-  h->time_interleave = (cf *)calloc((size_t)h->stream_items, sizeof(cf));
   h->cell_out = (cf *)calloc((size_t)h->mapped_items, sizeof(cf));
   h->frame_out = (cf *)calloc((size_t)h->mapped_items, sizeof(cf));
   h->zigzag = (cf *)calloc((size_t)h->mapped_items, sizeof(cf));
@@ -953,51 +989,68 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
   orc_bb_prbs(h->l1_randomize, KBCH_1_2);   /* init_l1_randomizer (framemapper:1928-1940) */
   return h;
 }
+
+/* the reference's single-PLP framemapperfint_cc (include/dvbt2ll/framemapperfint_cc.h:49) */
+orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, int fecblocks,
+                      int tiblocks, int carriermode, int fftsize, int guardinterval,
+                      int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
+                      int paprmode, int version, int preamble, int inputmode,
+                      int reservedbiasbits, int l1scrambled, int inband) {
+  const int plp[8] = {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband};
+  return orc_fm_create_mplp(1, plp, carriermode, fftsize, guardinterval, l1constellation, pilotpattern, t2frames,
+                            numdatasyms, paprmode, version, preamble, reservedbiasbits, l1scrambled);
+}
 int orc_fm_stream_items(const orc_fm *h) { return h->stream_items; }
 int orc_fm_mapped_items(const orc_fm *h) { return h->mapped_items; }
+int orc_fm_l1post_cells(const orc_fm *h) { return h->N_post / h->eta_mod; }
 void orc_fm_destroy(orc_fm *h) {
   if (!h) return;
+  for (int p = 0; p < ORC_MAX_PLP; p++) { free(h->plp[p].permutations); free(h->plp[p].time_interleave); }
   free(h->Heven); free(h->Hodd); free(h->HevenP2); free(h->HoddP2); free(h->HevenFC); free(h->HoddFC);
-  free(h->permutations); free(h->time_interleave); free(h->cell_out); free(h->frame_out);
-  free(h->zigzag); free(h->dummy); free(h);
+  free(h->cell_out); free(h->frame_out); free(h->zigzag); free(h->dummy); free(h);
 }
 
-/* general_work (framemapper:1948-2151), exactly one T2 frame */
+/* general_work (framemapper:1948-2151), exactly one T2 frame: in = each PLP's stream_items cells,
+ * PLPs in order */
 int orc_fm_work(orc_fm *h, const float *inf, float *outf) {
   const cf *in = (const cf *)inf;
   cf *out = (cf *)outf;
-  int cs = h->cell_size, M = h->mapped_items, S = h->stream_items;
+  int M = h->mapped_items, S = h->stream_items;
   int Lp = h->N_post / h->eta_mod;
-  /* cell interleaver :1973-1998 */
-  int cell_index = 0;
-  for (int s = 0; s < h->n_small + h->n_big; s++) {
-    int n = 0;
-    int fpt = s < h->n_small ? h->small_fec : h->big_fec;
-    for (int r = 0; r < fpt; r++) {
-      int shift = cs;
-      while (shift >= cs) {
-        int temp = n;
-        shift = 0;
-        for (int p = 0; p < h->pn_degree; p++) { shift |= temp & 1; shift <<= 1; temp >>= 1; }
-        n++;
+  for (int p = 0; p < h->nplp; p++) {
+    orc_plp *d = &h->plp[p];
+    int cs = d->cell_size;
+    /* cell interleaver :1973-1998 */
+    int cell_index = 0;
+    for (int s = 0; s < d->n_small + d->n_big; s++) {
+      int n = 0;
+      int fpt = s < d->n_small ? d->small_fec : d->big_fec;
+      for (int r = 0; r < fpt; r++) {
+        int shift = cs;
+        while (shift >= cs) {
+          int temp = n;
+          shift = 0;
+          for (int b = 0; b < d->pn_degree; b++) { shift |= temp & 1; shift <<= 1; temp >>= 1; }
+          n++;
+        }
+        for (int w = 0; w < cs; w++) d->time_interleave[((d->permutations[w] + shift) % cs) + cell_index] = *in++;
+        cell_index += cs;
       }
-      for (int w = 0; w < cs; w++) h->time_interleave[((h->permutations[w] + shift) % cs) + cell_index] = *in++;
-      cell_index += cs;
     }
-  }
-  /* time interleaver :1999-2028 */
-  cf *cellout = h->cell_out;
-  if (h->ti_blocks != 0) {
-    int ti_index = 0;
-    for (int s = 0; s < h->n_small + h->n_big; s++) {
-      int fpt = s < h->n_small ? h->small_fec : h->big_fec;
-      int ncols = 5 * fpt, rows = cs / 5;
-      for (int k = 0; k < rows; k++)
-        for (int w = 0; w < ncols; w++) *cellout++ = h->time_interleave[rows * w + ti_index + k];
-      ti_index += rows * ncols;
+    /* time interleaver :1999-2028, into the PLP's cells of the frame */
+    cf *cellout = h->cell_out + d->start;
+    if (d->ti_blocks != 0) {
+      int ti_index = 0;
+      for (int s = 0; s < d->n_small + d->n_big; s++) {
+        int fpt = s < d->n_small ? d->small_fec : d->big_fec;
+        int ncols = 5 * fpt, rows = cs / 5;
+        for (int k = 0; k < rows; k++)
+          for (int w = 0; w < ncols; w++) *cellout++ = d->time_interleave[rows * w + ti_index + k];
+        ti_index += rows * ncols;
+      }
+    } else {
+      for (int w = 0; w < d->stream_items; w++) *cellout++ = d->time_interleave[w];
     }
-  } else {
-    for (int w = 0; w < S; w++) *cellout++ = h->time_interleave[w];
   }
   /* frame assembly :2029-2103 */
   cf *dst = h->N_P2 == 1 ? h->frame_out : h->zigzag;

@@ -38,6 +38,9 @@ int orc_bb_kbch(const orc_bb *h);
 int orc_bb_forecast(const orc_bb *h, int noutput_items);
 /* returns noutput_items; *consumed = input bytes consumed */
 int orc_bb_work(orc_bb *h, int noutput_items, const uint8_t *in, uint8_t *out, int *consumed);
+/* one PLP of a multi-PLP frame: MATYPE SIS/MIS = multiple, MATYPE-2 ISI = isi (the PLP_ID;
+ * bbheader:288-298).  Parity unpinned (the reference's ctor fixes SIS, :168). */
+void orc_bb_set_isi(orc_bb *h, int isi);
 void orc_bb_destroy(orc_bb *h);
 
 /* LDPC encoder, reference-owned restatement of ldpc_calculate (lib/bbheaderbch_bb_impl.cc:533-646),
@@ -59,6 +62,14 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
                       int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
                       int paprmode, int version, int preamble, int inputmode,
                       int reservedbiasbits, int l1scrambled, int inband);
+/* nplp Type-1 data PLPs in one T2 frame (EN 302 755 8.3.6.3; the reference carries one,
+ * framemapper:152-250; PARITY UNPINNED for nplp > 1): plp = nplp x {framesize, rate, constellation,
+ * rotation, fecblocks, tiblocks, inputmode, inband}; the other arguments are the common fields.
+ * orc_fm_work's input is one frame of every PLP's cells, PLP 0 first. */
+orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int carriermode, int fftsize, int guardinterval,
+                           int l1constellation, int pilotpattern, int t2frames, int numdatasyms, int paprmode,
+                           int version, int preamble, int reservedbiasbits, int l1scrambled);
+int orc_fm_l1post_cells(const orc_fm *h);
 int orc_fm_stream_items(const orc_fm *h);
 int orc_fm_mapped_items(const orc_fm *h);
 /* one T2 frame: stream_items cells in -> mapped_items cells out; returns mapped_items */

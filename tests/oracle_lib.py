@@ -30,6 +30,10 @@ def lib():
         L.orc_bb_nbch.argtypes = [vp]
         L.orc_bb_kbch.argtypes = [vp]
         L.orc_bb_destroy.argtypes = [vp]
+        L.orc_bb_set_isi.argtypes = [vp, ci]
+        L.orc_fm_create_mplp.restype = vp
+        L.orc_fm_create_mplp.argtypes = [ci, vp] + [ci] * 12
+        L.orc_fm_l1post_cells.argtypes = [vp]
         L.orc_ldpc_create.restype = vp
         L.orc_ldpc_create.argtypes = [ci, ci]
         L.orc_ldpc_work.argtypes = [vp, ci, vp, vp]
@@ -71,9 +75,11 @@ def _p(a):
 
 
 class BB:
-    def __init__(self, framesize, rate, mode=0, inband=0, fecblocks=168, tsrate=4000000):
+    def __init__(self, framesize, rate, mode=0, inband=0, fecblocks=168, tsrate=4000000, isi=None):
         self.h = lib().orc_bb_create(framesize, rate, mode, inband, fecblocks, tsrate)
         assert self.h, "oracle bbheaderbch create failed"
+        if isi is not None:            # one PLP of a multi-PLP frame: MIS, MATYPE-2 = PLP_ID
+            lib().orc_bb_set_isi(self.h, isi)
         self.nbch = lib().orc_bb_nbch(self.h)
         self.kbch = lib().orc_bb_kbch(self.h)
 
@@ -143,6 +149,46 @@ class FM:
     def __del__(self):
         if getattr(self, "h", None):
             lib().orc_fm_destroy(self.h)
+
+
+class FMM(FM):
+    """framemapperfint for a multi-PLP frame (orc_fm_create_mplp; parity unpinned beyond one PLP): work()
+    takes one frame of every PLP's cells, PLP 0 first"""
+    def __init__(self, mcfg):
+        plp = np.array([list(p.plp_args()[:8]) for p in mcfg.plps], np.int32).reshape(-1)
+        self._plp = plp
+        self.h = lib().orc_fm_create_mplp(mcfg.nplp, _p(plp), *mcfg.common_args())
+        assert self.h, "oracle multi-PLP framemapper create failed"
+        self.stream_items = lib().orc_fm_stream_items(self.h)
+        self.mapped_items = lib().orc_fm_mapped_items(self.h)
+        self.l1post_cells = lib().orc_fm_l1post_cells(self.h)
+
+
+def mplp_cells(mcfg, first_frame, nframes):
+    """oracle per-PLP chain up to the framemapper input: for each frame, the PLPs' cells concatenated
+    (PLP k: TS seed k + 1, BBHEADER MIS with ISI = k when nplp > 1); returns (list of per-frame cell
+    arrays, per-PLP BB bits and codewords of the frames)"""
+    from dvbt2ll.configs import ts_for_frames
+    frames = [[] for _ in range(nframes)]
+    bb_bits, codewords = [], []
+    for k, p in enumerate(mcfg.plps):
+        F = p.fecblocks
+        bb = BB(*p.bb_args(), isi=k if mcfg.nplp > 1 else None)
+        ld, im = LDPC(p.framesize, p.rate), IM(*p.im_args())
+        ts, base = ts_for_frames(p, 0, first_frame + nframes, seed=k + 1)
+        off = 0
+        bits_k, cw_k = [], []
+        for f in range(first_frame + nframes):
+            bits, c = bb.work(ts[off:], F)
+            off += c
+            if f >= first_frame:
+                cw = ld.work(bits, F)
+                bits_k.append(bits)
+                cw_k.append(cw)
+                frames[f - first_frame].append(im.work(cw, F))
+        bb_bits.append(bits_k)
+        codewords.append(cw_k)
+    return [np.concatenate(c) for c in frames], bb_bits, codewords
 
 
 class PG:

@@ -33,6 +33,9 @@ def lib():
         L.t2probe_counts.argtypes = [ctypes.c_int] * 6 + [vp]
         L.t2probe_aux_lists.argtypes = [vp] * 9
         L.t2probe_l1post.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, vp]
+        L.t2probe_frame_mplp.argtypes = [vp] * 5
+        L.t2probe_chain_mplp.argtypes = [vp] * 10
+        L.t2probe_l1post_mplp.argtypes = [vp, ctypes.c_int, vp, vp]
         _L = L
     return _L
 
@@ -215,3 +218,47 @@ def stored_index(N, split):
 def stored_to_natural(row, N, split):
     """a symbol row in the chain's stored order -> natural FFT-input order"""
     return np.asarray(row)[stored_index(N, split)]
+
+
+def frame_plan_mplp(mcfg):
+    """the planner's multi-PLP frame (build_frame_mplp): gather maps, aux variants, PLP geometry"""
+    a = np.array(mcfg.mplp_array(), np.int32)
+    info = np.zeros(31, np.int32)
+    if lib().t2probe_frame_mplp(_p(a), _p(info), None, None, None):
+        return None
+    M, S, aux_len, t2frames = (int(x) for x in info[:4])
+    gin = np.zeros(M, np.int32)
+    gd = np.zeros(M, np.int32)
+    aux = np.zeros(t2frames * aux_len, np.complex64)
+    assert lib().t2probe_frame_mplp(_p(a), _p(info), _p(gin), _p(gd), _p(aux)) == 0
+    n = int(info[6])
+    return dict(M=M, S=S, aux_len=aux_len, t2frames=t2frames, Lp=int(info[4]), D=int(info[5]), nplp=n,
+                start=[int(x) for x in info[7:7 + n]], cs=[int(x) for x in info[15:15 + n]],
+                F=[int(x) for x in info[23:23 + n]], gather_in=gin, gather_d=gd, aux=aux.reshape(t2frames, aux_len))
+
+
+def chain_layout_mplp(mcfg):
+    a = np.array(mcfg.mplp_array(), np.int32)
+    pg3 = np.array([mcfg.misogroup, mcfg.equalization, mcfg.bandwidth], np.int32)
+    info = np.zeros(5, np.int32)
+    fr = frame_plan_mplp(mcfg)
+    pl = pilot_plan(mcfg.pg_args())
+    Nsym, N, S, P = pl["Nsym"], pl["N"], fr["S"], fr["nplp"]
+    cmap = np.zeros(Nsym * N, np.int32)
+    inv = np.zeros(S, np.uint16)
+    d0, dn, dn0 = (np.zeros(Nsym, np.int32) for _ in range(3))
+    part = np.zeros(S, np.int32)
+    bnd = np.zeros(2 * Nsym * (P + 1), np.int32)
+    assert lib().t2probe_chain_mplp(_p(a), _p(pg3), _p(info), _p(cmap), _p(inv), _p(d0), _p(dn), _p(dn0), _p(part),
+                                    _p(bnd)) == 0
+    return dict(Nsym=Nsym, N=N, S=S, split=int(info[3]), nplp=P, cmap=cmap.reshape(Nsym, N), inv=inv, d0=d0,
+                dn=dn, dn0=dn0, part=part, bnd=bnd.reshape(2 * Nsym, P + 1), frame=fr)
+
+
+def l1post_mplp(mcfg, frame_idx):
+    a = np.array(mcfg.mplp_array(), np.int32)
+    info = np.zeros(3, np.int32)
+    assert lib().t2probe_l1post_mplp(_p(a), frame_idx, None, _p(info)) == 0
+    out = np.zeros(int(info[2]), np.complex64)
+    assert lib().t2probe_l1post_mplp(_p(a), frame_idx, _p(out), _p(info)) == 0
+    return out, dict(nsig=int(info[0]), npost=int(info[1]), Lp=int(info[2]))
