@@ -1197,28 +1197,36 @@ template <class Bank, class Seg>
 static void bank_balance(std::vector<int32_t> &seq, int pos0, int U, const Bank &bank, const Seg &seg) {
   const int n = (int)seq.size(), o0 = pos0 & ~(U - 1);
   std::vector<uint16_t> used((size_t)((pos0 + n - o0) / (16 * U) + 1) * U, 0);
-  std::vector<int32_t> cand;
+  // a segment's candidates bucketed by bank pair, in segment order (pos = index in the segment): each
+  // pick looks at the 16 bucket heads only, O(16) instead of a scan of the remaining candidates
+  std::vector<std::pair<int32_t, int32_t>> bucket[16];
   for (int k0 = 0; k0 < n;) {
     int k1 = k0 + 1;
     while (k1 < n && seg(seq[k1]) == seg(seq[k0])) k1++;
-    cand.assign(seq.begin() + k0, seq.begin() + k1);
+    size_t head[16] = {0};
     int left[16] = {0};   // remaining candidates per bank pair
-    for (int c : cand) left[bank(c)]++;
+    for (auto &bk : bucket) bk.clear();
+    for (int i = k0; i < k1; i++) bucket[bank(seq[i])].push_back({i - k0, seq[i]});
+    for (int b = 0; b < 16; b++) left[b] = (int)bucket[b].size();
     for (int k = k0; k < k1; k++) {
       const int p = pos0 + k, cls = ((p - o0) / (16 * U)) * U + (p - o0) % U;
       // a candidate whose bank pair is still free in this class, the most plentiful such pair first
-      // (keeps the scarce ones for later positions); else the first candidate
-      size_t pick = 0;
-      int best = -1;
-      for (size_t i = 0; i < cand.size(); i++) {
-        const int b = bank(cand[i]);
-        if (!((used[cls] >> b) & 1) && left[b] > best) { best = left[b]; pick = i; }
+      // (keeps the scarce ones for later positions; ties: the earliest candidate); else the earliest
+      int pick = -1, best = -1, pick_pos = 1 << 30, first = -1, first_pos = 1 << 30;
+      for (int b = 0; b < 16; b++) {
+        if (head[b] == bucket[b].size()) continue;
+        const int pos = bucket[b][head[b]].first;
+        if (pos < first_pos) { first_pos = pos; first = b; }
+        if (!((used[cls] >> b) & 1) && (left[b] > best || (left[b] == best && pos < pick_pos))) {
+          best = left[b];
+          pick = b;
+          pick_pos = pos;
+        }
       }
-      const int b = bank(cand[pick]);
-      seq[k] = cand[pick];
-      used[cls] |= (uint16_t)(1u << b);
-      left[b]--;
-      cand.erase(cand.begin() + pick);
+      if (pick < 0) pick = first;
+      seq[k] = bucket[pick][head[pick]++].second;
+      used[cls] |= (uint16_t)(1u << pick);
+      left[pick]--;
     }
     k0 = k1;
   }

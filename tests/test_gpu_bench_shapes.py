@@ -143,3 +143,27 @@ def test_odd_stream_stride(gpu):
     for s in range(S):
         want = ref.run(first, B, ts=tss[s][0], ts_base=base)
         np.testing.assert_array_equal(got[s].view(np.uint32), want.view(np.uint32), err_msg="stream %d" % s)
+
+
+def test_chain_graph_back_to_back_one_slot(gpu):
+    """hipGraph mode: consecutive calls on one buffer slot are issued without waiting for each other
+    (a ring of DVBT2LL_CHAIN_GRAPH_RING instantiations per slot); each call's frames come out as the
+    direct launches give them, with more calls queued than the ring holds"""
+    import torch
+    cfg = CONFIGS["cfg1"]
+    n = 6
+    ts, base = ts_for_frames(cfg, 0, n)
+    d = torch.from_numpy(ts).cuda()
+    ch = dvbt2ll.Chain(cfg, max_frames=1)
+    per = ch.iq_per_frame
+    want = torch.empty((n, per, 2), dtype=torch.float32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for k in range(n):
+        ch.run_device(d.data_ptr(), base, len(ts), k, 1, want[k].data_ptr(), st)
+    torch.cuda.synchronize()
+    ch.set_graph(True)
+    got = torch.zeros((n, per, 2), dtype=torch.float32, device="cuda")
+    for k in range(n):   # no synchronisation between the calls
+        ch.run_device(d.data_ptr(), base, len(ts), k, 1, got[k].data_ptr(), st)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32), want.cpu().numpy().view(np.uint32))

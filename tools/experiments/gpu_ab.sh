@@ -12,7 +12,7 @@ cp $LIB exp_build/libproduct.so
 for round in 1 2; do
   for v in product "$@"; do
     cp exp_build/lib$v.so $LIB
-    timeout -k 10 240 python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --no-blocks --steps 20 --warmup 3 $BENCH_ARGS \
+    timeout -k 10 240 python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --no-blocks --no-mplp --steps 20 --warmup 3 $BENCH_ARGS \
       > "$O/b_${v}_$round.json" 2> "$O/b_${v}_$round.err" || { tail -5 "$O/b_${v}_$round.err"; cp exp_build/libproduct.so $LIB; exit 1; }
     python -c "import json,sys; d=json.load(open('$O/b_${v}_$round.json')); print('$v', {k: round(s['avg_launch_ms'],4) for k,s in d['stages'].items()}, round(d['value']))"
   done
