@@ -917,15 +917,17 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     md.data_off = pp.start;
     // the map kernel's TI store through the symbol partition (layout.part), reordered to its store
     // order (block r, index jj = 5 row + e with TI, else t) as int16 deltas from the TI position
-    // (a cell only moves within its symbol); the PLP's TI positions start at PLP_START
-    const int csp = (pp.cs + 3) & ~3;   // rows padded for the kernel's aligned quad loads
+    // (a cell only moves within its symbol); the PLP's TI positions start at PLP_START.  Within each
+    // chunk of 256 the delta of jj = 256 c + 64 k + l sits at 256 c + 4 l + k: the kernel's lane l
+    // stores cells 64 k + l and loads their four deltas with one 8-byte read (map_store_pairs)
+    const int csp = (pp.cs + 255) & ~255;   // rows padded to whole chunks
     std::vector<int16_t> pb((size_t)pp.F * csp + 4, 0);
     for (int rr = 0; rr < pp.F; rr++)
       for (int jj = 0; jj < pp.cs; jj++) {
         const int t = pp.ti_on ? (jj % 5) * (pp.cs / 5) + jj / 5 : jj;
         const int64_t sd = ti_dest(fp, k, rr, t), delta = layout.part[sd] - sd;
         if (delta < INT16_MIN || delta > INT16_MAX) return DVBT2LL_EINVAL;
-        pb[(size_t)rr * csp + jj] = (int16_t)delta;
+        pb[(size_t)rr * csp + (jj & ~255) + 4 * (jj & 63) + ((jj >> 6) & 3)] = (int16_t)delta;
       }
     if ((r = upload(pl->part, pb))) return r;
     md.part = pl->part.as<int16_t>();

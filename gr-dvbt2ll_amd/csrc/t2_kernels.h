@@ -88,7 +88,8 @@ struct MapDev {
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
   int data_off;            // chain: the PLP's first data cell (PLP_START) within the frame data region
   const int16_t *part;     // chain, 32K only: slot - TI position of (block r, TI-store index j), at
-                           // r*part_stride + j (rows padded to a multiple of 4 for 8-byte quad loads)
+                           // r*part_stride + (j & ~255) + 4 (j & 63) + ((j >> 6) & 3) (rows padded to
+                           // whole 256-chunks; map_store_pairs reads a lane's four with one 8-byte load)
   int part_stride;
   // per demuxed bit b of the row word: the column e feeding it (W-1-mux[e] = b) as its first codeword
   // bit e*R (-1: none) and its twist (int32: uniform scalar loads, no byte loads in the column loop)

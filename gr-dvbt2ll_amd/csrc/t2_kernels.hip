@@ -1184,22 +1184,28 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
   const int16_t *pr = d.part ? d.part + (int64_t)r * d.part_stride : nullptr;   // block-major int16 table
   if (pr) {
-    // four consecutive TI-store indices per thread: one 8-byte load of their partition deltas
-    // instead of four 2-byte loads (the memory instruction count, not the bytes, sets this loop's
-    // rate; the pair stores stay 2 bytes per cell).  Eight quads per thread per round: cs <= 8192
-    // in one round, with no loop-head wait on a previous round's pair stores (map -3 %)
-    constexpr int MQ = MAP_MB;
-    for (int q0 = tid; q0 < nq; q0 += MQ * NT) {
+    // TI-order cells in chunks of 256: wave w takes chunks c = c0 + u NT / 64 + w (u < 8), and its
+    // lane l stores cells 256 c + 64 k + l (k < 4), so each store instruction writes 64 consecutive
+    // TI-order cells (about 13 TI rows of five: 13 cache lines per instruction instead of ~51 with four
+    // consecutive cells per lane); the lane's four partition deltas are one 8-byte load (the chain
+    // stores them at 256 c + 4 l + k, t2_capi).  Eight chunks per wave per round: cs <= 8192 in one
+    // round, with no loop-head wait on a previous round's pair stores
+    constexpr int MQ = MAP_MB, NW = NT / 64;
+    const int lane = tid & 63, wv = tid >> 6, nch = (cs + 255) >> 8;
+    for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
       uint2 pq[MQ];
 #pragma unroll
-      for (int u = 0; u < MQ; u++) pq[u] = ld_off((const uint2 *)pr, (uint32_t)min(q0 + u * NT, nq - 1) * 8u);
+      for (int u = 0; u < MQ; u++) {
+        const int c = min(c0 + u * NW + wv, nch - 1);
+        pq[u] = ld_off((const uint2 *)pr, (uint32_t)(256 * c + 4 * lane) * 2u);
+      }
 #pragma unroll
       for (int u = 0; u < MQ; u++) {
-        const int q = q0 + u * NT;
-        if (q < nq) {
+        const int c = c0 + u * NW + wv;
+        if (c < nch) {
 #pragma unroll
           for (int k = 0; k < 4; k++) {
-            const int j = 4 * q + k;
+            const int j = 256 * c + 64 * k + lane;
             if (j < cs) {
               const int row = j / 5, e = j - 5 * row;
               const int tt = d.ti_on ? e * rows + row : j, oo = d.ti_on ? row * cols + e : j;
