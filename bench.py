@@ -799,6 +799,8 @@ def main():
                                    % (cfg.name, B, " (%d independent TS streams x %d frames, one launch)" % (NS, BS)
                                       if NS > 1 else "", info["fec_blocks_per_frame"], per),
                        "frames_per_step_per_gpu": B, "slots_streams_per_gpu": S,
+                       "symbols_per_frame": info["num_symbols"], "fft_size": info["fft_size"],
+                       "guard_samples": info["guard_interval"],
                        "ts_streams_per_launch": NS,
                        "parallelism": "%s x%d (no data-path collective)"
                                       % ("frame-sharded" if args.shard == "frames" else "independent streams", world),

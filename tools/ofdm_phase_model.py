@@ -13,7 +13,9 @@ between the kernel's phases.  Per symbol, on its CU:
     T_store = the symbol's IQ bytes at the measured per-CU store rate of tools/store_rate.hip (one
               workgroup storing alone: the CU's own write path, no contention; profiles/r4_store_rate.jsonl)
 
-in cycles at the launch's measured clock (GRBM_GUI_ACTIVE per XCD / the rocprof launch time).  Each
+in cycles at the launch's clock: GRBM_GUI_ACTIVE per XCD (cycles of the profiled launch, counted in the
+PMC run) over that launch's duration (the bench's HIP-event average of the same kernel, a separate run
+on the same box: the clock is an estimate, and the per-symbol cycles carry its error).  Each
 of the three alone is a lower bound on the symbol's time (the CU cannot run its LDS, its SIMDs or
 its write path faster), and so is the chip-wide one, all IQ bytes at the measured all-CU store rate.
 Their sum, the serial-sum model, is NOT a bound: VALU and LDS work of different waves overlap inside
@@ -55,15 +57,17 @@ def store_rates(path):
 
 
 def model(pmc, bench, rates):
-    st = bench["stages"]["ofdm"]
-    # cfg3: 2091008 IQ samples per frame = P1 (2048) + 60 symbols x (32768 + 2048 GI); 60 = 59 data + 1 P2
-    nsym = 60 * bench["config"]["frames_per_step_per_gpu"]
+    st, cf = bench["stages"]["ofdm"], bench["config"]
+    # symbols per frame from the bench line (round 4 on); older lines are cfg3: 2091008 IQ samples per
+    # frame = P1 (2048) + 60 symbols x (32768 + 2048 GI)
+    nsym = cf.get("symbols_per_frame", 60) * cf["frames_per_step_per_gpu"]
+    N, G = cf.get("fft_size", 32768), cf.get("guard_samples", 2048)
     launch_s = st["avg_launch_ms"] * 1e-3
     cycles = pmc["GRBM_GUI_ACTIVE"] / XCDS           # GPU cycles of the (profiled) launch
     clock = cycles / launch_s
     per_cu = nsym / CUS
     t_meas = cycles / per_cu
-    iq_bytes = 8 * (32768 + 2048)
+    iq_bytes = 8 * (N + G)
     lone, grid = rates
     t_valu = pmc["SQ_INSTS_VALU"] / nsym * 2 / 4
     t_lds = pmc["SQ_LDS_IDX_ACTIVE"] / nsym
