@@ -85,6 +85,22 @@ __global__ __launch_bounds__(NT) void lone_kernel(char *out, int K) {
   }
 }
 
+// the kernel's duty cycle: every CU alternates SLEEP x 64 x 127 idle cycles (the OFDM kernel's
+// compute phases) with one symbol's store and its drain, K symbols, the CUs' phases staggered by
+// blockIdx; (time - K x idle) / K = a symbol's store phase among the other CUs' stores
+template <int PAT>
+__global__ __launch_bounds__(NT) void duty_kernel(char *out, int K, int sleeps, int do_store) {
+  extern __shared__ char pad[];
+  if (threadIdx.x == 0xFFFFFFFFu) pad[0] = 0;
+  for (int i = 0; i < (int)(blockIdx.x & 7u) * sleeps / 8; i++) __builtin_amdgcn_s_sleep(127);
+  for (int s = 0; s < K; s++) {
+    for (int i = 0; i < sleeps; i++) __builtin_amdgcn_s_sleep(127);
+    if (do_store) store_symbol<PAT, true>(out + ((size_t)blockIdx.x * K + s) * SYM_BYTES, threadIdx.x, (float)s);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+  }
+}
+
 template <int PAT, bool NT_ST>
 __global__ __launch_bounds__(NT) void grid_kernel(char *out) {
   extern __shared__ char pad[];
@@ -144,6 +160,21 @@ static int run_grid(char *buf, int nsym, double clk, hipEvent_t e0, hipEvent_t e
   return 0;
 }
 
+template <int PAT>
+static int run_duty(char *buf, hipEvent_t e0, hipEvent_t e1) {
+  CK(hipFuncSetAttribute((const void *)duty_kernel<PAT>, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+  const int K = 45;
+  for (int sleeps : {0, 3, 6, 9}) {
+    const float ms = best_ms(e0, e1, [&] { hipLaunchKernelGGL((duty_kernel<PAT>), dim3(256), dim3(NT), 96 * 1024, 0, buf, K, sleeps, 1); });
+    const float sl = best_ms(e0, e1, [&] { hipLaunchKernelGGL((duty_kernel<PAT>), dim3(256), dim3(NT), 96 * 1024, 0, buf, K, sleeps, 0); });
+    CK(hipGetLastError());
+    std::printf("{\"case\": \"duty\", \"pattern\": \"%s\", \"cus\": 256, \"symbols_per_cu\": %d, \"idle_us_per_symbol\": %.3f, "
+                "\"ms\": %.4f, \"store_us_per_symbol\": %.3f}\n",
+                PAT_NAME[PAT], K, sl * 1e3 / K, ms, (ms - sl) * 1e3 / K);
+  }
+  return 0;
+}
+
 int main() {
   const int NSYM = 11520;
   char *buf = nullptr;
@@ -159,7 +190,8 @@ int main() {
       run_lone<O32, false, false>(buf, clk, e0, e1) || run_lone<CONTIG16, true, false>(buf, clk, e0, e1) ||
       run_lone<CONTIG16, true, true>(buf, clk, e0, e1) || run_lone<CONTIG8, true, false>(buf, clk, e0, e1) ||
       run_grid<O32, true>(buf, NSYM, clk, e0, e1) || run_grid<O32, false>(buf, NSYM, clk, e0, e1) ||
-      run_grid<CONTIG16, true>(buf, NSYM, clk, e0, e1) || run_grid<CONTIG8, true>(buf, NSYM, clk, e0, e1))
+      run_grid<CONTIG16, true>(buf, NSYM, clk, e0, e1) || run_grid<CONTIG8, true>(buf, NSYM, clk, e0, e1) ||
+      run_duty<O32>(buf, e0, e1) || run_duty<CONTIG16>(buf, e0, e1))
     return 1;
   CK(hipFree(buf));
   return 0;
