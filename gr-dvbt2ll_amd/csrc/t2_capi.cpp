@@ -6,6 +6,7 @@
 // with the caller's host buffers (GNU Radio's circular buffers).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -643,7 +644,7 @@ extern "C" void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h) { 
 struct ChainPlp {
   FecTables fec;
   MapTables map;
-  DevBuf perm, shift, part;
+  DevBuf perm, shift, part, pbase;
   DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], bpart[DVBT2LL_CHAIN_MAX_SLOTS];
   int64_t cw_stride = 0;
   int64_t ts_per_frame = 0;   // payload bytes per frame (NM positions; HEM: before sync-byte removal)
@@ -915,23 +916,33 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     md.ti_big = pp.ti_big;
     md.ti_nsmall = pp.ti_nsmall;
     md.data_off = pp.start;
-    // the map kernel's TI store through the symbol partition (layout.part), reordered to its store
-    // order (block r, index jj = 5 row + e with TI, else t) as int16 deltas from the TI position
-    // (a cell only moves within its symbol); the PLP's TI positions start at PLP_START.  Within each
-    // chunk of 256 the delta of jj = 256 c + 64 k + l sits at 256 c + 4 l + k: the kernel's lane l
-    // stores cells 64 k + l and loads their four deltas with one 8-byte read (map_store_pairs)
-    const int csp = (pp.cs + 255) & ~255;   // rows padded to whole chunks
-    std::vector<int16_t> pb((size_t)pp.F * csp + 4, 0);
-    for (int rr = 0; rr < pp.F; rr++)
-      for (int jj = 0; jj < pp.cs; jj++) {
-        const int t = pp.ti_on ? (jj % 5) * (pp.cs / 5) + jj / 5 : jj;
-        const int64_t sd = ti_dest(fp, k, rr, t), delta = layout.part[sd] - sd;
-        if (delta < INT16_MIN || delta > INT16_MAX) return DVBT2LL_EINVAL;
-        pb[(size_t)rr * csp + (jj & ~255) + 4 * (jj & 63) + ((jj >> 6) & 3)] = (int16_t)delta;
+    // the map kernel's TI store in stored-slot order (layout.part: frame data slot of each TI
+    // position; the PLP's positions start at PLP_START): block r's cells sorted by slot, entry p =
+    // its TI-store index t | (slot - the slot of its 64-cell chunk's first cell) << 16, plus each
+    // chunk's first slot.  A store instruction then writes 64 slots of one or two contiguous runs
+    // (the block's cells in a symbol (half) are one run, bank-balanced inside, t2_plan
+    // build_chain_layout) instead of gathering them from TI order
+    const int css = (pp.cs + 63) & ~63, nchk = css / 64;
+    std::vector<uint32_t> so((size_t)pp.F * css + 64, 0u);
+    std::vector<int32_t> sbv((size_t)pp.F * nchk + 1, 0);
+    std::vector<std::pair<int64_t, int>> cells(pp.cs);
+    for (int rr = 0; rr < pp.F; rr++) {
+      for (int t = 0; t < pp.cs; t++) cells[t] = {layout.part[ti_dest(fp, k, rr, t)], t};
+      std::sort(cells.begin(), cells.end());
+      for (int c = 0; c < nchk && 64 * c < pp.cs; c++) {
+        const int64_t base = cells[64 * c].first;
+        sbv[(size_t)rr * nchk + c] = (int32_t)base;
+        for (int p = 64 * c; p < std::min(pp.cs, 64 * c + 64); p++) {
+          const int64_t off = cells[p].first - base;
+          if (off < 0 || off > 0xFFFF) return DVBT2LL_EINVAL;
+          so[(size_t)rr * css + p] = (uint32_t)cells[p].second | ((uint32_t)off << 16);
+        }
       }
-    if ((r = upload(pl->part, pb))) return r;
-    md.part = pl->part.as<int16_t>();
-    md.part_stride = csp;
+    }
+    if ((r = upload(pl->part, so)) || (r = upload(pl->pbase, sbv))) return r;
+    md.slot_src = pl->part.as<uint32_t>();
+    md.slot_base = pl->pbase.as<int32_t>();
+    md.slot_stride = css;
     pl->F = pp.F;
     pl->inputmode = q.inputmode;
     pl->inband = q.inband;

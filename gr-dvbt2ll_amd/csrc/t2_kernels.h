@@ -87,10 +87,11 @@ struct MapDev {
   int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
   int data_off;            // chain: the PLP's first data cell (PLP_START) within the frame data region
-  const int16_t *part;     // chain, 32K only: slot - TI position of (block r, TI-store index j), at
-                           // r*part_stride + (j & ~255) + 4 (j & 63) + ((j >> 6) & 3) (rows padded to
-                           // whole 256-chunks; map_store_pairs reads a lane's four with one 8-byte load)
-  int part_stride;
+  // chain: block r's cells in stored-slot order, entry r * slot_stride + p = TI-store index t |
+  // (slot - slot_base[r * slot_stride / 64 + p / 64]) << 16 (map_store_pairs; null: store in TI order)
+  const uint32_t *slot_src;
+  const int32_t *slot_base;
+  int slot_stride;
   // per demuxed bit b of the row word: the column e feeding it (W-1-mux[e] = b) as its first codeword
   // bit e*R (-1: none) and its twist (int32: uniform scalar loads, no byte loads in the column loop)
   int colstart[16], coltw[16];

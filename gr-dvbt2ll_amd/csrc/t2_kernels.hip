@@ -1177,48 +1177,35 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
     }
   }
   __syncthreads();
-  // time-interleaver store of the index pairs: row-major over (row, e), 5 consecutive cells
-  // (10 B) per TI row (32K: through the half partition); the constellation lookup (QAM +
-  // rotated-constellation Q delay) is fused into the OFDM kernel's bin scatter
-  const int64_t fbase = (d.ti_on ? base : (int64_t)r * cs) + d.data_off;   // + PLP_START
-  // (frame-relative 32-bit element offsets: a partition delta can move a cell before fbase)
-  const int16_t *pr = d.part ? d.part + (int64_t)r * d.part_stride : nullptr;   // block-major int16 table
-  if (pr) {
-    // TI-order cells in chunks of 256: wave w takes chunks c = c0 + u NT / 64 + w (u < 8), and its
-    // lane l stores cells 256 c + 64 k + l (k < 4), so each store instruction writes 64 consecutive
-    // TI-order cells (about 13 TI rows of five: 13 cache lines per instruction instead of ~51 with four
-    // consecutive cells per lane); the lane's four partition deltas are one 8-byte load (the chain
-    // stores them at 256 c + 4 l + k, t2_capi).  Eight chunks per wave per round: cs <= 8192 in one
-    // round, with no loop-head wait on a previous round's pair stores
+  // time-interleaver store of the index pairs (row-major over (row, e), 5 consecutive cells (10 B)
+  // per TI row; the constellation lookup (QAM + rotated-constellation Q delay) is fused into the OFDM
+  // kernel's bin scatter).  Chain: in stored-slot order (MapDev::slot_src): wave w takes 64-cell
+  // chunks c = c0 + u NT / 64 + w (u < 8) and lane l stores slot p = 64 c + l from its stage entry, so
+  // each 2-byte store instruction writes 64 slots of one or two contiguous runs (2.3 cache lines per
+  // instruction for cfg3 against 5.7 from TI order, tools/experiments/ti_lines.py)
+  if (d.slot_src) {
+    const uint32_t *ss = d.slot_src + (int64_t)r * d.slot_stride;
+    const int32_t *sb = d.slot_base + (int64_t)r * (d.slot_stride >> 6);
     constexpr int MQ = MAP_MB, NW = NT / 64;
-    const int lane = tid & 63, wv = tid >> 6, nch = (cs + 255) >> 8;
+    const int lane = tid & 63, wv = tid >> 6, nch = (cs + 63) >> 6;
     for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
-      uint2 pq[MQ];
+      uint32_t e[MQ];
+      int32_t sbase[MQ];
 #pragma unroll
       for (int u = 0; u < MQ; u++) {
-        const int c = min(c0 + u * NW + wv, nch - 1);
-        pq[u] = ld_off((const uint2 *)pr, (uint32_t)(256 * c + 4 * lane) * 2u);
+        const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
+        e[u] = ld_off(ss, (uint32_t)(64 * c + lane) * 4u);
+        sbase[u] = sb[c];
       }
 #pragma unroll
       for (int u = 0; u < MQ; u++) {
         const int c = c0 + u * NW + wv;
-        if (c < nch) {
-#pragma unroll
-          for (int k = 0; k < 4; k++) {
-            const int j = 256 * c + 64 * k + lane;
-            if (j < cs) {
-              const int row = j / 5, e = j - 5 * row;
-              const int tt = d.ti_on ? e * rows + row : j, oo = d.ti_on ? row * cols + e : j;
-              const int16_t dl = (int16_t)(((k < 2 ? pq[u].x : pq[u].y) >> (16 * (k & 1))) & 0xFFFFu);
-              const uint32_t o = (uint32_t)fbase + (uint32_t)oo + (uint32_t)(int)dl;
-              st_off(dst, o * 2u, stage[tt]);
-            }
-          }
-        }
+        if (c < nch && 64 * c + lane < cs) st_off(dst, ((uint32_t)sbase[u] + (e[u] >> 16)) * 2u, stage[e[u] & 0xFFFFu]);
       }
     }
     return;
   }
+  const int64_t fbase = (d.ti_on ? base : (int64_t)r * cs) + d.data_off;   // + PLP_START
   for (int j = tid; j < cs; j += NT) {
     int tt = j, o = j;
     if (d.ti_on) {
