@@ -644,7 +644,7 @@ extern "C" void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h) { 
 struct ChainPlp {
   FecTables fec;
   MapTables map;
-  DevBuf perm, shift, part, pbase;
+  DevBuf perm, shift, part, pbase, poff, pnq;
   DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], bpart[DVBT2LL_CHAIN_MAX_SLOTS];
   int64_t cw_stride = 0;
   int64_t ts_per_frame = 0;   // payload bytes per frame (NM positions; HEM: before sync-byte removal)
@@ -917,32 +917,52 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     md.ti_nsmall = pp.ti_nsmall;
     md.data_off = pp.start;
     // the map kernel's TI store in stored-slot order (layout.part: frame data slot of each TI
-    // position; the PLP's positions start at PLP_START): block r's cells sorted by slot, entry p =
-    // its TI-store index t | (slot - the slot of its 64-cell chunk's first cell) << 16, plus each
-    // chunk's first slot.  A store instruction then writes 64 slots of one or two contiguous runs
-    // (the block's cells in a symbol (half) are one run, bank-balanced inside, t2_plan
-    // build_chain_layout) instead of gathering them from TI order
-    const int css = (pp.cs + 63) & ~63, nchk = css / 64;
-    std::vector<uint32_t> so((size_t)pp.F * css + 64, 0u);
-    std::vector<int32_t> sbv((size_t)pp.F * nchk + 1, 0);
+    // position; the PLP's positions start at PLP_START), in aligned quads of four slots: block r's
+    // quads sorted by slot, each with the TI-store indices of its four slots (0xFFFF: a slot of another
+    // block, at a run's edge), its offset from its 64-quad chunk's first quad, each chunk's first quad
+    // and the block's quad count.  A full quad is one 8-byte store, so a store instruction writes 512 B
+    // of one or two contiguous runs (the block's cells in a symbol (half) are one run, bank-balanced
+    // inside, t2_plan build_chain_layout)
+    std::vector<std::vector<std::pair<int64_t, int>>> blk(pp.F);
+    int qmax = 0;
     std::vector<std::pair<int64_t, int>> cells(pp.cs);
     for (int rr = 0; rr < pp.F; rr++) {
       for (int t = 0; t < pp.cs; t++) cells[t] = {layout.part[ti_dest(fp, k, rr, t)], t};
       std::sort(cells.begin(), cells.end());
-      for (int c = 0; c < nchk && 64 * c < pp.cs; c++) {
-        const int64_t base = cells[64 * c].first;
-        sbv[(size_t)rr * nchk + c] = (int32_t)base;
-        for (int p = 64 * c; p < std::min(pp.cs, 64 * c + 64); p++) {
-          const int64_t off = cells[p].first - base;
-          if (off < 0 || off > 0xFFFF) return DVBT2LL_EINVAL;
-          so[(size_t)rr * css + p] = (uint32_t)cells[p].second | ((uint32_t)off << 16);
-        }
-      }
+      auto &qv = blk[rr];   // (quad index, slot-in-quad | t << 2) per cell
+      for (auto &c : cells) qv.push_back({c.first >> 2, (int)(c.first & 3) | (c.second << 2)});
+      int nq = 0;
+      for (size_t i = 0; i < qv.size(); i++) nq += i == 0 || qv[i].first != qv[i - 1].first;
+      qmax = std::max(qmax, nq);
     }
-    if ((r = upload(pl->part, so)) || (r = upload(pl->pbase, sbv))) return r;
-    md.slot_src = pl->part.as<uint32_t>();
-    md.slot_base = pl->pbase.as<int32_t>();
-    md.slot_stride = css;
+    const int qst = (qmax + 63) & ~63, nchk = qst / 64;
+    std::vector<uint32_t> qsrc((size_t)pp.F * qst * 2 + 2, 0xFFFFFFFFu);
+    std::vector<uint16_t> qoff((size_t)pp.F * qst + 4, 0);
+    std::vector<int32_t> qb((size_t)pp.F * nchk + 1, 0), qn(pp.F, 0);
+    for (int rr = 0; rr < pp.F; rr++) {
+      int n = -1;
+      int64_t qprev = -1, cbase = 0;
+      for (auto &c : blk[rr]) {
+        if (c.first != qprev) {
+          qprev = c.first;
+          if (++n % 64 == 0) qb[(size_t)rr * nchk + n / 64] = (int32_t)(cbase = c.first);
+          if (c.first - cbase > 0xFFFF) return DVBT2LL_EINVAL;
+          qoff[(size_t)rr * qst + n] = (uint16_t)(c.first - cbase);
+        }
+        const int sl = c.second & 3, t = c.second >> 2;
+        uint32_t &w = qsrc[((size_t)rr * qst + n) * 2 + (sl >> 1)];
+        w = (w & ~(0xFFFFu << (16 * (sl & 1)))) | ((uint32_t)t << (16 * (sl & 1)));
+      }
+      qn[rr] = n + 1;
+    }
+    if ((r = upload(pl->part, qsrc)) || (r = upload(pl->pbase, qb)) || (r = upload(pl->poff, qoff)) ||
+        (r = upload(pl->pnq, qn)))
+      return r;
+    md.slot_quad = pl->part.as<uint2>();
+    md.slot_qoff = pl->poff.as<uint16_t>();
+    md.slot_qbase = pl->pbase.as<int32_t>();
+    md.slot_nq = pl->pnq.as<int32_t>();
+    md.slot_stride = qst;
     pl->F = pp.F;
     pl->inputmode = q.inputmode;
     pl->inband = q.inband;

@@ -87,10 +87,13 @@ struct MapDev {
   int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
   int data_off;            // chain: the PLP's first data cell (PLP_START) within the frame data region
-  // chain: block r's cells in stored-slot order, entry r * slot_stride + p = TI-store index t |
-  // (slot - slot_base[r * slot_stride / 64 + p / 64]) << 16 (map_store_pairs; null: store in TI order)
-  const uint32_t *slot_src;
-  const int32_t *slot_base;
+  // chain: block r's TI store in aligned quads of four frame slots, sorted by slot (map_store_pairs;
+  // null: store in TI order): quad n at r * slot_stride + n holds its slots' TI-store indices (0xFFFF:
+  // another block's slot) and its quad index minus slot_qbase[r * slot_stride / 64 + n / 64];
+  // slot_nq[r] quads
+  const uint2 *slot_quad;
+  const uint16_t *slot_qoff;
+  const int32_t *slot_qbase, *slot_nq;
   int slot_stride;
   // per demuxed bit b of the row word: the column e feeding it (W-1-mux[e] = b) as its first codeword
   // bit e*R (-1: none) and its twist (int32: uniform scalar loads, no byte loads in the column loop)

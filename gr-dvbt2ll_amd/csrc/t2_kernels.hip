@@ -1179,28 +1179,42 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   __syncthreads();
   // time-interleaver store of the index pairs (row-major over (row, e), 5 consecutive cells (10 B)
   // per TI row; the constellation lookup (QAM + rotated-constellation Q delay) is fused into the OFDM
-  // kernel's bin scatter).  Chain: in stored-slot order (MapDev::slot_src): wave w takes 64-cell
-  // chunks c = c0 + u NT / 64 + w (u < 8) and lane l stores slot p = 64 c + l from its stage entry, so
-  // each 2-byte store instruction writes 64 slots of one or two contiguous runs (2.3 cache lines per
-  // instruction for cfg3 against 5.7 from TI order, tools/experiments/ti_lines.py)
-  if (d.slot_src) {
-    const uint32_t *ss = d.slot_src + (int64_t)r * d.slot_stride;
-    const int32_t *sb = d.slot_base + (int64_t)r * (d.slot_stride >> 6);
-    constexpr int MQ = MAP_MB, NW = NT / 64;
-    const int lane = tid & 63, wv = tid >> 6, nch = (cs + 63) >> 6;
+  // kernel's bin scatter).  Chain: in stored-slot order, in aligned quads of four slots
+  // (MapDev::slot_quad): wave w takes 64-quad chunks c = c0 + u NT / 64 + w and lane l quad 64 c + l,
+  // one 8-byte store of its four stage entries (2-byte stores for a quad at a run's edge), so a store
+  // instruction writes 512 B of one or two contiguous runs
+  if (d.slot_quad) {
+    const uint2 *qs = d.slot_quad + (int64_t)r * d.slot_stride;
+    const uint16_t *qo = d.slot_qoff + (int64_t)r * d.slot_stride;
+    const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
+    const int nqd = d.slot_nq[r];
+    constexpr int MQ = 9, NW = NT / 64;
+    const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
+    uint32_t *dstw = (uint32_t *)dst;
     for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
-      uint32_t e[MQ];
-      int32_t sbase[MQ];
+      uint2 e[MQ];
+      uint32_t qa[MQ];
 #pragma unroll
       for (int u = 0; u < MQ; u++) {
         const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
-        e[u] = ld_off(ss, (uint32_t)(64 * c + lane) * 4u);
-        sbase[u] = sb[c];
+        e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
+        qa[u] = (uint32_t)qb[c] + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
       }
 #pragma unroll
       for (int u = 0; u < MQ; u++) {
         const int c = c0 + u * NW + wv;
-        if (c < nch && 64 * c + lane < cs) st_off(dst, ((uint32_t)sbase[u] + (e[u] >> 16)) * 2u, stage[e[u] & 0xFFFFu]);
+        if (c < nch && 64 * c + lane < nqd) {
+          const uint32_t t0 = e[u].x & 0xFFFFu, t1 = e[u].x >> 16, t2 = e[u].y & 0xFFFFu, t3 = e[u].y >> 16;
+          if (t0 != 0xFFFFu && t1 != 0xFFFFu && t2 != 0xFFFFu && t3 != 0xFFFFu) {
+            st_off((uint2 *)dstw, qa[u] * 8u,
+                   make_uint2((uint32_t)stage[t0] | ((uint32_t)stage[t1] << 16), (uint32_t)stage[t2] | ((uint32_t)stage[t3] << 16)));
+          } else {
+            if (t0 != 0xFFFFu) st_off(dst, (4u * qa[u] + 0u) * 2u, stage[t0]);
+            if (t1 != 0xFFFFu) st_off(dst, (4u * qa[u] + 1u) * 2u, stage[t1]);
+            if (t2 != 0xFFFFu) st_off(dst, (4u * qa[u] + 2u) * 2u, stage[t2]);
+            if (t3 != 0xFFFFu) st_off(dst, (4u * qa[u] + 3u) * 2u, stage[t3]);
+          }
+        }
       }
     }
     return;
