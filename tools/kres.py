@@ -5,7 +5,8 @@ import re
 import subprocess
 import sys
 
-src = "gr-dvbt2ll_amd/csrc/t2_kernels.hip"
+import os
+src = os.environ.get("KRES_SRC", "gr-dvbt2ll_amd/csrc/t2_kernels.hip")
 cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "-fPIC", "--offload-arch=gfx950", "-munsafe-fp-atomics",
        "-Rpass-analysis=kernel-resource-usage", "-c", src, "-o", "/tmp/kres.o"] + sys.argv[1:]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
