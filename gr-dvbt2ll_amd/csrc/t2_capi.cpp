@@ -916,18 +916,21 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     md.ti_big = pp.ti_big;
     md.ti_nsmall = pp.ti_nsmall;
     md.data_off = pp.start;
-    // the map kernel's TI store in stored-slot order (layout.part: frame data slot of each TI
-    // position; the PLP's positions start at PLP_START), in aligned quads of four slots: block r's
-    // quads sorted by slot, each with the TI-store indices of its four slots (0xFFFF: a slot of another
-    // block, at a run's edge), its offset from its 64-quad chunk's first quad, each chunk's first quad
-    // and the block's quad count.  A full quad is one 8-byte store, so a store instruction writes 512 B
+    // the map kernel's cell interleaver + TI store in stored-slot order (layout.part: frame data slot
+    // of each TI position; the PLP's positions start at PLP_START), in aligned quads of four slots:
+    // block r's quads sorted by slot, each with the cell-interleaver input index of the cell landing
+    // in each of its four slots (j with (ci_perm[j] + ci_shift[r]) mod cs = t, framemapper:1973-1998;
+    // 0xFFFF: a slot of another block, at a run's edge), its offset from its 64-quad chunk's first
+    // quad, each chunk's first quad and the block's quad count.  A full quad is one 8-byte store, so a store instruction writes 512 B
     // of one or two contiguous runs (the block's cells in a symbol (half) are one run, bank-balanced
     // inside, t2_plan build_chain_layout)
     std::vector<std::vector<std::pair<int64_t, int>>> blk(pp.F);
     int qmax = 0;
     std::vector<std::pair<int64_t, int>> cells(pp.cs);
+    std::vector<int> jin(pp.cs);   // cell-interleaver input index of each output position t
     for (int rr = 0; rr < pp.F; rr++) {
-      for (int t = 0; t < pp.cs; t++) cells[t] = {layout.part[ti_dest(fp, k, rr, t)], t};
+      for (int j = 0; j < pp.cs; j++) jin[(pp.ci_perm[j] + pp.ci_shift[rr]) % pp.cs] = j;
+      for (int t = 0; t < pp.cs; t++) cells[t] = {layout.part[ti_dest(fp, k, rr, t)], jin[t]};
       std::sort(cells.begin(), cells.end());
       auto &qv = blk[rr];   // (quad index, slot-in-quad | t << 2) per cell
       for (auto &c : cells) qv.push_back({c.first >> 2, (int)(c.first & 3) | (c.second << 2)});

@@ -87,9 +87,10 @@ struct MapDev {
   int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
   int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
   int data_off;            // chain: the PLP's first data cell (PLP_START) within the frame data region
-  // chain: block r's TI store in aligned quads of four frame slots, sorted by slot (map_store_pairs;
-  // null: store in TI order): quad n at r * slot_stride + n holds its slots' TI-store indices (0xFFFF:
-  // another block's slot) and its quad index minus slot_qbase[r * slot_stride / 64 + n / 64];
+  // chain: block r's cell interleaver + TI store in aligned quads of four frame slots, sorted by slot
+  // (map_store_pairs; null: cell interleaver through LDS, then the TI store in TI order): quad n at
+  // r * slot_stride + n holds the cell-interleaver input index of each of its slots (0xFFFF: another
+  // block's slot) and its quad index minus slot_qbase[r * slot_stride / 64 + n / 64];
   // slot_nq[r] quads
   const uint2 *slot_quad;
   const uint16_t *slot_qoff;

@@ -1129,6 +1129,53 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
   const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
   const int nq = (cs + 3) >> 2;
   const uint32_t *idxw = (const uint32_t *)idx;
+  // Chain: the cell interleaver and the time-interleaver store in one pass, in stored-slot order, in
+  // aligned quads of four frame slots (MapDev::slot_quad): wave w takes 64-quad chunks c = c0 + u NT / 64
+  // + w and lane l quad 64 c + l, whose four slots list the cell-interleaver INPUT index j of the cell
+  // landing there (the chain composes j = CI^-1(t) for the block's shift); the slot gets (idx[j],
+  // idx[j - 1]) (the rotated constellation's Q delay; the QAM lookup is fused into the OFDM kernel's bin
+  // scatter).  One 8-byte store per full quad (2-byte stores for a quad at a run's edge, whose other
+  // slots belong to neighbouring blocks), so a store instruction writes 512 B of one or two contiguous
+  // runs; no stage array and no cell-interleaver pass through LDS
+  if (d.slot_quad) {
+    const uint2 *qs = d.slot_quad + (int64_t)r * d.slot_stride;
+    const uint16_t *qo = d.slot_qoff + (int64_t)r * d.slot_stride;
+    const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
+    const int nqd = d.slot_nq[r];
+    constexpr int MQ = 9, NW = NT / 64;
+    const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
+    auto pair_of = [&](uint32_t j) -> uint32_t {
+      const uint32_t lo = idx[j], hi = d.rotation ? (uint32_t)idx[j == 0 ? (uint32_t)cs - 1u : j - 1u] : lo;
+      return lo | (hi << 8);
+    };
+    for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
+      uint2 e[MQ];
+      uint32_t qa[MQ];
+#pragma unroll
+      for (int u = 0; u < MQ; u++) {
+        const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
+        e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
+        qa[u] = (uint32_t)qb[c] + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
+      }
+#pragma unroll
+      for (int u = 0; u < MQ; u++) {
+        const int c = c0 + u * NW + wv;
+        if (c < nch && 64 * c + lane < nqd) {
+          const uint32_t j0 = e[u].x & 0xFFFFu, j1 = e[u].x >> 16, j2 = e[u].y & 0xFFFFu, j3 = e[u].y >> 16;
+          if (j0 != 0xFFFFu && j1 != 0xFFFFu && j2 != 0xFFFFu && j3 != 0xFFFFu) {
+            st_off((uint2 *)dst, qa[u] * 8u, make_uint2(pair_of(j0) | (pair_of(j1) << 16), pair_of(j2) | (pair_of(j3) << 16)));
+          } else {
+            if (j0 != 0xFFFFu) st_off(dst, (4u * qa[u] + 0u) * 2u, (uint16_t)pair_of(j0));
+            if (j1 != 0xFFFFu) st_off(dst, (4u * qa[u] + 1u) * 2u, (uint16_t)pair_of(j1));
+            if (j2 != 0xFFFFu) st_off(dst, (4u * qa[u] + 2u) * 2u, (uint16_t)pair_of(j2));
+            if (j3 != 0xFFFFu) st_off(dst, (4u * qa[u] + 3u) * 2u, (uint16_t)pair_of(j3));
+          }
+        }
+      }
+    }
+    return;
+  }
+
   // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell, four
   // consecutive cells per thread (one 8-byte load of their permutation entries and one 4-byte LDS
   // read of their indices, plus the previous cell's byte for the rotation)
@@ -1177,48 +1224,8 @@ __device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t fr
     }
   }
   __syncthreads();
-  // time-interleaver store of the index pairs (row-major over (row, e), 5 consecutive cells (10 B)
-  // per TI row; the constellation lookup (QAM + rotated-constellation Q delay) is fused into the OFDM
-  // kernel's bin scatter).  Chain: in stored-slot order, in aligned quads of four slots
-  // (MapDev::slot_quad): wave w takes 64-quad chunks c = c0 + u NT / 64 + w and lane l quad 64 c + l,
-  // one 8-byte store of its four stage entries (2-byte stores for a quad at a run's edge), so a store
-  // instruction writes 512 B of one or two contiguous runs
-  if (d.slot_quad) {
-    const uint2 *qs = d.slot_quad + (int64_t)r * d.slot_stride;
-    const uint16_t *qo = d.slot_qoff + (int64_t)r * d.slot_stride;
-    const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
-    const int nqd = d.slot_nq[r];
-    constexpr int MQ = 9, NW = NT / 64;
-    const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
-    uint32_t *dstw = (uint32_t *)dst;
-    for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
-      uint2 e[MQ];
-      uint32_t qa[MQ];
-#pragma unroll
-      for (int u = 0; u < MQ; u++) {
-        const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
-        e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
-        qa[u] = (uint32_t)qb[c] + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
-      }
-#pragma unroll
-      for (int u = 0; u < MQ; u++) {
-        const int c = c0 + u * NW + wv;
-        if (c < nch && 64 * c + lane < nqd) {
-          const uint32_t t0 = e[u].x & 0xFFFFu, t1 = e[u].x >> 16, t2 = e[u].y & 0xFFFFu, t3 = e[u].y >> 16;
-          if (t0 != 0xFFFFu && t1 != 0xFFFFu && t2 != 0xFFFFu && t3 != 0xFFFFu) {
-            st_off((uint2 *)dstw, qa[u] * 8u,
-                   make_uint2((uint32_t)stage[t0] | ((uint32_t)stage[t1] << 16), (uint32_t)stage[t2] | ((uint32_t)stage[t3] << 16)));
-          } else {
-            if (t0 != 0xFFFFu) st_off(dst, (4u * qa[u] + 0u) * 2u, stage[t0]);
-            if (t1 != 0xFFFFu) st_off(dst, (4u * qa[u] + 1u) * 2u, stage[t1]);
-            if (t2 != 0xFFFFu) st_off(dst, (4u * qa[u] + 2u) * 2u, stage[t2]);
-            if (t3 != 0xFFFFu) st_off(dst, (4u * qa[u] + 3u) * 2u, stage[t3]);
-          }
-        }
-      }
-    }
-    return;
-  }
+  // time-interleaver store of the index pairs: row-major over (row, e), 5 consecutive cells (10 B)
+  // per TI row
   const int64_t fbase = (d.ti_on ? base : (int64_t)r * cs) + d.data_off;   // + PLP_START
   for (int j = tid; j < cs; j += NT) {
     int tt = j, o = j;
