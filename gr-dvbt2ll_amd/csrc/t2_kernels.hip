@@ -708,8 +708,8 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel
 typedef int bch_v8i __attribute__((ext_vector_type(8)));
 typedef float bch_v16f __attribute__((ext_vector_type(16)));
 
-// Persistent workgroups, BCH_WG_PER_CU per CU.  Workgroup i serves K slice i % 8 (its XCD: that
-// XCD's L2 holds one eighth of the generator table) and a contiguous, equal share of the slice's
+// Persistent workgroups, BCH_WG_PER_CU per CU.  Workgroup i serves K slice i % BCH_KS (by its XCD: that
+// XCD's L2 holds 1 / BCH_KS of the generator table) and a contiguous, equal share of the slice's
 // (tile, chunk) units, tile-major: a tile is 128 FEC blocks (wave w: blocks 32 w .. 32 w + 31, one per
 // A row) x all bch_nt parity tiles, a chunk 32 message bytes = four K-steps of 64 bits.  Per chunk
 // the B fragments (t2_plan build_bch_mfma) are staged in LDS (double-buffered LDS-DMA, one barrier per
@@ -954,7 +954,7 @@ static hipError_t bch_launch(const FecDev &d, const FecIO &io, hipStream_t s) {
   const int lds = 2 * 4 * NT * 64 * 16;
   hipError_t e = lds_limit((const void *)bch_gemm_kernel<NT>, lds);
   if (e != hipSuccess) return e;
-  // persistent: BCH_WG_PER_CU workgroups per CU, a multiple of BCH_KS (one slice per XCD)
+  // persistent: BCH_WG_PER_CU workgroups per CU, a multiple of BCH_KS (slices by XCD)
   const int per_slice = (fec_grid(1 << 30, BCH_WG_PER_CU) + BCH_KS - 1) / BCH_KS;
   hipLaunchKernelGGL(bch_gemm_kernel<NT>, dim3(per_slice * BCH_KS), dim3(FEC_THREADS), lds, s, d, io);
   return hipGetLastError();
