@@ -725,7 +725,7 @@ def main():
         # secondary (not `value`): each step followed by the ordered IQ gather to rank 0, the
         # chain's one exchange step (point-to-point sends to the root over RCCL / xGMI)
         from dvbt2ll.distributed import gather_frames
-        kg = min(args.steps, 5)
+        kg = min(args.steps, 3)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
