@@ -99,29 +99,33 @@ def algorithmic_bytes(cfg, info):
 
 
 def minimal_bytes(cfg, info, iq_bytes=8):
-    """per-frame bytes each kernel of the fused chain must move through HBM at least:
-    fec reads the TS payload and writes packed codewords; map reads the codewords and writes one
-    2-byte constellation index pair per cell; ofdm reads the pairs and writes the IQ samples (its
-    per-symbol tables are shared by every frame of a launch and are not counted)"""
+    """per-frame bytes each kernel stage of the fused chain must move through HBM at least:
+    fec (BB + matrix-core BCH passes) reads the TS payload and writes the BBFRAMEs and their BCH parity;
+    map (the LDPC + map kernel) reads those and writes one 2-byte constellation index pair per cell;
+    ofdm reads the pairs and writes the IQ samples (per-symbol tables are shared by every frame of a
+    launch and are not counted)"""
     from dvbt2ll.configs import KBCH
     F = info["fec_blocks_per_frame"]
     nldpc = 64800 if cfg.framesize == 1 else 16200
     kbch = KBCH[(cfg.framesize, cfg.rate)]
     cs, S, IQ = info["cell_size"], info["stream_items"], info["iq_samples_per_frame"]
-    return {"fec": F * ((kbch - 80) // 8 + nldpc // 8), "map": F * (nldpc // 8 + 2 * cs),
+    # BCH parity bits: 168 (short), 160 (normal 2/3, 5/6), 192 (the other normal codes)
+    nbch = kbch + (168 if cfg.framesize == 0 else 160 if cfg.rate in (2, 5) else 192)
+    return {"fec": F * ((kbch - 80) // 8 + nbch // 8), "map": F * (nbch // 8 + 2 * cs),
             "ofdm": 2 * S + iq_bytes * IQ}
 
 
 KERNELS = ("fec", "map", "ofdm")
-# the kernels each stage launches per step (the chain's FEC: BB pass, BCH matrix-core pass, LDPC pass)
-STAGE_KERNELS = {"fec": ("fec_bb", "bch_gemm", "fec_ldpc"), "map": ("map",), "ofdm": ("ofdm",)}
+# the kernels each stage launches per step: fec = the BB pass and the BCH matrix-core pass, map = the LDPC +
+# map kernel (LDPC parity, bit interleaver, cell + time interleaver; with the frames' L1-post workgroups)
+STAGE_KERNELS = {"fec": ("fec_bb", "bch_gemm"), "map": ("ldpc_map",), "ofdm": ("ofdm",)}
 # rocprofv3 FETCH_SIZE / WRITE_SIZE (KiB) -> bytes.  gfx950 tallies 128-B read requests at 64 B
 # (MI355X_MICROARCH.md, HBM): x2 on the read side, calibrated per access width by tools/fetch_calib
-# (profiles/r2_fetch_calib.json); the kernels' dominant access widths: fec 16-B TS staging / codeword
-# loads and 16-B BBFRAME + 4-B parity stores, map 16-B codeword loads and 2-B index-pair stores, ofdm
-# 16-B data-slot loads and 16-B IQ stores (two samples per lane)
+# (profiles/r2_fetch_calib.json); the kernels' dominant access widths: fec 16-B TS staging / BBFRAME
+# loads and 16-B BBFRAME stores, map 16-B BBFRAME loads and 8-B index-pair quad stores, ofdm 16-B
+# data-slot loads and 16-B IQ stores (two samples per lane)
 LOAD_WIDTH = {"fec": 16, "map": 16, "ofdm": 16}
-STORE_WIDTH = {"fec": 4, "map": 2, "ofdm": 16}
+STORE_WIDTH = {"fec": 16, "map": 8, "ofdm": 16}
 
 
 def _calibration():
@@ -160,13 +164,13 @@ def pmc_passes(args):
                 for row in csv.DictReader(fh):
                     kn = row.get("Kernel_Name", "")
                     names.add(kn[:60])
-                    m = re.search(r"\b(fec_bb|bch_gemm|fec_ldpc|fec|map|ofdm)(32)?_kernel", kn)
+                    m = re.search(r"\b(fec_bb|bch_gemm|ldpc_map|fec|map|ofdm)(32)?_kernel", kn)
                     if m and row.get("Counter_Name") in ctrs:
                         vals.setdefault((m.group(1), row["Counter_Name"]), []).append(float(row["Counter_Value"]))
-        # per-launch means; the chain's FEC stage is three kernels launched once each per step (BB pass,
-        # BCH on the matrix cores, LDPC pass): their means add up
+        # per-launch means; the chain's FEC stage is two kernels launched once each per step (BB pass,
+        # BCH on the matrix cores): their means add up
         for (kn, c), v in vals.items():
-            k = "fec" if kn in STAGE_KERNELS["fec"] else kn
+            k = next((st for st, kns in STAGE_KERNELS.items() if kn in kns), kn)
             res[k][c] = res[k].get(c, 0.0) + sum(v) / len(v)
         shutil.rmtree(d, ignore_errors=True)
     cal = _calibration()
@@ -756,7 +760,8 @@ def main():
             stages[name] = {"avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": ab[name] * B,
                             "achieved_GBs": ab[name] * B / t / 1e9 if t > 0 else None}
             kname = ("ofdm32_kernel" if name == "ofdm" and info["fft_size"] == 32768 else
-                     "fec_bb_kernel + bch_gemm_kernel + fec_ldpc_kernel" if name == "fec" else name + "_kernel")
+                     "fec_bb_kernel + bch_gemm_kernel" if name == "fec" else
+                     "ldpc_map_kernel (+ L1-post workgroups)" if name == "map" else name + "_kernel")
             e = {"kernel": kname, "bound": "hbm", "avg_launch_ms": avg_ms, "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "min_bytes_per_launch": mb[name] * B,
                  "achieved": mb[name] * B / t / 1e9 if t > 0 else None,
@@ -774,12 +779,15 @@ def main():
                 e["traffic_over_min"] = e["traffic"] / (mb[name] * B)
                 e["traffic_fetch_write"] = pm.get("fetch_write_bytes")
                 e["calibration"] = pm.get("calibration")
-            if name == "fec":
+            if name in ("fec", "map"):
                 nb = info["fec_blocks_per_frame"] * B
                 e["fec_blocks_per_s"] = nb / t if t > 0 else None
-                e["note"] = ("integer BB/BCH/LDPC codec (the BCH as a GF(2) product on the matrix cores): "
-                             "latency/issue-bound, not HBM-bound (SURVEY 8(d)); frac is its minimal HBM bytes / "
-                             "time / peak; traffic and instruction counts are the three pass kernels' sums")
+                e["note"] = ("BB pass + BCH as a GF(2) product on the matrix cores (two kernels; traffic and "
+                             "instruction counts are their sums)" if name == "fec" else
+                             "LDPC parity + bit interleaver + cell / time interleaver of each FEC block in one "
+                             "kernel (the codeword stays in LDS), plus the frames' L1-post workgroups") + (
+                             ": integer codec work, latency/issue-bound, not HBM-bound (SURVEY 8(d)); frac is "
+                             "the minimal HBM bytes / time / peak")
                 if "SQ_INSTS_VALU" in pm and t > 0:
                     e["valu_wave_instr_per_block"] = pm["SQ_INSTS_VALU"] / nb
                     e["salu_wave_instr_per_block"] = pm.get("SQ_INSTS_SALU", 0) / nb

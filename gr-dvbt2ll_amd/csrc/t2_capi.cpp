@@ -130,7 +130,7 @@ struct FecTables {
 
 struct MapTables {
   MapPlan plan;
-  DevBuf lut, perm, shift;
+  DevBuf lut;
   MapDev dev{};
   int init(int framesize, int rate, int constellation, int rotation, const FecPlan &fec) {
     if (build_map(framesize, rate, constellation, rotation, plan)) return DVBT2LL_EINVAL;
@@ -386,8 +386,6 @@ extern "C" int dvbt2ll_interleavermod_general_work(dvbt2ll_interleavermod *h, in
   io.in = h->din.as<uint8_t>();
   io.out = h->dout.as<float2>();
   io.nblocks = nb;
-  io.packed_in = 0;
-  io.apply_ci = 0;
   HIP_TRY(launch_map(d, io, h->ctx.stream));
   HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)nb * d.cs * 8, hipMemcpyDeviceToHost, h->ctx.stream));
   HIP_TRY(hipStreamSynchronize(h->ctx.stream));
@@ -644,15 +642,15 @@ extern "C" void dvbt2ll_pilotgenp1insert_destroy(dvbt2ll_pilotgenp1insert *h) { 
 struct ChainPlp {
   FecTables fec;
   MapTables map;
-  DevBuf perm, shift, part, pbase, poff, pnq;
+  DevBuf part, pbase, poff, pnq;
   DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], bpart[DVBT2LL_CHAIN_MAX_SLOTS];
   int64_t cw_stride = 0;
   int64_t ts_per_frame = 0;   // payload bytes per frame (NM positions; HEM: before sync-byte removal)
   int pay = 0, F = 0, inputmode = 0, inband = 0;
 };
 
-// instantiated hipGraphs of the chain's kernels (per PLP: FEC BB pass, BCH matrix-core pass, LDPC pass;
-// per PLP: map (PLP 0's launch also generates the L1-post); OFDM) for one (nframes, IQ format, slot),
+// instantiated hipGraphs of the chain's kernels (per PLP: FEC BB pass, BCH matrix-core pass; per PLP: LDPC +
+// map (PLP 0's launch also generates the L1-post); OFDM) for one (nframes, IQ format, slot),
 // captured once from the ordinary launch path into a ring of instantiations.  A call takes the next
 // ring entry, waits for it only if it is still in flight, rewrites its kernel nodes' arguments
 // (hipGraphExecKernelNodeSetParams) and launches it.
@@ -698,6 +696,10 @@ struct dvbt2ll_chain {
   uint32_t l1_stride = 0;
   hipEvent_t slot_done[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   hipStream_t slot_stream[DVBT2LL_CHAIN_MAX_SLOTS] = {};
+  // test hook (dvbt2ll_chain_debug_keep_codewords): runs also store the codewords; per slot, whether its
+  // last run did
+  bool keep_cw = false;
+  bool cw_kept[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   bool slot_used[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   int nslots = 1, next_slot = 0, last_slot = 0;
   // hipGraph mode (dvbt2ll_chain_set_graph)
@@ -748,22 +750,23 @@ struct dvbt2ll_chain {
     evused = 0;
     return st;
   }
-  // the chain's kernels on stream s: every PLP's FEC (three passes), every PLP's map (PLP 0's launch has
-  // the extra workgroups that generate the frames' L1-post cells), OFDM.  ev1, ev2 (timing): recorded
-  // after the FEC passes and the map kernels
+  // the chain's kernels on stream s: every PLP's BB + matrix-core BCH passes, every PLP's LDPC + map
+  // (PLP 0's launch has the extra workgroups that generate the frames' L1-post cells), OFDM.  ev1, ev2
+  // (timing): recorded after the BB + BCH passes and after the LDPC + map kernels
   hipError_t launch_chain(const L1IO &lio, const FecIO *fio, const MapIO *mio, const OfdmIO &oio, hipStream_t s,
                           hipEvent_t ev1, hipEvent_t ev2) {
     hipError_t e = hipSuccess;
-    for (int k = 0; k < nplp && e == hipSuccess; k++) e = launch_fec(FEC_TS_TO_TEMPU, plps[k]->fec.dev, fio[k], s);
+    for (int k = 0; k < nplp && e == hipSuccess; k++) e = launch_fec(FEC_TS_TO_BBFRAME, plps[k]->fec.dev, fio[k], s);
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, s);
     for (int k = 0; k < nplp && e == hipSuccess; k++)
-      e = k == 0 ? launch_map(plps[k]->map.dev, mio[k], s, &l1.dev, &lio) : launch_map(plps[k]->map.dev, mio[k], s);
+      e = k == 0 ? launch_ldpc_map(plps[k]->fec.dev, fio[k], plps[k]->map.dev, mio[k], s, &l1.dev, &lio)
+                 : launch_ldpc_map(plps[k]->fec.dev, fio[k], plps[k]->map.dev, mio[k], s);
     if (e == hipSuccess && ev2) e = hipEventRecord(ev2, s);
     if (e == hipSuccess) e = launch_ofdm(ofdm.dev, oio, s);
     return e;
   }
-  // kernel nodes per run: 3 FEC passes and a map per PLP, one OFDM
-  int graph_nodes() const { return 4 * nplp + 1; }
+  // kernel nodes per run: 2 FEC passes and an LDPC + map kernel per PLP, one OFDM
+  int graph_nodes() const { return 3 * nplp + 1; }
   int graph_launch(const L1IO &lio, const FecIO *fio, const MapIO *mio, const OfdmIO &oio, int nframes, int slot,
                    hipStream_t s) {
     const int nk = graph_nodes();
@@ -843,8 +846,8 @@ struct dvbt2ll_chain {
       md[k] = plps[k]->map.dev;
     }
     for (int k = 0; k < nplp; k++)
-      for (int pass = 0; pass < 3; pass++) args.push_back({&fd[k], &fi[k]});
-    for (int k = 0; k < nplp; k++) args.push_back({&md[k], &mi[k], k ? &ld0 : &ld, k ? &li0 : &li});
+      for (int pass = 0; pass < 2; pass++) args.push_back({&fd[k], &fi[k]});
+    for (int k = 0; k < nplp; k++) args.push_back({&fd[k], &fi[k], &md[k], &mi[k], k ? &ld0 : &ld, k ? &li0 : &li});
     args.push_back({&od, &oi});
     for (int k = 0; k < nk; k++) {
       hipKernelNodeParams p = g->base[k];
@@ -904,19 +907,9 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     if (h->nplp > 1) pl->fec.dev.matype = MATYPE_MIS | k;
     if ((r = pl->fec.init_chain())) return r;
     if ((r = pl->map.init(q.framesize, q.rate, q.constellation, q.rotation, pl->fec.plan))) return r;
-    std::vector<int16_t> cip(pp.ci_perm.begin(), pp.ci_perm.end());
-    cip.resize(((cip.size() + 3) & ~(size_t)3) + 4, 0);   // the map kernel reads aligned quads
-    if ((r = upload(pl->perm, cip)) || (r = upload(pl->shift, pp.ci_shift))) return r;
     MapDev &md = pl->map.dev;
-    md.ci_perm = pl->perm.as<int16_t>();
-    md.ci_shift = pl->shift.as<int32_t>();
     md.F = pp.F;
-    md.ti_on = pp.ti_on;
-    md.ti_small = pp.ti_small;
-    md.ti_big = pp.ti_big;
-    md.ti_nsmall = pp.ti_nsmall;
-    md.data_off = pp.start;
-    // the map kernel's cell interleaver + TI store in stored-slot order (layout.part: frame data slot
+    // the LDPC + map kernel's cell interleaver + TI store in stored-slot order (layout.part: frame data slot
     // of each TI position; the PLP's positions start at PLP_START), in aligned quads of four slots:
     // block r's quads sorted by slot, each with the cell-interleaver input index of the cell landing
     // in each of its four slots (j with (ci_perm[j] + ci_shift[r]) mod cs = t, framemapper:1973-1998;
@@ -1199,13 +1192,10 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
     fio[k].ts_stride = nstreams > 1 ? ts_stride : 0;
     fio[k].bch_part = pl.bpart[slot].as<uint32_t>();
     fio[k].bch_part_blocks = (int64_t)pl.F * h->max_frames;
-    mio[k].in = cw.as<uint8_t>();
-    mio[k].cw_stride = pl.cw_stride;
+    fio[k].keep_cw = h->keep_cw;
     mio[k].out_pairs = pairs.as<uint16_t>();
     mio[k].frame_stride = h->pair_stride;
     mio[k].nblocks = pl.F * nf;
-    mio[k].packed_in = 1;
-    mio[k].apply_ci = 1;
   }
   oio.data = h->aux.as<float2>();
   oio.aux_off = 0;
@@ -1229,6 +1219,7 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
   HIP_TRY(hipEventRecord(h->slot_done[slot], s));
   h->slot_used[slot] = true;
   h->slot_stream[slot] = s;
+  h->cw_kept[slot] = h->keep_cw;
   h->last_slot = slot;
   h->next_slot = (slot + 1) % h->nslots;
   return DVBT2LL_OK;
@@ -1318,10 +1309,15 @@ extern "C" int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *l
 extern "C" int dvbt2ll_chain_debug_plp_codewords(dvbt2ll_chain *h, int plp, void *out, int64_t bytes) {
   if (!h || !out || bytes < 0 || plp < 0 || plp >= h->nplp) return DVBT2LL_EINVAL;
   const DevBuf &cw = h->plps[plp]->cw[h->last_slot];
-  if ((size_t)bytes > cw.n) return DVBT2LL_EINVAL;
+  if ((size_t)bytes > cw.n || !h->cw_kept[h->last_slot]) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(out, cw.p, (size_t)bytes, hipMemcpyDeviceToHost));
+  return DVBT2LL_OK;
+}
+extern "C" int dvbt2ll_chain_debug_keep_codewords(dvbt2ll_chain *h, int enable) {
+  if (!h) return DVBT2LL_EINVAL;
+  h->keep_cw = enable != 0;
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes) {

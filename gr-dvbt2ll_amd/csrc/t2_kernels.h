@@ -7,7 +7,8 @@ namespace t2 {
 
 // ---------------------------------------------------------------- FEC (BB + BCH + LDPC)
 enum FecMode {
-  FEC_TS_TO_TEMPU = 0,   // chain: TS bytes -> packed interleaver-input codeword (three passes)
+  FEC_TS_TO_BBFRAME = 0, // chain: TS bytes -> BBFRAME rows + BCH partial parities (BB pass, matrix-core
+                         // BCH pass); launch_ldpc_map continues from them
   FEC_TS_TO_BITS = 1,    // bbheaderbch block: TS bytes -> unpacked nbch bits
   FEC_BITS_TO_BITS = 2,  // ldpc block: unpacked nbch bits -> unpacked nldpc bits (natural)
 };
@@ -51,11 +52,14 @@ struct FecIO {
   // b / blocks_per_stream, whose TS bytes start at in + stream * ts_stride (same ts_base, ts_len)
   int blocks_per_stream;
   int64_t ts_stride;
-  // chain (FEC_TS_TO_TEMPU): BCH parity of launch block b at bch_part + b * BCH_PART_WORDS (zeroed by
-  // the BB pass, XOR-accumulated by the K slices of the matrix-core pass, read by the LDPC pass;
+  // chain (FEC_TS_TO_BBFRAME): BCH parity of launch block b at bch_part + b * BCH_PART_WORDS (zeroed by
+  // the BB pass, XOR-accumulated by the K slices of the matrix-core pass, read by launch_ldpc_map;
   // room for bch_part_blocks >= nblocks)
   uint32_t *bch_part;
   int64_t bch_part_blocks;
+  // launch_ldpc_map (test hook): 1 = also store each block's interleaver-input codeword into its row
+  // (the BBFRAME already there), 0 = the codeword stays in LDS
+  int keep_cw;
 };
 
 // ---------------------------------------------------------------- L1-post signalling (t2_plan.h L1PostPlan)
@@ -83,17 +87,13 @@ struct L1IO {
 
 // ---------------------------------------------------------------- bit interleave + QAM + CI
 struct MapDev {
-  const float2 *lut;       // 256
-  const int16_t *ci_perm;  // cs (chain only)
-  const int32_t *ci_shift; // F  (chain only)
-  int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il, F;
-  int ti_on, ti_small, ti_big, ti_nsmall;   // time interleaver geometry (chain only)
-  int data_off;            // chain: the PLP's first data cell (PLP_START) within the frame data region
-  // chain: block r's cell interleaver + TI store in aligned quads of four frame slots, sorted by slot
-  // (map_store_pairs; null: cell interleaver through LDS, then the TI store in TI order): quad n at
-  // r * slot_stride + n holds the cell-interleaver input index of each of its slots (0xFFFF: another
-  // block's slot) and its quad index minus slot_qbase[r * slot_stride / 64 + n / 64];
-  // slot_nq[r] quads
+  const float2 *lut;       // 256 (block API)
+  int mode, mod, W, R, cs, nldpc, nbch, q, rotation, parity_il;
+  int F;                   // chain: FEC blocks per frame (launch block b is FEC block b mod F of frame b / F)
+  // chain: block r's cell interleaver + time-interleaver store in aligned quads of four frame slots,
+  // sorted by slot (map_store_quads): quad n at r * slot_stride + n holds the cell-interleaver input
+  // index of each of its slots (0xFFFF: another block's slot) and its quad index minus
+  // slot_qbase[r * slot_stride / 64 + n / 64]; slot_nq[r] quads
   const uint2 *slot_quad;
   const uint16_t *slot_qoff;
   const int32_t *slot_qbase, *slot_nq;
@@ -103,16 +103,13 @@ struct MapDev {
   int colstart[16], coltw[16];
 };
 struct MapIO {
-  const uint8_t *in;   // packed tempu codewords (stride cw_stride) or unpacked natural bits
-  int64_t cw_stride;
-  float2 *out;         // cells (apply_ci = 0)
-  // apply_ci = 1 (chain): per cell the constellation index pair lo = idx[j], hi = idx[j-1]
+  const uint8_t *in;   // block API: unpacked natural-order codeword bits, nldpc per block
+  float2 *out;         // block API: cs cells per block
+  // chain (launch_ldpc_map): per cell the constellation index pair lo = idx[j], hi = idx[j-1]
   // (rotation) or idx[j], frame k's data region at out_pairs + k * frame_stride
   uint16_t *out_pairs;
   int64_t frame_stride;
   int nblocks;
-  int packed_in;       // 1: chain layout; 0: unpacked bits (interleavermod block)
-  int apply_ci;        // 1 (chain): cell + time interleave into the frame data region
 };
 
 // ---------------------------------------------------------------- OFDM symbols
@@ -184,9 +181,12 @@ struct GatherIO {
 };
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s);
-// l1d / l1io (optional, the chain): the frames' L1-post cells by extra workgroups of the same launch
-hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1Dev *l1d = nullptr,
-                      const L1IO *l1io = nullptr);
+hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s);
+// the chain after FEC_TS_TO_BBFRAME: LDPC of fio's BBFRAME rows + BCH partials, then the map (column twist,
+// demux, cell interleaver, TI store into mio.out_pairs) of the same blocks, one kernel; l1d / l1io
+// (optional): the frames' L1-post cells by extra workgroups of the same launch
+hipError_t launch_ldpc_map(const FecDev &fd, const FecIO &fio, const MapDev &md, const MapIO &mio, hipStream_t s,
+                           const L1Dev *l1d = nullptr, const L1IO *l1io = nullptr);
 hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s);
 hipError_t launch_gather(const GatherIO &io, hipStream_t s);
 hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s);

@@ -5,15 +5,17 @@
 //                division, chunk remainders moved by per-lane nibble tables) + LDPC as a
 //                quasi-cyclic array of 360-bit rotations with a bit-packed accumulate scan.
 //                Reference: lib/bbheaderbch_bb_impl.cc:648-742 (+ ldpc_calculate :625-646).
-//   map_kernel   one workgroup per FEC block: column-twist bit interleave + demux, then either
-//                the QAM LUT (interleavermod block) or the cell + time interleaver store of
-//                constellation index pairs (chain); extra workgroups generate the L1-post cells.
-//                Reference: lib/interleavermod_bc_impl.cc:270-704, framemapper :1973-2028.
+//   chain FEC     fec_bb_kernel, bch_gemm_kernel (the BCH as a GF(2) product on the matrix cores),
+//                 ldpc_map_kernel (LDPC, then the bit interleaver, cell and time interleaver of the
+//                 block's constellation index pairs; extra workgroups generate the L1-post cells).
+//                 Reference: bbheaderbch :625-742, lib/interleavermod_bc_impl.cc:270-704,
+//                 framemapper :1973-2028.
+//   map_kernel   block API: one workgroup per FEC block, column-twist bit interleave + demux + QAM.
 //   ofdm*_kernel one workgroup per (OFDM symbol, frame): bins scattered (chain) or gathered
 //                (pilotgen block) into a register/LDS IFFT, normalisation, output gain, guard
 //                interval, P1.  Reference: lib/framemapperfint_cc_impl.cc:1999-2142,
 //                lib/pilotgenp1insert_cc_impl.cc:2784-2907.
-// No MFMA: these are bitwise / permutation / complex-FFT paths.
+// MFMA only for the BCH product: the rest are bitwise / permutation / complex-FFT paths.
 #include "t2_kernels.h"
 
 #include <atomic>
@@ -95,21 +97,23 @@ static hipError_t lds_limit(const void *fn, int bytes) {
 
 // ============================================================================ FEC kernels
 // Block API (bbheaderbch / ldpc blocks): fec_kernel<MODE>, one fused pass per FEC block (BBFRAME,
-// BCH on one wave, LDPC).  The fused chain runs three passes instead (launch_fec FEC_TS_TO_TEMPU):
+// BCH on one wave, LDPC).  The chain runs three launches instead (launch_fec FEC_TS_TO_BBFRAME, then
+// launch_ldpc_map):
 //   fec_bb_kernel    TS -> BBFRAME bytes in the codeword row (header, CRC-8 sync replacement,
 //                    in-band field, BB scrambling)
 //   bch_gemm_kernel  BCH parity of every block as a GF(2) matrix product on the matrix cores
 //                    (blocks x message bits x parity bits, fp4 0/1 operands, exact f32 sums, parity
 //                    = sum & 1), K split into slices (each XCD's L2 holds its slices' share of
-//                    the generator table) whose partial parities are XORed by the LDPC pass
-//   fec_ldpc_kernel  info bytes + XOR of the partials -> LDPC parity -> interleaver-input codeword
+//                    the generator table) whose partial parities are XORed by the LDPC stage
+//   ldpc_map_kernel  info bytes + XOR of the partials -> LDPC parity -> interleaver-input codeword in
+//                    LDS -> the map (column twist, demux, cell + time interleaver), see below
 constexpr int FEC_THREADS = 256;
 constexpr int FEC_FRAME_BYTES = 6752;   // >= max nbch/8 (6750)
 constexpr int FEC_MAX_ENT = 648;        // max LDPC table entries (3/5 normal: 233280 / 360)
 constexpr int FEC_DW = 13;              // LDS words per LDPC info group (fused kernel): d_g || d_g[0..56)
-constexpr int FEC_DW_PASS = 16;         // chain LDPC pass: d_g || d_g[0..152), four windows without wrap
+constexpr int FEC_DW_PASS = 16;         // chain LDPC stage: d_g || d_g[0..152), four windows without wrap
 constexpr int FEC_WG_PER_CU = 7;        // fused kernel: resident workgroups per CU (72-VGPR budget)
-constexpr int FEC_PASS_WG_PER_CU = 8;   // chain BB / LDPC passes (64-VGPR budget, 32 waves per CU)
+constexpr int FEC_PASS_WG_PER_CU = 8;   // chain BB pass, LDPC + map kernel (64-VGPR budget, 32 waves per CU)
 constexpr int FEC_BCH_JB = 2;           // nibble-table lookups in flight per lane in the BCH combine
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW_PASS * 150 + 12 * 30); // max over codes of 64 ngroups + 48 q
 constexpr int BCH_ROWS = 128;           // bch_gemm_kernel: FEC blocks per workgroup (4 waves x 32)
@@ -655,7 +659,7 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
 }
 
 // chain pass 1: the BBFRAME of every launch block into its codeword row (bytes [0, L); bytes past L
-// of the last 16-byte unit are don't-care: the BCH pass multiplies them by zero rows, the LDPC pass
+// of the last 16-byte unit are don't-care: the BCH pass multiplies them by zero rows, the LDPC stage
 // rewrites them)
 __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -823,99 +827,49 @@ __global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(Fe
 // the info groups laid out, LDPC, then the interleaver-input words from word L / 4 on (the BB pass
 // wrote the words before): BCH parity | LDPC parity (parity interleaved: byte m = byte m % 45 of row
 // m / 45, or natural order a + q c for QPSK without parity interleaving)
-__global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_ldpc_kernel(FecDev d, FecIO io) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x;
-  const int L = d.kbch >> 3, NB = d.nbch >> 3, PB = d.P >> 3;
-  const FecCarve cv = fec_carve(CARVE_LDPC, d.kbch, d.nbch, d.q);
-  uint8_t *frame = smem + cv.frame;
-  uint32_t *ents = (uint32_t *)(smem + cv.ents);
-  uint32_t *D = (uint32_t *)(smem + cv.phase);
-  uint32_t *Wv = (uint32_t *)(smem + cv.w);
-  uint16_t *rowp = (uint16_t *)(smem + cv.rowp);
-  for (int i = tid; i < d.nent; i += FEC_THREADS) ents[i] = d.ldpc_ent[i];
-  for (int i = tid; i <= d.q; i += FEC_THREADS) rowp[i] = d.ldpc_rowptr[i];
-  __syncthreads();
-  const int ngroups = d.nbch / 360, q = d.q, cwb = d.nldpc >> 3, nqi = (L + 15) >> 4;
-  // each block's info units and BCH partials are requested one block ahead (in flight during the
-  // previous block)
-  uint4 pre[FEC_PRE];
-  uint32_t ppar = 0;
-  auto prefetch = [&](int b) {
-    const uint4 *rowq = (const uint4 *)(io.out + (int64_t)b * io.cw_stride);
-#pragma unroll
-    for (int k = 0; k < FEC_PRE; k++)
-      pre[k] = tid + FEC_THREADS * k < nqi ? rowq[tid + FEC_THREADS * k] : make_uint4(0u, 0u, 0u, 0u);
-    if (tid < (PB + 3) >> 2) ppar = io.bch_part[(int64_t)b * BCH_PART_WORDS + tid];
+// word i (bytes 4 i .. 4 i + 3, little-endian as stored) of block's interleaver-input codeword: the
+// BBFRAME and BCH parity bytes from frame, then the LDPC parity rows cur (fec_ldpc), parity-interleaved
+// (byte m = byte m mod 45 of row m / 45) by byte-aligning two row words where the code has the parity
+// interleaver, bit by bit otherwise; zero past the codeword
+__device__ __forceinline__ uint32_t ldpc_out_word(const FecDev &d, const uint8_t *frame, const uint32_t *cur, int i) {
+  const int NB = d.nbch >> 3, cwb = d.nldpc >> 3, q = d.q;
+  auto parity_byte = [&](int m) -> uint32_t {
+    if (d.parity_il) {
+      const int a = m / 45, k = m - 45 * a;
+      return (cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu;
+    }
+    uint32_t v = 0;
+    for (int e = 0; e < 8; e++) {
+      const int j = 8 * m + e, a = j % q, c = j / q;
+      v |= ((cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1u) << (7 - e);
+    }
+    return v;
   };
-  if ((int)blockIdx.x < io.nblocks) prefetch(blockIdx.x);
-  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
-    uint8_t *row = io.out + (int64_t)bi * io.cw_stride;
-#pragma unroll
-    for (int k = 0; k < FEC_PRE; k++)
-      if (tid + FEC_THREADS * k < nqi) ((uint4 *)frame)[tid + FEC_THREADS * k] = pre[k];
-    const uint32_t par = ppar;
-    if (bi + (int)gridDim.x < io.nblocks) prefetch(bi + gridDim.x);
-    __syncthreads();   // the 16-byte units past L land before the parity bytes overwrite them
-    if (tid < (PB + 3) >> 2)
-      for (int k = 0; k < 4 && 4 * tid + k < PB; k++) frame[L + 4 * tid + k] = (uint8_t)(par >> (8 * k));
-    __syncthreads();
-    // four words of a group per item, one 16-byte LDS write (the frame words shared by neighbouring
-    // output words are read once)
-    for (int it = tid; it < ngroups * (FEC_DW_PASS / 4); it += FEC_THREADS) {
-      const int g = it >> 2, k0 = 4 * (it & 3);
-      *(uint4 *)(D + g * FEC_DW_PASS + k0) = make_uint4(ldpc_group_val(frame, g, k0), ldpc_group_val(frame, g, k0 + 1),
-                                                        ldpc_group_val(frame, g, k0 + 2), ldpc_group_val(frame, g, k0 + 3));
+  if (4 * i + 4 <= NB) return ((const uint32_t *)frame)[i];
+  uint32_t v = 0;
+  if (d.parity_il && 4 * i >= NB && 4 * i + 4 <= cwb) {
+    // four parity bytes m .. m + 3 = bytes k .. k + 3 of row a (m = 45 a + k; rows of 12 big-endian
+    // words): one byte align of two row words, or bytewise where they cross into row a + 1
+    int a = (4 * i - NB) / 45, k = 4 * i - NB - 45 * a;
+    if (k <= 41) {
+      const uint32_t w0 = cur[a * 12 + (k >> 2)], w1 = cur[a * 12 + (k >> 2) + 1];
+      return __builtin_bswap32((k & 3) ? __builtin_amdgcn_alignbyte(w0, w1, (uint32_t)(4 - (k & 3))) : w0);
     }
-    __syncthreads();
-    const uint32_t *cur = fec_ldpc<FEC_DW_PASS>(d, D, ngroups, ents, rowp, Wv, tid);
-    auto parity_byte = [&](int m) -> uint32_t {
-      if (d.parity_il) {
-        const int a = m / 45, k = m - 45 * a;
-        return (cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu;
+    for (int e = 0; e < 4; e++) {
+      v |= ((cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu) << (8 * e);
+      if (++k == 45) {
+        k = 0;
+        a++;
       }
-      uint32_t v = 0;
-      for (int e = 0; e < 8; e++) {
-        const int j = 8 * m + e, a = j % q, c = j / q;
-        v |= ((cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1u) << (7 - e);
-      }
-      return v;
-    };
-    const uint32_t *framew = (const uint32_t *)frame;
-    uint32_t *dstw = (uint32_t *)row;
-    for (int i = (L >> 2) + tid; i < (cwb + 3) >> 2; i += FEC_THREADS) {
-      uint32_t v;
-      if (4 * i + 4 <= NB) {
-        v = framew[i];
-      } else if (d.parity_il && 4 * i >= NB && 4 * i + 4 <= cwb) {
-        // four parity bytes m .. m + 3 = bytes k .. k + 3 of row a (m = 45 a + k; rows of 12 big-endian
-        // words): one byte align of two row words, or bytewise where they cross into row a + 1
-        int a = (4 * i - NB) / 45, k = 4 * i - NB - 45 * a;
-        if (k <= 41) {
-          const uint32_t w0 = cur[a * 12 + (k >> 2)], w1 = cur[a * 12 + (k >> 2) + 1];
-          v = __builtin_bswap32((k & 3) ? __builtin_amdgcn_alignbyte(w0, w1, (uint32_t)(4 - (k & 3))) : w0);
-        } else {
-          v = 0;
-          for (int e = 0; e < 4; e++) {
-            v |= ((cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu) << (8 * e);
-            if (++k == 45) {
-              k = 0;
-              a++;
-            }
-          }
-        }
-      } else {
-        v = 0;
-        for (int e = 0; e < 4; e++) {
-          const int bidx = 4 * i + e;
-          const uint32_t by = bidx < NB ? (uint32_t)frame[bidx] : bidx < cwb ? parity_byte(bidx - NB) : 0u;
-          v |= by << (8 * e);
-        }
-      }
-      dstw[i] = v;
     }
-    __syncthreads();   // frame / phase regions are reused by the next block
+    return v;
   }
+  for (int e = 0; e < 4; e++) {
+    const int bidx = 4 * i + e;
+    const uint32_t by = bidx < NB ? (uint32_t)frame[bidx] : bidx < cwb ? parity_byte(bidx - NB) : 0u;
+    v |= by << (8 * e);
+  }
+  return v;
 }
 
 // resident FEC workgroups for a persistent launch: per_cu per CU of the current device
@@ -960,20 +914,21 @@ static hipError_t bch_launch(const FecDev &d, const FecIO &io, hipStream_t s) {
   return hipGetLastError();
 }
 
+static bool fec_chain_args_ok(const FecDev &d, const FecIO &io) {
+  return d.bch_mfma && io.bch_part && io.bch_part_blocks >= io.nblocks && d.bch_nt >= 4 && d.bch_nt <= 6 &&
+         d.bch_nq >= 1 && d.bch_nq * 32 <= io.cw_stride;
+}
+
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
   if (!fec_plan_fits(d)) return hipErrorInvalidValue;
   hipError_t e;
   switch (mode) {
-    case FEC_TS_TO_TEMPU:   // the fused chain: BB pass, BCH on the matrix cores, LDPC pass
-      if (!d.bch_mfma || !io.bch_part || io.bch_part_blocks < io.nblocks || d.bch_nt < 4 || d.bch_nt > 6 ||
-          d.bch_nq < 1 || d.bch_nq * 32 > io.cw_stride)
-        return hipErrorInvalidValue;
+    case FEC_TS_TO_BBFRAME:   // the chain: BB pass, BCH on the matrix cores (the LDPC follows in launch_ldpc_map)
+      if (!fec_chain_args_ok(d, io)) return hipErrorInvalidValue;
       e = fec_launch_persistent((const void *)fec_bb_kernel, CARVE_BB, FEC_PASS_WG_PER_CU, d, io, s);
       if (e == hipSuccess)
         e = d.bch_nt == 6 ? bch_launch<6>(d, io, s) : d.bch_nt == 5 ? bch_launch<5>(d, io, s) : bch_launch<4>(d, io, s);
-      if (e == hipSuccess)
-        e = fec_launch_persistent((const void *)fec_ldpc_kernel, CARVE_LDPC, FEC_PASS_WG_PER_CU, d, io, s);
       return e;
     case FEC_TS_TO_BITS:
       return fec_launch_persistent((const void *)fec_kernel<FEC_TS_TO_BITS>, CARVE_FUSED, FEC_WG_PER_CU, d, io, s);
@@ -984,33 +939,11 @@ hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s)
 
 // ============================================================================ map kernel
 constexpr int MAP_THREADS = 256;
-constexpr int MAP_MB = 8;                    // cells per thread per batched load round (CI and TI loops)
-constexpr int MAP_CQ = 8;                    // quads per thread staged in registers by the compact layout
 constexpr int MAP_LDS_MAX = 160 * 1024 - 256;
-// LDS: [LUT 2 KB][cell indices, cs bytes][codeword bytes | cell-interleaved index pairs (2 cs)]
-// (<= 99 KB for QPSK normal, 26 KB for 256-QAM normal)
+// block API LDS: [LUT 2 KB][cell indices, cs bytes][codeword as big-endian words + a slack word]
+// (<= 43 KB for QPSK normal); the chain's ldpc_map_kernel carves its own
 __host__ __device__ inline int map_idx_bytes(int cs) { return (cs + 15) & ~15; }
-// Compact chain layout (cs <= 4 MAP_CQ MAP_THREADS, e.g. 256-QAM normal): [codeword | cell indices]
-// in 2 idx-bytes, the cell-interleaved pairs (2 cs bytes) overlaying both once the indices are in
-// registers (map_store_pairs alias mode); no LUT (the chain's constellation lookup is in the OFDM
-// kernel).  16 KB instead of 26 KB for 256-QAM normal: 8 workgroups per CU instead of 6.
-// Register staging per thread: MAP_CQ quads (cs <= 8192: eight workgroups per CU at 64 VGPRs) or
-// 2 MAP_CQ (cs <= 16384, e.g. 64-QAM and 16-QAM normal: a second kernel instantiation with a
-// 96-VGPR budget, five to seven workgroups per CU by LDS); 0: not compact
-__host__ __device__ inline int map_compact_cq(int cs, int cw_bytes, int apply_ci) {
-  if (!apply_ci || cw_bytes > map_idx_bytes(cs)) return 0;
-  const int nq = (cs + 3) / 4;
-  return nq <= MAP_CQ * MAP_THREADS ? MAP_CQ : nq <= 2 * MAP_CQ * MAP_THREADS ? 2 * MAP_CQ : 0;
-}
-__host__ __device__ inline bool map_compact(int cs, int cw_bytes, int apply_ci) {
-  return map_compact_cq(cs, cw_bytes, apply_ci) != 0;
-}
-__host__ __device__ inline int map_smem(int cs, int cw_bytes, int apply_ci) {
-  if (map_compact(cs, cw_bytes, apply_ci)) return 2 * map_idx_bytes(cs);
-  int region = cw_bytes;
-  if (apply_ci && 2 * cs > region) region = 2 * cs;
-  return 2048 + map_idx_bytes(cs) + ((region + 15) & ~15);
-}
+__host__ __device__ inline int map_smem(int cs, int nldpc) { return 2048 + map_idx_bytes(cs) + ((nldpc / 8 + 4 + 15) & ~15); }
 
 // XCD-aware block order: the hardware deals consecutive workgroups round-robin over the 8 XCDs;
 // give each XCD a contiguous run of logical blocks so neighbours share its L2.
@@ -1112,129 +1045,53 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
 // chain: cell interleaver (framemapper:1973-1998) of block blk's (index, previous index) pairs through
 // LDS (stage, 2 cs bytes), then the time-interleaver (framemapper:1999-2028) store into the frame
 // data region out_pairs + (blk / F) frame_stride
-template <int NT, int CQ>
-__device__ void map_store_pairs(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
-                                uint16_t *stage, int blk, int tid, bool alias) {
-  const int cs = d.cs;
-  const int r = blk % d.F;
-  const int shift = d.ci_shift[r];
+// Chain: the cell interleaver and the time-interleaver store in one pass, in stored-slot order, in
+// aligned quads of four frame slots (MapDev::slot_quad): wave w takes 64-quad chunks c = c0 + u NT / 64
+// + w and lane l quad 64 c + l, whose four slots list the cell-interleaver INPUT index j of the cell
+// landing there (the chain composes j = CI^-1(t) for the block's shift); the slot gets (idx[j],
+// idx[j - 1]) (the rotated constellation's Q delay; the QAM lookup is fused into the OFDM kernel's bin
+// scatter).  One 8-byte store per full quad (2-byte stores for a quad at a run's edge, whose other
+// slots belong to neighbouring blocks), so a store instruction writes 512 B of one or two contiguous
+// runs; no stage array and no cell-interleaver pass through LDS
+template <int NT>
+__device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
+                                int blk, int tid) {
+  const int cs = d.cs, r = blk % d.F;
   uint16_t *dst = out_pairs + (int64_t)(blk / d.F) * frame_stride;   // frame data region
-  int r0 = r, nb = 1;
-  if (d.ti_on) {
-    const int ns = d.ti_nsmall * d.ti_small;
-    if (r < ns) { r0 = r - r % d.ti_small; nb = d.ti_small; }
-    else { r0 = r - (r - ns) % d.ti_big; nb = d.ti_big; }
-  }
-  const int rows = cs / 5, cols = 5 * nb;
-  const int64_t base = (int64_t)r0 * cs + 5 * (r - r0);
-  const int nq = (cs + 3) >> 2;
-  const uint32_t *idxw = (const uint32_t *)idx;
-  // Chain: the cell interleaver and the time-interleaver store in one pass, in stored-slot order, in
-  // aligned quads of four frame slots (MapDev::slot_quad): wave w takes 64-quad chunks c = c0 + u NT / 64
-  // + w and lane l quad 64 c + l, whose four slots list the cell-interleaver INPUT index j of the cell
-  // landing there (the chain composes j = CI^-1(t) for the block's shift); the slot gets (idx[j],
-  // idx[j - 1]) (the rotated constellation's Q delay; the QAM lookup is fused into the OFDM kernel's bin
-  // scatter).  One 8-byte store per full quad (2-byte stores for a quad at a run's edge, whose other
-  // slots belong to neighbouring blocks), so a store instruction writes 512 B of one or two contiguous
-  // runs; no stage array and no cell-interleaver pass through LDS
-  if (d.slot_quad) {
-    const uint2 *qs = d.slot_quad + (int64_t)r * d.slot_stride;
-    const uint16_t *qo = d.slot_qoff + (int64_t)r * d.slot_stride;
-    const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
-    const int nqd = d.slot_nq[r];
-    constexpr int MQ = 9, NW = NT / 64;
-    const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
-    auto pair_of = [&](uint32_t j) -> uint32_t {
-      const uint32_t lo = idx[j], hi = d.rotation ? (uint32_t)idx[j == 0 ? (uint32_t)cs - 1u : j - 1u] : lo;
-      return lo | (hi << 8);
-    };
-    for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
-      uint2 e[MQ];
-      uint32_t qa[MQ];
+  const uint2 *qs = d.slot_quad + (int64_t)r * d.slot_stride;
+  const uint16_t *qo = d.slot_qoff + (int64_t)r * d.slot_stride;
+  const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
+  const int nqd = d.slot_nq[r];
+  constexpr int MQ = 9, NW = NT / 64;
+  const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
+  auto pair_of = [&](uint32_t j) -> uint32_t {
+    const uint32_t lo = idx[j], hi = d.rotation ? (uint32_t)idx[j == 0 ? (uint32_t)cs - 1u : j - 1u] : lo;
+    return lo | (hi << 8);
+  };
+  for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
+    uint2 e[MQ];
+    uint32_t qa[MQ];
 #pragma unroll
-      for (int u = 0; u < MQ; u++) {
-        const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
-        e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
-        qa[u] = (uint32_t)qb[c] + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
-      }
+    for (int u = 0; u < MQ; u++) {
+      const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
+      e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
+      qa[u] = (uint32_t)qb[c] + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
+    }
 #pragma unroll
-      for (int u = 0; u < MQ; u++) {
-        const int c = c0 + u * NW + wv;
-        if (c < nch && 64 * c + lane < nqd) {
-          const uint32_t j0 = e[u].x & 0xFFFFu, j1 = e[u].x >> 16, j2 = e[u].y & 0xFFFFu, j3 = e[u].y >> 16;
-          if (j0 != 0xFFFFu && j1 != 0xFFFFu && j2 != 0xFFFFu && j3 != 0xFFFFu) {
-            st_off((uint2 *)dst, qa[u] * 8u, make_uint2(pair_of(j0) | (pair_of(j1) << 16), pair_of(j2) | (pair_of(j3) << 16)));
-          } else {
-            if (j0 != 0xFFFFu) st_off(dst, (4u * qa[u] + 0u) * 2u, (uint16_t)pair_of(j0));
-            if (j1 != 0xFFFFu) st_off(dst, (4u * qa[u] + 1u) * 2u, (uint16_t)pair_of(j1));
-            if (j2 != 0xFFFFu) st_off(dst, (4u * qa[u] + 2u) * 2u, (uint16_t)pair_of(j2));
-            if (j3 != 0xFFFFu) st_off(dst, (4u * qa[u] + 3u) * 2u, (uint16_t)pair_of(j3));
-          }
+    for (int u = 0; u < MQ; u++) {
+      const int c = c0 + u * NW + wv;
+      if (c < nch && 64 * c + lane < nqd) {
+        const uint32_t j0 = e[u].x & 0xFFFFu, j1 = e[u].x >> 16, j2 = e[u].y & 0xFFFFu, j3 = e[u].y >> 16;
+        if (j0 != 0xFFFFu && j1 != 0xFFFFu && j2 != 0xFFFFu && j3 != 0xFFFFu) {
+          st_off((uint2 *)dst, qa[u] * 8u, make_uint2(pair_of(j0) | (pair_of(j1) << 16), pair_of(j2) | (pair_of(j3) << 16)));
+        } else {
+          if (j0 != 0xFFFFu) st_off(dst, (4u * qa[u] + 0u) * 2u, (uint16_t)pair_of(j0));
+          if (j1 != 0xFFFFu) st_off(dst, (4u * qa[u] + 1u) * 2u, (uint16_t)pair_of(j1));
+          if (j2 != 0xFFFFu) st_off(dst, (4u * qa[u] + 2u) * 2u, (uint16_t)pair_of(j2));
+          if (j3 != 0xFFFFu) st_off(dst, (4u * qa[u] + 3u) * 2u, (uint16_t)pair_of(j3));
         }
       }
     }
-    return;
-  }
-
-  // cell interleave the (index, previous index) pairs through LDS: 2 bytes per cell, four
-  // consecutive cells per thread (one 8-byte load of their permutation entries and one 4-byte LDS
-  // read of their indices, plus the previous cell's byte for the rotation)
-  auto ci_quad = [&](int q, uint2 pq, uint32_t w, uint32_t prev) {
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const int j = 4 * q + e;
-      const uint32_t lo = (w >> (8 * e)) & 0xFFu, hi = d.rotation ? prev : lo;
-      prev = lo;
-      if (j < cs) {
-        int tt = (int)(int16_t)(((e < 2 ? pq.x : pq.y) >> (16 * (e & 1))) & 0xFFFFu) + shift;
-        tt = tt >= cs ? tt - cs : tt;
-        stage[tt] = (uint16_t)(lo | (hi << 8));
-      }
-    }
-  };
-  if (alias) {
-    // compact LDS (map_compact): stage overlays the cell indices, so every thread first takes its
-    // (at most CQ) quads of indices and permutation entries into registers, then all write
-    uint2 pq[CQ];
-    uint32_t wv[CQ], pv[CQ];
-#pragma unroll
-    for (int k = 0; k < CQ; k++) {
-      const int q = min(tid + k * NT, nq - 1);
-      pq[k] = ld_off((const uint2 *)d.ci_perm, (uint32_t)q * 8u);
-      wv[k] = idxw[q];
-      pv[k] = idx[q == 0 ? cs - 1 : 4 * q - 1];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < CQ; k++) {
-      const int q = tid + k * NT;
-      if (q < nq) ci_quad(q, pq[k], wv[k], pv[k]);
-    }
-  } else {
-    constexpr int MQ = MAP_MB / 2;
-    for (int q0 = tid; q0 < nq; q0 += MQ * NT) {
-      uint2 pq[MQ];
-#pragma unroll
-      for (int u = 0; u < MQ; u++) pq[u] = ld_off((const uint2 *)d.ci_perm, (uint32_t)min(q0 + u * NT, nq - 1) * 8u);
-#pragma unroll
-      for (int u = 0; u < MQ; u++) {
-        const int q = q0 + u * NT;
-        if (q < nq) ci_quad(q, pq[u], idxw[q], idx[q == 0 ? cs - 1 : 4 * q - 1]);
-      }
-    }
-  }
-  __syncthreads();
-  // time-interleaver store of the index pairs: row-major over (row, e), 5 consecutive cells (10 B)
-  // per TI row
-  const int64_t fbase = (d.ti_on ? base : (int64_t)r * cs) + d.data_off;   // + PLP_START
-  for (int j = tid; j < cs; j += NT) {
-    int tt = j, o = j;
-    if (d.ti_on) {
-      const int row = j / 5, e = j - 5 * row;
-      tt = e * rows + row;
-      o = row * cols + e;
-    }
-    st_off(dst, ((uint32_t)fbase + (uint32_t)o) * 2u, stage[tt]);
   }
 }
 
@@ -1387,12 +1244,73 @@ hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s) {
   return hipGetLastError();
 }
 
-// The chain's launches prepend ceil8(L1 frames) workgroups that generate the frames' L1-post cells
-// (they run beside the map workgroups instead of as a launch of their own; a multiple of 8 keeps
-// each map workgroup's XCD)
-static_assert(MAP_THREADS == L1_NT, "the map launch's L1-post workgroups run l1post_frame at L1_NT threads");
-template <int CQ>
-__global__ __launch_bounds__(MAP_THREADS, CQ <= MAP_CQ ? 8 : 5) void map_kernel(MapDev d, MapIO io, L1Dev l1d, L1IO l1io) {
+// Block API (interleavermod): one 256-thread workgroup per FEC block: the natural-order codeword bits
+// (one byte per bit; the parity interleaver applied on the read) packed into LDS as big-endian words,
+// column twist + demux (map_cells), QAM lookup and the rotated constellation's cyclic Q delay
+// (interleavermod:529-598, 626-677) into complex64 cells
+__global__ __launch_bounds__(MAP_THREADS) void map_kernel(MapDev d, MapIO io) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, blk = blockIdx.x;
+  float2 *lut = (float2 *)smem;
+  uint8_t *idx = smem + 2048;
+  uint32_t *cww = (uint32_t *)(smem + 2048 + map_idx_bytes(d.cs));
+  const int cs = d.cs, nl = d.nldpc, nlw = (nl + 31) >> 5, nbch = d.nbch, q = d.q;
+  for (int i = tid; i < 256; i += MAP_THREADS) lut[i] = d.lut[i];
+  // bit i of the interleaver input is bit 31 - (i & 31) of word i >> 5
+  const uint8_t *src = io.in + (int64_t)blk * nl;
+  for (int k = tid; k <= nlw; k += MAP_THREADS) {
+    uint32_t v = 0;
+    for (int e = 0; e < 32; e++) {
+      int i = 32 * k + e, sidx = i;
+      if (i >= nl) break;
+      if (d.parity_il && i >= nbch) {        // tempu[nbch + 360 t + s] = in[nbch + q s + t]
+        int r = i - nbch, t = r / 360, s = r - 360 * t;
+        sidx = nbch + q * s + t;
+      }
+      v |= (uint32_t)(src[sidx] & 1) << (31 - e);
+    }
+    cww[k] = v;
+  }
+  __syncthreads();
+  map_cells<MAP_THREADS>(d, cww, idx, tid);
+  __syncthreads();
+  float2 *dst = io.out + (int64_t)blk * cs;
+  for (int j = tid; j < cs; j += MAP_THREADS) {
+    float2 v = lut[idx[j]];
+    if (d.rotation) v.y = lut[idx[j == 0 ? cs - 1 : j - 1]].y;
+    dst[j] = v;
+  }
+}
+
+hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s) {
+  if (io.nblocks <= 0) return hipSuccess;
+  const int smem = map_smem(d.cs, d.nldpc);
+  if (smem > MAP_LDS_MAX) return hipErrorInvalidValue;
+  hipError_t e = lds_limit((const void *)map_kernel, MAP_LDS_MAX);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(map_kernel, dim3(io.nblocks), dim3(MAP_THREADS), smem, s, d, io);
+  return hipGetLastError();
+}
+
+// ============================================================================ chain: LDPC + map
+// One 256-thread workgroup per FEC block of the launch (after ceil8(L1 frames) workgroups that generate
+// the frames' L1-post cells): the block's BBFRAME and the XOR of its BCH partial
+// parities (the BB and matrix-core passes' output) -> LDPC parity (fec_ldpc) -> the interleaver-input
+// codeword, built in LDS -> column twist + demux (map_cells) -> cell interleaver + time-interleaver
+// store of the index pairs (map_store_quads).  The codeword never goes through HBM (the LDPC stage's
+// 8 KB store and the map stage's 8 KB load per normal block); fio.keep_cw (test hook) stores it anyway.
+// LDS: the LDPC carve (CARVE_LDPC), then, once the codeword words sit in registers, [codeword as
+// big-endian words + a slack word | cell indices] overlaying it.
+constexpr int LM_WORDS = 8;   // codeword words per thread: (nldpc / 8 + 3) / 4 <= LM_WORDS FEC_THREADS
+__host__ __device__ inline int lm_cww_words(int nldpc) { return ((nldpc + 31) / 32 + 1 + 3) & ~3; }
+__host__ __device__ inline int lm_smem(const FecDev &fd, int cs) {
+  const int a = fec_carve(CARVE_LDPC, fd.kbch, fd.nbch, fd.q).total, b = 4 * lm_cww_words(fd.nldpc) + map_idx_bytes(cs);
+  return a > b ? a : b;
+}
+static_assert(FEC_THREADS == MAP_THREADS, "ldpc_map_kernel runs the map phases at FEC_THREADS");
+
+__global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void ldpc_map_kernel(FecDev fd, FecIO fio, MapDev md,
+                                                                                   MapIO mio, L1Dev l1d, L1IO l1io) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int nl1 = (l1io.nframes + 7) & ~7;
@@ -1401,71 +1319,79 @@ __global__ __launch_bounds__(MAP_THREADS, CQ <= MAP_CQ ? 8 : 5) void map_kernel(
     return;
   }
   const int blk = xcd_major((int)blockIdx.x - nl1, (int)gridDim.x - nl1);
-  const bool compact = map_compact_cq(d.cs, d.nldpc / 8 + 4, io.apply_ci) == CQ;
-  float2 *lut = (float2 *)smem;
-  uint8_t *idx = compact ? smem + map_idx_bytes(d.cs) : smem + 2048;
-  uint8_t *cw = compact ? smem : smem + 2048 + map_idx_bytes(d.cs);
-  // chain: (idx[j], idx[j-1]) at cell-interleaved position t
-  uint16_t *stage = compact ? (uint16_t *)smem : (uint16_t *)cw;
-  const int cs = d.cs, nl = d.nldpc;
-  if (!io.apply_ci)
-    for (int i = tid; i < 256; i += MAP_THREADS) lut[i] = d.lut[i];
-  // ---- interleaver input bits (tempu) into LDS as big-endian words: bit i of the codeword is
-  //      bit 31 - (i & 31) of word i >> 5
-  uint32_t *cww = (uint32_t *)cw;
-  const int nlw = (nl + 31) >> 5;
-  if (io.packed_in) {
-    const uint32_t *src = (const uint32_t *)(io.in + (int64_t)blk * io.cw_stride);
-    if ((((uintptr_t)src) & 15) == 0 && 4 * ((nlw + 3) & ~3) <= (int)io.cw_stride &&
-        4 * ((nlw + 3) & ~3) <= (compact ? map_idx_bytes(cs) : 1 << 30)) {
-      // 16-byte loads (the codeword stride and the LDS area hold the rounded-up word count)
-      for (int k = tid; k < (nlw + 3) >> 2; k += MAP_THREADS) {
-        const uint4 w = ((const uint4 *)src)[k];
-        *(uint4 *)(cww + 4 * k) = make_uint4(__builtin_bswap32(w.x), __builtin_bswap32(w.y), __builtin_bswap32(w.z),
-                                             __builtin_bswap32(w.w));
-      }
-    } else {
-      for (int i = tid; i < nlw; i += MAP_THREADS) cww[i] = __builtin_bswap32(src[i]);
-    }
-  } else {
-    const uint8_t *src = io.in + (int64_t)blk * nl;
-    const int nbch = d.nbch, q = d.q;
-    for (int k = tid; k < nlw; k += MAP_THREADS) {
-      uint32_t v = 0;
-      for (int e = 0; e < 32; e++) {
-        int i = 32 * k + e, sidx = i;
-        if (i >= nl) break;
-        if (d.parity_il && i >= nbch) {        // tempu[nbch + 360 t + s] = in[nbch + q s + t]
-          int r = i - nbch, t = r / 360, s = r - 360 * t;
-          sidx = nbch + q * s + t;
-        }
-        v |= (uint32_t)(src[sidx] & 1) << (31 - e);
-      }
-      cww[k] = v;
-    }
+  const int L = fd.kbch >> 3, PB = fd.P >> 3;
+  const FecCarve cv = fec_carve(CARVE_LDPC, fd.kbch, fd.nbch, fd.q);
+  uint8_t *frame = smem + cv.frame;
+  uint32_t *ents = (uint32_t *)(smem + cv.ents);
+  uint32_t *D = (uint32_t *)(smem + cv.phase);
+  uint32_t *Wv = (uint32_t *)(smem + cv.w);
+  uint16_t *rowp = (uint16_t *)(smem + cv.rowp);
+  const int ngroups = fd.nbch / 360, q = fd.q, nw = ((fd.nldpc >> 3) + 3) >> 2, nqi = (L + 15) >> 4;
+  uint8_t *row = fio.out + (int64_t)blk * fio.cw_stride;
+  {
+    // the BBFRAME's 16-byte units and the BCH partial parity requested before the tables are staged
+    const uint4 *rowq = (const uint4 *)row;
+    uint4 u[FEC_PRE];
+#pragma unroll
+    for (int k = 0; k < FEC_PRE; k++)
+      u[k] = tid + FEC_THREADS * k < nqi ? rowq[tid + FEC_THREADS * k] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t par = tid < (PB + 3) >> 2 ? fio.bch_part[(int64_t)blk * BCH_PART_WORDS + tid] : 0u;
+    for (int i = tid; i < fd.nent; i += FEC_THREADS) ents[i] = fd.ldpc_ent[i];
+    for (int i = tid; i <= q; i += FEC_THREADS) rowp[i] = fd.ldpc_rowptr[i];
+#pragma unroll
+    for (int k = 0; k < FEC_PRE; k++)
+      if (tid + FEC_THREADS * k < nqi) ((uint4 *)frame)[tid + FEC_THREADS * k] = u[k];
+    __syncthreads();   // the 16-byte units past L land before the parity bytes overwrite them
+    if (tid < (PB + 3) >> 2)
+      for (int k = 0; k < 4 && 4 * tid + k < PB; k++) frame[L + 4 * tid + k] = (uint8_t)(par >> (8 * k));
+    __syncthreads();
+  }
+  // four words of a group per item, one 16-byte LDS write
+  for (int it = tid; it < ngroups * (FEC_DW_PASS / 4); it += FEC_THREADS) {
+    const int g = it >> 2, k0 = 4 * (it & 3);
+    *(uint4 *)(D + g * FEC_DW_PASS + k0) = make_uint4(ldpc_group_val(frame, g, k0), ldpc_group_val(frame, g, k0 + 1),
+                                                      ldpc_group_val(frame, g, k0 + 2), ldpc_group_val(frame, g, k0 + 3));
   }
   __syncthreads();
-  map_cells<MAP_THREADS>(d, cww, idx, tid);
-  __syncthreads();
-  // ---- constellation + cyclic Q delay; chain: cell interleaver (framemapper:1973-1998) on the
-  //      cell indices in LDS, then QAM fused into the time-interleaver (framemapper:1999-2028)
-  //      store pattern: FEC block r of its TI block fills columns 5(r-r0)..+4 of a rows x 5nb
-  //      array read row by row, so cells land in the frame data region in transmission order.
-  if (!io.apply_ci) {
-    float2 *dst = io.out + (int64_t)blk * cs;
-    for (int j = tid; j < cs; j += MAP_THREADS) {
-      float2 v = lut[idx[j]];
-      if (d.rotation) v.y = lut[idx[j == 0 ? cs - 1 : j - 1]].y;
-      dst[j] = v;
-    }
-    return;
+  const uint32_t *cur = fec_ldpc<FEC_DW_PASS>(fd, D, ngroups, ents, rowp, Wv, tid);
+  uint32_t w[LM_WORDS];
+#pragma unroll
+  for (int k = 0; k < LM_WORDS; k++) {
+    const int i = tid + FEC_THREADS * k;
+    w[k] = i < nw ? ldpc_out_word(fd, frame, cur, i) : 0u;
   }
-  map_store_pairs<MAP_THREADS, CQ>(d, io.out_pairs, io.frame_stride, idx, stage, blk, tid, compact);
+  if (fio.keep_cw) {   // test hook: the row as the three-pass FEC stored it (words below L / 4 hold the BBFRAME)
+    uint32_t *dstw = (uint32_t *)row;
+#pragma unroll
+    for (int k = 0; k < LM_WORDS; k++) {
+      const int i = tid + FEC_THREADS * k;
+      if (i >= (L >> 2) && i < nw) dstw[i] = w[k];
+    }
+  }
+  __syncthreads();   // the LDPC areas are dead: the codeword and the cell indices overlay them
+  uint32_t *cww = (uint32_t *)smem;
+  const int ncw = lm_cww_words(fd.nldpc);
+#pragma unroll
+  for (int k = 0; k < LM_WORDS; k++) {
+    const int i = tid + FEC_THREADS * k;
+    if (i < ncw) cww[i] = __builtin_bswap32(w[k]);
+  }
+  uint8_t *idx = smem + 4 * ncw;
+  __syncthreads();
+  map_cells<FEC_THREADS>(md, cww, idx, tid);
+  __syncthreads();
+  map_store_quads<FEC_THREADS>(md, mio.out_pairs, mio.frame_stride, idx, blk, tid);
 }
 
-hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1Dev *l1d, const L1IO *l1io) {
-  if (io.nblocks <= 0) return hipSuccess;
-  int smem = map_smem(d.cs, d.nldpc / 8 + 4, io.apply_ci);
+hipError_t launch_ldpc_map(const FecDev &fd, const FecIO &fio, const MapDev &md, const MapIO &mio, hipStream_t s,
+                           const L1Dev *l1d, const L1IO *l1io) {
+  if (fio.nblocks <= 0) return hipSuccess;
+  // the chain's layout only: packed BBFRAME rows from FEC_TS_TO_BBFRAME, the quad-table TI store
+  if (!fec_plan_fits(fd) || !fec_chain_args_ok(fd, fio) || mio.nblocks != fio.nblocks || !md.slot_quad ||
+      !mio.out_pairs || md.nldpc != fd.nldpc || md.cs * md.F <= 0 ||
+      lm_cww_words(fd.nldpc) > LM_WORDS * FEC_THREADS || (fd.nldpc / 8 + 3) / 4 > LM_WORDS * FEC_THREADS)
+    return hipErrorInvalidValue;
+  int smem = lm_smem(fd, md.cs);
   L1Dev ld{};
   L1IO li{};
   if (l1d && l1io && l1io->nframes > 0) {
@@ -1475,15 +1401,10 @@ hipError_t launch_map(const MapDev &d, const MapIO &io, hipStream_t s, const L1D
     smem = smem > L1_LDS_WORDS * 4 ? smem : L1_LDS_WORDS * 4;
   }
   if (smem > MAP_LDS_MAX) return hipErrorInvalidValue;
-  const bool big = map_compact_cq(d.cs, d.nldpc / 8 + 4, io.apply_ci) == 2 * MAP_CQ;
-  const void *fn = big ? (const void *)map_kernel<2 * MAP_CQ> : (const void *)map_kernel<MAP_CQ>;
-  hipError_t e = lds_limit(fn, MAP_LDS_MAX);
+  hipError_t e = lds_limit((const void *)ldpc_map_kernel, MAP_LDS_MAX);
   if (e != hipSuccess) return e;
   const int nl1 = (li.nframes + 7) & ~7;
-  if (big)
-    hipLaunchKernelGGL(map_kernel<2 * MAP_CQ>, dim3(io.nblocks + nl1), dim3(MAP_THREADS), smem, s, d, io, ld, li);
-  else
-    hipLaunchKernelGGL(map_kernel<MAP_CQ>, dim3(io.nblocks + nl1), dim3(MAP_THREADS), smem, s, d, io, ld, li);
+  hipLaunchKernelGGL(ldpc_map_kernel, dim3(fio.nblocks + nl1), dim3(FEC_THREADS), smem, s, fd, fio, md, mio, ld, li);
   return hipGetLastError();
 }
 

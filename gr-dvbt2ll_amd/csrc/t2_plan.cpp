@@ -1266,7 +1266,7 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
   cl.sym_n0 = cl.sym_n;
   // Slot order within each symbol (32K: within each stored half): FEC-block-major, and within a
   // block's run the order bank_balance picks for the OFDM scatter's write groups.  The OFDM kernels
-  // stream any order (inv follows it); block-major runs give the map kernel, which stores one FEC
+  // stream any order (inv follows it); block-major runs give the LDPC + map kernel, which stores one FEC
   // block per workgroup, one contiguous run per symbol (half) instead of 10-byte TI-row runs
   // scattered over the symbol (its per-cell deltas take any order inside a run).
   // (blocks numbered PLP-major: PLP k's block r is g0_k + r, so each symbol half's slots are PLP-major too)

@@ -180,7 +180,7 @@ inline int ofdm_stored_index(int N, int k) {
 }
 std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t> &bin_map);
 
-// Fused chain layout.  The map kernel writes each FEC block's cells through the cell and time
+// Fused chain layout.  The LDPC + map kernel writes each FEC block's cells through the cell and time
 // interleavers into the frame data region, which is then in transmission (TI output) order:
 // symbol j's data cells are the contiguous slots [sym_d0[j], sym_d0[j] + sym_n[j]).  The OFDM
 // kernel streams that range with unit-stride loads and scatters each cell into its IFFT bin in

@@ -96,7 +96,7 @@ EXPORTS += ["dvbt2ll_bbheaderbch_set_isi"]
 EXPORTS += ["dvbt2ll_framemapper_mplp_" + f for f in ("create", "output_multiple", "stream_items", "forecast",
                                                       "general_work", "destroy")]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create_mplp", "num_plps", "get_plp_info", "run_plps",
-                                           "debug_plp_codewords")]
+                                           "debug_plp_codewords", "debug_keep_codewords")]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_streams", "run_host", "set_output", "set_slots", "set_graph", "set_timing",
                                            "get_timing", "debug_codewords", "debug_cell_pairs", "debug_cells",
                                            "synchronize", "sync_errors",
@@ -136,6 +136,7 @@ def lib():
     L.dvbt2ll_chain_set_timing.argtypes = [vp, ci]
     L.dvbt2ll_chain_get_timing.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64), ci]
     L.dvbt2ll_chain_debug_codewords.argtypes = [vp, vp, i64]
+    L.dvbt2ll_chain_debug_keep_codewords.argtypes = [vp, ci]
     L.dvbt2ll_chain_debug_cell_pairs.argtypes = [vp, vp, i64]
     L.dvbt2ll_chain_debug_cells.argtypes = [vp, vp, i64]
     L.dvbt2ll_chain_synchronize.argtypes = [vp]

@@ -125,6 +125,11 @@ class Chain:
         check(lib().dvbt2ll_chain_get_timing(self._h, ms, n, 4), "timing")
         return list(ms), list(n)
 
+    def debug_keep_codewords(self, enable=True):
+        """test hook: the following runs also store the packed codewords (the LDPC + map kernel keeps
+        them on chip otherwise); debug_codewords / debug_plp_codewords need it"""
+        check(lib().dvbt2ll_chain_debug_keep_codewords(self._h, int(bool(enable))), "keep codewords")
+
     def debug_codewords(self, nblocks):
         stride = self.info["cw_stride_bytes"]
         out = np.zeros(nblocks * stride, np.uint8)

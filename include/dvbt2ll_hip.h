@@ -219,10 +219,14 @@ int dvbt2ll_chain_set_output(dvbt2ll_chain *h, float gain, int format);
 int dvbt2ll_chain_set_timing(dvbt2ll_chain *h, int enable);
 int dvbt2ll_chain_get_timing(dvbt2ll_chain *h, double *ms, int64_t *launches, int nstages);
 /* test hooks (host outputs, synchronous), last run's frame 0: packed codewords (tempu
- * order); the frame data region in the slot order the OFDM kernel reads, as stored
+ * order; only when that run stored them, see dvbt2ll_chain_debug_keep_codewords, else
+ * DVBT2LL_EINVAL); the frame data region in the slot order the OFDM kernel reads, as stored
  * (uint16 constellation index pairs: lo = the cell's index, hi = the index whose Q part
  * it carries, i.e. the previous cell's under rotation) and as complex64 cells */
 int dvbt2ll_chain_debug_codewords(dvbt2ll_chain *h, void *out, int64_t bytes);
+/* test hook: enable != 0 -> the following runs also store every FEC block's packed codeword in the
+ * chain's codeword buffer (the LDPC + map kernel otherwise keeps it on chip) */
+int dvbt2ll_chain_debug_keep_codewords(dvbt2ll_chain *h, int enable);
 int dvbt2ll_chain_debug_cell_pairs(dvbt2ll_chain *h, void *out, int64_t cells);
 int dvbt2ll_chain_debug_cells(dvbt2ll_chain *h, void *out, int64_t cells);
 /* TS sync bytes != 0x47 consumed by all run calls so far (bbheaderbch_bb_impl.cc:675, 703);

@@ -328,6 +328,7 @@ def test_chain_codewords_all_codes(gpu, framesize, rate, mode, inband, const):
                                 fecblocks=3)
     nb = 2 * cfg.fecblocks
     ch = dvbt2ll.Chain(cfg, max_frames=2)
+    ch.debug_keep_codewords()
     ch.run(0, 2)
     got = ch.debug_codewords(nb)
     ts, base = ts_for_frames(cfg, 0, 2)

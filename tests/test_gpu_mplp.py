@@ -79,6 +79,7 @@ def test_mplp_chain_codewords(gpu, name):
     m = MPLP_CONFIGS[name]
     _, _, bits, cws = oracle_frames(m, 1)
     ch = dvbt2ll.Chain(m, max_frames=1)
+    ch.debug_keep_codewords()
     _run(ch, m, 0, 1)
     for k, p in enumerate(m.plps):
         got = ch.debug_plp_codewords(k, p.fecblocks)

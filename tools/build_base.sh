@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build exp_build/libbase.so from the committed (HEAD, or $1) kernel / C-API / planner sources, for a
-# same-box A/B of uncommitted product changes (tools/experiments/gpu_ab.sh TAG base)
+# same-box A/B of uncommitted product changes (tools/experiments/gpu_ab.sh TAG base); EXTRA_OBJ: objects
+# linked in as well (e.g. a stub of a symbol the current Python binding expects)
 set -e
 REV=${1:-HEAD}
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -16,6 +17,6 @@ $H -x c++ -std=c++17 -O3 -fPIC -ffp-contract=off -D__HIP_PLATFORM_AMD__ -c t2_pl
 $H -std=c++17 -O3 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -c t2_kernels.hip -o k.o
 $H -std=c++17 -O3 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -c t2_capi.cpp -o c.o
 mkdir -p $R/exp_build
-$H --offload-arch=gfx950 -shared -fPIC -o $R/exp_build/libbase.so p.o k.o c.o
+$H --offload-arch=gfx950 -shared -fPIC -o $R/exp_build/libbase.so p.o k.o c.o $EXTRA_OBJ
 rm -rf $T
 echo built $R/exp_build/libbase.so from $REV
