@@ -1064,9 +1064,14 @@ __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t fr
   const int nqd = d.slot_nq[r];
   constexpr int MQ = 9, NW = NT / 64;
   const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
+  // (idx[j], idx[j - 1] under rotation, else idx[j]) without branches, so a quad's eight byte reads
+  // go out together (a branch per read had put an LDS wait after each); j = 0xFFFF (another block's
+  // slot) reads idx[0], and the caller drops it
+  const uint32_t rmask = d.rotation ? 0xFFFFFFFFu : 0u;
   auto pair_of = [&](uint32_t j) -> uint32_t {
-    const uint32_t lo = idx[j], hi = d.rotation ? (uint32_t)idx[j == 0 ? (uint32_t)cs - 1u : j - 1u] : lo;
-    return lo | (hi << 8);
+    j = j == 0xFFFFu ? 0u : j;
+    const uint32_t jm = j == 0 ? (uint32_t)cs - 1u : j - 1u, jh = (jm & rmask) | (j & ~rmask);
+    return (uint32_t)idx[j] | ((uint32_t)idx[jh] << 8);
   };
   for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
     uint2 e[MQ];
@@ -1080,15 +1085,16 @@ __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t fr
 #pragma unroll
     for (int u = 0; u < MQ; u++) {
       const int c = c0 + u * NW + wv;
+      const uint32_t j0 = e[u].x & 0xFFFFu, j1 = e[u].x >> 16, j2 = e[u].y & 0xFFFFu, j3 = e[u].y >> 16;
+      const uint32_t p0 = pair_of(j0), p1 = pair_of(j1), p2 = pair_of(j2), p3 = pair_of(j3);
       if (c < nch && 64 * c + lane < nqd) {
-        const uint32_t j0 = e[u].x & 0xFFFFu, j1 = e[u].x >> 16, j2 = e[u].y & 0xFFFFu, j3 = e[u].y >> 16;
         if (j0 != 0xFFFFu && j1 != 0xFFFFu && j2 != 0xFFFFu && j3 != 0xFFFFu) {
-          st_off((uint2 *)dst, qa[u] * 8u, make_uint2(pair_of(j0) | (pair_of(j1) << 16), pair_of(j2) | (pair_of(j3) << 16)));
+          st_off((uint2 *)dst, qa[u] * 8u, make_uint2(p0 | (p1 << 16), p2 | (p3 << 16)));
         } else {
-          if (j0 != 0xFFFFu) st_off(dst, (4u * qa[u] + 0u) * 2u, (uint16_t)pair_of(j0));
-          if (j1 != 0xFFFFu) st_off(dst, (4u * qa[u] + 1u) * 2u, (uint16_t)pair_of(j1));
-          if (j2 != 0xFFFFu) st_off(dst, (4u * qa[u] + 2u) * 2u, (uint16_t)pair_of(j2));
-          if (j3 != 0xFFFFu) st_off(dst, (4u * qa[u] + 3u) * 2u, (uint16_t)pair_of(j3));
+          if (j0 != 0xFFFFu) st_off(dst, (4u * qa[u] + 0u) * 2u, (uint16_t)p0);
+          if (j1 != 0xFFFFu) st_off(dst, (4u * qa[u] + 1u) * 2u, (uint16_t)p1);
+          if (j2 != 0xFFFFu) st_off(dst, (4u * qa[u] + 2u) * 2u, (uint16_t)p2);
+          if (j3 != 0xFFFFu) st_off(dst, (4u * qa[u] + 3u) * 2u, (uint16_t)p3);
         }
       }
     }
