@@ -130,7 +130,7 @@ struct FecTables {
 
 struct MapTables {
   MapPlan plan;
-  DevBuf lut;
+  DevBuf lut, colbuf;
   MapDev dev{};
   int init(int framesize, int rate, int constellation, int rotation, const FecPlan &fec) {
     if (build_map(framesize, rate, constellation, rotation, plan)) return DVBT2LL_EINVAL;
@@ -142,11 +142,10 @@ struct MapTables {
     dev.parity_il = fec.parity_interleave ? 1 : 0;
     dev.F = 1;
     // column feeding bit b of the demuxed row word (b = W - 1 - mux[e]): its start bit and twist
-    for (int b = 0; b < 16; b++) dev.colstart[b] = -1, dev.coltw[b] = 0;
-    for (int e = 0; e < plan.W && plan.mode != 0; e++) {
-      dev.colstart[plan.W - 1 - plan.mux[e]] = e * plan.R;
-      dev.coltw[plan.W - 1 - plan.mux[e]] = plan.twist[e];
-    }
+    std::vector<int2> col(16, int2{-1, 0});
+    for (int e = 0; e < plan.W && plan.mode != 0; e++) col[plan.W - 1 - plan.mux[e]] = int2{e * plan.R, plan.twist[e]};
+    if ((r = upload(colbuf, col))) return r;
+    dev.col = colbuf.as<int2>();
     return 0;
   }
 };

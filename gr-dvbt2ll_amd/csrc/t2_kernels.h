@@ -98,9 +98,10 @@ struct MapDev {
   const uint16_t *slot_qoff;
   const int32_t *slot_qbase, *slot_nq;
   int slot_stride;
-  // per demuxed bit b of the row word: the column e feeding it (W-1-mux[e] = b) as its first codeword
-  // bit e*R (-1: none) and its twist (int32: uniform scalar loads, no byte loads in the column loop)
-  int colstart[16], coltw[16];
+  // per demuxed bit b of the row word: the column e feeding it (W-1-mux[e] = b) as (its first codeword
+  // bit e*R (-1: none), its twist); int32 in device memory: uniform scalar loads where map_cells uses
+  // them, no byte loads in the column loop
+  const int2 *col;         // 16
 };
 struct MapIO {
   const uint8_t *in;   // block API: unpacked natural-order codeword bits, nldpc per block

@@ -1024,9 +1024,10 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
       uint64_t xa[2] = {0, 0}, xb[2] = {0, 0};
 #pragma unroll
       for (int b = 0; b < 16; b++) {
-        const int c0 = d.colstart[b];
+        const int2 cw = d.col[b];   // scalar loads at the point of use (kernel-argument arrays stayed live
+        const int c0 = cw.x;         // in SGPRs through the whole kernel and spilled)
         if (c0 < 0) continue;
-        int off = j0 - d.coltw[b];
+        int off = j0 - cw.y;
         off += off < 0 ? R : 0;
         uint32_t win = window(c0 + off);
         if (off + 16 > R) {                      // the column wraps inside these 16 rows

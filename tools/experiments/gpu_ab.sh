@@ -11,7 +11,7 @@ cp $LIB exp_build/libproduct.so
 [ -x exp_build/mfma_probe ] && [ -z "$NOPROBE" ] && { timeout -k 10 60 exp_build/mfma_probe "$O/mfma_probe.bin" > "$O/mfma_probe.log" 2>&1 || { cat "$O/mfma_probe.log"; exit 1; }; cat "$O/mfma_probe.log"; }
 for round in 1 2; do
   for v in product "$@"; do
-    cp exp_build/lib$v.so $LIB
+    cp exp_build/lib$v.so $LIB || { echo "missing exp_build/lib$v.so"; cp exp_build/libproduct.so $LIB; exit 1; }
     timeout -k 10 240 python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --no-blocks --no-mplp --steps 20 --warmup 3 $BENCH_ARGS \
       > "$O/b_${v}_$round.json" 2> "$O/b_${v}_$round.err" || { tail -5 "$O/b_${v}_$round.err"; cp exp_build/libproduct.so $LIB; exit 1; }
     python -c "import json,sys; d=json.load(open('$O/b_${v}_$round.json')); print('$v', {k: round(s['avg_launch_ms'],4) for k,s in d['stages'].items()}, round(d['value']))"

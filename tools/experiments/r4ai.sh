@@ -1,0 +1,6 @@
+set -o pipefail
+# the map's column table in device memory instead of kernel-argument arrays (no SGPR spills in
+# ldpc_map_kernel), product against HEAD (base); 192 frames per step
+h=$(timeout -k 10 120 python tools/experiments/lib_iq_hash.py exp_build/libbase.so) && echo "base $h" &&
+echo "product $(timeout -k 10 120 python tools/experiments/lib_iq_hash.py gr-dvbt2ll_amd/dvbt2ll/libdvbt2ll_hip.so)" &&
+BENCH_ARGS="--frames 192" NOPROBE=1 timeout -k 10 900 tools/experiments/gpu_ab.sh r4ai base
