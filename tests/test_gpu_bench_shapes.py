@@ -7,6 +7,8 @@
   against a float64 IFFT).  Large launches are where 32-bit offsets and per-frame strides would fail.
 * cfg5 as BASELINE words it: an 8-stream batch through dvbt2ll_chain_run_streams, direct and hipGraph
   launches; every stream equals a single-stream handle on its own TS and stream 7 equals the oracle.
+* the largest cfg3 launch a handle admits (1359 frames: the 32-bit index-pair offsets), and the refusal
+  of one frame more.
 * misaligned TS input: a device TS pointer 188 bytes into the buffer (188 % 16 = 12) and
   a run_streams stride that is odd; the FEC kernel's byte-load staging path must give the aligned
   call's IQ bit for bit."""
@@ -65,6 +67,34 @@ def test_cfg3_bench_launch_192_frames_two_slots(gpu):
     ref, pg = _oracle_frames(cfg, [191])
     iq_check.check_frame_exact(got[191], ref[191], cfg.pg_args(), pg.guard, pg.normalization, "cfg3 frame 191 of 192")
     iq_check.check_frame(got[191], ref[191], pg.vlength, pg.guard, pg.normalization, pg.p1(), "cfg3 frame 191 of 192")
+
+
+def test_cfg3_max_batch_32bit_offsets(gpu):
+    """the largest launch a cfg3 handle accepts: the OFDM kernel addresses the index-pair buffer with
+    32-bit byte offsets, so create admits max_frames <= (2^32 - 1) // (2 * pair_stride) (pair_stride =
+    the frame's data cells rounded up to 8, t2_capi chain_build) and refuses one more.  One launch of all
+    of them (1359 frames, 2.8 G IQ samples, above the bench's 768) gives the IQ of a one-frame handle for
+    the first, a middle and the last frame, bit for bit"""
+    import torch
+    cfg = CONFIGS["cfg3"]
+    one = dvbt2ll.Chain(cfg, max_frames=1)
+    stride = (one.info["stream_items"] + 7) // 8 * 8
+    B = ((1 << 32) - 1) // (2 * stride)
+    assert B > 768
+    with pytest.raises(dvbt2ll.DVBT2Error):
+        dvbt2ll.Chain(cfg, max_frames=B + 1)
+    ch = dvbt2ll.Chain(cfg, max_frames=B)
+    per = ch.iq_per_frame
+    ts, base = ts_for_frames(cfg, 0, B)
+    ts_d = torch.from_numpy(ts).cuda()
+    del ts
+    iq = torch.empty((B * per, 2), dtype=torch.float32, device="cuda")
+    ch.run_device(ts_d.data_ptr(), base, ts_d.numel(), 0, B, iq.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for k in (0, B // 2, B - 1):
+        got = iq[k * per:(k + 1) * per].cpu().numpy().view(np.complex64).reshape(-1)
+        want = one.run(k, 1)
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg="frame %d of %d" % (k, B))
 
 
 @pytest.mark.parametrize("graph", [False, True], ids=["direct", "graph"])
