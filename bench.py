@@ -48,9 +48,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=768,
-                    help="T2 frames per step per GPU (768 cfg3 frames = 176 s of airtime; 192 / 384 / 768 frames per "
-                         "step measured 205.7 / 210.5 / 212.5 G IQ samples/s: the kernels' grid tails amortise)")
+    ap.add_argument("--frames", type=int, default=1280,
+                    help="T2 frames per step per GPU (1280 cfg3 frames = 293 s of airtime; at most 1359 per cfg3 "
+                         "launch; 640 / 768 / 896 / 1152 / 1280 / 1344 frames per step measured 218.6 / 223.6 / "
+                         "223.6 / 227.6 / 227.4 / 227.7 G IQ samples/s on one box, profiles/r4_frames_sweep.txt)")
     ap.add_argument("--config", default="cfg3")
     ap.add_argument("--no-pmc", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -730,22 +731,27 @@ def main():
         # chain's one exchange step (point-to-point sends to the root over RCCL / xGMI)
         from dvbt2ll.distributed import gather_frames
         kg = min(args.steps, 3)
+        # at most 512 frames per rank gathered per step: the root's output tensor (N x G frames of
+        # complex64 IQ, 68 GB at N = 8) must fit beside the chain's two slots in 288 GB of HBM
+        G = min(B, 512)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for s_ in range(kg):
             step(s_, serial=True)
             torch.cuda.current_stream().wait_stream(streams[0])
-            gather_frames(iq[s_ % S], world * B, per)
+            gather_frames(iq[s_ % S][:G * per], world * G, per)
         torch.cuda.synchronize()
         dist.barrier()
         eg = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
         dist.all_reduce(eg, op=dist.ReduceOp.MAX)
         eg = float(eg.item())
         gathered = {"value": world * B * kg * per / eg / 1e6, "unit": "Msamples/s", "steps": kg,
-                    "ms_per_step": eg / kg * 1e3, "bytes_to_root_per_step": (world - 1) * B * per * 8,
-                    "note": "secondary: every step's complex64 IQ gathered in frame order on rank 0 "
-                            "(dvbt2ll.distributed.gather_frames, grouped send/recv); not `value`"}
+                    "ms_per_step": eg / kg * 1e3, "gathered_frames_per_rank": G,
+                    "bytes_to_root_per_step": (world - 1) * G * per * 8,
+                    "note": "secondary: every step (all B frames encoded) followed by the ordered gather of its "
+                            "first G frames' complex64 IQ per rank to rank 0 (dvbt2ll.distributed.gather_frames, "
+                            "grouped send/recv); not `value`"}
     frames_total = B * args.steps * world
     samples_total = frames_total * per
     fec_total = frames_total * info["fec_blocks_per_frame"]

@@ -73,14 +73,14 @@ def test_cfg3_max_batch_32bit_offsets(gpu):
     """the largest launch a cfg3 handle accepts: the OFDM kernel addresses the index-pair buffer with
     32-bit byte offsets, so create admits max_frames <= (2^32 - 1) // (2 * pair_stride) (pair_stride =
     the frame's data cells rounded up to 8, t2_capi chain_build) and refuses one more.  One launch of all
-    of them (1359 frames, 2.8 G IQ samples, above the bench's 768) gives the IQ of a one-frame handle for
+    of them (1359 frames, 2.8 G IQ samples, above the bench's 1280) gives the IQ of a one-frame handle for
     the first, a middle and the last frame, bit for bit"""
     import torch
     cfg = CONFIGS["cfg3"]
     one = dvbt2ll.Chain(cfg, max_frames=1)
     stride = (one.info["stream_items"] + 7) // 8 * 8
     B = ((1 << 32) - 1) // (2 * stride)
-    assert B > 768
+    assert B >= 1280
     with pytest.raises(dvbt2ll.DVBT2Error):
         dvbt2ll.Chain(cfg, max_frames=B + 1)
     ch = dvbt2ll.Chain(cfg, max_frames=B)
