@@ -63,8 +63,9 @@ def parse():
     ap.add_argument("--shard", choices=("frames", "streams"), default="frames",
                     help="frames: one TS stream, disjoint frame ranges per rank; streams: an independent "
                          "TS stream per rank (seed = rank + 1), SURVEY 8(e)'s two modes")
-    ap.add_argument("--slots", type=int, default=2,
-                    help="chain buffer slots = HIP streams the steps alternate over (1 = serial)")
+    ap.add_argument("--slots", type=int, default=3,
+                    help="chain buffer slots = HIP streams the steps alternate over (1 = serial); at 1280 frames "
+                         "per step 3 slots measured +1.5 %% over 2 (profiles/r4_frames_sweep.txt)")
     ap.add_argument("--streams", type=int, default=1,
                     help="independent TS streams per launch (seeds 1..S, dvbt2ll_chain_run_streams; BASELINE cfg4 "
                          "x4 / cfg5 x8): each step encodes --frames // S frames of every stream")
