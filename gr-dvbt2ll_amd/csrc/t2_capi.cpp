@@ -966,10 +966,17 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     // payload bytes per frame: in-band type B takes 13 bytes of the first BBFRAME of each frame
     // (bbheader:327-355, fec_block == 0)
     pl->ts_per_frame = (int64_t)pp.F * pl->pay - (q.inband ? 13 : 0);
-    h->qbase_host.push_back(nq);
-    const int entries = 1 << pl->map.plan.mod;
-    for (int i = 0; i < entries; i++) qall.push_back(pl->map.plan.lut[i]);
-    nq += entries;
+    // PLPs with the same constellation and rotation share one table (their LUTs are equal)
+    int qb0 = -1;
+    for (int k2 = 0; k2 < k && qb0 < 0; k2++)
+      if (plps[k2].constellation == q.constellation && plps[k2].rotation == q.rotation) qb0 = h->qbase_host[k2];
+    if (qb0 < 0) {
+      qb0 = nq;
+      const int entries = 1 << pl->map.plan.mod;
+      for (int i = 0; i < entries; i++) qall.push_back(pl->map.plan.lut[i]);
+      nq += entries;
+    }
+    h->qbase_host.push_back(qb0);
     h->plps.push_back(std::move(pl));
   }
   // stored bins -> padded LDS slots within their half (the kernel writes them as they are)

@@ -1884,7 +1884,7 @@ struct TableStage {
 #pragma unroll
       for (int k = 0; k < QK; k++) {
         const int i = tid + k * NT;
-        if (i < 256) q[k] = d.qam[i];
+        if (i < 256 && i < d.nq) q[k] = d.qam[i];   // a multi-PLP table may hold fewer than 256 entries
       }
     }
   }
@@ -1900,7 +1900,7 @@ struct TableStage {
 #pragma unroll
       for (int k = 0; k < QK; k++) {
         const int i = tid + k * NT;
-        if (i < 256) {
+        if (i < 256 && i < nq) {
           qre[i] = q[k].x;
           qim[i] = q[k].y;
         }

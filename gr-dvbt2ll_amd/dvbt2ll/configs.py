@@ -255,6 +255,11 @@ def _mplp_configs():
             _plp(c4, fecblocks=12),
             _plp(c4, framesize=E.FECFRAME_SHORT, rate=E.C2_3, constellation=E.MOD_256QAM, rotation=E.ROTATION_ON,
                  fecblocks=10, tiblocks=1)]),
+        # two 8K PLPs without a 256-QAM one: the OFDM kernel's constellation tables hold 4 + 16 = 20 entries
+        # (fewer than the 256 a single-PLP table holds)
+        "mplp2_8k_lowq": mplp_from(c4, "mplp2-8k-16qam1/2+qpsk3/4", [
+            _plp(c4, fecblocks=12, tiblocks=2),
+            _plp(c4, rate=E.C3_4, constellation=E.MOD_QPSK, fecblocks=5, tiblocks=1)]),
         # three 32K PLPs (one in-band type B, v1.3.1 L1 scrambling)
         "mplp3_32k": mplp_from(CONFIGS["cfg5"], "mplp3-32k-v131", [
             _plp(CONFIGS["cfg5"], fecblocks=60, tiblocks=1),

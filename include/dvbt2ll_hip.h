@@ -243,6 +243,9 @@ void dvbt2ll_chain_destroy(dvbt2ll_chain *h);
  * L1-post carries the PLP loops.  The reference carries exactly one PLP
  * (lib/framemapperfint_cc_impl.cc:152-250: num_plp = 1; L1-post serialised at :1553-1691): nplp = 1
  * is its frame bit for bit, nplp > 1 is not pinned by it (PARITY UNPINNED).
+ * The OFDM kernels hold one constellation table per distinct (constellation, rotation) pair of the
+ * frame's PLPs (PLPs that agree share it): at most 2 x (4 + 16 + 64 + 256) = 680 entries, so every
+ * combination of up to DVBT2LL_MAX_PLP PLPs fits the kernels' 1024-entry table area.
  * ------------------------------------------------------------------------- */
 #define DVBT2LL_MAX_PLP 8
 typedef struct {
