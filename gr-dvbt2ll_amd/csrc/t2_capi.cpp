@@ -462,14 +462,22 @@ extern "C" void dvbt2ll_framemapperfint_destroy(dvbt2ll_framemapperfint *h) { de
 
 // ============================================================================ framemapper, multi-PLP
 static bool mplp_to_plan(const dvbt2ll_mplp_params &m, FmParams &fm, std::vector<PlpParams> &plps,
-                         std::vector<int> &tsrate);
+                         std::vector<int> &tsrate, int *nss);
 
 struct dvbt2ll_framemapper_mplp {
   DeviceCtx ctx;
   FramePlan plan;
   L1Tables l1;
-  DevBuf map, aux, din, dout;   // din: one frame of every PLP's cells, PLP 0 first
+  // din: the current interleaving frame of every PLP (PLP k's S_if cells at in_off); map: one gather row per
+  // frame phase (frame mod unit)
+  DevBuf map, aux, din, dout;
   int t2_frame_num = 0;
+  int64_t frame = 0;            // T2 frames produced (the phase of the next one is frame mod unit)
+  // cells port k consumes at the T2 frame frame + i: a whole interleaving frame on its first T2 frame
+  int need(int k, int64_t i) const {
+    const PlpPlan &pl = plan.plp[k];
+    return (frame + i) % pl.P == 0 ? pl.S_if : 0;
+  }
 };
 extern "C" int dvbt2ll_framemapper_mplp_create(const dvbt2ll_mplp_params *p, int device, dvbt2ll_framemapper_mplp **out) {
   if (!p || !out) return DVBT2LL_EINVAL;
@@ -477,10 +485,11 @@ extern "C" int dvbt2ll_framemapper_mplp_create(const dvbt2ll_mplp_params *p, int
   FmParams fm;
   std::vector<PlpParams> plps;
   std::vector<int> tsrate;
-  if (!mplp_to_plan(*p, fm, plps, tsrate)) return DVBT2LL_EINVAL;
+  int nss = 1;
+  if (!mplp_to_plan(*p, fm, plps, tsrate, &nss)) return DVBT2LL_EINVAL;
   std::unique_ptr<dvbt2ll_framemapper_mplp> h(new (std::nothrow) dvbt2ll_framemapper_mplp());
   if (!h) return DVBT2LL_ENOMEM;
-  if (build_frame_mplp(fm, plps, h->plan)) return DVBT2LL_EINVAL;
+  if (build_frame_mplp(fm, plps, h->plan, false, nss)) return DVBT2LL_EINVAL;
   int r = h->ctx.init(device);
   if (r) return r;
   if ((r = upload(h->map, h->plan.gather_in)) || (r = upload(h->aux, h->plan.aux)) || (r = h->l1.init(h->plan)))
@@ -494,7 +503,13 @@ extern "C" int dvbt2ll_framemapper_mplp_stream_items(const dvbt2ll_framemapper_m
 }
 extern "C" int dvbt2ll_framemapper_mplp_forecast(const dvbt2ll_framemapper_mplp *h, int nout, int *nin) {
   if (!h || !nin) return DVBT2LL_EINVAL;
-  for (int k = 0; k < h->plan.nplp; k++) nin[k] = h->plan.plp[k].S * (nout / h->plan.M);   // framemapper:1942-1946
+  // framemapper:1942-1946: the cells of nout / M frames; a TIME_IL_TYPE 1 PLP's interleaving frame is
+  // consumed whole on its first T2 frame
+  for (int k = 0; k < h->plan.nplp; k++) {
+    int64_t n = 0;
+    for (int i = 0; i < nout / h->plan.M; i++) n += h->need(k, i);
+    nin[k] = (int)std::min<int64_t>(n, INT32_MAX);
+  }
   return DVBT2LL_OK;
 }
 extern "C" int dvbt2ll_framemapper_mplp_general_work(dvbt2ll_framemapper_mplp *h, int nout, const int *nin,
@@ -505,13 +520,15 @@ extern "C" int dvbt2ll_framemapper_mplp_general_work(dvbt2ll_framemapper_mplp *h
     for (int k = 0; k < f.nplp; k++) consumed[k] = 0;
   if (nout < f.M) return 0;
   for (int k = 0; k < f.nplp; k++)
-    if (!in[k] || nin[k] < f.plp[k].S) return DVBT2LL_ESHORT;
-  // one T2 frame per call, one frame of every port (framemapper:2147)
+    if (h->need(k, 0) && (!in[k] || nin[k] < h->need(k, 0))) return DVBT2LL_ESHORT;
+  // one T2 frame per call, one frame of every port (framemapper:2147); a port whose PLP starts an interleaving
+  // frame here delivers all of it
   HIP_TRY(hipSetDevice(h->ctx.device));
-  if (h->din.ensure((size_t)f.S * 8) || h->dout.ensure((size_t)f.M * 8)) return DVBT2LL_ENOMEM;
+  if (h->din.ensure((size_t)f.S_in * 8) || h->dout.ensure((size_t)f.M * 8)) return DVBT2LL_ENOMEM;
   for (int k = 0; k < f.nplp; k++)
-    HIP_TRY(hipMemcpyAsync(h->din.as<float2>() + f.plp[k].start, in[k], (size_t)f.plp[k].S * 8, hipMemcpyHostToDevice,
-                           h->ctx.stream));
+    if (h->need(k, 0))
+      HIP_TRY(hipMemcpyAsync(h->din.as<float2>() + f.plp[k].in_off, in[k], (size_t)f.plp[k].S_if * 8,
+                             hipMemcpyHostToDevice, h->ctx.stream));
   L1IO lio{};
   lio.out = h->aux.as<float2>() + AUX_L1PRE + 1840;
   lio.first_frame = h->t2_frame_num;
@@ -520,15 +537,16 @@ extern "C" int dvbt2ll_framemapper_mplp_general_work(dvbt2ll_framemapper_mplp *h
   GatherIO io{};
   io.in = h->din.as<float2>();
   io.out = h->dout.as<float2>();
-  io.map = h->map.as<int32_t>();
+  io.map = h->map.as<int32_t>() + (size_t)(h->frame % f.unit) * f.M;
   io.aux = h->aux.as<float2>();
   io.M = f.M;
   HIP_TRY(launch_gather(io, h->ctx.stream));
   HIP_TRY(hipMemcpyAsync(out, h->dout.p, (size_t)f.M * 8, hipMemcpyDeviceToHost, h->ctx.stream));
   HIP_TRY(hipStreamSynchronize(h->ctx.stream));
-  h->t2_frame_num = (h->t2_frame_num + 1) % f.t2frames;
   if (consumed)
-    for (int k = 0; k < f.nplp; k++) consumed[k] = f.plp[k].S;
+    for (int k = 0; k < f.nplp; k++) consumed[k] = h->need(k, 0);
+  h->t2_frame_num = (h->t2_frame_num + 1) % f.t2frames;
+  h->frame++;
   return f.M;
 }
 extern "C" void dvbt2ll_framemapper_mplp_destroy(dvbt2ll_framemapper_mplp *h) { delete h; }
@@ -644,8 +662,11 @@ struct ChainPlp {
   DevBuf part, pbase, poff, pnq;
   DevBuf cw[DVBT2LL_CHAIN_MAX_SLOTS], bpart[DVBT2LL_CHAIN_MAX_SLOTS];
   int64_t cw_stride = 0;
-  int64_t ts_per_frame = 0;   // payload bytes per frame (NM positions; HEM: before sync-byte removal)
+  int64_t ts_per_frame = 0;   // payload bytes per interleaving frame (NM positions; HEM: before sync-byte removal)
   int pay = 0, F = 0, inputmode = 0, inband = 0;
+  int P = 1;                  // T2 frames per interleaving frame (TIME_IL_TYPE 1: P_I); F, ts_per_frame are per
+                              // interleaving frame
+  int64_t blocks(int64_t frames) const { return (frames + P - 1) / P * F; }   // FEC blocks of `frames` T2 frames
 };
 
 // instantiated hipGraphs of the chain's kernels (per PLP: FEC BB pass, BCH matrix-core pass; per PLP: LDPC +
@@ -861,8 +882,8 @@ struct dvbt2ll_chain {
   }
   int alloc_slot(int k) {
     for (auto &pl : plps)
-      if (pl->cw[k].ensure((size_t)pl->F * max_frames * pl->cw_stride) ||
-          pl->bpart[k].ensure((size_t)pl->F * max_frames * BCH_PART_WORDS * sizeof(uint32_t)))
+      if (pl->cw[k].ensure((size_t)pl->blocks(max_frames) * pl->cw_stride) ||
+          pl->bpart[k].ensure((size_t)pl->blocks(max_frames) * BCH_PART_WORDS * sizeof(uint32_t)))
         return DVBT2LL_ENOMEM;
     if (pairs[k].ensure((size_t)pair_stride * max_frames * 2) || l1buf[k].ensure((size_t)l1_stride * max_frames * 8))
       return DVBT2LL_ENOMEM;
@@ -881,13 +902,16 @@ struct dvbt2ll_chain {
 
 // the common construction of single- and multi-PLP chains: fm's common fields with plps' PLPs
 static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<PlpParams> &plps,
-                       const std::vector<int> &tsrate, int misogroup, int equalization, int bandwidth, int device) {
+                       const std::vector<int> &tsrate, int misogroup, int equalization, int bandwidth, int device,
+                       int nss = 1) {
   PgParams pg{fm.carriermode, fm.fftsize, fm.pilotpattern, fm.guardinterval, fm.numdatasyms, fm.paprmode, fm.version,
               fm.preamble, misogroup, equalization, bandwidth, fft_points(fm.fftsize)};
-  if (build_frame_mplp(fm, plps, h->frame) || build_pilot(pg, h->pilot)) return DVBT2LL_EINVAL;
+  if (build_frame_mplp(fm, plps, h->frame, false, nss) || build_pilot(pg, h->pilot)) return DVBT2LL_EINVAL;
   if (h->pilot.active != h->frame.M) return DVBT2LL_EINVAL;
   const FramePlan &fp = h->frame;
+  if (h->max_frames < fp.unit) return DVBT2LL_EINVAL;   // runs cover whole interleaving frames
   h->nplp = fp.nplp;
+  h->pair_stride = ((int64_t)fp.S + 7) / 8 * 8;
   int r = h->ctx.init(device);
   if (r) return r;
   // OFDM side: aux bins from cmap, data cells streamed per symbol and scattered through inv
@@ -909,38 +933,57 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     MapDev &md = pl->map.dev;
     md.F = pp.F;
     // the LDPC + map kernel's cell interleaver + TI store in stored-slot order (layout.part: frame data slot
-    // of each TI position; the PLP's positions start at PLP_START), in aligned quads of four slots:
-    // block r's quads sorted by slot, each with the cell-interleaver input index of the cell landing
-    // in each of its four slots (j with (ci_perm[j] + ci_shift[r]) mod cs = t, framemapper:1973-1998;
-    // 0xFFFF: a slot of another block, at a run's edge), its offset from its 64-quad chunk's first
-    // quad, each chunk's first quad and the block's quad count.  A full quad is one 8-byte store, so a store instruction writes 512 B
-    // of one or two contiguous runs (the block's cells in a symbol (half) are one run, bank-balanced
-    // inside, t2_plan build_chain_layout)
+    // of each frame data index; a TIME_IL_TYPE 1 PLP's block r writes the P_I T2 frames of its interleaving
+    // frame, frame i's slots at i * pair_stride), in aligned quads of four slots: block r's quads sorted by
+    // slot, each with the cell-interleaver input index of the cell landing in each of its four slots (j with
+    // (ci_perm[j] + ci_shift[r]) mod cs = t, framemapper:1973-1998; 0xFFFF: a slot of another block, at a
+    // run's edge), its offset from its 64-quad chunk's first quad, each chunk's first quad and the block's
+    // quad count.  A full quad is one 8-byte store, so a store instruction writes 512 B of one or two
+    // contiguous runs (the block's cells in a symbol (half) are one run, bank-balanced inside, t2_plan
+    // build_chain_layout).  A chunk whose quads would span more than 0xFFFF quads (a block's cells in two
+    // T2 frames) ends early: the rest of its 64 entries are empty quads (no store).
     std::vector<std::vector<std::pair<int64_t, int>>> blk(pp.F);
+    std::vector<std::vector<int>> qpos(pp.F);   // per block: its quads' entry index (with the chunk padding)
     int qmax = 0;
     std::vector<std::pair<int64_t, int>> cells(pp.cs);
     std::vector<int> jin(pp.cs);   // cell-interleaver input index of each output position t
     for (int rr = 0; rr < pp.F; rr++) {
       for (int j = 0; j < pp.cs; j++) jin[(pp.ci_perm[j] + pp.ci_shift[rr]) % pp.cs] = j;
-      for (int t = 0; t < pp.cs; t++) cells[t] = {layout.part[ti_dest(fp, k, rr, t)], jin[t]};
+      for (int t = 0; t < pp.cs; t++) {
+        const CellDest cd = cell_dest(fp, k, rr, t);
+        cells[t] = {(int64_t)cd.phase * h->pair_stride + layout.part[cd.pos], jin[t]};
+      }
       std::sort(cells.begin(), cells.end());
       auto &qv = blk[rr];   // (quad index, slot-in-quad | t << 2) per cell
       for (auto &c : cells) qv.push_back({c.first >> 2, (int)(c.first & 3) | (c.second << 2)});
-      int nq = 0;
-      for (size_t i = 0; i < qv.size(); i++) nq += i == 0 || qv[i].first != qv[i - 1].first;
-      qmax = std::max(qmax, nq);
+      int n = -1;
+      int64_t qprev = -1, cbase = 0;
+      for (auto &c : qv) {
+        if (c.first == qprev) continue;
+        qprev = c.first;
+        ++n;
+        if (n % 64 && c.first - cbase > 0xFFFF) n = (n + 63) & ~63;   // start a new chunk here
+        if (n % 64 == 0) cbase = c.first;
+        qpos[rr].push_back(n);
+      }
+      qmax = std::max(qmax, n + 1);
     }
     const int qst = (qmax + 63) & ~63, nchk = qst / 64;
     std::vector<uint32_t> qsrc((size_t)pp.F * qst * 2 + 2, 0xFFFFFFFFu);
     std::vector<uint16_t> qoff((size_t)pp.F * qst + 4, 0);
     std::vector<int32_t> qb((size_t)pp.F * nchk + 1, 0), qn(pp.F, 0);
     for (int rr = 0; rr < pp.F; rr++) {
-      int n = -1;
+      int n = -1, qi = -1;
       int64_t qprev = -1, cbase = 0;
       for (auto &c : blk[rr]) {
         if (c.first != qprev) {
           qprev = c.first;
-          if (++n % 64 == 0) qb[(size_t)rr * nchk + n / 64] = (int32_t)(cbase = c.first);
+          n = qpos[rr][++qi];
+          if (n % 64 == 0) {
+            cbase = c.first;
+            if (cbase > INT32_MAX) return DVBT2LL_EINVAL;
+            qb[(size_t)rr * nchk + n / 64] = (int32_t)cbase;
+          }
           if (c.first - cbase > 0xFFFF) return DVBT2LL_EINVAL;
           qoff[(size_t)rr * qst + n] = (uint16_t)(c.first - cbase);
         }
@@ -959,11 +1002,12 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     md.slot_nq = pl->pnq.as<int32_t>();
     md.slot_stride = qst;
     pl->F = pp.F;
+    pl->P = pp.P;
     pl->inputmode = q.inputmode;
     pl->inband = q.inband;
     pl->cw_stride = ((pl->fec.plan.nldpc / 8) + 255) / 256 * 256;
     pl->pay = (pl->fec.plan.kbch - 80) / 8;
-    // payload bytes per frame: in-band type B takes 13 bytes of the first BBFRAME of each frame
+    // payload bytes per interleaving frame: in-band type B takes 13 bytes of its first BBFRAME
     // (bbheader:327-355, fec_block == 0)
     pl->ts_per_frame = (int64_t)pp.F * pl->pay - (q.inband ? 13 : 0);
     // PLPs with the same constellation and rotation share one table (their LUTs are equal)
@@ -1037,7 +1081,6 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     od.plp_bnd = h->plp_bnd.as<int32_t>();
     od.plp_qbase = h->plp_qbase.as<int32_t>();
   }
-  h->pair_stride = ((int64_t)fp.S + 7) / 8 * 8;
   h->iq_per_frame = (int64_t)pp.Nsym * (pp.N + pp.G) + 2048;
   // the OFDM kernel addresses index pairs and aux cells with 32-bit byte offsets
   if ((uint64_t)h->pair_stride * h->max_frames * 2 >= (1ull << 32) || auxv.size() * 8 >= (1ull << 32) ||
@@ -1066,7 +1109,7 @@ extern "C" int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, d
 }
 
 static bool mplp_to_plan(const dvbt2ll_mplp_params &m, FmParams &fm, std::vector<PlpParams> &plps,
-                         std::vector<int> &tsrate) {
+                         std::vector<int> &tsrate, int *nss) {
   if (m.nplp < 1 || m.nplp > DVBT2LL_MAX_PLP) return false;
   const dvbt2ll_plp_params &q0 = m.plp[0];
   fm = FmParams{q0.framesize, q0.rate, q0.constellation, q0.rotation, q0.fecblocks, q0.tiblocks, m.carriermode,
@@ -1077,9 +1120,10 @@ static bool mplp_to_plan(const dvbt2ll_mplp_params &m, FmParams &fm, std::vector
   for (int k = 0; k < m.nplp; k++) {
     const dvbt2ll_plp_params &q = m.plp[k];
     plps.push_back(PlpParams{q.framesize, q.rate, q.constellation, q.rotation, q.fecblocks, q.tiblocks, q.inputmode,
-                             q.inband});
+                             q.inband, q.plp_type, q.ti_type, q.ti_frames});
     tsrate.push_back(q.tsrate);
   }
+  *nss = m.num_subslices;
   return true;
 }
 
@@ -1089,7 +1133,8 @@ extern "C" int dvbt2ll_chain_create_mplp(const dvbt2ll_mplp_chain_params *p, int
   FmParams fm;
   std::vector<PlpParams> plps;
   std::vector<int> tsrate;
-  if (!mplp_to_plan(p->fm, fm, plps, tsrate)) return DVBT2LL_EINVAL;
+  int nss = 1;
+  if (!mplp_to_plan(p->fm, fm, plps, tsrate, &nss)) return DVBT2LL_EINVAL;
   std::unique_ptr<dvbt2ll_chain> h(new (std::nothrow) dvbt2ll_chain());
   if (!h) return DVBT2LL_ENOMEM;
   h->max_frames = p->max_frames;
@@ -1104,11 +1149,13 @@ extern "C" int dvbt2ll_chain_create_mplp(const dvbt2ll_mplp_chain_params *p, int
   h->p.bandwidth = p->bandwidth;
   h->p.max_frames = p->max_frames;
   h->p.tsrate = q0.tsrate;
-  int r = chain_build(h.get(), fm, plps, tsrate, p->misogroup, p->equalization, p->bandwidth, device);
+  int r = chain_build(h.get(), fm, plps, tsrate, p->misogroup, p->equalization, p->bandwidth, device, nss);
   if (r) return r;
   *out = h.release();
   return DVBT2LL_OK;
 }
+
+extern "C" int dvbt2ll_chain_unit_frames(const dvbt2ll_chain *h) { return h ? h->frame.unit : 0; }
 
 extern "C" int dvbt2ll_chain_num_plps(const dvbt2ll_chain *h) { return h ? h->nplp : 0; }
 
@@ -1126,6 +1173,7 @@ extern "C" int dvbt2ll_chain_get_plp_info(const dvbt2ll_chain *h, int plp, dvbt2
   info->fft_size = h->pilot.N;
   info->guard_interval = h->pilot.G;
   info->cw_stride_bytes = pl.cw_stride;
+  info->frames_per_if = pl.P;
   return DVBT2LL_OK;
 }
 
@@ -1148,6 +1196,8 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
   if (!h || !ts || !iq_dev || nframes < 1 || nstreams < 1 || (int64_t)nframes * nstreams > h->max_frames ||
       first_frame < 0 || (nstreams > 1 && (h->nplp > 1 || ts_stride < len[0])))
     return DVBT2LL_EINVAL;
+  // whole interleaving frames of every PLP (TIME_IL_TYPE 1: P_I T2 frames each)
+  if (first_frame % h->frame.unit || nframes % h->frame.unit) return DVBT2LL_EINVAL;
   const int nf = nframes * nstreams;   // frames of the launch, stream-major
   hipStream_t s = stream ? (hipStream_t)stream : h->ctx.stream;
   for (int k = 0; k < h->nplp; k++) {
@@ -1155,7 +1205,7 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
     if (!ts[k] || base[k] < 0 || base[k] % 188 != 0) return DVBT2LL_EINVAL;
     // the TS slice must cover every byte the frames consume plus the packet before the
     // first one touched (its CRC-8 replaces the next sync byte, bbheader:701-713)
-    int64_t start = first_frame * pl.ts_per_frame, end = (first_frame + nframes) * pl.ts_per_frame;
+    int64_t start = first_frame / pl.P * pl.ts_per_frame, end = (first_frame + nframes) / pl.P * pl.ts_per_frame;
     if (pl.inputmode) {
       start = 188 * (start / 187) + (start % 187);
       end = 188 * (end / 187) + (end % 187) + 1;
@@ -1189,19 +1239,21 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
     fio[k].in = (const uint8_t *)ts[k];
     fio[k].ts_base = base[k];
     fio[k].ts_len = len[k];
-    fio[k].first_block = first_frame * pl.F;
+    // launch block b: FEC block b mod F of interleaving frame b / F, which fills T2 frames P (b / F) ..
+    // P (b / F) + P - 1 of the launch (pairs at P pair_stride per interleaving frame)
+    fio[k].first_block = first_frame / pl.P * pl.F;
     fio[k].out = cw.as<uint8_t>();
     fio[k].cw_stride = pl.cw_stride;
-    fio[k].nblocks = pl.F * nf;
+    fio[k].nblocks = (int)pl.blocks(nf);
     fio[k].sync_err = h->sync_err.as<uint32_t>();
-    fio[k].blocks_per_stream = nstreams > 1 ? pl.F * nframes : 0;
+    fio[k].blocks_per_stream = nstreams > 1 ? (int)pl.blocks(nframes) : 0;
     fio[k].ts_stride = nstreams > 1 ? ts_stride : 0;
     fio[k].bch_part = pl.bpart[slot].as<uint32_t>();
-    fio[k].bch_part_blocks = (int64_t)pl.F * h->max_frames;
+    fio[k].bch_part_blocks = pl.blocks(h->max_frames);
     fio[k].keep_cw = h->keep_cw;
     mio[k].out_pairs = pairs.as<uint16_t>();
-    mio[k].frame_stride = h->pair_stride;
-    mio[k].nblocks = pl.F * nf;
+    mio[k].frame_stride = h->pair_stride * pl.P;
+    mio[k].nblocks = (int)pl.blocks(nf);
   }
   oio.data = h->aux.as<float2>();
   oio.aux_off = 0;

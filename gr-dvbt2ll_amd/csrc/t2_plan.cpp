@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <algorithm>
+#include <numeric>
 
 #include "gen/dvbt2_std_tables.h"
 
@@ -510,11 +511,20 @@ int build_frame(const FmParams &p, FramePlan &fp, bool host_l1post) {
 // plus 89 configurable (:1577-1639) and 48 dynamic (:1672-1687) bits per further PLP
 static int ksig_post(int nplp) { return 350 + (nplp - 1) * (89 + 48); }
 
-int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, FramePlan &fp, bool host_l1post) {
-  const int nplp = (int)plps.size();
+int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, FramePlan &fp, bool host_l1post,
+                     int nss) {
+  const int nplp = (int)plps_in.size();
   if (nplp < 1 || nplp > MAX_PLP) return -1;
   if (p.t2frames < 1 || p.t2frames > 255 || p.numdatasyms < 1) return -1;
+  if (nss == 0) nss = 1;
+  if (nss < 1 || nss > 32767) return -1;   // SUB_SLICES_PER_FRAME: 15 bits
+  std::vector<PlpParams> plps = plps_in;
+  for (auto &q : plps) {                   // 0 = the reference's values
+    if (q.plp_type == 0) q.plp_type = 1;
+    if (q.ti_frames == 0) q.ti_frames = 1;
+  }
   fp.nplp = nplp;
+  fp.nss = nss;
   fp.plp_in = plps;
   fp.plp.assign(nplp, PlpPlan());
   int N = fft_points(p.fftsize);
@@ -548,10 +558,20 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, Fram
     // tiblocks > fecblocks is accepted like the reference (framemapper:1114-1119): the surplus TI
     // blocks are "small" ones of floor(fecblocks / tiblocks) = 0 FEC blocks, which carry no cells
     if (q.tiblocks < 0 || q.tiblocks > 255) return -1;
+    // TIME_IL_TYPE 1 (EN 302 755 6.5): one TI block per interleaving frame over P_I T2 frames; the
+    // superframe holds whole interleaving frames (FIRST_FRAME_IDX 0, FRAME_INTERVAL 1)
+    if ((q.plp_type != 1 && q.plp_type != 2) || (q.ti_type != 0 && q.ti_type != 1) || q.ti_frames < 1 ||
+        q.ti_frames > 255 || (q.ti_type == 0 && q.ti_frames != 1) || (q.ti_type == 1 && q.tiblocks != 1) ||
+        ((int64_t)q.fecblocks * pl.cs) % q.ti_frames || p.t2frames % q.ti_frames)
+      return -1;
     pl.F = q.fecblocks;
-    pl.S = pl.cs * pl.F;
-    pl.start = fp.S;
-    fp.S += pl.S;
+    pl.P = q.ti_frames;
+    pl.S_if = pl.cs * pl.F;
+    pl.S = pl.S_if / pl.P;
+    pl.type2 = q.plp_type == 2;
+    pl.in_off = fp.S_in;
+    fp.S_in += pl.S_if;
+    fp.unit = std::lcm(fp.unit, pl.P);
     int deg;
     ci_permutation(pl.cs, pl.ci_perm, &deg);
     int small_fec, big_fec, n_big, n_small;
@@ -581,6 +601,28 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, Fram
       }
     }
   }
+  // 8.3.6.3: Type-1 PLPs back to back in PLP_ID order, then the Type-2 PLPs' sub-slices
+  int ntype2 = 0;
+  for (int k = 0; k < nplp; k++)
+    if (!fp.plp[k].type2) {
+      fp.plp[k].start = fp.S;
+      fp.S += fp.plp[k].S;
+    } else {
+      ntype2++;
+    }
+  if (!ntype2 && nss != 1) return -1;
+  fp.t2start = ntype2 ? fp.S : 0;
+  fp.ssi = 0;
+  for (int k = 0; k < nplp; k++) {
+    PlpPlan &pl = fp.plp[k];
+    if (!pl.type2) continue;
+    if (pl.S % nss) return -1;
+    pl.ss = pl.S / nss;
+    pl.ss_off = fp.ssi;
+    pl.start = fp.t2start + fp.ssi;   // PLP_START: its first sub-slice
+    fp.ssi += pl.ss;
+  }
+  if (ntype2) fp.S = fp.t2start + fp.ssi * nss;
   {
     const PlpPlan &p0 = fp.plp[0];
     fp.cs = p0.cs; fp.F = p0.F; fp.ci_perm = p0.ci_perm; fp.ci_shift = p0.ci_shift;
@@ -591,9 +633,10 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, Fram
   int fixed = fp.S + 1840 + fp.Lp + (fp.N_FC - fp.C_FC);
   if (fp.M < fixed) return -1;   // reference: "too many FEC blocks in T2 frame"
   fp.D = fp.M - fixed;
-  // data cell (TI output order) -> framemapper input index: the inverse time interleave
-  // (framemapper:1999-2028) and cell interleave of its PLP; the input holds the PLPs' frames back to back
-  std::vector<int> data_in(fp.S);
+  // data cell of a T2 frame of phase ph (global frame mod unit) -> framemapper input index: the inverse time
+  // interleave (framemapper:1999-2028) and cell interleave of its PLP, whose interleaving frame (S_if cells) is
+  // at in_off of the input
+  std::vector<std::vector<int>> data_in(fp.unit, std::vector<int>(fp.S));
   for (int k = 0; k < nplp; k++) {
     const PlpPlan &pl = fp.plp[k];
     std::vector<int> perm_inv(pl.cs);
@@ -601,7 +644,8 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, Fram
     for (int r = 0; r < pl.F; r++)
       for (int t = 0; t < pl.cs; t++) {
         const int w = perm_inv[((t - pl.ci_shift[r]) % pl.cs + pl.cs) % pl.cs];
-        data_in[ti_dest(fp, k, r, t)] = pl.start + r * pl.cs + w;
+        const CellDest cd = cell_dest(fp, k, r, t);
+        for (int ph = cd.phase; ph < fp.unit; ph += pl.P) data_in[ph][cd.pos] = pl.in_off + r * pl.cs + w;
       }
   }
 
@@ -629,20 +673,18 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, Fram
   if (fp.N_FC) fi_tables(N, fp.N_FC, HeF, HoF);
   if ((int)He.size() != fp.C_DATA || (int)HeP.size() != fp.C_P2) return -1;
   fp.gather_d.assign(M, 0);
-  fp.gather_in.assign(M, 0);
+  fp.gather_in.assign((size_t)fp.unit * M, 0);
   const int aux_dummy = AUX_L1PRE + 1840 + Lp;
   auto resolve = [&](int o, int f) {
     int v = zz[f];
-    int code_d, code_in;
-    if (v < 1840) code_d = code_in = -(AUX_L1PRE + v) - 1;
-    else if (v < 1840 + Lp) code_d = code_in = -(AUX_L1PRE + v) - 1;
-    else if (v < 1840 + Lp + fp.S) {
-      code_d = v - 1840 - Lp;
-      code_in = data_in[code_d];
-    } else if (v < 1840 + Lp + fp.S + fp.D) code_d = code_in = -(aux_dummy + (v - 1840 - Lp - fp.S)) - 1;
-    else code_d = code_in = -AUX_ZERO - 1;
+    int code_d;
+    if (v < 1840) code_d = -(AUX_L1PRE + v) - 1;
+    else if (v < 1840 + Lp) code_d = -(AUX_L1PRE + v) - 1;
+    else if (v < 1840 + Lp + fp.S) code_d = v - 1840 - Lp;
+    else if (v < 1840 + Lp + fp.S + fp.D) code_d = -(aux_dummy + (v - 1840 - Lp - fp.S)) - 1;
+    else code_d = -AUX_ZERO - 1;
     fp.gather_d[o] = code_d;
-    fp.gather_in[o] = code_in;
+    for (int ph = 0; ph < fp.unit; ph++) fp.gather_in[(size_t)ph * M + o] = code_d >= 0 ? data_in[ph][code_d] : code_d;
   };
   int o = 0, base = 0, symbol = 0;
   for (int j = 0; j < fp.N_P2; j++, symbol++, base += fp.C_P2) {
@@ -706,25 +748,31 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, Fram
   return 0;
 }
 
-namespace {
 // L1-post signalling bits before the CRC-32 (framemapper:1553-1691, no auxiliary streams), the
 // configurable (:1577-1639) and dynamic (:1672-1687) PLP loops over the frame's PLPs (the reference's
 // one PLP: PLP_ID 0, PLP_START 0): FRAME_IDX (8 bits at *fidx_pos) = frame_idx
 std::vector<uint8_t> l1post_signal(const FmParams &p, const FramePlan &fp, int frame_idx, int *fidx_pos) {
   const bool v131 = p.version == 2, resv = p.reservedbiasbits && v131;
   Bits b;
-  b.put(1, 15); b.put((uint64_t)fp.nplp, 8); b.put(0, 4); b.put(0, 8); b.put(0, 3); b.put(729833333u, 32);
+  b.put((uint64_t)fp.nss, 15); b.put((uint64_t)fp.nplp, 8); b.put(0, 4); b.put(0, 8); b.put(0, 3); b.put(729833333u, 32);
   for (int k = 0; k < fp.nplp; k++) {
     const PlpParams &q = fp.plp_in[k];
-    b.put((uint64_t)k, 8); b.put(1, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3); b.put(0, 8); b.put(1, 8);
+    // PLP_ID, PLP_TYPE (001 Type 1, 010 Type 2), PLP_PAYLOAD_TYPE TS, FF_FLAG, FIRST_RF_IDX,
+    // FIRST_FRAME_IDX 0, PLP_GROUP_ID 1
+    b.put((uint64_t)k, 8); b.put((uint64_t)q.plp_type, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3); b.put(0, 8);
+    b.put(1, 8);
+    // PLP_COD, PLP_MOD, PLP_ROTATION, PLP_FEC_TYPE, PLP_NUM_BLOCKS_MAX, FRAME_INTERVAL 1, TIME_IL_LENGTH
+    // (N_TI for TIME_IL_TYPE 0, P_I for 1), TIME_IL_TYPE, IN_BAND_A_FLAG
     b.put(q.rate, 3); b.put(q.constellation, 3); b.put(q.rotation, 1); b.put(q.framesize, 2);
-    b.put(q.fecblocks, 10); b.put(1, 8); b.put(q.tiblocks, 8); b.put(0, 1); b.put(0, 1);
+    b.put(q.fecblocks, 10); b.put(1, 8); b.put((uint64_t)(q.ti_type ? q.ti_frames : q.tiblocks), 8);
+    b.put((uint64_t)q.ti_type, 1); b.put(0, 1);
     b.put((q.inband && v131) ? 1 : 0, 1); b.put(resv ? 0x7ff : 0, 11);
     b.put(p.version == 0 ? 0 : q.inputmode + 1, 2); b.put(0, 1); b.put(0, 1);
   }
   b.put(0, 2); b.put(resv ? 0x3fffffff : 0, 30);
   if (fidx_pos) *fidx_pos = (int)b.b.size();
-  b.put((uint64_t)frame_idx, 8); b.put(0, 22); b.put(0, 22); b.put(0, 8);
+  // FRAME_IDX, SUB_SLICE_INTERVAL, TYPE_2_START (both 0 without Type-2 PLPs), L1_CHANGE_COUNTER
+  b.put((uint64_t)frame_idx, 8); b.put((uint64_t)fp.ssi, 22); b.put((uint64_t)fp.t2start, 22); b.put(0, 8);
   b.put(0, 3); b.put(resv ? 0xff : 0, 8);
   for (int k = 0; k < fp.nplp; k++) {
     b.put((uint64_t)k, 8); b.put((uint64_t)fp.plp[k].start, 22); b.put(fp.plp[k].F, 10);
@@ -734,6 +782,7 @@ std::vector<uint8_t> l1post_signal(const FmParams &p, const FramePlan &fp, int f
   return b.b;
 }
 
+namespace {
 const int KBCH12 = 7032, NBCH12 = 7200;
 
 // shortening (framemapper:2190-2214): which of the 7032 information positions stay zero
@@ -1166,16 +1215,22 @@ std::vector<int32_t> ofdm_stored_rows(int N, int Nsym, const std::vector<int32_t
   return out;
 }
 
-int64_t ti_dest(const FramePlan &fp, int plp, int r, int t) {
+int64_t ti_index(const FramePlan &fp, int plp, int r, int t) {
   const PlpPlan &pl = fp.plp[plp];
   const int cs = pl.cs;
-  if (!pl.ti_on) return pl.start + (int64_t)r * cs + t;
+  if (!pl.ti_on) return (int64_t)r * cs + t;
   const int ns = pl.ti_nsmall * pl.ti_small;
   int r0, nb;
   if (r < ns) { r0 = r - r % pl.ti_small; nb = pl.ti_small; }
   else { r0 = r - (r - ns) % pl.ti_big; nb = pl.ti_big; }
   const int rows = cs / 5, e = t / rows, row = t - e * rows;
-  return pl.start + (int64_t)r0 * cs + (int64_t)row * (5 * nb) + 5 * (r - r0) + e;
+  return (int64_t)r0 * cs + (int64_t)row * (5 * nb) + 5 * (r - r0) + e;
+}
+
+int32_t plp_cell_pos(const FramePlan &fp, int plp, int c) {
+  const PlpPlan &pl = fp.plp[plp];
+  if (!pl.type2) return pl.start + c;
+  return fp.t2start + (c / pl.ss) * fp.ssi + pl.ss_off + c % pl.ss;
 }
 
 // LDS bank pair of a stored bin as the OFDM kernels' scatter writes it (8-byte slot within its half,
@@ -1270,11 +1325,16 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
   // block per workgroup, one contiguous run per symbol (half) instead of 10-byte TI-row runs
   // scattered over the symbol (its per-cell deltas take any order inside a run).
   // (blocks numbered PLP-major: PLP k's block r is g0_k + r, so each symbol half's slots are PLP-major too)
+  // (a TIME_IL_TYPE 1 PLP's blocks by the first T2 frame of its interleaving frame: its other frames' cells
+  // come from the same blocks, at the same positions when the frame boundary falls between TI rows)
   std::vector<int32_t> blk_of(fp.S), plp_of_blk;
   for (int k = 0, g0 = 0; k < fp.nplp; g0 += fp.plp[k].F, k++)
     for (int r = 0; r < fp.plp[k].F; r++) {
       plp_of_blk.push_back(k);
-      for (int t = 0; t < fp.plp[k].cs; t++) blk_of[ti_dest(fp, k, r, t)] = g0 + r;
+      for (int t = 0; t < fp.plp[k].cs; t++) {
+        const CellDest cd = cell_dest(fp, k, r, t);
+        if (cd.phase == 0) blk_of[cd.pos] = g0 + r;
+      }
     }
   const int P = fp.nplp;
   cl.plp_bnd.assign((size_t)2 * pp.Nsym * (P + 1), 0);

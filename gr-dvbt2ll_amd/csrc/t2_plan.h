@@ -66,16 +66,25 @@ struct FmParams {
       guardinterval, l1constellation, pilotpattern, t2frames, numdatasyms, paprmode, version,
       preamble, inputmode, reservedbiasbits, l1scrambled, inband;
 };
-// One Type-1 data PLP of a multi-PLP frame (EN 302 755 8.3.6.3).  The reference carries exactly one
-// PLP (framemapper:152-250: num_plp 1, plp_type 1, time_il_type 0, frame_interval 1); a frame here
-// carries nplp of them, PLP_ID = index, each with its own FEC, constellation, cell and time
-// interleaver, its TI output occupying data cells [start, start + S) after the L1 signalling, PLPs
-// back to back in PLP_ID order.  TI type 0 with P_I = 1 keeps every T2 frame independent.
+// One data PLP of a multi-PLP frame (EN 302 755 6.5, 8.3.6.3).  The reference carries exactly one PLP
+// (framemapper:152-250: num_plp 1, plp_type 1, time_il_type 0, frame_interval 1); a frame here carries
+// nplp of them, PLP_ID = index, each with its own FEC, constellation, cell and time interleaver.
+//  - TIME_IL_TYPE 0 (the reference's): one interleaving frame (fecblocks FEC blocks, tiblocks TI blocks)
+//    per T2 frame.  TIME_IL_TYPE 1: one TI block (tiblocks = 1) of fecblocks FEC blocks per interleaving
+//    frame, spread over P_I = ti_frames T2 frames: T2 frame i of interleaving frame m (global frame
+//    m P_I + i) carries its TI output cells [i S, (i + 1) S), S = fecblocks cs / P_I.  FRAME_INTERVAL 1.
+//  - Type-1 PLPs occupy one run of S data cells each, back to back in PLP_ID order after the L1
+//    signalling (PLP_START = start); then the Type-2 PLPs, sub-sliced: sub-slice j (S / nss cells) of
+//    every Type-2 PLP in PLP_ID order, then sub-slice j + 1 (SUB_SLICE_INTERVAL ssi, TYPE_2_START t2start).
 struct PlpParams {
   int framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband;
+  int plp_type = 1, ti_type = 0, ti_frames = 1;
 };
 struct PlpPlan {
-  int cs = 0, F = 0, S = 0, start = 0;
+  int cs = 0, F = 0, S = 0, start = 0;   // F: FEC blocks per interleaving frame; S: cells per T2 frame
+  int S_if = 0, P = 1;                   // cells per interleaving frame (F cs), its T2 frames (P_I)
+  int type2 = 0, ss = 0, ss_off = 0;     // Type 2: sub-slice cells, offset within a sub-slice group
+  int in_off = 0;                        // framemapper block: the PLP's interleaving frame in its input buffer
   int ti_on = 0, ti_small = 1, ti_big = 1, ti_nsmall = 0;
   std::vector<int16_t> ci_perm;          // cs
   std::vector<int32_t> ci_shift;         // F
@@ -119,6 +128,9 @@ struct L1PostPlan {
 // The single-PLP fields (cs, F, ci_perm, ci_shift, ti_*) are PLP 0's; S is the total over the PLPs.
 struct FramePlan {
   int nplp = 1;
+  int nss = 1, ssi = 0, t2start = 0;     // SUB_SLICES_PER_FRAME, SUB_SLICE_INTERVAL, TYPE_2_START
+  int unit = 1;                          // T2 frames per launch unit: lcm of the PLPs' P_I (the frame phases)
+  int S_in = 0;                          // framemapper block input: every PLP's interleaving frame (sum S_if)
   std::vector<PlpParams> plp_in;         // the PLPs' parameters
   std::vector<PlpPlan> plp;
   int cs = 0, F = 0, S = 0, M = 0, N_P2 = 0, C_P2 = 0, C_DATA = 0, N_FC = 0, C_FC = 0;
@@ -128,8 +140,9 @@ struct FramePlan {
   std::vector<int32_t> ci_shift;         // F (per FEC block of a frame)
   std::vector<int32_t> gather_d;         // M: mapped cell -> frame data-region index (TI output order) | aux
   int ti_on = 0, ti_small = 1, ti_big = 1, ti_nsmall = 0;   // TI blocks: ti_nsmall of ti_small FEC blocks, then ti_big
-  std::vector<int32_t> gather_in;        // M: mapped cell -> framemapper input index | aux (input: one frame of
-                                         //   every PLP's cells, PLP 0 first)
+  std::vector<int32_t> gather_in;        // unit x M: per frame phase (global frame mod unit), mapped cell ->
+                                         //   framemapper input index | aux (input: the current interleaving
+                                         //   frame of every PLP, PLP k's S_if cells at plp[k].in_off)
   // host_l1post: t2frames x aux_len with every variant's L1-post cells (the CPU tests' cross-check);
   // else one variant whose L1-post cells [AUX_L1PRE + 1840, + Lp) are left zero for the GPU
   std::vector<cf32> aux;
@@ -139,10 +152,15 @@ struct FramePlan {
 // host_l1post: also encode every t2_frame_num variant's L1-post on the host (tests only; the
 // product generates L1-post per frame on the GPU from fp.l1)
 int build_frame(const FmParams &p, FramePlan &fp, bool host_l1post = false);
-// nplp PLPs; the per-PLP fields of p (framesize .. fecblocks, tiblocks, inputmode, inband) are ignored
-int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, FramePlan &fp, bool host_l1post = false);
+// nplp PLPs; the per-PLP fields of p (framesize .. fecblocks, tiblocks, inputmode, inband) are ignored;
+// nss: SUB_SLICES_PER_FRAME (1 without Type-2 PLPs)
+int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, FramePlan &fp, bool host_l1post = false,
+                     int nss = 1);
 // fp.l1 from the parameters and fp's L1 geometry (called by build_frame)
 int build_l1post_plan(const FmParams &p, FramePlan &fp);
+// the L1-post signalling bits before the CRC-32 (one per byte) of FRAME_IDX frame_idx; *fidx_pos: FRAME_IDX's
+// first bit (framemapper:1553-1691 with the frame's PLP loops)
+std::vector<uint8_t> l1post_signal(const FmParams &p, const FramePlan &fp, int frame_idx, int *fidx_pos);
 // one FRAME_IDX variant's Lp L1-post cells, encoded bit by bit on the host (tests only)
 int l1post_host(const FmParams &p, const FramePlan &fp, int frame_idx, cf32 *dst);
 
@@ -222,9 +240,21 @@ struct AuxLists {
 // l1post kernel writes); l1_len = 0: indirect codes are aux index + 1 into the frame's variant
 int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf32> &auxv, int aux_len,
                     int t2frames, AuxLists &al, int l1_lo = 0, int l1_len = 0);
-// time-interleaver output index (frame data order) of cell-interleaved cell t of FEC block r of PLP plp
-int64_t ti_dest(const FramePlan &fp, int plp, int r, int t);
-inline int64_t ti_dest(const FramePlan &fp, int r, int t) { return ti_dest(fp, 0, r, t); }
+// time-interleaver output index (within the interleaving frame, [0, S_if)) of cell-interleaved cell t of FEC
+// block r of PLP plp (framemapper:1999-2028)
+int64_t ti_index(const FramePlan &fp, int plp, int r, int t);
+// frame data-region index of cell c (< S) of PLP plp in a T2 frame (8.3.6.3: Type-1 run or Type-2 sub-slices)
+int32_t plp_cell_pos(const FramePlan &fp, int plp, int c);
+// where cell t of FEC block r of PLP plp lands: T2 frame `phase` of its interleaving frame, data index `pos`
+struct CellDest {
+  int phase;
+  int32_t pos;
+};
+inline CellDest cell_dest(const FramePlan &fp, int plp, int r, int t) {
+  const int64_t u = ti_index(fp, plp, r, t);
+  const int S = fp.plp[plp].S;
+  return CellDest{(int)(u / S), plp_cell_pos(fp, plp, (int)(u % S))};
+}
 
 // framemapper cell counts {N_P2, C_P2, C_DATA, N_FC, C_FC} (framemapper:290-356, 425-915); -1 if invalid
 int frame_cell_counts(int fftsize, int carriermode, int pp, int papr, int gi, int preamble, int out[5]);

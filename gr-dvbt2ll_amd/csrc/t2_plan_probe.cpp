@@ -10,9 +10,11 @@ using namespace t2;
 
 // multi-PLP parameters as laid out by include/dvbt2ll_hip.h dvbt2ll_mplp_params (ints): 12 common fields
 // {carriermode, fftsize, guardinterval, l1constellation, pilotpattern, t2frames, numdatasyms, paprmode,
-// version, preamble, reservedbiasbits, l1scrambled}, nplp, then MAX_PLP x 9 per-PLP fields {framesize,
-// rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, tsrate}
-static bool parse_mplp(const int *a, FmParams &f, std::vector<PlpParams> &plps) {
+// version, preamble, reservedbiasbits, l1scrambled}, nplp, then MAX_PLP x 12 per-PLP fields {framesize,
+// rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, tsrate, plp_type, ti_type,
+// ti_frames}, then num_subslices
+constexpr int PLP_INTS = 12;
+static bool parse_mplp(const int *a, FmParams &f, std::vector<PlpParams> &plps, int *nss) {
   const int n = a[12];
   if (n < 1 || n > MAX_PLP) return false;
   const int *q0 = a + 13;
@@ -20,27 +22,36 @@ static bool parse_mplp(const int *a, FmParams &f, std::vector<PlpParams> &plps) 
                a[9], q0[6], a[10], a[11], q0[7]};
   plps.clear();
   for (int k = 0; k < n; k++) {
-    const int *q = a + 13 + 9 * k;
-    plps.push_back(PlpParams{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]});
+    const int *q = a + 13 + PLP_INTS * k;
+    plps.push_back(PlpParams{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[9], q[10], q[11]});
   }
+  *nss = a[13 + PLP_INTS * MAX_PLP];
   return true;
 }
 
 extern "C" {
 
-// multi-PLP frame plan: info [M, S, aux_len, t2frames, Lp, D, nplp, starts[8], cs[8], F[8]]
+// multi-PLP frame plan: info [M, S, aux_len, t2frames, Lp, D, nplp, starts[8], cs[8], F[8], unit, nss, ssi,
+// t2start, S_in, S[8], P[8], in_off[8], type2[8]] (68 ints); gather_in unit x M
 int t2probe_frame_mplp(const int *mp, int *info, int32_t *gather_in, int32_t *gather_d, float *aux) {
   FmParams p;
   std::vector<PlpParams> plps;
   FramePlan fp;
-  if (!parse_mplp(mp, p, plps) || build_frame_mplp(p, plps, fp, true)) return -1;
+  int nss = 1;
+  if (!parse_mplp(mp, p, plps, &nss) || build_frame_mplp(p, plps, fp, true, nss)) return -1;
   int v[7] = {fp.M, fp.S, fp.aux_len, fp.t2frames, fp.Lp, fp.D, fp.nplp};
   memcpy(info, v, sizeof(v));
   for (int k = 0; k < 8; k++) {
-    info[7 + k] = k < fp.nplp ? fp.plp[k].start : 0;
-    info[15 + k] = k < fp.nplp ? fp.plp[k].cs : 0;
-    info[23 + k] = k < fp.nplp ? fp.plp[k].F : 0;
+    const bool in = k < fp.nplp;
+    info[7 + k] = in ? fp.plp[k].start : 0;
+    info[15 + k] = in ? fp.plp[k].cs : 0;
+    info[23 + k] = in ? fp.plp[k].F : 0;
+    info[36 + k] = in ? fp.plp[k].S : 0;
+    info[44 + k] = in ? fp.plp[k].P : 0;
+    info[52 + k] = in ? fp.plp[k].in_off : 0;
+    info[60 + k] = in ? fp.plp[k].type2 : 0;
   }
+  info[31] = fp.unit; info[32] = fp.nss; info[33] = fp.ssi; info[34] = fp.t2start; info[35] = fp.S_in;
   if (gather_in) memcpy(gather_in, fp.gather_in.data(), fp.gather_in.size() * 4);
   if (gather_d) memcpy(gather_d, fp.gather_d.data(), fp.gather_d.size() * 4);
   if (aux) memcpy(aux, fp.aux.data(), fp.aux.size() * 8);
@@ -52,13 +63,14 @@ int t2probe_chain_mplp(const int *mp, const int *pg3, int *info, int32_t *cmap, 
                        int32_t *dn, int32_t *dn0, int32_t *part, int32_t *bnd) {
   FmParams f;
   std::vector<PlpParams> plps;
-  if (!parse_mplp(mp, f, plps)) return -1;
+  int nss = 1;
+  if (!parse_mplp(mp, f, plps, &nss)) return -1;
   PgParams g{f.carriermode, f.fftsize, f.pilotpattern, f.guardinterval, f.numdatasyms, f.paprmode, f.version,
              f.preamble, pg3[0], pg3[1], pg3[2], fft_points(f.fftsize)};
   FramePlan fp;
   PilotPlan pp;
   ChainLayout cl;
-  if (build_frame_mplp(f, plps, fp) || build_pilot(g, pp) || build_chain_layout(fp, pp, cl)) return -1;
+  if (build_frame_mplp(f, plps, fp, false, nss) || build_pilot(g, pp) || build_chain_layout(fp, pp, cl)) return -1;
   info[0] = pp.Nsym; info[1] = pp.N; info[2] = fp.S; info[3] = ofdm_split(pp.N) ? 1 : 0; info[4] = fp.nplp;
   if (cmap) memcpy(cmap, cl.cmap.data(), cl.cmap.size() * 4);
   if (inv) memcpy(inv, cl.inv.data(), cl.inv.size() * 2);
@@ -70,12 +82,26 @@ int t2probe_chain_mplp(const int *mp, const int *pg3, int *info, int32_t *cmap, 
   return 0;
 }
 
+// multi-PLP L1-post signalling bits before the CRC-32 (one byte per bit) of FRAME_IDX frame_idx; returns the count
+int t2probe_l1post_bits_mplp(const int *mp, int frame_idx, uint8_t *out, int cap) {
+  FmParams p;
+  std::vector<PlpParams> plps;
+  FramePlan fp;
+  int nss = 1;
+  if (!parse_mplp(mp, p, plps, &nss) || build_frame_mplp(p, plps, fp, false, nss)) return -1;
+  const std::vector<uint8_t> b = l1post_signal(p, fp, frame_idx, nullptr);
+  if ((int)b.size() > cap) return -1;
+  if (out) memcpy(out, b.data(), b.size());
+  return (int)b.size();
+}
+
 // multi-PLP L1-post of one FRAME_IDX from the bit-by-bit host encoder; out Lp complex; info [nsig, npost, Lp]
 int t2probe_l1post_mplp(const int *mp, int frame_idx, float *out, int *info) {
   FmParams p;
   std::vector<PlpParams> plps;
   FramePlan fp;
-  if (!parse_mplp(mp, p, plps) || build_frame_mplp(p, plps, fp)) return -1;
+  int nss = 1;
+  if (!parse_mplp(mp, p, plps, &nss) || build_frame_mplp(p, plps, fp, false, nss)) return -1;
   if (info) { info[0] = fp.l1.nsig; info[1] = fp.l1.npost; info[2] = fp.l1.lp; }
   return out ? l1post_host(p, fp, frame_idx, (cf32 *)out) : 0;
 }

@@ -50,13 +50,18 @@ MAX_PLP = 8   # DVBT2LL_MAX_PLP
 
 class _PlpParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
-        "framesize", "rate", "constellation", "rotation", "fecblocks", "tiblocks", "inputmode", "inband", "tsrate")]
+        "framesize", "rate", "constellation", "rotation", "fecblocks", "tiblocks", "inputmode", "inband", "tsrate",
+        "plp_type", "ti_type", "ti_frames")]
+
+
+PLP_INTS = len(_PlpParams._fields_)
 
 
 class _MplpParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "carriermode", "fftsize", "guardinterval", "l1constellation", "pilotpattern", "t2frames", "numdatasyms",
-        "paprmode", "version", "preamble", "reservedbiasbits", "l1scrambled", "nplp")] + [("plp", _PlpParams * MAX_PLP)]
+        "paprmode", "version", "preamble", "reservedbiasbits", "l1scrambled", "nplp")] + [
+        ("plp", _PlpParams * MAX_PLP), ("num_subslices", ctypes.c_int)]
 
     @classmethod
     def from_config(cls, mcfg):
@@ -64,7 +69,8 @@ class _MplpParams(ctypes.Structure):
         a = mcfg.mplp_array()
         p = cls(*a[:13])
         for k in range(MAX_PLP):
-            p.plp[k] = _PlpParams(*a[13 + 9 * k:22 + 9 * k])
+            p.plp[k] = _PlpParams(*a[13 + PLP_INTS * k:13 + PLP_INTS * (k + 1)])
+        p.num_subslices = a[13 + PLP_INTS * MAX_PLP]
         return p
 
 
@@ -78,7 +84,7 @@ class _ChainInfo(ctypes.Structure):
                 ("ts_bytes_per_frame", ctypes.c_int64), ("iq_samples_per_frame", ctypes.c_int64),
                 ("cell_size", ctypes.c_int), ("stream_items", ctypes.c_int), ("mapped_items", ctypes.c_int),
                 ("num_symbols", ctypes.c_int), ("fft_size", ctypes.c_int), ("guard_interval", ctypes.c_int),
-                ("cw_stride_bytes", ctypes.c_int64)]
+                ("cw_stride_bytes", ctypes.c_int64), ("frames_per_if", ctypes.c_int)]
 
 
 BLOCKS = ("bbheaderbch", "ldpc", "interleavermod", "framemapperfint", "pilotgenp1insert")
@@ -95,7 +101,7 @@ EXPORTS += ["dvbt2ll_framemapperfint_stream_items", "dvbt2ll_pilotgenp1insert_ac
 EXPORTS += ["dvbt2ll_bbheaderbch_set_isi"]
 EXPORTS += ["dvbt2ll_framemapper_mplp_" + f for f in ("create", "output_multiple", "stream_items", "forecast",
                                                       "general_work", "destroy")]
-EXPORTS += ["dvbt2ll_chain_" + f for f in ("create_mplp", "num_plps", "get_plp_info", "run_plps",
+EXPORTS += ["dvbt2ll_chain_" + f for f in ("create_mplp", "num_plps", "unit_frames", "get_plp_info", "run_plps",
                                            "debug_plp_codewords", "debug_keep_codewords")]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_streams", "run_host", "set_output", "set_slots", "set_graph", "set_timing",
                                            "get_timing", "debug_codewords", "debug_cell_pairs", "debug_cells",
@@ -154,6 +160,7 @@ def lib():
     L.dvbt2ll_framemapper_mplp_destroy.restype = None
     L.dvbt2ll_chain_create_mplp.argtypes = [ctypes.POINTER(_MplpChainParams), ci, ctypes.POINTER(vp)]
     L.dvbt2ll_chain_num_plps.argtypes = [vp]
+    L.dvbt2ll_chain_unit_frames.argtypes = [vp]
     L.dvbt2ll_chain_get_plp_info.argtypes = [vp, ci, ctypes.POINTER(_ChainInfo)]
     L.dvbt2ll_chain_run_plps.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i64), ctypes.POINTER(i64), i64, ci,
                                          vp, vp]

@@ -121,9 +121,11 @@ class pilotgenp1insert_cc(_Block):
 
 
 class framemapper_mplp_cc:
-    """framemapperfint_cc with one input port per Type-1 data PLP (the reference
-    carries one PLP, lib/framemapperfint_cc_impl.cc:152-250): make(MplpConfig); one T2 frame per
-    general_work call, consuming stream_items(k) cells from every port k"""
+    """framemapperfint_cc with one input port per data PLP (the reference carries one
+    PLP, lib/framemapperfint_cc_impl.cc:152-250): make(MplpConfig); one T2 frame per general_work call,
+    consuming stream_items(k) cells from every port k -- or, for a TIME_IL_TYPE 1 PLP, its whole
+    interleaving frame on the first of its P_I T2 frames and nothing on the others (forecast() and
+    last_consumed say which)"""
     in_dtype = np.complex64
     out_dtype = np.complex64
 

@@ -18,8 +18,8 @@ IQ_SC16 = 1   # DVBT2LL_IQ_SC16
 
 class Chain:
     def __init__(self, cfg, max_frames=1, device=0):
-        """cfg: a T2Config (the reference's single-PLP frame) or an MplpConfig (several Type-1 data PLPs,
-        dvbt2ll_chain_create_mplp)"""
+        """cfg: a T2Config (the reference's single-PLP frame) or an MplpConfig (several data PLPs, Type 1 / 2,
+        TIME_IL_TYPE 0 / 1; dvbt2ll_chain_create_mplp)"""
         self.cfg = cfg
         h = ctypes.c_void_p()
         self._h = None
@@ -35,6 +35,8 @@ class Chain:
         self._h = h
         self.max_frames = max_frames
         self.nplp = lib().dvbt2ll_chain_num_plps(self._h)
+        # runs cover whole interleaving frames: first_frame and nframes multiples of unit_frames
+        self.unit_frames = lib().dvbt2ll_chain_unit_frames(self._h)
         info = _ChainInfo()
         check(lib().dvbt2ll_chain_get_info(self._h, ctypes.byref(info)), "chain info")
         self.info = {f: getattr(info, f) for f, _ in _ChainInfo._fields_}

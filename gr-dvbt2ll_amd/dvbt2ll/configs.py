@@ -89,13 +89,16 @@ CONFIGS = {
 }
 
 MAX_PLP = 8   # DVBT2LL_MAX_PLP
+PLP_INTS = 12   # ints of dvbt2ll_plp_params
 
 
 @dataclass(frozen=True)
 class PlpConfig:
-    """one Type-1 data PLP of a multi-PLP T2 frame (EN 302 755 8.3.6.3; the reference carries one,
-    lib/framemapperfint_cc_impl.cc:152-250): its FEC, constellation, time interleaver and input stream.
-    Quacks like T2Config for ts_for_frames / the per-PLP blocks."""
+    """one data PLP of a multi-PLP T2 frame (EN 302 755 8.3.6.3; the reference carries one Type-1 PLP with
+    TIME_IL_TYPE 0, lib/framemapperfint_cc_impl.cc:152-250): its FEC, constellation, time interleaver and
+    input stream.  plp_type 2: sub-sliced (MplpConfig.num_subslices).  ti_type 1: one TI block
+    (tiblocks = 1) of `fecblocks` FEC blocks per interleaving frame, spread over ti_frames (P_I) T2 frames
+    (EN 302 755 6.5).  Quacks like T2Config for ts_for_frames / the per-PLP blocks."""
     framesize: int
     rate: int
     constellation: int
@@ -105,6 +108,14 @@ class PlpConfig:
     inputmode: int = E.INPUTMODE_NORMAL
     inband: int = E.INBAND_OFF
     tsrate: int = 4000000
+    plp_type: int = 1
+    ti_type: int = 0
+    ti_frames: int = 1
+
+    @property
+    def if_frames(self):
+        """T2 frames per interleaving frame (P_I)"""
+        return self.ti_frames if self.ti_type else 1
 
     def bb_args(self):
         return (self.framesize, self.rate, self.inputmode, self.inband, self.fecblocks, self.tsrate)
@@ -113,14 +124,15 @@ class PlpConfig:
         return (self.framesize, self.rate, self.constellation, self.rotation)
 
     def plp_args(self):
+        """the dvbt2ll_plp_params layout (include/dvbt2ll_hip.h)"""
         return (self.framesize, self.rate, self.constellation, self.rotation, self.fecblocks, self.tiblocks,
-                self.inputmode, self.inband, self.tsrate)
+                self.inputmode, self.inband, self.tsrate, self.plp_type, self.ti_type, self.ti_frames)
 
 
 @dataclass(frozen=True)
 class MplpConfig:
-    """a T2 frame carrying len(plps) Type-1 data PLPs (PLP_ID = index, PLP 0's TS seed 1, PLP k's k + 1)
-    with the common (frame / L1 / OFDM) parameters"""
+    """a T2 frame carrying len(plps) data PLPs (PLP_ID = index, PLP 0's TS seed 1, PLP k's k + 1) with the
+    common (frame / L1 / OFDM) parameters; num_subslices = SUB_SLICES_PER_FRAME of its Type-2 PLPs"""
     name: str
     plps: tuple
     carriermode: int
@@ -138,10 +150,21 @@ class MplpConfig:
     misogroup: int = E.MISO_TX1
     equalization: int = E.EQUALIZATION_OFF
     bandwidth: int = E.BANDWIDTH_8_0_MHZ
+    num_subslices: int = 1
 
     @property
     def nplp(self):
         return len(self.plps)
+
+    @property
+    def unit_frames(self):
+        """T2 frames of the chain's launch unit: the least common multiple of the PLPs' interleaving-frame
+        lengths (every run covers whole interleaving frames of every PLP)"""
+        import math
+        u = 1
+        for p in self.plps:
+            u = u * p.if_frames // math.gcd(u, p.if_frames)
+        return u
 
     @property
     def vlength(self):
@@ -157,8 +180,8 @@ class MplpConfig:
         assert 1 <= self.nplp <= MAX_PLP
         a = list(self.common_args()) + [self.nplp]
         for k in range(MAX_PLP):
-            a += list(self.plps[k].plp_args()) if k < self.nplp else [0] * 9
-        return a
+            a += list(self.plps[k].plp_args()) if k < self.nplp else [0] * PLP_INTS
+        return a + [self.num_subslices]
 
     def pg_args(self):
         return (self.carriermode, self.fftsize, self.pilotpattern, self.guardinterval, self.numdatasyms,
@@ -225,12 +248,16 @@ def ts_for_frames(cfg, first_frame, nframes, seed=1):
     """TS bytes needed to encode T2 frames [first_frame, first_frame+nframes).  Returns
     (buffer, base_offset) where base_offset is the absolute stream offset of buffer[0]; the
     buffer starts one packet before the first packet touched so the CRC-8 of the preceding
-    packet is available (NM).  Payload per frame: F BBFRAME payloads, less the 13 in-band type
-    B bytes of the frame's first BBFRAME when in-band signalling is on (bbheader:327-355)."""
+    packet is available (NM).  Payload per interleaving frame (one T2 frame, or P_I of them for a
+    TIME_IL_TYPE 1 PLP): F BBFRAME payloads, less the 13 in-band type B bytes of its first BBFRAME
+    when in-band signalling is on (bbheader:327-355)."""
     hem = cfg.inputmode != E.INPUTMODE_NORMAL
+    P = getattr(cfg, "if_frames", 1)
+    assert first_frame % P == 0, "a run starts at an interleaving frame"
+    u0, u1 = first_frame // P, -(-(first_frame + nframes) // P)
     per_frame = cfg.fecblocks * payload_bytes_per_block(cfg) - (13 if cfg.inband != E.INBAND_OFF else 0)
-    start = payload_pos(first_frame * per_frame, hem)
-    end = payload_pos((first_frame + nframes) * per_frame, hem) + 1
+    start = payload_pos(u0 * per_frame, hem)
+    end = payload_pos(u1 * per_frame, hem) + 1
     p0 = max(0, start // 188 - 1)
     p1 = (end + 187) // 188
     return ts_packets(p0, p1 - p0, seed), p0 * 188
@@ -271,3 +298,42 @@ def _mplp_configs():
 
 
 MPLP_CONFIGS = _mplp_configs()
+
+
+def _if_configs():
+    """frames whose PLPs use EN 302 755 beyond the reference's one Type-1 TIME_IL_TYPE 0 PLP (SURVEY 8(f)
+    rank 4): TIME_IL_TYPE 1 (one TI block spread over P_I T2 frames) and sub-sliced Type-2 PLPs"""
+    c3, c1, c4, c5 = CONFIGS["cfg3"], CONFIGS["cfg1"], CONFIGS["cfg4"], CONFIGS["cfg5"]
+    return {
+        # cfg3's frame as one TIME_IL_TYPE 1 PLP: 390 FEC blocks in one TI block over P_I = 2 T2 frames (each
+        # T2 frame carries cfg3's 195 blocks' worth of cells; the frame boundary falls between TI rows)
+        "ti1_32k_p2": mplp_from(c3, "ti1-32kext-256qam3/5rot-PI2", [
+            _plp(c3, fecblocks=390, tiblocks=1, ti_type=1, ti_frames=2)]),
+        # cfg4's 8K frame as one TIME_IL_TYPE 1 PLP over P_I = 4 T2 frames (96 FEC blocks, HEM input), four T2
+        # frames per superframe
+        "ti1_8k_p4": mplp_from(c4, "ti1-8k-16qam1/2-PI4-hem", [
+            _plp(c4, fecblocks=96, tiblocks=1, ti_type=1, ti_frames=4, inputmode=E.INPUTMODE_HIEFF)]).with_(
+                t2frames=4),
+        # cfg3's frame as a Type-1 PLP (256-QAM 3/5 rotated) and a Type-2 PLP (64-QAM 2/3, in-band type B,
+        # v1.3.1) in 50 sub-slices
+        "t2sub_32k": mplp_from(c3, "t2sub-32kext-type1+type2x50", [
+            _plp(c3, fecblocks=100),
+            _plp(c3, rate=E.C2_3, constellation=E.MOD_64QAM, rotation=E.ROTATION_OFF, fecblocks=70, tiblocks=2,
+                 plp_type=2, inband=E.INBAND_ON, tsrate=5555555)]).with_(num_subslices=50, version=E.VERSION_131),
+        # the GRC's 4K short frame with both extensions at once: a Type-2 TIME_IL_TYPE 1 PLP (256-QAM 4/5 short,
+        # 4 FEC blocks over P_I = 2 frames: 405 TI rows, so the frame boundary cuts a row), a Type-1 QPSK PLP and
+        # a Type-2 16-QAM HEM PLP, 6 sub-slices
+        "mix_4k": mplp_from(c1, "mix-4k-short-type2PI2+type1+type2", [
+            _plp(c1, fecblocks=4, tiblocks=1, ti_type=1, ti_frames=2, plp_type=2),
+            _plp(c1, rate=E.C1_2, constellation=E.MOD_QPSK, rotation=E.ROTATION_OFF, fecblocks=1, tiblocks=1),
+            _plp(c1, rate=E.C3_5, constellation=E.MOD_16QAM, fecblocks=1, tiblocks=1, plp_type=2,
+                 inputmode=E.INPUTMODE_HIEFF)]).with_(num_subslices=6),
+        # 32K, two PLPs with different interleaving-frame lengths (P_I = 2 and 4: launch unit 4 frames)
+        "ti1_32k_p2p4": mplp_from(c5, "ti1-32k-PI2+PI4", [
+            _plp(c5, fecblocks=120, tiblocks=1, ti_type=1, ti_frames=2),
+            _plp(c5, rate=E.C1_2, constellation=E.MOD_16QAM, rotation=E.ROTATION_ON, fecblocks=200, tiblocks=1,
+                 ti_type=1, ti_frames=4)]).with_(t2frames=4),
+    }
+
+
+IF_CONFIGS = _if_configs()

@@ -13,15 +13,22 @@ import torch.distributed as dist
 from .configs import ts_for_frames
 
 
-def frame_range(total_frames, rank, world, first_frame=0):
-    """contiguous, ragged-safe split of [first_frame, first_frame + total_frames): (first, count)"""
-    base, extra = divmod(int(total_frames), int(world))
+def frame_range(total_frames, rank, world, first_frame=0, unit=1):
+    """contiguous, ragged-safe split of [first_frame, first_frame + total_frames): (first, count).  unit:
+    the chain's launch unit (dvbt2ll_chain_unit_frames: the least common multiple of its PLPs' interleaving-
+    frame lengths; a TIME_IL_TYPE 1 PLP's interleaving frame spans P_I T2 frames); every shard is whole units,
+    so first_frame and total_frames must be multiples of it"""
+    unit = int(unit)
+    if total_frames % unit or first_frame % unit:
+        raise ValueError("frames [%d, +%d) are not whole launch units of %d T2 frames"
+                         % (first_frame, total_frames, unit))
+    base, extra = divmod(int(total_frames) // unit, int(world))
     count = base + (1 if rank < extra else 0)
-    first = first_frame + rank * base + min(rank, extra)
-    return first, count
+    first = first_frame // unit + rank * base + min(rank, extra)
+    return first * unit, count * unit
 
 
-def gather_frames(local, total_frames, per_frame, group=None, dst=0):
+def gather_frames(local, total_frames, per_frame, group=None, dst=0, unit=1):
     """ordered gather of per-rank frame shards (local: [count * per_frame, ...] tensor) to rank dst,
     the chain's one exchange step: RCCL has no gather primitive, so every other rank
     sends its shard point-to-point (one grouped batch of isend / irecv, ncclGroupStart/End under the
@@ -31,8 +38,8 @@ def gather_frames(local, total_frames, per_frame, group=None, dst=0):
     empty-shard case has not run on a multi-GPU node)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    counts = [frame_range(total_frames, r, world)[1] for r in range(world)]
-    firsts = [frame_range(total_frames, r, world)[0] for r in range(world)]
+    counts = [frame_range(total_frames, r, world, unit=unit)[1] for r in range(world)]
+    firsts = [frame_range(total_frames, r, world, unit=unit)[0] for r in range(world)]
     assert local.shape[0] == counts[rank] * per_frame, "shard size mismatch"
     # every rank joins one collective first: under RCCL a grouped send/recv that is the group's
     # first operation and leaves some ranks out (empty shards) is undefined
@@ -58,20 +65,29 @@ def gather_frames(local, total_frames, per_frame, group=None, dst=0):
 
 
 def encode_sharded(chain, first_frame, total_frames, group=None, gather=True, seed=1):
-    """each rank encodes its contiguous share of the frames on its own GPU (synthetic TS slice
-    generated for exactly those frames); optional ordered gather of the IQ to rank 0."""
+    """each rank encodes its contiguous share of the frames -- whole launch units (interleaving frames) --
+    on its own GPU (synthetic TS slice generated for exactly those frames; a multi-PLP chain's PLP k uses
+    seed + k); optional ordered gather of the IQ to rank 0."""
+    from .configs import MplpConfig
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    first, count = frame_range(total_frames, rank, world, first_frame)
+    unit = getattr(chain, "unit_frames", 1)
+    first, count = frame_range(total_frames, rank, world, first_frame, unit)
     per = chain.iq_per_frame
     iq = torch.zeros((count * per, 2), dtype=torch.float32, device="cuda")
     if count:
         if count > chain.max_frames:
             raise ValueError("shard of %d frames exceeds chain max_frames %d" % (count, chain.max_frames))
-        ts, base = ts_for_frames(chain.cfg, first, count, seed)
-        ts_d = torch.from_numpy(ts).cuda()
-        chain.run_device(ts_d.data_ptr(), base, len(ts), first, count, iq.data_ptr(),
-                         torch.cuda.current_stream().cuda_stream)
+        st = torch.cuda.current_stream().cuda_stream
+        if isinstance(chain.cfg, MplpConfig):
+            tss = [ts_for_frames(p, first, count, seed + k) for k, p in enumerate(chain.cfg.plps)]
+            bufs = [torch.from_numpy(ts).cuda() for ts, _ in tss]
+            chain.run_plps([b.data_ptr() for b in bufs], [b for _, b in tss], [len(t) for t, _ in tss], first, count,
+                           iq.data_ptr(), st)
+        else:
+            ts, base = ts_for_frames(chain.cfg, first, count, seed)
+            ts_d = torch.from_numpy(ts).cuda()
+            chain.run_device(ts_d.data_ptr(), base, len(ts), first, count, iq.data_ptr(), st)
     if not gather:
         return iq
-    return gather_frames(iq, total_frames, per, group)
+    return gather_frames(iq, total_frames, per, group, unit=unit)

@@ -159,6 +159,10 @@ typedef struct {
   int64_t iq_samples_per_frame;
   int cell_size, stream_items, mapped_items, num_symbols, fft_size, guard_interval;
   int64_t cw_stride_bytes;     /* packed codeword stride in the internal buffer */
+  /* T2 frames per interleaving frame of the PLP (1, or P_I for TIME_IL_TYPE 1, dvbt2ll_plp_params);
+   * fec_blocks_per_frame and ts_bytes_per_frame then count one interleaving frame; stream_items stays
+   * the cells per T2 frame */
+  int frames_per_if;
 } dvbt2ll_chain_info;
 int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, dvbt2ll_chain **out);
 int dvbt2ll_chain_get_info(const dvbt2ll_chain *h, dvbt2ll_chain_info *info);
@@ -250,6 +254,18 @@ void dvbt2ll_chain_destroy(dvbt2ll_chain *h);
 #define DVBT2LL_MAX_PLP 8
 typedef struct {
   int framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, tsrate;
+  /* EN 302 755 beyond the reference's PLP (which is plp_type 1, ti_type 0, ti_frames 1,
+   * lib/framemapperfint_cc_impl.cc:159, 198-200; PARITY UNPINNED otherwise):
+   *   plp_type  1: Type-1 data PLP, one run of cells at its PLP_START (0 is read as 1);
+   *             2: Type-2 data PLP, cut into num_subslices sub-slices (8.3.6.3);
+   *   ti_type   TIME_IL_TYPE (6.5): 0 = one interleaving frame of fecblocks FEC blocks in tiblocks TI
+   *             blocks per T2 frame (the reference's); 1 = one TI block (tiblocks must be 1) of fecblocks
+   *             FEC blocks per interleaving frame, spread over ti_frames = P_I consecutive T2 frames
+   *             (TIME_IL_LENGTH = P_I, FRAME_INTERVAL 1): T2 frame i of interleaving frame m (frames
+   *             m P_I + i) carries TI output cells [i D, (i + 1) D), D = fecblocks x cell size / P_I;
+   *   ti_frames P_I (0 is read as 1; must be 1 for ti_type 0; fecblocks x cell size divisible by it).
+   * fecblocks is then PLP_NUM_BLOCKS: the FEC blocks of one interleaving frame. */
+  int plp_type, ti_type, ti_frames;
 } dvbt2ll_plp_params;
 typedef struct {
   /* the common (frame, L1, OFDM) fields of framemapperfint_cc::make */
@@ -257,6 +273,13 @@ typedef struct {
       version, preamble, reservedbiasbits, l1scrambled;
   int nplp;                                  /* 1 .. DVBT2LL_MAX_PLP */
   dvbt2ll_plp_params plp[DVBT2LL_MAX_PLP];   /* plp[k]: PLP_ID k */
+  /* SUB_SLICES_PER_FRAME of the Type-2 PLPs (0 is read as 1; must be 1 without Type-2 PLPs): the frame's
+   * data cells are the Type-1 PLPs back to back in PLP_ID order, then sub-slice 0 of every Type-2 PLP
+   * (PLP_ID order), sub-slice 1 of every Type-2 PLP, ...; each Type-2 PLP's cells per T2 frame divisible
+   * by it.  A chain whose PLPs have interleaving frames of several T2 frames runs whole launch units:
+   * first_frame and nframes multiples of the least common multiple of the PLPs' P_I
+   * (dvbt2ll_chain_unit_frames). */
+  int num_subslices;
 } dvbt2ll_mplp_params;
 
 /* one PLP of a multi-PLP frame: the BBHEADER of every later BBFRAME says MATYPE SIS/MIS = multiple
@@ -266,7 +289,9 @@ int dvbt2ll_bbheaderbch_set_isi(dvbt2ll_bbheaderbch *h, int isi);
 
 /* framemapperfint_cc with one input port per PLP (the per-PLP bbheaderbch -> ldpc -> interleavermod
  * chains feed port k with PLP k's cells): one T2 frame per general_work call, consuming
- * stream_items(k) cells from every port (framemapper:1942-1946, 2147 per port) */
+ * stream_items(k) cells from every port (framemapper:1942-1946, 2147 per port); a TIME_IL_TYPE 1 PLP's port
+ * instead delivers its whole interleaving frame (fecblocks x cell size cells) on the interleaving frame's
+ * first T2 frame and nothing on the other P_I - 1 (forecast and consumed say so per port) */
 typedef struct dvbt2ll_framemapper_mplp dvbt2ll_framemapper_mplp;
 int dvbt2ll_framemapper_mplp_create(const dvbt2ll_mplp_params *p, int device, dvbt2ll_framemapper_mplp **out);
 int dvbt2ll_framemapper_mplp_output_multiple(const dvbt2ll_framemapper_mplp *h);     /* mapped_items */
@@ -286,6 +311,10 @@ typedef struct {
 } dvbt2ll_mplp_chain_params;
 int dvbt2ll_chain_create_mplp(const dvbt2ll_mplp_chain_params *p, int device, dvbt2ll_chain **out);
 int dvbt2ll_chain_num_plps(const dvbt2ll_chain *h);
+/* T2 frames of the chain's launch unit: the least common multiple of its PLPs' interleaving-frame lengths
+ * (1 for TIME_IL_TYPE 0 PLPs).  Every run's first_frame and nframes are multiples of it (else
+ * DVBT2LL_EINVAL); create fails when max_frames is smaller. */
+int dvbt2ll_chain_unit_frames(const dvbt2ll_chain *h);
 /* PLP plp's FEC blocks, payload and TS bytes per frame, cell size, cells per frame (stream_items) and
  * codeword stride; the frame-wide fields as dvbt2ll_chain_get_info (which reports PLP 0's) */
 int dvbt2ll_chain_get_plp_info(const dvbt2ll_chain *h, int plp, dvbt2ll_chain_info *info);

@@ -544,23 +544,35 @@ int orc_im_work(orc_im *h, int nout, const uint8_t *in, float *out, int *consume
 #define KSIG_POST 350
 #define NBCH_PARITY 168
 
-/* One Type-1 data PLP of the frame.  The reference carries exactly one (framemapper:152-250:
+/* One data PLP of the frame.  The reference carries exactly one (framemapper:152-250:
  * num_plp = 1, plp_type = 1, time_il_type = 0, frame_interval = 1); this restatement generalises its
- * per-PLP state to nplp PLPs of EN 302 755 8.3.6.3 (PARITY UNPINNED beyond nplp = 1): PLP p has PLP_ID p,
- * its own FEC / constellation / cell interleaver / time interleaver, and its TI output occupies the
- * data cells [start, start + stream_items) after the L1 signalling, PLPs in PLP_ID order. */
+ * per-PLP state to nplp PLPs of EN 302 755 (PARITY UNPINNED beyond the reference's frame):
+ *  - PLP p has PLP_ID p, its own FEC / constellation / cell interleaver / time interleaver;
+ *  - 6.5 time interleaving, TIME_IL_TYPE 0 (the reference's): one interleaving frame (fec_blocks FEC
+ *    blocks in ti_blocks TI blocks) per T2 frame; TIME_IL_TYPE 1: one TI block of fec_blocks FEC blocks
+ *    per interleaving frame, spread over P_I = ti_frames consecutive T2 frames, T2 frame i of the
+ *    interleaving frame carrying the TI output cells [i D, (i + 1) D), D = fec_blocks cell_size / P_I
+ *    (FRAME_INTERVAL 1: the PLP is in every T2 frame; interleaving frame m = T2 frames m P_I ..);
+ *  - 8.3.6.3 mapping: Type-1 PLPs first, back to back in PLP_ID order, each one run of D cells at its
+ *    PLP_START; then the Type-2 PLPs, each cut into N_subslices sub-slices of D / N_subslices cells,
+ *    sub-slice j of every Type-2 PLP (PLP_ID order) before sub-slice j + 1 of any
+ *    (SUB_SLICE_INTERVAL = the Type-2 cells per T2 frame / N_subslices, TYPE_2_START = the Type-1 cells). */
 #define ORC_MAX_PLP 16
+#define ORC_PLP_INTS 11
 typedef struct {
-  int cell_size, stream_items, start, pn_degree;
+  int cell_size, stream_items, start, pn_degree;   /* stream_items: cells per T2 frame (D) */
   int ti_blocks, fec_blocks, small_fec, big_fec, n_big, n_small;
   int plp_cod, plp_mod, rotation, fec_type, inband_b, plp_mode;
+  int plp_type, ti_type, ti_frames, if_items, phase;   /* if_items = fec_blocks cell_size */
+  int ss, ss_off;                                      /* Type 2: sub-slice cells, offset in a sub-slice group */
   int *permutations;
-  cf *time_interleave;
+  cf *time_interleave, *ti_out;                        /* CI output, TI output of the interleaving frame */
 } orc_plp;
 
 struct orc_fm {
   int nplp, ksig_post;               /* ksig_post: L1-post signalling bits incl. CRC (KSIG_POST = 350 for one PLP) */
   orc_plp plp[ORC_MAX_PLP];
+  int nss, ssi, t2start, ntype2;     /* SUB_SLICES_PER_FRAME, SUB_SLICE_INTERVAL, TYPE_2_START, Type-2 PLPs */
   int stream_items, mapped_items, l1_constellation, eta_mod, t2_frames, t2_frame_num;
   int l1_scrambled, N_P2, C_P2, N_FC, C_FC, C_DATA, N_post, N_punc, num_data_symbols;
   /* L1 fields that are not constant (framemapper ctor :114-250) */
@@ -646,7 +658,7 @@ static void add_l1pre(orc_fm *h, cf *out) {
 static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
   uint8_t info[FRAME_SIZE_SHORT], t[FRAME_SIZE_SHORT], map[KBCH_1_2];
   int o = 0;
-  put_bits(info, &o, 1, 15);                 /* SUB_SLICES_PER_FRAME */
+  put_bits(info, &o, (unsigned)h->nss, 15);  /* SUB_SLICES_PER_FRAME (1 without Type-2 PLPs) */
   put_bits(info, &o, (unsigned)h->nplp, 8);  /* NUM_PLP */
   put_bits(info, &o, 0, 4);                  /* NUM_AUX */
   put_bits(info, &o, 0, 8);                  /* AUX_CONFIG_RFU */
@@ -655,7 +667,7 @@ static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
   for (int p = 0; p < h->nplp; p++) {
     const orc_plp *q = &h->plp[p];
     put_bits(info, &o, (unsigned)p, 8);      /* PLP_ID */
-    put_bits(info, &o, 1, 3);                /* PLP_TYPE: data type 1 */
+    put_bits(info, &o, (unsigned)q->plp_type, 3);   /* PLP_TYPE: data type 1 (001) or 2 (010) */
     put_bits(info, &o, 3, 5);                /* PLP_PAYLOAD_TYPE: TS */
     info[o++] = 0;                           /* FF_FLAG */
     put_bits(info, &o, 0, 3);                /* FIRST_RF_IDX */
@@ -666,9 +678,10 @@ static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
     info[o++] = (uint8_t)q->rotation;
     put_bits(info, &o, (unsigned)q->fec_type, 2);
     put_bits(info, &o, (unsigned)q->fec_blocks, 10);   /* PLP_NUM_BLOCKS_MAX */
-    put_bits(info, &o, 1, 8);                /* FRAME_INTERVAL */
-    put_bits(info, &o, (unsigned)q->ti_blocks, 8);     /* TIME_IL_LENGTH */
-    info[o++] = 0;                           /* TIME_IL_TYPE */
+    put_bits(info, &o, 1, 8);                /* FRAME_INTERVAL (I_JUMP) */
+    /* TIME_IL_LENGTH: N_TI (type 0) or P_I (type 1), EN 302 755 7.2.3.1 */
+    put_bits(info, &o, (unsigned)(q->ti_type ? q->ti_frames : q->ti_blocks), 8);
+    info[o++] = (uint8_t)q->ti_type;         /* TIME_IL_TYPE */
     info[o++] = 0;                           /* IN_BAND_A_FLAG */
     info[o++] = (uint8_t)q->inband_b;
     put_bits(info, &o, (unsigned)h->post_reserved1, 11);
@@ -679,8 +692,8 @@ static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
   put_bits(info, &o, 0, 2);                  /* FEF_LENGTH_MSB */
   put_bits(info, &o, (unsigned)h->post_reserved2, 30);
   put_bits(info, &o, (unsigned)t2_frame_num, 8);         /* FRAME_IDX */
-  put_bits(info, &o, 0, 22);                 /* SUB_SLICE_INTERVAL */
-  put_bits(info, &o, 0, 22);                 /* TYPE_2_START */
+  put_bits(info, &o, (unsigned)h->ssi, 22);      /* SUB_SLICE_INTERVAL (0 without Type-2 PLPs) */
+  put_bits(info, &o, (unsigned)h->t2start, 22);  /* TYPE_2_START (0 without Type-2 PLPs) */
   put_bits(info, &o, 0, 8);                  /* L1_CHANGE_COUNTER */
   put_bits(info, &o, 0, 3);                  /* START_RF_IDX */
   put_bits(info, &o, (unsigned)h->post_reserved3, 8);
@@ -688,7 +701,7 @@ static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
     /* PLP_ID (dynamic): the reference's plp_id_dynamic is never set, i.e. 0 for its one PLP */
     put_bits(info, &o, (unsigned)p, 8);
     put_bits(info, &o, (unsigned)h->plp[p].start, 22);       /* PLP_START (cell address after L1) */
-    put_bits(info, &o, (unsigned)h->plp[p].fec_blocks, 10);  /* PLP_NUM_BLOCKS */
+    put_bits(info, &o, (unsigned)h->plp[p].fec_blocks, 10);  /* PLP_NUM_BLOCKS (of the interleaving frame) */
     put_bits(info, &o, (unsigned)h->post_reserved4, 8);
   }
   put_bits(info, &o, (unsigned)h->post_reserved5, 8);
@@ -802,13 +815,14 @@ static void active_counts(int fft, int carriermode, int pp, int papr, int gi, in
   }
 }
 
-/* framemapperfint ctor (framemapper:41-1190) for nplp Type-1 PLPs; plp: nplp x 8 ints per PLP
- * {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband} */
-orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int carriermode, int fftsize, int guardinterval,
-                           int l1constellation, int pilotpattern, int t2frames, int numdatasyms, int paprmode,
-                           int version, int preamble, int reservedbiasbits, int l1scrambled) {
+/* framemapperfint ctor (framemapper:41-1190) for nplp data PLPs; plp: nplp x ORC_PLP_INTS ints per PLP
+ * {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, plp_type (1, 2),
+ * ti_type (0, 1), ti_frames (P_I)}; num_subslices: SUB_SLICES_PER_FRAME (1 without Type-2 PLPs) */
+orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int num_subslices, int carriermode, int fftsize,
+                           int guardinterval, int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
+                           int paprmode, int version, int preamble, int reservedbiasbits, int l1scrambled) {
   int fft = fft_points(fftsize);
-  if (!fft || t2frames < 1 || nplp < 1 || nplp > ORC_MAX_PLP) return NULL;
+  if (!fft || t2frames < 1 || nplp < 1 || nplp > ORC_MAX_PLP || num_subslices < 1) return NULL;
   orc_fm *h = (orc_fm *)calloc(1, sizeof(orc_fm));
   int siso = preamble == PREAMBLE_T2_SISO || preamble == PREAMBLE_T2_LITE_SISO;
   int v131 = version == VERSION_131, resv = reservedbiasbits && v131;
@@ -817,13 +831,22 @@ orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int carriermode, int fftsiz
   /* KSIG_POST = 350 bits for one PLP (framemapperfint_cc_impl.h:32); each further PLP adds its 89
    * configurable (:1577-1639) and 48 dynamic (:1672-1687) bits */
   h->ksig_post = KSIG_POST + (nplp - 1) * (89 + 48);
+  h->nss = num_subslices;
   for (int p = 0; p < nplp; p++) {
-    const int *q = plp + 8 * p;
+    const int *q = plp + ORC_PLP_INTS * p;
     orc_plp *d = &h->plp[p];
     if (q[4] < 1 || q[2] < 0 || q[2] > 3) { orc_fm_destroy(h); return NULL; }
     d->cell_size = q[0] == FECFRAME_NORMAL ? cs_n[q[2]] : cs_s[q[2]];
     d->fec_blocks = q[4];
     d->ti_blocks = q[5];
+    d->plp_type = q[8];
+    d->ti_type = q[9];
+    d->ti_frames = q[10];
+    /* type 1 interleaving: one TI block spread over P_I >= 1 frames; type 0: P_I = 1 */
+    if ((d->plp_type != 1 && d->plp_type != 2) || (d->ti_type != 0 && d->ti_type != 1) || d->ti_frames < 1 ||
+        (d->ti_type == 0 && d->ti_frames != 1) || (d->ti_type == 1 && d->ti_blocks != 1) ||
+        ((long)d->fec_blocks * d->cell_size) % d->ti_frames) { orc_fm_destroy(h); return NULL; }
+    if (d->plp_type == 2) h->ntype2++;
     /* L1-post fields of the PLP (framemapper:165-221) */
     d->plp_cod = q[1];                         /* C1_2..C5_6 -> 0..5, C1_3 -> 6, C2_5 -> 7 (:165-193) */
     d->plp_mod = q[2];
@@ -964,11 +987,31 @@ orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int carriermode, int fftsiz
       d->n_big = d->fec_blocks % d->ti_blocks;
       d->n_small = d->ti_blocks - d->n_big;
     }
-    d->stream_items = cs * d->fec_blocks;
-    d->start = h->stream_items;                /* PLP_START: PLPs back to back after the L1 signalling */
-    h->stream_items += d->stream_items;
-    d->time_interleave = (cf *)calloc((size_t)d->stream_items, sizeof(cf));
+    d->if_items = cs * d->fec_blocks;
+    d->stream_items = d->if_items / d->ti_frames;
+    d->time_interleave = (cf *)calloc((size_t)d->if_items, sizeof(cf));
+    d->ti_out = (cf *)calloc((size_t)d->if_items, sizeof(cf));
   }
+  /* 8.3.6.3: Type-1 PLPs back to back in PLP_ID order, then the sub-sliced Type-2 PLPs */
+  if (!h->ntype2 && num_subslices != 1) { orc_fm_destroy(h); return NULL; }
+  for (int p = 0; p < nplp; p++)
+    if (h->plp[p].plp_type == 1) {
+      h->plp[p].start = h->stream_items;         /* PLP_START: the cells before it */
+      h->stream_items += h->plp[p].stream_items;
+    }
+  h->t2start = h->ntype2 ? h->stream_items : 0;
+  for (int p = 0, off = 0; p < nplp; p++) {
+    orc_plp *d = &h->plp[p];
+    if (d->plp_type != 2) continue;
+    if (d->stream_items % num_subslices) { orc_fm_destroy(h); return NULL; }
+    d->ss = d->stream_items / num_subslices;
+    d->ss_off = off;
+    d->start = h->stream_items + off;           /* PLP_START: its first sub-slice */
+    off += d->ss;
+    h->ssi = off;                               /* SUB_SLICE_INTERVAL */
+  }
+  for (int p = 0; p < nplp; p++)
+    if (h->plp[p].plp_type == 2) h->stream_items += h->plp[p].stream_items;
   if (h->N_FC == 0) { h->mapped_items = h->N_P2 * h->C_P2 + numdatasyms * h->C_DATA; h->num_data_symbols = numdatasyms; }
   else { h->mapped_items = h->N_P2 * h->C_P2 + (numdatasyms - 1) * h->C_DATA + h->N_FC; h->num_data_symbols = numdatasyms - 1; }
   int fixed = h->stream_items + 1840 + h->N_post / h->eta_mod + (h->N_FC - h->C_FC);
@@ -996,8 +1039,9 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
                       int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
                       int paprmode, int version, int preamble, int inputmode,
                       int reservedbiasbits, int l1scrambled, int inband) {
-  const int plp[8] = {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband};
-  return orc_fm_create_mplp(1, plp, carriermode, fftsize, guardinterval, l1constellation, pilotpattern, t2frames,
+  const int plp[ORC_PLP_INTS] = {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband,
+                                 1, 0, 1};
+  return orc_fm_create_mplp(1, plp, 1, carriermode, fftsize, guardinterval, l1constellation, pilotpattern, t2frames,
                             numdatasyms, paprmode, version, preamble, reservedbiasbits, l1scrambled);
 }
 int orc_fm_stream_items(const orc_fm *h) { return h->stream_items; }
@@ -1005,13 +1049,25 @@ int orc_fm_mapped_items(const orc_fm *h) { return h->mapped_items; }
 int orc_fm_l1post_cells(const orc_fm *h) { return h->N_post / h->eta_mod; }
 void orc_fm_destroy(orc_fm *h) {
   if (!h) return;
-  for (int p = 0; p < ORC_MAX_PLP; p++) { free(h->plp[p].permutations); free(h->plp[p].time_interleave); }
+  for (int p = 0; p < ORC_MAX_PLP; p++) {
+    free(h->plp[p].permutations); free(h->plp[p].time_interleave); free(h->plp[p].ti_out);
+  }
   free(h->Heven); free(h->Hodd); free(h->HevenP2); free(h->HoddP2); free(h->HevenFC); free(h->HoddFC);
   free(h->cell_out); free(h->frame_out); free(h->zigzag); free(h->dummy); free(h);
 }
 
-/* general_work (framemapper:1948-2151), exactly one T2 frame: in = each PLP's stream_items cells,
- * PLPs in order */
+void orc_fm_seek(orc_fm *h, long frame) {
+  h->t2_frame_num = (int)(frame % h->t2_frames);
+  for (int p = 0; p < h->nplp; p++) h->plp[p].phase = (int)(frame % h->plp[p].ti_frames);
+}
+
+int orc_fm_consume(const orc_fm *h, int plp) {
+  if (plp < 0 || plp >= h->nplp) return 0;
+  return h->plp[plp].phase == 0 ? h->plp[plp].if_items : 0;
+}
+
+/* general_work (framemapper:1948-2151), exactly one T2 frame: in = the cells each PLP consumes this
+ * frame (orc_fm_consume: a whole interleaving frame on its first T2 frame, else none), PLPs in order */
 int orc_fm_work(orc_fm *h, const float *inf, float *outf) {
   const cf *in = (const cf *)inf;
   cf *out = (cf *)outf;
@@ -1020,37 +1076,48 @@ int orc_fm_work(orc_fm *h, const float *inf, float *outf) {
   for (int p = 0; p < h->nplp; p++) {
     orc_plp *d = &h->plp[p];
     int cs = d->cell_size;
-    /* cell interleaver :1973-1998 */
-    int cell_index = 0;
-    for (int s = 0; s < d->n_small + d->n_big; s++) {
-      int n = 0;
-      int fpt = s < d->n_small ? d->small_fec : d->big_fec;
-      for (int r = 0; r < fpt; r++) {
-        int shift = cs;
-        while (shift >= cs) {
-          int temp = n;
-          shift = 0;
-          for (int b = 0; b < d->pn_degree; b++) { shift |= temp & 1; shift <<= 1; temp >>= 1; }
-          n++;
-        }
-        for (int w = 0; w < cs; w++) d->time_interleave[((d->permutations[w] + shift) % cs) + cell_index] = *in++;
-        cell_index += cs;
-      }
-    }
-    /* time interleaver :1999-2028, into the PLP's cells of the frame */
-    cf *cellout = h->cell_out + d->start;
-    if (d->ti_blocks != 0) {
-      int ti_index = 0;
+    if (d->phase == 0) {   /* a new interleaving frame: cell + time interleave it (framemapper:1973-2028) */
+      /* cell interleaver :1973-1998 */
+      int cell_index = 0;
       for (int s = 0; s < d->n_small + d->n_big; s++) {
+        int n = 0;
         int fpt = s < d->n_small ? d->small_fec : d->big_fec;
-        int ncols = 5 * fpt, rows = cs / 5;
-        for (int k = 0; k < rows; k++)
-          for (int w = 0; w < ncols; w++) *cellout++ = d->time_interleave[rows * w + ti_index + k];
-        ti_index += rows * ncols;
+        for (int r = 0; r < fpt; r++) {
+          int shift = cs;
+          while (shift >= cs) {
+            int temp = n;
+            shift = 0;
+            for (int b = 0; b < d->pn_degree; b++) { shift |= temp & 1; shift <<= 1; temp >>= 1; }
+            n++;
+          }
+          for (int w = 0; w < cs; w++) d->time_interleave[((d->permutations[w] + shift) % cs) + cell_index] = *in++;
+          cell_index += cs;
+        }
       }
-    } else {
-      for (int w = 0; w < d->stream_items; w++) *cellout++ = d->time_interleave[w];
+      /* time interleaver :1999-2028, into the interleaving frame's TI output */
+      cf *cellout = d->ti_out;
+      if (d->ti_blocks != 0) {
+        int ti_index = 0;
+        for (int s = 0; s < d->n_small + d->n_big; s++) {
+          int fpt = s < d->n_small ? d->small_fec : d->big_fec;
+          int ncols = 5 * fpt, rows = cs / 5;
+          for (int k = 0; k < rows; k++)
+            for (int w = 0; w < ncols; w++) *cellout++ = d->time_interleave[rows * w + ti_index + k];
+          ti_index += rows * ncols;
+        }
+      } else {
+        for (int w = 0; w < d->if_items; w++) *cellout++ = d->time_interleave[w];
+      }
     }
+    /* this T2 frame's share of the TI output into the PLP's cells of the frame (8.3.6.3) */
+    const cf *src = d->ti_out + (size_t)d->phase * d->stream_items;
+    if (d->plp_type == 1) {
+      for (int c = 0; c < d->stream_items; c++) h->cell_out[d->start + c] = src[c];
+    } else {
+      for (int c = 0; c < d->stream_items; c++)
+        h->cell_out[h->t2start + (c / d->ss) * h->ssi + d->ss_off + c % d->ss] = src[c];
+    }
+    d->phase = (d->phase + 1) % d->ti_frames;
   }
   /* frame assembly :2029-2103 */
   cf *dst = h->N_P2 == 1 ? h->frame_out : h->zigzag;

@@ -62,17 +62,27 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
                       int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
                       int paprmode, int version, int preamble, int inputmode,
                       int reservedbiasbits, int l1scrambled, int inband);
-/* nplp Type-1 data PLPs in one T2 frame (EN 302 755 8.3.6.3; the reference carries one,
- * framemapper:152-250; PARITY UNPINNED for nplp > 1): plp = nplp x {framesize, rate, constellation,
- * rotation, fecblocks, tiblocks, inputmode, inband}; the other arguments are the common fields.
- * orc_fm_work's input is one frame of every PLP's cells, PLP 0 first. */
-orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int carriermode, int fftsize, int guardinterval,
-                           int l1constellation, int pilotpattern, int t2frames, int numdatasyms, int paprmode,
-                           int version, int preamble, int reservedbiasbits, int l1scrambled);
+/* nplp data PLPs in one T2 frame (EN 302 755 6.5, 8.3.6.3; the reference carries one Type-1 PLP with
+ * TIME_IL_TYPE 0, framemapper:152-250; PARITY UNPINNED beyond that frame): plp = nplp x
+ * {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, plp_type (1 | 2),
+ * ti_type (TIME_IL_TYPE 0 | 1), ti_frames (P_I: 1 for type 0; type 1: one TI block, tiblocks = 1, of
+ * fecblocks FEC blocks spread over P_I T2 frames)}; num_subslices = SUB_SLICES_PER_FRAME of the Type-2
+ * PLPs (1 without any); the other arguments are the common fields. */
+orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int num_subslices, int carriermode, int fftsize,
+                           int guardinterval, int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
+                           int paprmode, int version, int preamble, int reservedbiasbits, int l1scrambled);
 int orc_fm_l1post_cells(const orc_fm *h);
+/* data cells per T2 frame (every PLP) */
 int orc_fm_stream_items(const orc_fm *h);
 int orc_fm_mapped_items(const orc_fm *h);
-/* one T2 frame: stream_items cells in -> mapped_items cells out; returns mapped_items */
+/* cells PLP plp consumes at the next orc_fm_work: its whole interleaving frame (fecblocks x cell size) on
+ * the first T2 frame of the interleaving frame, else 0 */
+int orc_fm_consume(const orc_fm *h, int plp);
+/* the state at absolute T2 frame `frame` (t2_frame_num = frame mod t2frames; every PLP at frame mod P_I of
+ * its interleaving frame -- the next work call must start interleaving frames of the PLPs it consumes) */
+void orc_fm_seek(orc_fm *h, long frame);
+/* one T2 frame: the consumed cells of every PLP (PLP 0 first) in -> mapped_items cells out; returns
+ * mapped_items */
 int orc_fm_work(orc_fm *h, const float *in, float *out);
 void orc_fm_destroy(orc_fm *h);
 

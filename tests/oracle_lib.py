@@ -32,7 +32,9 @@ def lib():
         L.orc_bb_destroy.argtypes = [vp]
         L.orc_bb_set_isi.argtypes = [vp, ci]
         L.orc_fm_create_mplp.restype = vp
-        L.orc_fm_create_mplp.argtypes = [ci, vp] + [ci] * 12
+        L.orc_fm_create_mplp.argtypes = [ci, vp] + [ci] * 13
+        L.orc_fm_consume.argtypes = [vp, ci]
+        L.orc_fm_seek.argtypes = [vp, ctypes.c_long]
         L.orc_fm_l1post_cells.argtypes = [vp]
         L.orc_ldpc_create.restype = vp
         L.orc_ldpc_create.argtypes = [ci, ci]
@@ -152,33 +154,45 @@ class FM:
 
 
 class FMM(FM):
-    """framemapperfint for a multi-PLP frame (orc_fm_create_mplp; parity unpinned beyond one PLP): work()
-    takes one frame of every PLP's cells, PLP 0 first"""
+    """framemapperfint for a multi-PLP frame (orc_fm_create_mplp; parity unpinned beyond the reference's one
+    Type-1 PLP): work() takes the cells every PLP consumes this T2 frame (consume(k): a whole interleaving
+    frame on its first T2 frame, else none), PLP 0 first"""
     def __init__(self, mcfg):
-        plp = np.array([list(p.plp_args()[:8]) for p in mcfg.plps], np.int32).reshape(-1)
+        plp = np.array([list(p.plp_args()[:8]) + [p.plp_type, p.ti_type, p.ti_frames] for p in mcfg.plps],
+                       np.int32).reshape(-1)
         self._plp = plp
-        self.h = lib().orc_fm_create_mplp(mcfg.nplp, _p(plp), *mcfg.common_args())
+        self.h = lib().orc_fm_create_mplp(mcfg.nplp, _p(plp), mcfg.num_subslices, *mcfg.common_args())
         assert self.h, "oracle multi-PLP framemapper create failed"
         self.stream_items = lib().orc_fm_stream_items(self.h)
         self.mapped_items = lib().orc_fm_mapped_items(self.h)
         self.l1post_cells = lib().orc_fm_l1post_cells(self.h)
 
+    def consume(self, k):
+        return lib().orc_fm_consume(self.h, k)
+
+    def seek(self, frame):
+        """start at absolute T2 frame `frame` (a launch unit boundary)"""
+        lib().orc_fm_seek(self.h, int(frame))
+
 
 def mplp_cells(mcfg, first_frame, nframes):
-    """oracle per-PLP chain up to the framemapper input: for each frame, the PLPs' cells concatenated
-    (PLP k: TS seed k + 1, BBHEADER MIS with ISI = k when nplp > 1); returns (list of per-frame cell
-    arrays, per-PLP BB bits and codewords of the frames)"""
+    """oracle per-PLP chain up to the framemapper input: for each T2 frame, the cells the PLPs consume
+    there, concatenated (PLP k: TS seed k + 1, BBHEADER MIS with ISI = k when nplp > 1; a TIME_IL_TYPE 1
+    PLP delivers its interleaving frame's F FEC blocks on the first of its P_I T2 frames and nothing on
+    the others); returns (list of per-frame cell arrays, per-PLP BB bits and codewords of the
+    interleaving frames starting in the frames)"""
     from dvbt2ll.configs import ts_for_frames
+    assert first_frame % mcfg.unit_frames == 0
     frames = [[] for _ in range(nframes)]
     bb_bits, codewords = [], []
     for k, p in enumerate(mcfg.plps):
-        F = p.fecblocks
+        F, P = p.fecblocks, p.if_frames
         bb = BB(*p.bb_args(), isi=k if mcfg.nplp > 1 else None)
         ld, im = LDPC(p.framesize, p.rate), IM(*p.im_args())
         ts, base = ts_for_frames(p, 0, first_frame + nframes, seed=k + 1)
         off = 0
         bits_k, cw_k = [], []
-        for f in range(first_frame + nframes):
+        for f in range(0, first_frame + nframes, P):
             bits, c = bb.work(ts[off:], F)
             off += c
             if f >= first_frame:
@@ -188,7 +202,7 @@ def mplp_cells(mcfg, first_frame, nframes):
                 frames[f - first_frame].append(im.work(cw, F))
         bb_bits.append(bits_k)
         codewords.append(cw_k)
-    return [np.concatenate(c) for c in frames], bb_bits, codewords
+    return [np.concatenate(c) if c else np.zeros(0, np.complex64) for c in frames], bb_bits, codewords
 
 
 class PG:

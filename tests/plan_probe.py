@@ -36,6 +36,7 @@ def lib():
         L.t2probe_frame_mplp.argtypes = [vp] * 5
         L.t2probe_chain_mplp.argtypes = [vp] * 10
         L.t2probe_l1post_mplp.argtypes = [vp, ctypes.c_int, vp, vp]
+        L.t2probe_l1post_bits_mplp.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int]
         _L = L
     return _L
 
@@ -223,18 +224,21 @@ def stored_to_natural(row, N, split):
 def frame_plan_mplp(mcfg):
     """the planner's multi-PLP frame (build_frame_mplp): gather maps, aux variants, PLP geometry"""
     a = np.array(mcfg.mplp_array(), np.int32)
-    info = np.zeros(31, np.int32)
+    info = np.zeros(68, np.int32)
     if lib().t2probe_frame_mplp(_p(a), _p(info), None, None, None):
         return None
     M, S, aux_len, t2frames = (int(x) for x in info[:4])
-    gin = np.zeros(M, np.int32)
+    unit = int(info[31])
+    gin = np.zeros(unit * M, np.int32)
     gd = np.zeros(M, np.int32)
     aux = np.zeros(t2frames * aux_len, np.complex64)
     assert lib().t2probe_frame_mplp(_p(a), _p(info), _p(gin), _p(gd), _p(aux)) == 0
     n = int(info[6])
+    lst = lambda o: [int(x) for x in info[o:o + n]]   # noqa: E731
     return dict(M=M, S=S, aux_len=aux_len, t2frames=t2frames, Lp=int(info[4]), D=int(info[5]), nplp=n,
-                start=[int(x) for x in info[7:7 + n]], cs=[int(x) for x in info[15:15 + n]],
-                F=[int(x) for x in info[23:23 + n]], gather_in=gin, gather_d=gd, aux=aux.reshape(t2frames, aux_len))
+                start=lst(7), cs=lst(15), F=lst(23), unit=unit, nss=int(info[32]), ssi=int(info[33]),
+                t2start=int(info[34]), S_in=int(info[35]), plp_S=lst(36), P=lst(44), in_off=lst(52), type2=lst(60),
+                gather_in=gin.reshape(unit, M), gather_d=gd, aux=aux.reshape(t2frames, aux_len))
 
 
 def chain_layout_mplp(mcfg):
@@ -253,6 +257,15 @@ def chain_layout_mplp(mcfg):
                                     _p(bnd)) == 0
     return dict(Nsym=Nsym, N=N, S=S, split=int(info[3]), nplp=P, cmap=cmap.reshape(Nsym, N), inv=inv, d0=d0,
                 dn=dn, dn0=dn0, part=part, bnd=bnd.reshape(2 * Nsym, P + 1), frame=fr)
+
+
+def l1post_bits_mplp(mcfg, frame_idx):
+    """the planner's L1-post signalling bits before the CRC-32 (one per byte)"""
+    a = np.array(mcfg.mplp_array(), np.int32)
+    out = np.zeros(4096, np.uint8)
+    n = lib().t2probe_l1post_bits_mplp(_p(a), int(frame_idx), _p(out), len(out))
+    assert n > 0
+    return out[:n]
 
 
 def l1post_mplp(mcfg, frame_idx):

@@ -79,3 +79,51 @@ def test_gloo_ordered_gather(total, world):
         p.join(180)
         assert p.exitcode == 0
     assert q.get(timeout=5)
+
+
+def _if_worker(rank, world, port, total, q):
+    """TIME_IL_TYPE 1 sharding: each rank encodes its whole launch units (interleaving frames of P_I = 2 T2
+    frames) from scratch -- its PLPs' TS slices and the oracle framemapper seeked to its first frame -- and
+    the ordered gather equals the sequential run"""
+    import sys
+    sys.path[:0] = [os.path.join(os.path.dirname(__file__)),
+                    os.path.join(os.path.dirname(__file__), "..", "gr-dvbt2ll_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle_lib as O
+        from dvbt2ll.configs import IF_CONFIGS
+        m = IF_CONFIGS["mix_4k"]
+        u = m.unit_frames
+        first, count = D.frame_range(total, rank, world, unit=u)
+        fm = O.FMM(m)
+        fm.seek(first)
+        cells, _, _ = O.mplp_cells(m, first, count)
+        mine = np.stack([fm.work(c) for c in cells]) if count else np.zeros((0, fm.mapped_items), np.complex64)
+        per = fm.mapped_items
+        local = torch.from_numpy(mine.reshape(-1).view(np.float32).reshape(-1, 2).copy())
+        got = D.gather_frames(local, total, per, unit=u)
+        if rank == 0:
+            seq = O.FMM(m)
+            want = np.stack([seq.work(c) for c in O.mplp_cells(m, 0, total)[0]])
+            q.put(bool(np.array_equal(got.numpy(), want.reshape(-1).view(np.float32).reshape(-1, 2))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total,world", [(6, 2), (4, 3)])
+def test_gloo_if_sharded_equals_sequential(total, world):
+    """mix_4k (a P_I = 2 Type-2 PLP beside two type-0 PLPs): shards of whole interleaving frames, ragged
+    (6 frames over 2 ranks: 4 + 2) and with an empty shard (4 frames over 3 ranks)"""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_if_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    assert q.get(timeout=5)

@@ -37,7 +37,7 @@ def test_mplp_frame_matches_oracle(name):
     for f in range(min(3, m.t2frames + 1)):
         cells = (rng.standard_normal(fr["S"]) + 1j * rng.standard_normal(fr["S"])).astype(np.complex64)
         want = fm.work(cells)
-        got = _apply(fr["gather_in"], cells, fr["aux"][f % m.t2frames])
+        got = _apply(fr["gather_in"][0], cells, fr["aux"][f % m.t2frames])
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg="%s frame %d" % (name, f))
 
 
@@ -57,7 +57,7 @@ def test_one_plp_is_the_reference_frame():
     m = mplp_from(c, "one", [_plp(c)])
     fr1 = PP.frame_plan(c.fm_args())
     frm = PP.frame_plan_mplp(m)
-    np.testing.assert_array_equal(fr1["gather_in"], frm["gather_in"])
+    np.testing.assert_array_equal(fr1["gather_in"], frm["gather_in"][0])
     np.testing.assert_array_equal(fr1["aux"].view(np.uint32), frm["aux"].view(np.uint32))
     cells = (rng.standard_normal(fr1["S"]) + 1j * rng.standard_normal(fr1["S"])).astype(np.complex64)
     np.testing.assert_array_equal(O.FM(*c.fm_args()).work(cells).view(np.uint32), O.FMM(m).work(cells).view(np.uint32))
