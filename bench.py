@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-latency", action="store_true", help="skip the one-frame latency calls")
     ap.add_argument("--no-blocks", action="store_true", help="skip the per-block general_work timing")
     ap.add_argument("--no-mplp", action="store_true", help="skip the secondary multi-PLP (2-PLP 32K frame) timing")
+    ap.add_argument("--no-host", action="store_true", help="skip the secondary host-delivered (streaming host path) "
+                                                           "timing")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--shard", choices=("frames", "streams"), default="frames",
                     help="frames: one TS stream, disjoint frame ranges per rank; streams: an independent "
@@ -453,6 +455,103 @@ def mplp_rate(frames, steps, warmup, name="mplp2_32k"):
                     "one stream, no cross-step overlap; not `value`"}
 
 
+def pcie_peaks(nbytes=1 << 30, reps=5):
+    """page-locked copy rates of this box (GB/s): device -> host, host -> device, and both at once on two
+    streams (the denominators of host_delivered's fractions)"""
+    import torch
+    dev = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    dev2 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    host2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def rate(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return reps * nbytes / (time.perf_counter() - t0) / 1e9
+
+    def both():
+        with torch.cuda.stream(s1):
+            host.copy_(dev, non_blocking=True)
+        with torch.cuda.stream(s2):
+            dev2.copy_(host2, non_blocking=True)
+    d2h = rate(lambda: host.copy_(dev, non_blocking=True))
+    h2d = rate(lambda: dev.copy_(host, non_blocking=True))
+    bidir = rate(both)
+    del dev, dev2, host, host2
+    return {"d2h_GBs": d2h, "h2d_GBs": h2d, "bidirectional_GBs_each_way": bidir,
+            "note": "1 GiB page-locked copies, torch (hipMemcpyAsync), %d reps each" % reps}
+
+
+def host_delivered(cfg, chunk, chunks, peaks):
+    """secondary (not `value`): the streaming host path -- host TS in, host IQ out -- through
+    dvbt2ll_chain_host_submit / _host_wait (a ring of DVBT2LL_HOST_RING submissions on copy-in / compute /
+    copy-out streams), page-locked buffers, chunk frames per submission, the sink's ring of three host IQ
+    buffers recycled as a sink would consume them; cf32 and sc16 (x0.2).  Rates are samples delivered
+    into host memory per second of wall time, PCIe bytes moved per second, and their fraction of the box's
+    page-locked D2H copy rate"""
+    import torch
+    import dvbt2ll
+    from dvbt2ll.configs import ts_for_frames
+    ch = dvbt2ll.Chain(cfg, max_frames=chunk)
+    per = ch.iq_per_frame
+    n = chunk * chunks
+    ts, base = ts_for_frames(cfg, 0, n)
+    ts_pin = torch.from_numpy(ts).pin_memory()
+    out = {}
+    for fmt, name in ((dvbt2ll.IQ_CF32, "cf32"), (dvbt2ll.IQ_SC16, "sc16_x0.2")):
+        ch.set_output(0.2 if fmt == dvbt2ll.IQ_SC16 else 1.0, fmt)
+        sb = 4 if fmt == dvbt2ll.IQ_SC16 else 8
+        ring = [torch.empty(chunk * per * sb, dtype=torch.uint8).pin_memory() for _ in range(3)]
+
+        def run(k0, k1):
+            t = []
+            for k in range(k0, k1):
+                if k - k0 >= 3:
+                    ch.host_wait(t[k - k0 - 3])             # the sink has taken that buffer
+                t.append(ch.host_submit(ts_pin.data_ptr(), base, len(ts), k * chunk, chunk,
+                                        ring[k % 3].data_ptr()))
+            ch.host_wait(t[-1])
+        run(0, 3)                                           # warm-up: buffers, first-touch
+        t0 = time.perf_counter()
+        run(0, chunks)
+        dt = time.perf_counter() - t0
+        samples = n * per
+        d2h = samples * sb
+        h2d = len(ts)
+        out[name] = {"value": samples / dt / 1e6, "unit": "Msamples/s", "seconds": dt,
+                     "d2h_GBs": d2h / dt / 1e9, "h2d_GBs": h2d / dt / 1e9,
+                     "frac_of_d2h_peak": d2h / dt / 1e9 / peaks["d2h_GBs"] if peaks else None}
+        del ring
+    out.update({"frames": n, "frames_per_submission": chunk, "workload": cfg.name,
+                "pcie_peaks": peaks,
+                "note": "secondary: host TS -> host IQ through the streaming ring (page-locked buffers, overlapped "
+                        "copy-in / kernels / copy-out); PCIe-bound, never `value`"})
+    return out
+
+
+def hbm_footprint(info, B, S, R, world, ts_len, sc16, gather_frames):
+    """bytes the bench allocates in HBM per rank (rank 0 holds the gather's output too): the chain's S buffer
+    slots (codewords, BCH partials, index pairs, L1 cells), S complex64 IQ buffers (+ S sc16 ones while the
+    sc16 pass runs), R resident TS batches, and rank 0's gathered IQ"""
+    F = info["fec_blocks_per_frame"]
+    slot = F * B * (info["cw_stride_bytes"] + 32) + (info["stream_items"] + 8) * B * 2 + B * 8 * 2048
+    iq = B * info["iq_samples_per_frame"] * 8
+    total = S * slot + S * iq + R * ts_len
+    if sc16:
+        total += S * iq // 2
+    if world > 1:
+        total += world * gather_frames * info["iq_samples_per_frame"] * 8
+    return total
+
+
+HBM_BYTES = 288e9   # MI355X HBM3E per GPU
+
+
 def metric_for(cfg_name):
     """BASELINE.json's metric string for cfg3 (the configuration it is quoted on); the same metric
     named by its configuration for the others"""
@@ -644,6 +743,12 @@ def main():
     # stream s % slots into its own IQ buffer, so one step's kernels fill the CUs the previous
     # step's kernel tails leave idle (dvbt2ll_chain_set_slots); every step still does all the work
     S = max(1, args.slots)
+    # the default shapes must fit HBM at N = 8 too (rank 0 also holds the ordered gather's output)
+    G = min(B, 512)
+    need = hbm_footprint(info, B, S, R, world, max(m[2] for m in ts_meta), not args.no_sc16, G)
+    if need > 0.9 * HBM_BYTES:
+        raise SystemExit("bench.py: %.1f GB of HBM needed per rank, more than 90 %% of %.0f GB" % (need / 1e9,
+                                                                                              HBM_BYTES / 1e9))
     chain.set_slots(S)
     iq = [torch.empty((B * per, 2), dtype=torch.float32, device="cuda") for _ in range(S)]
     streams = [torch.cuda.Stream() for _ in range(S)]
@@ -726,15 +831,18 @@ def main():
     mplp = None
     if not args.no_mplp and world == 1 and rank == 0 and args.config == "cfg3":
         mplp = mplp_rate(B, args.steps, args.warmup)
+    host = None
+    if not args.no_host and world == 1 and rank == 0:
+        host = host_delivered(cfg, 32 if info["fft_size"] == 32768 else 128, 24, pcie_peaks())
     gathered = None
     if dist and args.shard == "frames" and NS == 1:
         # secondary (not `value`): each step followed by the ordered IQ gather to rank 0, the
         # chain's one exchange step (point-to-point sends to the root over RCCL / xGMI)
         from dvbt2ll.distributed import gather_frames
         kg = min(args.steps, 3)
-        # at most 512 frames per rank gathered per step: the root's output tensor (N x G frames of
-        # complex64 IQ, 68 GB at N = 8) must fit beside the chain's two slots in 288 GB of HBM
-        G = min(B, 512)
+        # at most G = 512 frames per rank gathered per step: the root's output tensor (N x G frames of
+        # complex64 IQ, 68 GB at N = 8) beside the chain's slots and IQ buffers (hbm_footprint, checked
+        # against 288 GB before anything is allocated; the multi-PLP chain is not built under N > 1)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -845,6 +953,8 @@ def main():
             out["gather_to_rank0"] = gathered
         if mplp:
             out["mplp_2plp_32k"] = mplp
+        if host:
+            out["host_delivered"] = host
         if blocks:
             out["per_block_general_work"] = blocks
         if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only (host cores are shared)

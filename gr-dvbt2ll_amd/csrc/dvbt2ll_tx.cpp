@@ -1,7 +1,9 @@
 // dvbt2ll_tx -- native command-line DVB-T2 transmitter over the C ABI (include/dvbt2ll_hip.h):
 // MPEG-TS file in, baseband IQ file out, whole T2 frames per GPU call.  It is the file-sink
 // form of the shipped flowgraph apps/vv009-4kshort.grc (TS source -> the five blocks ->
-// multiply_const -> sink): TS bytes -> dvbt2ll_chain_run_host -> complex64 or sc16 samples.
+// multiply_const -> sink): TS bytes -> the chain's streaming host path (dvbt2ll_chain_host_submit /
+// _host_wait: a ring of DVBT2LL_HOST_RING batches in flight, page-locked buffers, so reading batch k + 1,
+// encoding batch k and writing batch k - 2 overlap) -> complex64 or sc16 samples.
 //
 //   dvbt2ll_tx --preset cfg3 --in stream.ts --out iq.sc16 --format sc16 --gain 0.2
 //
@@ -163,10 +165,34 @@ int main(int argc, char **argv) {
   std::vector<uint8_t> ts;                 // stream bytes [ts_base, ts_base + ts.size())
   int64_t ts_base = 0;
   bool eof = false;
-  std::vector<uint8_t> iq((size_t)batch * info.iq_samples_per_frame * sample_bytes);
-  int64_t done = 0;
+  // the ring: batch k's TS span and IQ in page-locked buffers of slot k % R until it is written out
+  constexpr int R = DVBT2LL_HOST_RING;
+  const size_t iq_slot = (size_t)batch * info.iq_samples_per_frame * sample_bytes;
+  const size_t ts_slot = (size_t)(payload_pos((int64_t)batch * pay_frame, hem) + 4 * 188);
+  void *ts_pin[R] = {}, *iq_pin[R] = {};
+  int64_t ticket[R] = {}, slot_frames[R] = {};
+  for (int k = 0; k < R; k++)
+    if (!(ts_pin[k] = dvbt2ll_host_alloc(ts_slot)) || !(iq_pin[k] = dvbt2ll_host_alloc(iq_slot))) {
+      std::fprintf(stderr, "dvbt2ll_tx: page-locked host buffers: out of memory\n");
+      st = DVBT2LL_ENOMEM;
+    }
+  int64_t done = 0, written = 0, submitted = 0;
+  // write out the oldest batch in flight (waits for its copy-out)
+  auto drain_one = [&]() -> bool {
+    const int sl = (int)(written % R);
+    int e = dvbt2ll_chain_host_wait(h, ticket[sl]);
+    if (e) { std::fprintf(stderr, "dvbt2ll_tx: run: %s\n", dvbt2ll_strerror(e)); st = e; return false; }
+    const size_t bytes = (size_t)slot_frames[sl] * info.iq_samples_per_frame * sample_bytes;
+    if (std::fwrite(iq_pin[sl], 1, bytes, fout) != bytes) {
+      std::fprintf(stderr, "dvbt2ll_tx: write failed: %s\n", std::strerror(errno));
+      st = -1;
+      return false;
+    }
+    written++;
+    return true;
+  };
   const auto t0 = std::chrono::steady_clock::now();
-  while (frames < 0 || done < frames) {
+  while (!st && (frames < 0 || done < frames)) {
     int n = batch;
     if (frames >= 0 && frames - done < n) n = (int)(frames - done);
     // stream bytes the frames [done, done + n) consume, plus the packet before the first
@@ -190,15 +216,18 @@ int main(int argc, char **argv) {
       end = payload_pos((done + n) * pay_frame, hem) + 1;
     }
     if (n == 0) break;
-    st = dvbt2ll_chain_run_host(h, ts.data(), ts_base, (int64_t)ts.size(), done, n, iq.data());
+    if (submitted - written == R && !drain_one()) break;   // the slot's previous batch goes out first
+    const int sl = (int)(submitted % R);
+    const int64_t span = end - lo;
+    if ((size_t)span > ts_slot) { st = DVBT2LL_EINVAL; break; }
+    std::memcpy(ts_pin[sl], ts.data() + (lo - ts_base), (size_t)span);
+    st = dvbt2ll_chain_host_submit(h, ts_pin[sl], lo, span, done, n, iq_pin[sl], &ticket[sl]);
     if (st) { std::fprintf(stderr, "dvbt2ll_tx: run: %s\n", dvbt2ll_strerror(st)); break; }
-    const size_t bytes = (size_t)n * info.iq_samples_per_frame * sample_bytes;
-    if (std::fwrite(iq.data(), 1, bytes, fout) != bytes) {
-      std::fprintf(stderr, "dvbt2ll_tx: write failed: %s\n", std::strerror(errno));
-      st = -1;
-      break;
-    }
+    slot_frames[sl] = n;
+    submitted++;
     done += n;
+  }
+  while (!st && written < submitted && drain_one()) {
   }
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::fprintf(stderr, "dvbt2ll_tx: %lld T2 frames, %lld samples (%s, gain %g) in %.3f s: %.1f Msamples/s\n",
@@ -206,6 +235,12 @@ int main(int argc, char **argv) {
                dt > 0 ? done * info.iq_samples_per_frame / dt / 1e6 : 0.0);
   if (fin != stdin) std::fclose(fin);
   if (fout != stdout) std::fclose(fout);
+  (void)dvbt2ll_chain_synchronize(h);
+  for (int k = 0; k < R; k++) {
+    if (submitted > written) (void)dvbt2ll_chain_host_wait(h, ticket[k]);   // nothing in flight on the buffers
+    dvbt2ll_host_free(ts_pin[k]);
+    dvbt2ll_host_free(iq_pin[k]);
+  }
   dvbt2ll_chain_destroy(h);
   return st ? 1 : 0;
 }

@@ -692,8 +692,43 @@ struct ChainGraph {
   }
 };
 
+// the asynchronous host path (dvbt2ll_chain_host_submit): a ring of submissions, each with its own device TS
+// and IQ buffers and three events; the TS copy-in, the kernels and the IQ copy-out of a submission run on
+// three streams ordered by those events, so consecutive submissions overlap (copy-in of k + 1 and copy-out
+// of k - 1 beside the kernels of k)
+struct HostRing {
+  hipStream_t in = nullptr, comp = nullptr, out = nullptr;
+  struct Entry {
+    DevBuf ts, iq;
+    hipEvent_t h2d = nullptr, kern = nullptr, d2h = nullptr;
+    int64_t ticket = -1;   // the submission holding the entry (-1: never used)
+  } e[DVBT2LL_HOST_RING];
+  int64_t next_ticket = 0;
+  int init(int device) {
+    if (in) return 0;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipStreamCreateWithFlags(&in, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&comp, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&out, hipStreamNonBlocking));
+    for (auto &x : e) {
+      HIP_TRY(hipEventCreateWithFlags(&x.h2d, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&x.kern, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&x.d2h, hipEventDisableTiming));
+    }
+    return 0;
+  }
+  ~HostRing() {
+    for (auto &x : e)
+      for (hipEvent_t ev : {x.h2d, x.kern, x.d2h})
+        if (ev) (void)hipEventDestroy(ev);
+    for (hipStream_t st : {in, comp, out})
+      if (st) (void)hipStreamDestroy(st);
+  }
+};
+
 struct dvbt2ll_chain {
   DeviceCtx ctx;
+  HostRing host;
   dvbt2ll_chain_params p{};   // single-PLP create parameters (PLP 0's for a multi-PLP chain)
   int nplp = 1;
   std::vector<std::unique_ptr<ChainPlp>> plps;
@@ -1189,6 +1224,18 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
   return dvbt2ll_chain_run_streams(h, ts_dev, 0, 1, ts_base, ts_len, first_frame, nframes, iq_dev, stream);
 }
 
+// stream bytes [lo, end) that frames [first, first + n) of PLP pl consume: their payload plus the packet before
+// the first one touched (its CRC-8 replaces the next sync byte, bbheader:701-713)
+static void ts_span(const ChainPlp &pl, int64_t first, int64_t n, int64_t *lo, int64_t *end) {
+  int64_t start = first / pl.P * pl.ts_per_frame, e = (first + n) / pl.P * pl.ts_per_frame;
+  if (pl.inputmode) {
+    start = 188 * (start / 187) + (start % 187);
+    e = 188 * (e / 187) + (e % 187) + 1;
+  }
+  *lo = start >= 188 ? (start / 188) * 188 - 188 : 0;
+  *end = e;
+}
+
 // one run over nstreams independent single-PLP streams (nplp == 1) or over one frame sequence of
 // every PLP (nstreams == 1): ts[k], base[k], len[k] per PLP (stream s of a batch at ts[0] + s * ts_stride)
 static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *base, const int64_t *len,
@@ -1203,14 +1250,9 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
   for (int k = 0; k < h->nplp; k++) {
     const ChainPlp &pl = *h->plps[k];
     if (!ts[k] || base[k] < 0 || base[k] % 188 != 0) return DVBT2LL_EINVAL;
-    // the TS slice must cover every byte the frames consume plus the packet before the
-    // first one touched (its CRC-8 replaces the next sync byte, bbheader:701-713)
-    int64_t start = first_frame / pl.P * pl.ts_per_frame, end = (first_frame + nframes) / pl.P * pl.ts_per_frame;
-    if (pl.inputmode) {
-      start = 188 * (start / 187) + (start % 187);
-      end = 188 * (end / 187) + (end % 187) + 1;
-    }
-    int64_t lo = start >= 188 ? (start / 188) * 188 - 188 : 0;
+    // the TS slice must cover every byte the frames consume plus the packet before the first one touched
+    int64_t lo, end;
+    ts_span(pl, first_frame, nframes, &lo, &end);
     if (base[k] > lo || base[k] + len[k] < end) return DVBT2LL_EINVAL;
   }
   HIP_TRY(hipSetDevice(h->ctx.device));
@@ -1339,6 +1381,71 @@ extern "C" int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t 
   HIP_TRY(hipMemcpyAsync(iq, h->iq_tmp.p, iq_bytes, hipMemcpyDeviceToHost, h->ctx.stream));
   HIP_TRY(hipStreamSynchronize(h->ctx.stream));
   return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_host_submit(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
+                                         int64_t first_frame, int nframes, void *iq, int64_t *ticket) {
+  if (!h || !ts || !iq || !ticket || h->nplp != 1 || nframes < 1 || nframes > h->max_frames || first_frame < 0 ||
+      ts_base < 0 || ts_base % 188)
+    return DVBT2LL_EINVAL;
+  const ChainPlp &pl = *h->plps[0];
+  int64_t lo, end;
+  ts_span(pl, first_frame, nframes, &lo, &end);
+  if (ts_base > lo || ts_base + ts_len < end) return DVBT2LL_EINVAL;
+  int r = h->host.init(h->ctx.device);
+  if (r) return r;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  HostRing &R = h->host;
+  const int64_t t = R.next_ticket;
+  HostRing::Entry &x = R.e[t % DVBT2LL_HOST_RING];
+  // the entry's previous submission must have left its buffers: its copy-out is the last thing it does
+  if (x.ticket >= 0) HIP_TRY(hipEventSynchronize(x.d2h));
+  const size_t iq_bytes = (size_t)nframes * h->iq_per_frame * (h->ofdm.dev.fmt == DVBT2LL_IQ_SC16 ? 4 : 8);
+  if (x.ts.ensure((size_t)(end - lo) + 16) || x.iq.ensure(iq_bytes)) return DVBT2LL_ENOMEM;
+  HIP_TRY(hipMemcpyAsync(x.ts.p, (const uint8_t *)ts + (lo - ts_base), (size_t)(end - lo), hipMemcpyHostToDevice,
+                         R.in));
+  HIP_TRY(hipEventRecord(x.h2d, R.in));
+  HIP_TRY(hipStreamWaitEvent(R.comp, x.h2d, 0));
+  if ((r = dvbt2ll_chain_run_device(h, x.ts.p, lo, end - lo, first_frame, nframes, x.iq.p, R.comp))) return r;
+  HIP_TRY(hipEventRecord(x.kern, R.comp));
+  HIP_TRY(hipStreamWaitEvent(R.out, x.kern, 0));
+  HIP_TRY(hipMemcpyAsync(iq, x.iq.p, iq_bytes, hipMemcpyDeviceToHost, R.out));
+  HIP_TRY(hipEventRecord(x.d2h, R.out));
+  x.ticket = t;
+  R.next_ticket = t + 1;
+  *ticket = t;
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_host_wait(dvbt2ll_chain *h, int64_t ticket) {
+  if (!h || ticket < 0 || ticket >= h->host.next_ticket) return DVBT2LL_EINVAL;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  const HostRing::Entry &x = h->host.e[ticket % DVBT2LL_HOST_RING];
+  // an entry reused by a later submission was waited for at that submission
+  if (x.ticket == ticket) HIP_TRY(hipEventSynchronize(x.d2h));
+  return DVBT2LL_OK;
+}
+
+extern "C" int dvbt2ll_chain_run_host_pipelined(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
+                                                int64_t first_frame, int nframes, void *iq, int chunk_frames) {
+  if (!h || nframes < 1 || chunk_frames < 0) return DVBT2LL_EINVAL;
+  const int c = chunk_frames ? std::min(chunk_frames, h->max_frames) : h->max_frames;
+  const size_t per = (size_t)h->iq_per_frame * (h->ofdm.dev.fmt == DVBT2LL_IQ_SC16 ? 4 : 8);
+  int64_t t = -1;
+  for (int f = 0; f < nframes; f += c) {
+    const int n = std::min(c, nframes - f);
+    int r = dvbt2ll_chain_host_submit(h, ts, ts_base, ts_len, first_frame + f, n, (char *)iq + (size_t)f * per, &t);
+    if (r) return r;
+  }
+  return dvbt2ll_chain_host_wait(h, t);
+}
+
+extern "C" void *dvbt2ll_host_alloc(size_t bytes) {
+  void *p = nullptr;
+  return hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+extern "C" void dvbt2ll_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
 }
 
 extern "C" int dvbt2ll_chain_set_output(dvbt2ll_chain *h, float gain, int format) {

@@ -101,6 +101,8 @@ EXPORTS += ["dvbt2ll_framemapperfint_stream_items", "dvbt2ll_pilotgenp1insert_ac
 EXPORTS += ["dvbt2ll_bbheaderbch_set_isi"]
 EXPORTS += ["dvbt2ll_framemapper_mplp_" + f for f in ("create", "output_multiple", "stream_items", "forecast",
                                                       "general_work", "destroy")]
+EXPORTS += ["dvbt2ll_chain_" + f for f in ("host_submit", "host_wait", "run_host_pipelined")]
+EXPORTS += ["dvbt2ll_host_alloc", "dvbt2ll_host_free"]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create_mplp", "num_plps", "unit_frames", "get_plp_info", "run_plps",
                                            "debug_plp_codewords", "debug_keep_codewords")]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create", "get_info", "run_device", "run_streams", "run_host", "set_output", "set_slots", "set_graph", "set_timing",
@@ -137,6 +139,13 @@ def lib():
     L.dvbt2ll_chain_run_streams.argtypes = [vp, vp, i64, ci, i64, i64, i64, ci, vp, vp]
     L.dvbt2ll_chain_run_host.argtypes = [vp, vp, i64, i64, i64, ci, vp]
     L.dvbt2ll_chain_set_output.argtypes = [vp, ctypes.c_float, ci]
+    L.dvbt2ll_chain_host_submit.argtypes = [vp, vp, i64, i64, i64, ci, vp, ctypes.POINTER(i64)]
+    L.dvbt2ll_chain_host_wait.argtypes = [vp, i64]
+    L.dvbt2ll_chain_run_host_pipelined.argtypes = [vp, vp, i64, i64, i64, ci, vp, ci]
+    L.dvbt2ll_host_alloc.restype = vp
+    L.dvbt2ll_host_alloc.argtypes = [ctypes.c_size_t]
+    L.dvbt2ll_host_free.argtypes = [vp]
+    L.dvbt2ll_host_free.restype = None
     L.dvbt2ll_chain_set_slots.argtypes = [vp, ci]
     L.dvbt2ll_chain_set_graph.argtypes = [vp, ci]
     L.dvbt2ll_chain_set_timing.argtypes = [vp, ci]

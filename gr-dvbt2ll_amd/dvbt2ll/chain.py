@@ -117,6 +117,30 @@ class Chain:
               "chain run")
         return iq
 
+    def host_submit(self, ts_ptr, ts_base, ts_len, first_frame, nframes, iq_ptr):
+        """streaming host path (dvbt2ll_chain_host_submit): host TS -> host IQ for nframes frames on the handle's
+        copy-in / compute / copy-out streams; returns a ticket at once (the buffers stay the caller's until
+        host_wait(ticket))"""
+        t = ctypes.c_int64(0)
+        check(lib().dvbt2ll_chain_host_submit(self._h, ctypes.c_void_p(ts_ptr), int(ts_base), int(ts_len),
+                                              int(first_frame), int(nframes), ctypes.c_void_p(iq_ptr),
+                                              ctypes.byref(t)), "host submit")
+        return t.value
+
+    def host_wait(self, ticket):
+        check(lib().dvbt2ll_chain_host_wait(self._h, int(ticket)), "host wait")
+
+    def run_host_pipelined(self, ts, ts_base, first_frame, nframes, iq, chunk_frames=0):
+        """host numpy TS -> host numpy IQ (complex64, or (n, 2) int16 after set_output(.., IQ_SC16)) through the
+        submission ring in chunks of chunk_frames (0: max_frames); synchronous"""
+        ts = np.ascontiguousarray(ts, np.uint8)
+        assert iq.flags.c_contiguous and iq.nbytes >= nframes * self.iq_per_frame * self.iq_bytes_per_sample
+        check(lib().dvbt2ll_chain_run_host_pipelined(self._h, ts.ctypes.data_as(ctypes.c_void_p), int(ts_base),
+                                                     len(ts), int(first_frame), int(nframes),
+                                                     iq.ctypes.data_as(ctypes.c_void_p), int(chunk_frames)),
+              "run host pipelined")
+        return iq
+
     def set_timing(self, enable):
         check(lib().dvbt2ll_chain_set_timing(self._h, int(bool(enable))), "timing")
 

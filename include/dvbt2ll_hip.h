@@ -207,6 +207,28 @@ int dvbt2ll_chain_set_graph(dvbt2ll_chain *h, int enable);
 /* host buffers, synchronous */
 int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                            int64_t first_frame, int nframes, void *iq);
+/* Streaming host path (the reference's output is host memory feeding a sink,
+ * lib/pilotgenp1insert_cc_impl.cc:2785-2906 -> apps/vv009-4kshort.grc:801-1623).  A submission copies the
+ * TS bytes its frames need from host ts (laid out as run_device's: absolute stream offset ts_base, ts_len
+ * bytes) to the device, encodes the frames and copies their IQ (the current dvbt2ll_chain_set_output format)
+ * to host iq, on three HIP streams of the handle ordered by events, into the next entry of a ring of
+ * DVBT2LL_HOST_RING device buffer sets: submission k + 1's copy-in and k - 1's copy-out run beside k's
+ * kernels.  Returns at once with a ticket (the host blocks only when the ring entry's previous submission
+ * is still in flight); ts and iq must stay valid, and iq unread, until dvbt2ll_chain_host_wait(ticket)
+ * returns.  Page-locked host buffers (dvbt2ll_host_alloc, or hipHostRegister) move at the PCIe rate;
+ * pageable ones work, but the runtime stages their copies and the submit call waits for them.
+ * Single-PLP chains; nframes <= max_frames; submissions complete in order. */
+#define DVBT2LL_HOST_RING 3
+int dvbt2ll_chain_host_submit(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
+                              int64_t first_frame, int nframes, void *iq, int64_t *ticket);
+int dvbt2ll_chain_host_wait(dvbt2ll_chain *h, int64_t ticket);
+/* frames [first_frame, first_frame + nframes) through the ring in chunks of chunk_frames (0: max_frames),
+ * frame f's IQ at iq + (f - first_frame) * iq_samples_per_frame samples; synchronous */
+int dvbt2ll_chain_run_host_pipelined(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
+                                     int64_t first_frame, int nframes, void *iq, int chunk_frames);
+/* page-locked host memory for the streaming path (hipHostMalloc); NULL on failure */
+void *dvbt2ll_host_alloc(size_t bytes);
+void dvbt2ll_host_free(void *p);
 /* IQ output of the chain (default: gain 1, DVBT2LL_IQ_CF32 = pilotgenp1insert_cc's own complex64
  * output).  gain multiplies every normalised sample, as the blocks_multiply_const_xx that follows
  * pilotgen in apps/vv009-4kshort.grc:335-385 (const 0.2) does.  DVBT2LL_IQ_SC16 stores each sample

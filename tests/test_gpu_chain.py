@@ -134,24 +134,24 @@ def test_chain_set_output_rejects_bad_format(gpu):
         ch.set_output(1.0, 7)
 
 
-@pytest.mark.parametrize("name,sets,fmt,gain", [("cfg1", [], "cf32", 1.0), ("cfg1", [], "sc16", 0.2),
-                                                ("cfg1", ["inputmode=1"], "sc16", 0.2)])
-def test_tx_tool_matches_chain(gpu, tmp_path, name, sets, fmt, gain):
-    """dvbt2ll_tx (TS file -> IQ file, rolling TS buffer over several GPU calls) writes exactly
-    the chain's output for the same stream"""
+@pytest.mark.parametrize("name,sets,fmt,gain,nfr,batch", [
+    ("cfg1", [], "cf32", 1.0, 3, 2), ("cfg1", [], "sc16", 0.2, 3, 2), ("cfg1", ["inputmode=1"], "sc16", 0.2, 3, 2),
+    ("cfg1", [], "cf32", 1.0, 8, 1), ("cfg4", ["inband=1"], "sc16", 0.2, 7, 2)])
+def test_tx_tool_matches_chain(gpu, tmp_path, name, sets, fmt, gain, nfr, batch):
+    """dvbt2ll_tx (TS file -> IQ file, rolling TS buffer, batches in flight on the streaming ring: 8 and 4
+    batches wrap its DVBT2LL_HOST_RING entries) writes exactly the chain's output for the same stream"""
     import subprocess
     from pathlib import Path
     cfg = CONFIGS[name]
     for s in sets:
         k, v = s.split("=")
         cfg = cfg.with_(**{k: int(v)})
-    nfr = 3
     ts, base = ts_for_frames(cfg, 0, nfr)
     assert base == 0
     (tmp_path / "in.ts").write_bytes(ts.tobytes())
     tool = Path(__file__).resolve().parents[1] / "gr-dvbt2ll_amd" / "dvbt2ll" / "dvbt2ll_tx"
     args = [str(tool), "--preset", name, "--in", str(tmp_path / "in.ts"), "--out", str(tmp_path / "iq.bin"),
-            "--format", fmt, "--gain", str(gain), "--batch", "2", "--frames", str(nfr)]
+            "--format", fmt, "--gain", str(gain), "--batch", str(batch), "--frames", str(nfr)]
     for s in sets:
         args += ["--set", s]
     r = subprocess.run(args, capture_output=True, text=True, timeout=120)
