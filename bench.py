@@ -626,6 +626,23 @@ def spawn_ranks(args):
     return 0
 
 
+def shard_plan(shard, B, NS, R, rank, world):
+    """each rank's R resident batches: (first frame, frames per stream, TS stream seeds).  shard "frames": one
+    TS stream per launch slot k (seed k + 1), the frames split contiguously across ranks and batches
+    (dvbt2ll.distributed.frame_range), disjoint; shard "streams": rank r encodes its own NS independent
+    streams (seeds r NS + 1 .. r NS + NS) from frame 0 -- SURVEY 8(e)'s two modes.  NS > 1: one launch
+    encodes B // NS frames of each of NS streams (dvbt2ll_chain_run_streams)"""
+    from dvbt2ll.distributed import frame_range
+    if B % NS:
+        raise SystemExit("--frames must be a multiple of --streams")
+    BS = B // NS
+    if shard == "streams":
+        first0, seed = 0, rank * NS + 1
+    else:
+        first0, seed = frame_range(world * R * BS, rank, world)[0], 1
+    return [(first0 + r * BS, BS, list(range(seed, seed + NS))) for r in range(R)]
+
+
 def dry_run(args, rank, world):
     """the multi-rank plumbing without HIP: placeholder frames (frame k's samples all hold k) are
     produced per rank from its frame_range shard, K steps are timed between barriers with the
@@ -639,11 +656,21 @@ def dry_run(args, rank, world):
         dist.init_process_group(args.backend or "gloo", timeout=datetime.timedelta(seconds=args.init_timeout))
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     B, per = min(args.frames, 16), 1024
-    first, count = frame_range(world * B, rank, world)
+    NS = max(1, args.streams)
+    if args.shard == "streams":
+        # each rank its own NS streams (shard_plan), B // NS frames of each per step; placeholder frame
+        # = seed * 1000 + frame
+        plan = shard_plan("streams", B, NS, 1, rank, world)[0]
+        first, count, seeds = plan[0], plan[1] * NS, plan[2]
+        vals = torch.tensor([sd * 1000 + plan[0] + k for sd in seeds for k in range(plan[1])], dtype=torch.float32)
+    else:
+        first, count = frame_range(world * B, rank, world)
+        seeds = [1]
+        vals = torch.arange(first, first + count, dtype=torch.float32)
     buf = torch.empty((count * per, 2), dtype=torch.float32)
 
     def step():
-        buf.view(count, per, 2)[:] = torch.arange(first, first + count, dtype=torch.float32)[:, None, None]
+        buf.view(count, per, 2)[:] = vals[:, None, None]
     for _ in range(args.warmup):
         step()
     if world > 1:
@@ -656,6 +683,27 @@ def dry_run(args, rank, world):
     e = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    if args.shard == "streams":
+        # every rank's stream set (no gather: independent streams are replicas)
+        allseeds = [None] * world
+        if world > 1:
+            dist.all_gather_object(allseeds, seeds)
+        else:
+            allseeds = [seeds]
+        ok = bool((buf.view(count, per, 2)[:, 0, 0] == vals).all())
+        if rank == 0:
+            flat = sorted(sd for ss in allseeds for sd in ss)
+            print(json.dumps({"metric": "dry run: placeholder frames/s (no HIP)",
+                              "value": world * count * args.steps / float(e), "unit": "frames/s", "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup, "dry_run": True, "shard": "streams",
+                              "streams_per_rank": NS, "stream_seeds": allseeds,
+                              "seeds_disjoint_complete": flat == list(range(1, world * NS + 1)),
+                              "frames_ok": ok, "world_size_verified": world == args.gpus,
+                              "launcher": "bench.py spawn" if os.environ.get("DVBT2LL_BENCH_SPAWNED") else
+                                          ("external" if world > 1 else "single process")}))
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
     shards = [list(frame_range(world * B, r, world)) for r in range(world)]
     g = gather_frames(buf, world * B, per) if world > 1 else buf
     if rank == 0:
@@ -712,26 +760,14 @@ def main():
     chain = dvbt2ll.Chain(cfg, max_frames=B, device=local_rank)
     info = chain.info
     per = chain.iq_per_frame
-    # R distinct resident batches per rank; frames split contiguously across ranks
-    # (dvbt2ll.distributed.frame_range), disjoint across ranks and batches
-    from dvbt2ll.distributed import frame_range
+    # R distinct resident batches per rank (shard_plan)
     R = 2
-    rank_first, _ = frame_range(world * R * B, rank, world)
-    seed = 1
-    if args.shard == "streams":
-        rank_first, seed = 0, rank * max(1, args.streams) + 1
     NS = max(1, args.streams)
-    if NS > 1:
-        # multi-stream batch: NS independent TS streams (seeds seed..seed+NS-1), B // NS frames of each
-        # per step, one launch (dvbt2ll_chain_run_streams)
-        if B % NS:
-            raise SystemExit("--frames must be a multiple of --streams")
-        rank_first = frame_range(world * R * (B // NS), rank, world)[0] if args.shard == "frames" else 0
+    plan = shard_plan(args.shard, B, NS, R, rank, world)
     BS = B // NS
     ts_dev, ts_meta = [], []
-    for r in range(R):
-        first = rank_first + r * BS
-        tss = [ts_for_frames(cfg, first, BS, seed + k) for k in range(NS)]
+    for r, (first, _, seeds) in enumerate(plan):
+        tss = [ts_for_frames(cfg, first, BS, sd) for sd in seeds]
         base, n = tss[0][1], len(tss[0][0])
         stride = (n + 255) // 256 * 256
         buf = np.zeros((NS, stride), np.uint8)

@@ -64,7 +64,7 @@ def gather_frames(local, total_frames, per_frame, group=None, dst=0, unit=1):
     return out
 
 
-def encode_sharded(chain, first_frame, total_frames, group=None, gather=True, seed=1):
+def encode_sharded(chain, first_frame, total_frames, group=None, gather=True, seed=1, device="cuda"):
     """each rank encodes its contiguous share of the frames -- whole launch units (interleaving frames) --
     on its own GPU (synthetic TS slice generated for exactly those frames; a multi-PLP chain's PLP k uses
     seed + k); optional ordered gather of the IQ to rank 0."""
@@ -74,19 +74,19 @@ def encode_sharded(chain, first_frame, total_frames, group=None, gather=True, se
     unit = getattr(chain, "unit_frames", 1)
     first, count = frame_range(total_frames, rank, world, first_frame, unit)
     per = chain.iq_per_frame
-    iq = torch.zeros((count * per, 2), dtype=torch.float32, device="cuda")
+    iq = torch.zeros((count * per, 2), dtype=torch.float32, device=device)
     if count:
         if count > chain.max_frames:
             raise ValueError("shard of %d frames exceeds chain max_frames %d" % (count, chain.max_frames))
-        st = torch.cuda.current_stream().cuda_stream
+        st = torch.cuda.current_stream().cuda_stream if device != "cpu" else 0
         if isinstance(chain.cfg, MplpConfig):
             tss = [ts_for_frames(p, first, count, seed + k) for k, p in enumerate(chain.cfg.plps)]
-            bufs = [torch.from_numpy(ts).cuda() for ts, _ in tss]
+            bufs = [torch.from_numpy(ts).to(device) for ts, _ in tss]
             chain.run_plps([b.data_ptr() for b in bufs], [b for _, b in tss], [len(t) for t, _ in tss], first, count,
                            iq.data_ptr(), st)
         else:
             ts, base = ts_for_frames(chain.cfg, first, count, seed)
-            ts_d = torch.from_numpy(ts).cuda()
+            ts_d = torch.from_numpy(ts).to(device)
             chain.run_device(ts_d.data_ptr(), base, len(ts), first, count, iq.data_ptr(), st)
     if not gather:
         return iq

@@ -60,3 +60,34 @@ def test_bench_rank_failure_fails_fast():
     assert "rank exit codes" in r.stderr and "--fail-rank" in r.stderr
     assert dt < 30, dt
     assert not r.stdout.strip()                    # no JSON line from a failed run
+
+
+@pytest.mark.parametrize("n,streams", [(2, 2), (3, 1)])
+def test_bench_spawn_stream_sharding(n, streams):
+    """`--shard streams` (SURVEY 8(e)'s independent-stream mode): every rank encodes its own TS streams
+    (seeds r S + 1 .. r S + S, bench.shard_plan), disjoint and together complete, with no data-path
+    collective; timing max-reduced over ranks as for frame sharding"""
+    r = _bench("--gpus", str(n), "--dry-run", "--shard", "streams", "--streams", str(streams), "--frames",
+               str(4 * streams), "--steps", "2", "--warmup", "1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["shard"] == "streams" and d["n_gpus"] == n and d["world_size_verified"]
+    assert d["seeds_disjoint_complete"] and d["frames_ok"]
+    assert d["stream_seeds"] == [list(range(k * streams + 1, k * streams + streams + 1)) for k in range(n)]
+
+
+def test_shard_plan_modes():
+    sys.path.insert(0, str(ROOT))
+    import bench
+    # frames: disjoint contiguous batches across ranks and the R resident batches
+    seen = []
+    for rank in range(3):
+        for first, cnt, seeds in bench.shard_plan("frames", 8, 2, 2, rank, 3):
+            assert seeds == [1, 2] and cnt == 4
+            seen += list(range(first, first + cnt))
+    assert sorted(seen) == list(range(24)) and len(set(seen)) == 24
+    assert bench.shard_plan("streams", 6, 3, 2, 1, 2) == [(0, 2, [4, 5, 6]), (2, 2, [4, 5, 6])]
+    with pytest.raises(SystemExit):
+        bench.shard_plan("frames", 5, 2, 2, 0, 1)

@@ -127,3 +127,57 @@ def test_gloo_if_sharded_equals_sequential(total, world):
         p.join(180)
         assert p.exitcode == 0
     assert q.get(timeout=5)
+
+
+class _FakeChain:
+    """stands in for dvbt2ll.Chain on the CPU (no HIP): run_device writes placeholder frames (frame k's samples
+    all hold k) through the IQ pointer, after checking that the TS slice it was handed is exactly the global
+    stream's bytes for its frames"""
+    def __init__(self, cfg, max_frames, per=64):
+        self.cfg, self.max_frames, self.iq_per_frame, self.unit_frames = cfg, max_frames, per, 1
+        self.calls = []
+
+    def run_device(self, ts_ptr, base, n, first, count, iq_ptr, stream):
+        import ctypes
+        ts = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(ts_ptr))
+        assert np.array_equal(ts, ts_for_frames(self.cfg, first, count)[0])
+        frames = np.repeat(np.arange(first, first + count, dtype=np.float32), self.iq_per_frame * 2)
+        ctypes.memmove(iq_ptr, frames.ctypes.data, frames.nbytes)
+        self.calls.append((first, count))
+
+
+def _enc_worker(rank, world, port, total, q):
+    import sys
+    sys.path[:0] = [os.path.join(os.path.dirname(__file__)),
+                    os.path.join(os.path.dirname(__file__), "..", "gr-dvbt2ll_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ch = _FakeChain(CONFIGS["cfg1"], max_frames=total)
+        got = D.encode_sharded(ch, 0, total, device="cpu")
+        first, count = D.frame_range(total, rank, world)
+        assert ch.calls == ([(first, count)] if count else [])   # empty shards launch nothing
+        if rank == 0:
+            want = np.repeat(np.arange(total, dtype=np.float32), ch.iq_per_frame * 2).reshape(-1, 2)
+            q.put(bool(np.array_equal(got.numpy(), want)))
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_encode_sharded_more_ranks_than_frames():
+    """encode_sharded with 3 ranks and 2 frames: rank 2's shard is empty (no launch, no send), the ordered
+    gather still delivers both frames to rank 0"""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_enc_worker, args=(r, 3, port, 2, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    assert q.get(timeout=5)
