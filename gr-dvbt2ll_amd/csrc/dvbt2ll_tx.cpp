@@ -6,10 +6,15 @@
 // encoding batch k and writing batch k - 2 overlap) -> complex64 or sc16 samples.
 //
 //   dvbt2ll_tx --preset cfg3 --in stream.ts --out iq.sc16 --format sc16 --gain 0.2
+//   dvbt2ll_tx --mplp mix_4k --in plp0.ts --in plp1.ts --in plp2.ts --out iq.cf32
+//
+// --mplp runs a multi-PLP frame preset (one TS file per PLP, dvbt2ll_chain_create_mplp / _run_plps_host;
+// batches are whole launch units, dvbt2ll_chain_unit_frames).
 //
 // The TS is consumed as one continuous stream (absolute offsets from the start of the file);
 // frame k is encoded with the stream state the reference blocks would hold at that point.
 // Trailing bytes that do not complete a T2 frame are left unused.
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <cstdint>
@@ -39,10 +44,32 @@ const Preset kPresets[] = {
     {"cfg1q", 0, 0, 0, 1, 2, 3, 0, 2, 0, 3, 6, 2, 3},   // BASELINE config 1 as worded: QPSK 1/2
 };
 
+// multi-PLP presets (gr-dvbt2ll_amd/dvbt2ll/configs.py MPLP_CONFIGS / IF_CONFIGS of the same names): the
+// common fields of dvbt2ll_mplp_params, then per PLP {framesize, rate, constellation, rotation, fecblocks,
+// tiblocks, inputmode, inband, tsrate, plp_type, ti_type, ti_frames, frame_interval, first_frame_idx}
+struct MplpPreset {
+  const char *name;
+  int common[12];
+  int nplp;
+  dvbt2ll_plp_params plp[3];
+  int num_subslices;
+};
+const MplpPreset kMplpPresets[] = {
+    // the GRC's 4K short frame as three Type-1 PLPs (256-QAM 4/5 rotated, QPSK 1/2, 16-QAM 3/5 HEM)
+    {"mplp3_4k", {0, 2, 0, 3, 6, 2, 3, 0, 0, 0, 0, 0}, 3,
+     {{0, 4, 3, 1, 2, 1, 0, 0, 4000000, 1, 0, 1, 1, 0}, {0, 0, 0, 0, 1, 0, 0, 0, 4000000, 1, 0, 1, 1, 0},
+      {0, 1, 1, 1, 1, 2, 1, 0, 4000000, 1, 0, 1, 1, 0}}, 1},
+    // the same frame with a Type-2 TIME_IL_TYPE 1 PLP (P_I = 2), a Type-1 PLP and a Type-2 HEM PLP, 6 sub-slices
+    {"mix_4k", {0, 2, 0, 3, 6, 2, 3, 0, 0, 0, 0, 0}, 3,
+     {{0, 4, 3, 1, 4, 1, 0, 0, 4000000, 2, 1, 2, 1, 0}, {0, 0, 0, 0, 1, 1, 0, 0, 4000000, 1, 0, 1, 1, 0},
+      {0, 1, 1, 1, 1, 1, 1, 0, 4000000, 2, 0, 1, 1, 0}}, 6},
+};
+
 void usage(FILE *f) {
   std::fprintf(f,
                "usage: dvbt2ll_tx --in TS_FILE --out IQ_FILE [options]\n"
                "  --preset cfg1..cfg5|cfg1q parameter preset (default cfg1, the shipped flowgraph)\n"
+               "  --mplp mplp3_4k|mix_4k    multi-PLP frame preset: give one --in per PLP\n"
                "  --set NAME=VALUE        override one chain parameter (framemapperfint_cc names:\n"
                "                          framesize rate constellation rotation fecblocks tiblocks\n"
                "                          carriermode fftsize guardinterval l1constellation\n"
@@ -79,11 +106,125 @@ int *field(dvbt2ll_chain_params &p, const std::string &n) {
 // stream position of payload byte J (HEM drops each packet's sync byte)
 int64_t payload_pos(int64_t J, bool hem) { return hem ? 188 * (J / 187) + 1 + J % 187 : J; }
 
+// one TS input: the stream window [base, base + buf.size()) of a file read as the frames need it
+struct TsIn {
+  FILE *f = nullptr;
+  std::vector<uint8_t> buf;
+  int64_t base = 0;
+  bool eof = false;
+  // make [lo, end) available (dropping bytes before lo); false if the file ends first
+  bool span(int64_t lo, int64_t end) {
+    if (lo > base) {
+      const size_t drop = (size_t)std::min<int64_t>(lo - base, (int64_t)buf.size());
+      buf.erase(buf.begin(), buf.begin() + drop);
+      base = lo;
+    }
+    while (!eof && base + (int64_t)buf.size() < end) {
+      size_t old = buf.size();
+      buf.resize(old + (1 << 20));
+      size_t got = std::fread(buf.data() + old, 1, buf.size() - old, f);
+      buf.resize(old + got);
+      if (got == 0) eof = true;
+    }
+    return base + (int64_t)buf.size() >= end;
+  }
+};
+
+// the multi-PLP transmitter: whole launch units per batch, each PLP's TS span from its own file
+int run_mplp(const MplpPreset &ps, const std::vector<std::string> &ins, const std::string &out_path, int fmt,
+             float gain, int64_t frames, int batch, int device, bool print_params) {
+  dvbt2ll_mplp_chain_params p;
+  std::memset(&p, 0, sizeof(p));
+  dvbt2ll_mplp_params &m = p.fm;
+  int *c[12] = {&m.carriermode, &m.fftsize, &m.guardinterval, &m.l1constellation, &m.pilotpattern, &m.t2frames,
+                &m.numdatasyms, &m.paprmode, &m.version, &m.preamble, &m.reservedbiasbits, &m.l1scrambled};
+  for (int i = 0; i < 12; i++) *c[i] = ps.common[i];
+  m.nplp = ps.nplp;
+  for (int k = 0; k < ps.nplp; k++) m.plp[k] = ps.plp[k];
+  m.num_subslices = ps.num_subslices;
+  p.bandwidth = 4;   // BANDWIDTH_8_0_MHZ
+  if (print_params) {   // the dvbt2ll_mplp_params ints (configs.MplpConfig.mplp_array layout)
+    for (int i = 0; i < 12; i++) std::printf("%d ", *c[i]);
+    std::printf("%d", m.nplp);
+    for (int k = 0; k < DVBT2LL_MAX_PLP; k++) {
+      const dvbt2ll_plp_params &q = m.plp[k];
+      const int v[14] = {q.framesize, q.rate, q.constellation, q.rotation, q.fecblocks, q.tiblocks, q.inputmode,
+                         q.inband, q.tsrate, q.plp_type, q.ti_type, q.ti_frames, q.frame_interval,
+                         q.first_frame_idx};
+      for (int x : v) std::printf(" %d", x);
+    }
+    std::printf(" %d\n", m.num_subslices);
+    return 0;
+  }
+  if ((int)ins.size() != ps.nplp || out_path.empty()) {
+    std::fprintf(stderr, "dvbt2ll_tx: --mplp %s needs %d --in files and --out\n", ps.name, ps.nplp);
+    return 2;
+  }
+  dvbt2ll_chain *h = nullptr;
+  p.max_frames = batch;
+  int st = dvbt2ll_chain_create_mplp(&p, device, &h);
+  const int unit = st ? 1 : dvbt2ll_chain_unit_frames(h);
+  if (!st && batch % unit) st = DVBT2LL_EINVAL;   // batches of whole launch units
+  if (!st) st = dvbt2ll_chain_set_output(h, gain, fmt);
+  if (st) {
+    std::fprintf(stderr, "dvbt2ll_tx: chain: %s (batch must be a multiple of the launch unit)\n", dvbt2ll_strerror(st));
+    dvbt2ll_chain_destroy(h);
+    return 1;
+  }
+  dvbt2ll_chain_info pi[DVBT2LL_MAX_PLP];
+  std::vector<TsIn> ts(ps.nplp);
+  for (int k = 0; k < ps.nplp && !st; k++) {
+    st = dvbt2ll_chain_get_plp_info(h, k, &pi[k]);
+    ts[k].f = std::fopen(ins[k].c_str(), "rb");
+    if (!ts[k].f) { std::fprintf(stderr, "dvbt2ll_tx: cannot open %s\n", ins[k].c_str()); st = -1; }
+  }
+  FILE *fout = st ? nullptr : (out_path == "-" ? stdout : std::fopen(out_path.c_str(), "wb"));
+  if (!st && !fout) { std::fprintf(stderr, "dvbt2ll_tx: cannot open %s\n", out_path.c_str()); st = -1; }
+  const size_t sb = fmt == DVBT2LL_IQ_SC16 ? 4 : 8;
+  std::vector<uint8_t> iq;
+  if (!st) iq.resize((size_t)batch * pi[0].iq_samples_per_frame * sb);
+  int64_t done = 0;
+  while (!st && (frames < 0 || done < frames)) {
+    int n = batch;
+    if (frames >= 0 && frames - done < n) n = (int)((frames - done) / unit * unit);
+    const void *ptr[DVBT2LL_MAX_PLP];
+    int64_t base[DVBT2LL_MAX_PLP], len[DVBT2LL_MAX_PLP];
+    for (; n > 0; n -= unit) {   // the most whole units every PLP's input still covers
+      bool ok = true;
+      for (int k = 0; k < ps.nplp && ok; k++) {
+        const dvbt2ll_plp_params &q = ps.plp[k];
+        const int P = pi[k].frames_per_if;
+        const bool hem = q.inputmode != 0;
+        const int64_t pay = (int64_t)pi[k].fec_blocks_per_frame * pi[k].payload_bytes_per_block - (q.inband ? 13 : 0);
+        const int64_t start = payload_pos(done / P * pay, hem), end = payload_pos((done + n) / P * pay, hem) + 1;
+        const int64_t lo = start >= 188 ? (start / 188) * 188 - 188 : 0;
+        ok = ts[k].span(lo, end);
+        ptr[k] = ts[k].buf.data();
+        base[k] = ts[k].base;
+        len[k] = (int64_t)ts[k].buf.size();
+      }
+      if (ok) break;
+    }
+    if (n <= 0) break;
+    st = dvbt2ll_chain_run_plps_host(h, ptr, base, len, done, n, iq.data());
+    if (st) { std::fprintf(stderr, "dvbt2ll_tx: run: %s\n", dvbt2ll_strerror(st)); break; }
+    const size_t bytes = (size_t)n * pi[0].iq_samples_per_frame * sb;
+    if (std::fwrite(iq.data(), 1, bytes, fout) != bytes) { st = -1; break; }
+    done += n;
+  }
+  std::fprintf(stderr, "dvbt2ll_tx: %s: %lld T2 frames\n", ps.name, (long long)done);
+  for (auto &t : ts)
+    if (t.f) std::fclose(t.f);
+  if (fout && fout != stdout) std::fclose(fout);
+  dvbt2ll_chain_destroy(h);
+  return st ? 1 : 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
-  std::string in_path, out_path, preset = "cfg1";
-  std::vector<std::string> sets;
+  std::string in_path, out_path, preset = "cfg1", mplp;
+  std::vector<std::string> sets, ins;
   int fmt = DVBT2LL_IQ_CF32, batch = 16, device = 0;
   bool print_params = false;
   int64_t frames = -1;
@@ -98,7 +239,8 @@ int main(int argc, char **argv) {
       return argv[++i];
     };
     if (a == "-h" || a == "--help") { usage(stdout); return 0; }
-    else if (a == "--in") in_path = next();
+    else if (a == "--in") ins.push_back(in_path = next());
+    else if (a == "--mplp") mplp = next();
     else if (a == "--out") out_path = next();
     else if (a == "--preset") preset = next();
     else if (a == "--set") sets.push_back(next());
@@ -115,6 +257,12 @@ int main(int argc, char **argv) {
     else { std::fprintf(stderr, "dvbt2ll_tx: unknown option %s\n", a.c_str()); usage(stderr); return 2; }
   }
 
+  if (!mplp.empty()) {
+    for (auto &q : kMplpPresets)
+      if (mplp == q.name) return run_mplp(q, ins, out_path, fmt, gain, frames, batch, device, print_params);
+    std::fprintf(stderr, "dvbt2ll_tx: unknown multi-PLP preset %s\n", mplp.c_str());
+    return 2;
+  }
   dvbt2ll_chain_params p;
   std::memset(&p, 0, sizeof(p));
   const Preset *ps = nullptr;

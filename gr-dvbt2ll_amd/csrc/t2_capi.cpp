@@ -173,6 +173,7 @@ struct L1Tables {
     dev.crc_k = l.crc_k;
     dev.nsig = l.nsig; dev.fidx_pos = l.fidx_pos; dev.npost = l.npost; dev.lp = l.lp; dev.mode = l.mode;
     dev.ncols = l.ncols; dev.rows = l.rows; dev.q = l.q; dev.pbits = l.pbits; dev.t2frames = fp.t2frames;
+    dev.ncls = l.ncls;
     memcpy(dev.mux, l.mux, sizeof(dev.mux));
     return 0;
   }
@@ -476,7 +477,7 @@ struct dvbt2ll_framemapper_mplp {
   // cells port k consumes at the T2 frame frame + i: a whole interleaving frame on its first T2 frame
   int need(int k, int64_t i) const {
     const PlpPlan &pl = plan.plp[k];
-    return (frame + i) % pl.P == 0 ? pl.S_if : 0;
+    return (frame + i) % pl.cycle() == pl.FF ? pl.S_if : 0;
   }
 };
 extern "C" int dvbt2ll_framemapper_mplp_create(const dvbt2ll_mplp_params *p, int device, dvbt2ll_framemapper_mplp **out) {
@@ -666,7 +667,8 @@ struct ChainPlp {
   int pay = 0, F = 0, inputmode = 0, inband = 0;
   int P = 1;                  // T2 frames per interleaving frame (TIME_IL_TYPE 1: P_I); F, ts_per_frame are per
                               // interleaving frame
-  int64_t blocks(int64_t frames) const { return (frames + P - 1) / P * F; }   // FEC blocks of `frames` T2 frames
+  int cyc = 1;                // T2 frames from one interleaving frame to the next (P_I x FRAME_INTERVAL)
+  int64_t blocks(int64_t frames) const { return (frames + cyc - 1) / cyc * F; }   // FEC blocks of `frames` T2 frames
 };
 
 // instantiated hipGraphs of the chain's kernels (per PLP: FEC BB pass, BCH matrix-core pass; per PLP: LDPC +
@@ -736,8 +738,10 @@ struct dvbt2ll_chain {
   PilotPlan pilot;
   OfdmTables ofdm;
   DevBuf aux, inv, sym_d0, sym_n, sym_n0, ts_tmp, iq_tmp;
+  DevBuf ts_plp_tmp[DVBT2LL_MAX_PLP];   // run_plps_host: each PLP's TS on the device
   DevBuf abin, aval, aind, agrp, azr;   // non-data bins as compact lists (t2_plan.h AuxLists)
   DevBuf plp_bnd, plp_qbase, qam_all;   // multi-PLP frames: slot ranges per PLP, the PLPs' constellations
+  DevBuf cls_inv;                       // per frame class: its data slots' bins at inv + cls_inv[c]
   std::vector<int32_t> plp_bnd_host;
   std::vector<int> qbase_host;
   DevBuf sync_err;                      // TS sync bytes != 0x47 consumed by run calls (bbheader:675, 703)
@@ -950,8 +954,11 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
   int r = h->ctx.init(device);
   if (r) return r;
   // OFDM side: aux bins from cmap, data cells streamed per symbol and scattered through inv
-  ChainLayout layout;
-  if (build_chain_layout(fp, h->pilot, layout)) return DVBT2LL_EINVAL;
+  // one layout per frame class (FRAME_INTERVAL > 1: the T2 frames carry different PLPs); class 0's is `layout`
+  std::vector<ChainLayout> layouts(fp.ncls);
+  for (int c = 0; c < fp.ncls; c++)
+    if (build_chain_layout(fp, h->pilot, layouts[c], c)) return DVBT2LL_EINVAL;
+  const ChainLayout &layout = layouts[0];
   int nq = 0;   // the PLPs' constellation tables back to back (multi-PLP); 256 entries for one PLP
   std::vector<cf32> qall;
   for (int k = 0; k < h->nplp; k++) {
@@ -966,7 +973,10 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     if ((r = pl->fec.init_chain())) return r;
     if ((r = pl->map.init(q.framesize, q.rate, q.constellation, q.rotation, pl->fec.plan))) return r;
     MapDev &md = pl->map.dev;
-    md.F = pp.F;
+    // the quad table covers one launch unit (fp.unit T2 frames): rows r' = m' F + r for the unit's
+    // interleaving frames m' < fp.unit / cycle and their FEC blocks r
+    const int nif = fp.unit / pp.cycle(), Fu = pp.F * nif;
+    md.F = Fu;
     // the LDPC + map kernel's cell interleaver + TI store in stored-slot order (layout.part: frame data slot
     // of each frame data index; a TIME_IL_TYPE 1 PLP's block r writes the P_I T2 frames of its interleaving
     // frame, frame i's slots at i * pair_stride), in aligned quads of four slots: block r's quads sorted by
@@ -977,16 +987,18 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     // contiguous runs (the block's cells in a symbol (half) are one run, bank-balanced inside, t2_plan
     // build_chain_layout).  A chunk whose quads would span more than 0xFFFF quads (a block's cells in two
     // T2 frames) ends early: the rest of its 64 entries are empty quads (no store).
-    std::vector<std::vector<std::pair<int64_t, int>>> blk(pp.F);
-    std::vector<std::vector<int>> qpos(pp.F);   // per block: its quads' entry index (with the chunk padding)
+    std::vector<std::vector<std::pair<int64_t, int>>> blk(Fu);
+    std::vector<std::vector<int>> qpos(Fu);   // per block: its quads' entry index (with the chunk padding)
     int qmax = 0;
     std::vector<std::pair<int64_t, int>> cells(pp.cs);
     std::vector<int> jin(pp.cs);   // cell-interleaver input index of each output position t
-    for (int rr = 0; rr < pp.F; rr++) {
-      for (int j = 0; j < pp.cs; j++) jin[(pp.ci_perm[j] + pp.ci_shift[rr]) % pp.cs] = j;
+    for (int rr = 0; rr < Fu; rr++) {
+      const int r = rr % pp.F, f0 = rr / pp.F * pp.cycle();
+      for (int j = 0; j < pp.cs; j++) jin[(pp.ci_perm[j] + pp.ci_shift[r]) % pp.cs] = j;
       for (int t = 0; t < pp.cs; t++) {
-        const CellDest cd = cell_dest(fp, k, rr, t);
-        cells[t] = {(int64_t)cd.phase * h->pair_stride + layout.part[cd.pos], jin[t]};
+        const CellDest cd = cell_dest(fp, k, r, t, f0);
+        const int fu = f0 + cd.off;   // T2 frame of the unit, of class fu mod ncls
+        cells[t] = {(int64_t)fu * h->pair_stride + layouts[fu % fp.ncls].part[cd.pos], jin[t]};
       }
       std::sort(cells.begin(), cells.end());
       auto &qv = blk[rr];   // (quad index, slot-in-quad | t << 2) per cell
@@ -1004,10 +1016,10 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
       qmax = std::max(qmax, n + 1);
     }
     const int qst = (qmax + 63) & ~63, nchk = qst / 64;
-    std::vector<uint32_t> qsrc((size_t)pp.F * qst * 2 + 2, 0xFFFFFFFFu);
-    std::vector<uint16_t> qoff((size_t)pp.F * qst + 4, 0);
-    std::vector<int32_t> qb((size_t)pp.F * nchk + 1, 0), qn(pp.F, 0);
-    for (int rr = 0; rr < pp.F; rr++) {
+    std::vector<uint32_t> qsrc((size_t)Fu * qst * 2 + 2, 0xFFFFFFFFu);
+    std::vector<uint16_t> qoff((size_t)Fu * qst + 4, 0);
+    std::vector<int32_t> qb((size_t)Fu * nchk + 1, 0), qn(Fu, 0);
+    for (int rr = 0; rr < Fu; rr++) {
       int n = -1, qi = -1;
       int64_t qprev = -1, cbase = 0;
       for (auto &c : blk[rr]) {
@@ -1038,6 +1050,7 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     md.slot_stride = qst;
     pl->F = pp.F;
     pl->P = pp.P;
+    pl->cyc = pp.cycle();
     pl->inputmode = q.inputmode;
     pl->inband = q.inband;
     pl->cw_stride = ((pl->fec.plan.nldpc / 8) + 255) / 256 * 256;
@@ -1058,22 +1071,45 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     h->qbase_host.push_back(qb0);
     h->plps.push_back(std::move(pl));
   }
-  // stored bins -> padded LDS slots within their half (the kernel writes them as they are)
+  // stored bins -> padded LDS slots within their half (the kernel writes them as they are), the frame classes'
+  // tables back to back (each class's bins from an 8-slot boundary: the kernel reads aligned quads / octets)
   const int nsub_h = ofdm_split(h->pilot.N) ? h->pilot.N / 2 : h->pilot.N;
-  std::vector<uint16_t> inv_pad(layout.inv.size());
-  for (size_t si = 0; si < layout.inv.size(); si++)
-    inv_pad[si] = (uint16_t)ofdm_padded_bin(h->pilot.N, layout.inv[si] % nsub_h);
-  inv_pad.resize(((layout.inv.size() + 7) & ~(size_t)7) + 8, 0);   // the kernel reads aligned quads
-  if ((r = upload(h->inv, inv_pad)) || (r = upload(h->sym_d0, layout.sym_d0)) ||
-      (r = upload(h->sym_n, layout.sym_n)) || (r = upload(h->sym_n0, layout.sym_n0)))
+  std::vector<uint16_t> inv_pad;
+  std::vector<int32_t> cls_inv, sd0, sdn, sdn0, bnd_all;
+  for (const ChainLayout &lc : layouts) {
+    cls_inv.push_back((int32_t)inv_pad.size());
+    for (size_t si = 0; si < lc.inv.size(); si++)
+      inv_pad.push_back((uint16_t)ofdm_padded_bin(h->pilot.N, lc.inv[si] % nsub_h));
+    inv_pad.resize(((inv_pad.size() + 7) & ~(size_t)7) + 8, 0);
+    sd0.insert(sd0.end(), lc.sym_d0.begin(), lc.sym_d0.end());
+    sdn.insert(sdn.end(), lc.sym_n.begin(), lc.sym_n.end());
+    sdn0.insert(sdn0.end(), lc.sym_n0.begin(), lc.sym_n0.end());
+    bnd_all.insert(bnd_all.end(), lc.plp_bnd.begin(), lc.plp_bnd.end());
+  }
+  if ((r = upload(h->inv, inv_pad)) || (r = upload(h->sym_d0, sd0)) || (r = upload(h->sym_n, sdn)) ||
+      (r = upload(h->sym_n0, sdn0)) || (r = upload(h->cls_inv, cls_inv)))
     return r;
   const PilotPlan &pp = h->pilot;
   // one aux row (pilot values, L1-pre, dummy cells): the L1-post cells come per frame from the GPU
   std::vector<cf32> auxv = fp.aux;
   for (int i = 0; i < 12; i++) auxv[AUX_PILOT0 + i] = pp.pilot_values[i];
   if ((r = h->ofdm.init(pp, layout.cmap, fp.aux_len, 1))) return r;
+  // the classes' aux lists back to back (a class's dummy cells differ), group offsets rebased
   AuxLists al;
-  if (build_aux_lists(layout, pp.N, pp.Nsym, auxv, fp.aux_len, 1, al, AUX_L1PRE + 1840, fp.Lp)) return DVBT2LL_EINVAL;
+  for (const ChainLayout &lc : layouts) {
+    AuxLists ac;
+    if (build_aux_lists(lc, pp.N, pp.Nsym, auxv, fp.aux_len, 1, ac, AUX_L1PRE + 1840, fp.Lp)) return DVBT2LL_EINVAL;
+    if (ac.dbin.size() % 4) return DVBT2LL_EINVAL;   // groups of direct quads stay aligned
+    for (size_t g = 0; g + 3 < ac.grp.size(); g += 4) {
+      ac.grp[g] += (int32_t)al.dbin.size();
+      ac.grp[g + 2] += (int32_t)al.ind.size();
+    }
+    al.dbin.insert(al.dbin.end(), ac.dbin.begin(), ac.dbin.end());
+    al.dval.insert(al.dval.end(), ac.dval.begin(), ac.dval.end());
+    al.ind.insert(al.ind.end(), ac.ind.begin(), ac.ind.end());
+    al.grp.insert(al.grp.end(), ac.grp.begin(), ac.grp.end());
+    al.zrun.insert(al.zrun.end(), ac.zrun.begin(), ac.zrun.end());
+  }
   if ((r = h->l1.init(fp))) return r;
   h->l1_stride = (uint32_t)((fp.Lp + 3) & ~3);
   for (auto &b : al.dbin)
@@ -1101,15 +1137,17 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
   od.sym_d0 = h->sym_d0.as<int32_t>();
   od.sym_n = h->sym_n.as<int32_t>();
   od.sym_n0 = h->sym_n0.as<int32_t>();
+  od.ncls = fp.ncls;
+  od.cls_inv = h->cls_inv.as<int32_t>();
   od.nplp = h->nplp;
   if (h->nplp == 1) {
     od.qam = h->plps[0]->map.dev.lut;   // the 256-entry table (entries past the constellation are zero)
     od.nq = 256;
   } else {
     if (nq > OFDM_MAX_QAM) return DVBT2LL_EINVAL;
-    h->plp_bnd_host = layout.plp_bnd;
+    h->plp_bnd_host = layout.plp_bnd;   // class 0's (the debug hook's frame 0)
     std::vector<int32_t> qb(h->qbase_host.begin(), h->qbase_host.end());
-    if ((r = upload(h->qam_all, qall)) || (r = upload(h->plp_bnd, layout.plp_bnd)) || (r = upload(h->plp_qbase, qb)))
+    if ((r = upload(h->qam_all, qall)) || (r = upload(h->plp_bnd, bnd_all)) || (r = upload(h->plp_qbase, qb)))
       return r;
     od.qam = h->qam_all.as<float2>();
     od.nq = nq;
@@ -1155,7 +1193,7 @@ static bool mplp_to_plan(const dvbt2ll_mplp_params &m, FmParams &fm, std::vector
   for (int k = 0; k < m.nplp; k++) {
     const dvbt2ll_plp_params &q = m.plp[k];
     plps.push_back(PlpParams{q.framesize, q.rate, q.constellation, q.rotation, q.fecblocks, q.tiblocks, q.inputmode,
-                             q.inband, q.plp_type, q.ti_type, q.ti_frames});
+                             q.inband, q.plp_type, q.ti_type, q.ti_frames, q.frame_interval, q.first_frame_idx});
     tsrate.push_back(q.tsrate);
   }
   *nss = m.num_subslices;
@@ -1208,7 +1246,7 @@ extern "C" int dvbt2ll_chain_get_plp_info(const dvbt2ll_chain *h, int plp, dvbt2
   info->fft_size = h->pilot.N;
   info->guard_interval = h->pilot.G;
   info->cw_stride_bytes = pl.cw_stride;
-  info->frames_per_if = pl.P;
+  info->frames_per_if = pl.cyc;
   return DVBT2LL_OK;
 }
 
@@ -1227,7 +1265,7 @@ extern "C" int dvbt2ll_chain_run_device(dvbt2ll_chain *h, const void *ts_dev, in
 // stream bytes [lo, end) that frames [first, first + n) of PLP pl consume: their payload plus the packet before
 // the first one touched (its CRC-8 replaces the next sync byte, bbheader:701-713)
 static void ts_span(const ChainPlp &pl, int64_t first, int64_t n, int64_t *lo, int64_t *end) {
-  int64_t start = first / pl.P * pl.ts_per_frame, e = (first + n) / pl.P * pl.ts_per_frame;
+  int64_t start = first / pl.cyc * pl.ts_per_frame, e = (first + n) / pl.cyc * pl.ts_per_frame;
   if (pl.inputmode) {
     start = 188 * (start / 187) + (start % 187);
     e = 188 * (e / 187) + (e % 187) + 1;
@@ -1283,7 +1321,7 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
     fio[k].ts_len = len[k];
     // launch block b: FEC block b mod F of interleaving frame b / F, which fills T2 frames P (b / F) ..
     // P (b / F) + P - 1 of the launch (pairs at P pair_stride per interleaving frame)
-    fio[k].first_block = first_frame / pl.P * pl.F;
+    fio[k].first_block = first_frame / pl.cyc * pl.F;
     fio[k].out = cw.as<uint8_t>();
     fio[k].cw_stride = pl.cw_stride;
     fio[k].nblocks = (int)pl.blocks(nf);
@@ -1294,7 +1332,7 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
     fio[k].bch_part_blocks = pl.blocks(h->max_frames);
     fio[k].keep_cw = h->keep_cw;
     mio[k].out_pairs = pairs.as<uint16_t>();
-    mio[k].frame_stride = h->pair_stride * pl.P;
+    mio[k].frame_stride = h->pair_stride * h->frame.unit;
     mio[k].nblocks = (int)pl.blocks(nf);
   }
   oio.data = h->aux.as<float2>();
@@ -1383,6 +1421,26 @@ extern "C" int dvbt2ll_chain_run_host(dvbt2ll_chain *h, const void *ts, int64_t 
   return DVBT2LL_OK;
 }
 
+extern "C" int dvbt2ll_chain_run_plps_host(dvbt2ll_chain *h, const void *const *ts, const int64_t *ts_base,
+                                           const int64_t *ts_len, int64_t first_frame, int nframes, void *iq) {
+  if (!h || !ts || !ts_base || !ts_len || !iq || nframes < 1 || nframes > h->max_frames) return DVBT2LL_EINVAL;
+  HIP_TRY(hipSetDevice(h->ctx.device));
+  const void *dev[DVBT2LL_MAX_PLP];
+  for (int k = 0; k < h->nplp; k++) {
+    if (!ts[k] || ts_len[k] < 0) return DVBT2LL_EINVAL;
+    if (h->ts_plp_tmp[k].ensure((size_t)ts_len[k] + 16)) return DVBT2LL_ENOMEM;
+    HIP_TRY(hipMemcpyAsync(h->ts_plp_tmp[k].p, ts[k], (size_t)ts_len[k], hipMemcpyHostToDevice, h->ctx.stream));
+    dev[k] = h->ts_plp_tmp[k].p;
+  }
+  const size_t iq_bytes = (size_t)nframes * h->iq_per_frame * (h->ofdm.dev.fmt == DVBT2LL_IQ_SC16 ? 4 : 8);
+  if (h->iq_tmp.ensure(iq_bytes)) return DVBT2LL_ENOMEM;
+  int r = dvbt2ll_chain_run_plps(h, dev, ts_base, ts_len, first_frame, nframes, h->iq_tmp.p, nullptr);
+  if (r) return r;
+  HIP_TRY(hipMemcpyAsync(iq, h->iq_tmp.p, iq_bytes, hipMemcpyDeviceToHost, h->ctx.stream));
+  HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  return DVBT2LL_OK;
+}
+
 extern "C" int dvbt2ll_chain_host_submit(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                                          int64_t first_frame, int nframes, void *iq, int64_t *ticket) {
   if (!h || !ts || !iq || !ticket || h->nplp != 1 || nframes < 1 || nframes > h->max_frames || first_frame < 0 ||
@@ -1440,12 +1498,22 @@ extern "C" int dvbt2ll_chain_run_host_pipelined(dvbt2ll_chain *h, const void *ts
   return dvbt2ll_chain_host_wait(h, t);
 }
 
+// page-aligned heap memory, page-locked by hipHostRegister (the copies then run at the PCIe rate, as from
+// hipHostMalloc memory; the buffer stays ordinary heap memory, which the host sanitizer build tracks)
 extern "C" void *dvbt2ll_host_alloc(size_t bytes) {
+  const size_t n = ((bytes ? bytes : 1) + 4095) & ~(size_t)4095;
   void *p = nullptr;
-  return hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+  if (posix_memalign(&p, 4096, n)) return nullptr;
+  if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) {
+    std::free(p);
+    return nullptr;
+  }
+  return p;
 }
 extern "C" void dvbt2ll_host_free(void *p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  (void)hipHostUnregister(p);
+  std::free(p);
 }
 
 extern "C" int dvbt2ll_chain_set_output(dvbt2ll_chain *h, float gain, int format) {

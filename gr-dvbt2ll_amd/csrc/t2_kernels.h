@@ -64,7 +64,7 @@ struct FecIO {
 
 // ---------------------------------------------------------------- L1-post signalling (t2_plan.h L1PostPlan)
 struct L1Dev {
-  const uint32_t *tmpl;      // signal bits, FRAME_IDX and CRC zero
+  const uint32_t *tmpl;      // per frame class (frame mod ncls): signal bits, FRAME_IDX and CRC zero
   const uint32_t *crc_c;     // nsig - 32
   const uint32_t *scr;       // L1 scrambler bits or null
   const uint16_t *sig_pos;   // nsig
@@ -74,7 +74,7 @@ struct L1Dev {
   const uint16_t *sel;       // npost
   const float2 *lut;         // 64 (QPSK / 16QAM / 64QAM)
   uint32_t crc_k;
-  int nsig, fidx_pos, npost, lp, mode, ncols, rows, q, pbits, t2frames;
+  int nsig, fidx_pos, npost, lp, mode, ncols, rows, q, pbits, t2frames, ncls;
   uint8_t mux[12];
 };
 struct L1IO {
@@ -140,6 +140,11 @@ struct OfdmDev {
   int nplp;
   const int32_t *plp_bnd;
   const int32_t *plp_qbase;   // nplp: PLP p's table starts at entry plp_qbase[p] of qam
+  // frame classes (FRAME_INTERVAL > 1: t2_plan.h FrameClass): frame f uses class c = f mod ncls, whose
+  // per-symbol tables (sym_*, agrp, azr, plp_bnd) are the rows of symbol c Nsym + j and whose data slots'
+  // bins start at inv + cls_inv[c]
+  int ncls;
+  const int32_t *cls_inv;
   // scatter mode: non-data bins as compact lists per (symbol, half) group 2 j + h (t2_plan.h
   // AuxLists): agrp[g] = {direct offset, direct count, indirect offset, indirect count}
   const uint16_t *abin;     // direct padded bins, quads (0xFFFF = padding)

@@ -1145,10 +1145,11 @@ __device__ void l1post_frame(const L1Dev &d, const L1IO &io, int f, uint32_t *ld
   const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);
   const uint32_t fidx = (uint32_t)(frame % d.t2frames);   // FRAME_IDX = t2_frame_num (:1648-1651)
   const int nsw = (d.nsig + 31) >> 5, L = d.nsig - 32;
+  const uint32_t *tmpl = d.tmpl + (d.ncls > 1 ? (int)(fidx % (uint32_t)d.ncls) * nsw : 0);   // the frame's class
   for (int w = tid; w < L1_CW_WORDS; w += L1_NT) cw[w] = 0;
   // signal bits: the template with this frame's FRAME_IDX (8 bits, MSB first, at fidx_pos)
   if (tid < nsw) {
-    uint32_t v = d.tmpl[tid];
+    uint32_t v = tmpl[tid];
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const int p = d.fidx_pos + k;
@@ -1253,7 +1254,8 @@ __global__ __launch_bounds__(L1_NT) void l1post_kernel(L1Dev d, L1IO io) {
 }
 
 static bool l1_args_ok(const L1Dev &d) {
-  return d.nsig <= 32 * L1_SIG_WORDS && d.nsig >= 33 && d.pbits == 9000 && d.q > 0 && d.t2frames > 0;
+  return d.nsig <= 32 * L1_SIG_WORDS && d.nsig >= 33 && d.pbits == 9000 && d.q > 0 && d.t2frames > 0 && d.ncls > 0 &&
+         d.t2frames % d.ncls == 0;
 }
 
 hipError_t launch_l1post(const L1Dev &d, const L1IO &io, hipStream_t s) {
@@ -1941,15 +1943,18 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   BinSource src{map, data, cbase, abase, d.inv, io.pairs, qre, qim, 0u, 0u, 0u, d.abin, d.aval, d.aind, nullptr,
                 nullptr, 1, nullptr, nullptr};
   if (d.inv) {
+    // the frame's class (FRAME_INTERVAL > 1): its rows of the per-symbol tables, its slots' bins
+    const int c = d.ncls > 1 ? (int)(frame % d.ncls) : 0, jc = c * d.Nsym + j;
+    src.inv = d.inv + d.cls_inv[c];
     src.data = io.l1;                              // indirect entries: this frame's L1-post cells
     src.abase = (uint32_t)f * io.l1_stride - 1u;
-    src.d0 = (uint32_t)d.sym_d0[j];
-    src.dn = (uint32_t)d.sym_n[j];
-    src.dn0 = (uint32_t)d.sym_n0[j];
-    src.agrp = d.agrp + 2 * j;
-    src.azr = d.azr + 2 * j;
+    src.d0 = (uint32_t)d.sym_d0[jc];
+    src.dn = (uint32_t)d.sym_n[jc];
+    src.dn0 = (uint32_t)d.sym_n0[jc];
+    src.agrp = d.agrp + 2 * jc;
+    src.azr = d.azr + 2 * jc;
     src.nplp = d.nplp;
-    src.bnd = d.plp_bnd ? d.plp_bnd + 2 * j * (d.nplp + 1) : nullptr;
+    src.bnd = d.plp_bnd ? d.plp_bnd + 2 * jc * (d.nplp + 1) : nullptr;
     src.qbase = d.plp_qbase;
   }
   if (io.carriers_only) {                          // test hook (gather mode): bins in natural order
@@ -2241,9 +2246,12 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     // ofdm_stored_index); the even half's DFT-16 runs while the odd half's first loads are in flight
     float *qre = (float *)(smem + O32_QAM), *qim = qre + d.nq;
     const float2 tq = tid < d.nq ? d.qam[tid] : make_float2(0.f, 0.f);   // nq <= OFDM_MAX_QAM = O32_NT
-    BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv, io.pairs, qre, qim, (uint32_t)d.sym_d0[j], (uint32_t)d.sym_n[j],
-                  (uint32_t)d.sym_n0[j], d.abin, d.aval, d.aind, d.agrp + 2 * j, d.azr + 2 * j, d.nplp,
-                  d.plp_bnd ? d.plp_bnd + 2 * j * (d.nplp + 1) : nullptr, d.plp_qbase};
+    // the frame's class (FRAME_INTERVAL > 1): its rows of the per-symbol tables, its slots' bins
+    const int c = d.ncls > 1 ? (int)(frame % d.ncls) : 0, jc = c * d.Nsym + j;
+    BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv + d.cls_inv[c], io.pairs, qre, qim,
+                  (uint32_t)d.sym_d0[jc], (uint32_t)d.sym_n[jc], (uint32_t)d.sym_n0[jc], d.abin, d.aval, d.aind,
+                  d.agrp + 2 * jc, d.azr + 2 * jc, d.nplp,
+                  d.plp_bnd ? d.plp_bnd + 2 * jc * (d.nplp + 1) : nullptr, d.plp_qbase};
     const uint32_t dummy = (uint32_t)(O32_H + (O32_H >> O32_PS)) + (uint32_t)(tid & 63);
     // (measured and dropped: both halves' scatter inputs prefetched into registers before the
     // first half is written, in one batch or half 1 behind half 0's arrival: +11 % kernel time)
@@ -2338,7 +2346,8 @@ static hipError_t launch_ofdm_t(const OfdmDev &d, const OfdmIO &io, hipStream_t 
 
 hipError_t launch_ofdm(const OfdmDev &d, const OfdmIO &io, hipStream_t s) {
   if (io.nframes <= 0) return hipSuccess;
-  if (d.inv && (d.nq < 1 || d.nq > OFDM_MAX_QAM || d.nplp < 1 || d.nplp > 8 || (d.nplp > 1 && (!d.plp_bnd || !d.plp_qbase))))
+  if (d.inv && (d.nq < 1 || d.nq > OFDM_MAX_QAM || d.nplp < 1 || d.nplp > 8 || (d.nplp > 1 && (!d.plp_bnd || !d.plp_qbase)) ||
+                d.ncls < 1 || !d.cls_inv))
     return hipErrorInvalidValue;
   switch (d.N) {
     case 1024: return launch_ofdm_t<1024>(d, io, s);

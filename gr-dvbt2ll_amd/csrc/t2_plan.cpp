@@ -522,6 +522,7 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
   for (auto &q : plps) {                   // 0 = the reference's values
     if (q.plp_type == 0) q.plp_type = 1;
     if (q.ti_frames == 0) q.ti_frames = 1;
+    if (q.frame_interval == 0) q.frame_interval = 1;
   }
   fp.nplp = nplp;
   fp.nss = nss;
@@ -558,20 +559,24 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
     // tiblocks > fecblocks is accepted like the reference (framemapper:1114-1119): the surplus TI
     // blocks are "small" ones of floor(fecblocks / tiblocks) = 0 FEC blocks, which carry no cells
     if (q.tiblocks < 0 || q.tiblocks > 255) return -1;
-    // TIME_IL_TYPE 1 (EN 302 755 6.5): one TI block per interleaving frame over P_I T2 frames; the
-    // superframe holds whole interleaving frames (FIRST_FRAME_IDX 0, FRAME_INTERVAL 1)
+    // TIME_IL_TYPE 1 (EN 302 755 6.5): one TI block per interleaving frame over P_I T2 frames; FRAME_INTERVAL
+    // I_JUMP with FIRST_FRAME_IDX < I_JUMP (7.2.3.1); the superframe holds whole I_JUMP P_I cycles
     if ((q.plp_type != 1 && q.plp_type != 2) || (q.ti_type != 0 && q.ti_type != 1) || q.ti_frames < 1 ||
         q.ti_frames > 255 || (q.ti_type == 0 && q.ti_frames != 1) || (q.ti_type == 1 && q.tiblocks != 1) ||
-        ((int64_t)q.fecblocks * pl.cs) % q.ti_frames || p.t2frames % q.ti_frames)
+        ((int64_t)q.fecblocks * pl.cs) % q.ti_frames || q.frame_interval < 1 || q.frame_interval > 255 ||
+        q.first_frame < 0 || q.first_frame >= q.frame_interval || p.t2frames % (q.ti_frames * q.frame_interval))
       return -1;
     pl.F = q.fecblocks;
     pl.P = q.ti_frames;
+    pl.I = q.frame_interval;
+    pl.FF = q.first_frame;
+    fp.ncls = std::lcm(fp.ncls, pl.I);
     pl.S_if = pl.cs * pl.F;
     pl.S = pl.S_if / pl.P;
     pl.type2 = q.plp_type == 2;
     pl.in_off = fp.S_in;
     fp.S_in += pl.S_if;
-    fp.unit = std::lcm(fp.unit, pl.P);
+    fp.unit = std::lcm(fp.unit, pl.cycle());
     int deg;
     ci_permutation(pl.cs, pl.ci_perm, &deg);
     int small_fec, big_fec, n_big, n_small;
@@ -601,28 +606,51 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
       }
     }
   }
-  // 8.3.6.3: Type-1 PLPs back to back in PLP_ID order, then the Type-2 PLPs' sub-slices
+  // 8.3.6.3 per frame class: the present Type-1 PLPs back to back in PLP_ID order, then the present Type-2
+  // PLPs' sub-slices
   int ntype2 = 0;
-  for (int k = 0; k < nplp; k++)
-    if (!fp.plp[k].type2) {
-      fp.plp[k].start = fp.S;
-      fp.S += fp.plp[k].S;
-    } else {
-      ntype2++;
-    }
-  if (!ntype2 && nss != 1) return -1;
-  fp.t2start = ntype2 ? fp.S : 0;
-  fp.ssi = 0;
   for (int k = 0; k < nplp; k++) {
     PlpPlan &pl = fp.plp[k];
     if (!pl.type2) continue;
+    ntype2++;
     if (pl.S % nss) return -1;
     pl.ss = pl.S / nss;
-    pl.ss_off = fp.ssi;
-    pl.start = fp.t2start + fp.ssi;   // PLP_START: its first sub-slice
-    fp.ssi += pl.ss;
   }
-  if (ntype2) fp.S = fp.t2start + fp.ssi * nss;
+  if (!ntype2 && nss != 1) return -1;
+  fp.cls.assign(fp.ncls, FrameClass());
+  fp.S = 0;
+  for (int c = 0; c < fp.ncls; c++) {
+    FrameClass &fc = fp.cls[c];
+    fc.present.assign(nplp, 0);
+    fc.start.assign(nplp, 0);
+    fc.ss_off.assign(nplp, 0);
+    for (int k = 0; k < nplp; k++) fc.present[k] = c % fp.plp[k].I == fp.plp[k].FF;
+    for (int k = 0; k < nplp; k++)
+      if (fc.present[k] && !fp.plp[k].type2) {
+        fc.start[k] = fc.S;
+        fc.S += fp.plp[k].S;
+      }
+    bool any2 = false;
+    for (int k = 0; k < nplp; k++) any2 = any2 || (fc.present[k] && fp.plp[k].type2);
+    fc.t2start = any2 ? fc.S : 0;
+    for (int k = 0; k < nplp; k++) {
+      if (!fc.present[k] || !fp.plp[k].type2) continue;
+      fc.ss_off[k] = fc.ssi;
+      fc.start[k] = fc.S + fc.ssi;   // PLP_START: its first sub-slice
+      fc.ssi += fp.plp[k].ss;
+    }
+    fc.S += fc.ssi * nss;
+    fp.S = std::max(fp.S, fc.S);
+  }
+  {
+    const FrameClass &c0 = fp.cls[0];
+    fp.ssi = c0.ssi;
+    fp.t2start = c0.t2start;
+    for (int k = 0; k < nplp; k++) {
+      fp.plp[k].start = c0.start[k];
+      fp.plp[k].ss_off = c0.ss_off[k];
+    }
+  }
   {
     const PlpPlan &p0 = fp.plp[0];
     fp.cs = p0.cs; fp.F = p0.F; fp.ci_perm = p0.ci_perm; fp.ci_shift = p0.ci_shift;
@@ -630,13 +658,18 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
   }
   fp.num_data_symbols = fp.N_FC ? p.numdatasyms - 1 : p.numdatasyms;
   fp.M = fp.N_P2 * fp.C_P2 + fp.num_data_symbols * fp.C_DATA + fp.N_FC;
-  int fixed = fp.S + 1840 + fp.Lp + (fp.N_FC - fp.C_FC);
-  if (fp.M < fixed) return -1;   // reference: "too many FEC blocks in T2 frame"
-  fp.D = fp.M - fixed;
+  const int fixed0 = 1840 + fp.Lp + (fp.N_FC - fp.C_FC);
+  if (fp.M < fp.S + fixed0) return -1;   // reference: "too many FEC blocks in T2 frame"
+  fp.D = 0;
+  for (auto &fc : fp.cls) {
+    fc.D = fp.M - fixed0 - fc.S;
+    fp.D = std::max(fp.D, fc.D);
+  }
   // data cell of a T2 frame of phase ph (global frame mod unit) -> framemapper input index: the inverse time
-  // interleave (framemapper:1999-2028) and cell interleave of its PLP, whose interleaving frame (S_if cells) is
-  // at in_off of the input
-  std::vector<std::vector<int>> data_in(fp.unit, std::vector<int>(fp.S));
+  // interleave (framemapper:1999-2028) and cell interleave of its PLP, whose current interleaving frame (S_if
+  // cells) is at in_off of the input
+  std::vector<std::vector<int>> data_in(fp.unit);
+  for (int ph = 0; ph < fp.unit; ph++) data_in[ph].assign(fp.cls[ph % fp.ncls].S, 0);
   for (int k = 0; k < nplp; k++) {
     const PlpPlan &pl = fp.plp[k];
     std::vector<int> perm_inv(pl.cs);
@@ -644,8 +677,10 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
     for (int r = 0; r < pl.F; r++)
       for (int t = 0; t < pl.cs; t++) {
         const int w = perm_inv[((t - pl.ci_shift[r]) % pl.cs + pl.cs) % pl.cs];
-        const CellDest cd = cell_dest(fp, k, r, t);
-        for (int ph = cd.phase; ph < fp.unit; ph += pl.P) data_in[ph][cd.pos] = pl.in_off + r * pl.cs + w;
+        for (int f0 = 0; f0 < fp.unit; f0 += pl.cycle()) {   // the unit's interleaving frames of the PLP
+          const CellDest cd = cell_dest(fp, k, r, t, f0);
+          data_in[f0 + cd.off][cd.pos] = pl.in_off + r * pl.cs + w;
+        }
       }
   }
 
@@ -672,19 +707,23 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
   fi_tables(N, fp.C_P2, HeP, HoP);
   if (fp.N_FC) fi_tables(N, fp.N_FC, HeF, HoF);
   if ((int)He.size() != fp.C_DATA || (int)HeP.size() != fp.C_P2) return -1;
-  fp.gather_d.assign(M, 0);
   fp.gather_in.assign((size_t)fp.unit * M, 0);
+  for (auto &fc : fp.cls) fc.gather_d.assign(M, 0);
   const int aux_dummy = AUX_L1PRE + 1840 + Lp;
   auto resolve = [&](int o, int f) {
-    int v = zz[f];
-    int code_d;
-    if (v < 1840) code_d = -(AUX_L1PRE + v) - 1;
-    else if (v < 1840 + Lp) code_d = -(AUX_L1PRE + v) - 1;
-    else if (v < 1840 + Lp + fp.S) code_d = v - 1840 - Lp;
-    else if (v < 1840 + Lp + fp.S + fp.D) code_d = -(aux_dummy + (v - 1840 - Lp - fp.S)) - 1;
-    else code_d = -AUX_ZERO - 1;
-    fp.gather_d[o] = code_d;
-    for (int ph = 0; ph < fp.unit; ph++) fp.gather_in[(size_t)ph * M + o] = code_d >= 0 ? data_in[ph][code_d] : code_d;
+    const int v = zz[f];
+    for (int c = 0; c < fp.ncls; c++) {
+      const FrameClass &fc = fp.cls[c];
+      int code_d;
+      if (v < 1840) code_d = -(AUX_L1PRE + v) - 1;
+      else if (v < 1840 + Lp) code_d = -(AUX_L1PRE + v) - 1;
+      else if (v < 1840 + Lp + fc.S) code_d = v - 1840 - Lp;
+      else if (v < 1840 + Lp + fc.S + fc.D) code_d = -(aux_dummy + (v - 1840 - Lp - fc.S)) - 1;
+      else code_d = -AUX_ZERO - 1;
+      fp.cls[c].gather_d[o] = code_d;
+      for (int ph = c; ph < fp.unit; ph += fp.ncls)
+        fp.gather_in[(size_t)ph * M + o] = code_d >= 0 ? data_in[ph][code_d] : code_d;
+    }
   };
   int o = 0, base = 0, symbol = 0;
   for (int j = 0; j < fp.N_P2; j++, symbol++, base += fp.C_P2) {
@@ -699,6 +738,7 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
     const std::vector<int> &H = symbol % 2 ? HoF : HeF;
     for (int k = 0; k < fp.N_FC; k++) resolve(o++, base + H[k]);
   }
+  fp.gather_d = fp.cls[0].gather_d;
 
   // ---- L1 signalling cells
   bool v131 = p.version == 2, resv = p.reservedbiasbits && v131;
@@ -753,18 +793,20 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
 // one PLP: PLP_ID 0, PLP_START 0): FRAME_IDX (8 bits at *fidx_pos) = frame_idx
 std::vector<uint8_t> l1post_signal(const FmParams &p, const FramePlan &fp, int frame_idx, int *fidx_pos) {
   const bool v131 = p.version == 2, resv = p.reservedbiasbits && v131;
+  const FrameClass &fc = fp.cls[frame_idx % fp.ncls];
   Bits b;
   b.put((uint64_t)fp.nss, 15); b.put((uint64_t)fp.nplp, 8); b.put(0, 4); b.put(0, 8); b.put(0, 3); b.put(729833333u, 32);
   for (int k = 0; k < fp.nplp; k++) {
     const PlpParams &q = fp.plp_in[k];
     // PLP_ID, PLP_TYPE (001 Type 1, 010 Type 2), PLP_PAYLOAD_TYPE TS, FF_FLAG, FIRST_RF_IDX,
     // FIRST_FRAME_IDX 0, PLP_GROUP_ID 1
-    b.put((uint64_t)k, 8); b.put((uint64_t)q.plp_type, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3); b.put(0, 8);
-    b.put(1, 8);
-    // PLP_COD, PLP_MOD, PLP_ROTATION, PLP_FEC_TYPE, PLP_NUM_BLOCKS_MAX, FRAME_INTERVAL 1, TIME_IL_LENGTH
+    b.put((uint64_t)k, 8); b.put((uint64_t)q.plp_type, 3); b.put(3, 5); b.put(0, 1); b.put(0, 3);
+    b.put((uint64_t)q.first_frame, 8); b.put(1, 8);
+    // PLP_COD, PLP_MOD, PLP_ROTATION, PLP_FEC_TYPE, PLP_NUM_BLOCKS_MAX, FRAME_INTERVAL, TIME_IL_LENGTH
     // (N_TI for TIME_IL_TYPE 0, P_I for 1), TIME_IL_TYPE, IN_BAND_A_FLAG
     b.put(q.rate, 3); b.put(q.constellation, 3); b.put(q.rotation, 1); b.put(q.framesize, 2);
-    b.put(q.fecblocks, 10); b.put(1, 8); b.put((uint64_t)(q.ti_type ? q.ti_frames : q.tiblocks), 8);
+    b.put(q.fecblocks, 10); b.put((uint64_t)q.frame_interval, 8);
+    b.put((uint64_t)(q.ti_type ? q.ti_frames : q.tiblocks), 8);
     b.put((uint64_t)q.ti_type, 1); b.put(0, 1);
     b.put((q.inband && v131) ? 1 : 0, 1); b.put(resv ? 0x7ff : 0, 11);
     b.put(p.version == 0 ? 0 : q.inputmode + 1, 2); b.put(0, 1); b.put(0, 1);
@@ -772,10 +814,12 @@ std::vector<uint8_t> l1post_signal(const FmParams &p, const FramePlan &fp, int f
   b.put(0, 2); b.put(resv ? 0x3fffffff : 0, 30);
   if (fidx_pos) *fidx_pos = (int)b.b.size();
   // FRAME_IDX, SUB_SLICE_INTERVAL, TYPE_2_START (both 0 without Type-2 PLPs), L1_CHANGE_COUNTER
-  b.put((uint64_t)frame_idx, 8); b.put((uint64_t)fp.ssi, 22); b.put((uint64_t)fp.t2start, 22); b.put(0, 8);
+  b.put((uint64_t)frame_idx, 8); b.put((uint64_t)fc.ssi, 22); b.put((uint64_t)fc.t2start, 22); b.put(0, 8);
   b.put(0, 3); b.put(resv ? 0xff : 0, 8);
   for (int k = 0; k < fp.nplp; k++) {
-    b.put((uint64_t)k, 8); b.put((uint64_t)fp.plp[k].start, 22); b.put(fp.plp[k].F, 10);
+    // PLP_ID, PLP_START, PLP_NUM_BLOCKS (both 0 for a PLP absent from this T2 frame)
+    b.put((uint64_t)k, 8); b.put(fc.present[k] ? (uint64_t)fc.start[k] : 0, 22);
+    b.put(fc.present[k] ? (uint64_t)fp.plp[k].F : 0, 10);
     b.put(resv ? 0xff : 0, 8);
   }
   b.put(resv ? 0xff : 0, 8);
@@ -824,9 +868,17 @@ int build_l1post_plan(const FmParams &p, FramePlan &fp) {
   l.nsig = L + 32;
   if (l.nsig > L1_MAX_SIG || l.nsig != ksig_post(fp.nplp) || l.fidx_pos + 8 > L) return -1;
   const int nw = (l.nsig + 31) / 32;
-  l.tmpl.assign(nw, 0);
-  for (int i = 0; i < L; i++)
-    if (sig[i]) l.tmpl[i >> 5] |= 1u << (31 - (i & 31));
+  // one template per frame class (FRAME_IDX c is a frame of class c; its FRAME_IDX bits are cleared)
+  l.ncls = fp.ncls;
+  l.tmpl.assign((size_t)nw * fp.ncls, 0);
+  for (int c = 0; c < fp.ncls; c++) {
+    int fpos = 0;
+    std::vector<uint8_t> sc = l1post_signal(p, fp, c, &fpos);
+    if ((int)sc.size() != L || fpos != l.fidx_pos) return -1;
+    for (int k = 0; k < 8; k++) sc[fpos + k] = 0;
+    for (int i = 0; i < L; i++)
+      if (sc[i]) l.tmpl[(size_t)c * nw + (i >> 5)] |= 1u << (31 - (i & 31));
+  }
   // CRC-32/MPEG-2 (register init all ones, no final XOR) is affine in the message: crc(m) = crc(0^L)
   // ^ XOR of c_i over the set bits, c_i = the register after a lone 1 at position i
   l.crc_k = crc32_mpeg2(std::vector<uint8_t>((size_t)L, 0));
@@ -1227,10 +1279,11 @@ int64_t ti_index(const FramePlan &fp, int plp, int r, int t) {
   return (int64_t)r0 * cs + (int64_t)row * (5 * nb) + 5 * (r - r0) + e;
 }
 
-int32_t plp_cell_pos(const FramePlan &fp, int plp, int c) {
+int32_t plp_cell_pos(const FramePlan &fp, int plp, int c, int cls) {
   const PlpPlan &pl = fp.plp[plp];
-  if (!pl.type2) return pl.start + c;
-  return fp.t2start + (c / pl.ss) * fp.ssi + pl.ss_off + c % pl.ss;
+  const FrameClass &fc = fp.cls[cls];
+  if (!pl.type2) return fc.start[plp] + c;
+  return fc.t2start + (c / pl.ss) * fc.ssi + fc.ss_off[plp] + c % pl.ss;
 }
 
 // LDS bank pair of a stored bin as the OFDM kernels' scatter writes it (8-byte slot within its half,
@@ -1287,25 +1340,27 @@ static void bank_balance(std::vector<int32_t> &seq, int pos0, int U, const Bank 
   }
 }
 
-int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl) {
-  if (pp.active != fp.M || pp.N > 32768) return -1;
+int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl, int cls) {
+  if (pp.active != fp.M || pp.N > 32768 || cls < 0 || cls >= fp.ncls) return -1;
+  const FrameClass &fc = fp.cls[cls];
+  const int S = fc.S;
   // bins -> frame data order (TI output) via the framemapper's composed map
   std::vector<int32_t> nat(pp.bin_map.size());
   for (size_t i = 0; i < nat.size(); i++) {
     int32_t c = pp.bin_map[i];
-    nat[i] = c >= 0 ? fp.gather_d[c] : c;
+    nat[i] = c >= 0 ? fc.gather_d[c] : c;
   }
   cl.cmap = ofdm_stored_rows(pp.N, pp.Nsym, nat);
-  cl.inv.assign(fp.S, 0);
+  cl.inv.assign(S, 0);
   cl.sym_d0.assign(pp.Nsym, 0);
   cl.sym_n.assign(pp.Nsym, 0);
-  std::vector<char> seen(fp.S, 0);
+  std::vector<char> seen(S, 0);
   for (int j = 0; j < pp.Nsym; j++) {
-    int lo = fp.S, hi = -1, n = 0;
+    int lo = S, hi = -1, n = 0;
     for (int k = 0; k < pp.N; k++) {
       int32_t c = cl.cmap[(size_t)j * pp.N + k];
       if (c < 0) continue;
-      if (c >= fp.S || seen[c]) return -1;
+      if (c >= S || seen[c]) return -1;
       seen[c] = 1;
       cl.inv[c] = (uint16_t)k;
       lo = std::min(lo, c);
@@ -1316,7 +1371,7 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
     cl.sym_d0[j] = n ? lo : 0;
     cl.sym_n[j] = n;
   }
-  for (int s = 0; s < fp.S; s++)
+  for (int s = 0; s < S; s++)
     if (!seen[s]) return -1;
   cl.sym_n0 = cl.sym_n;
   // Slot order within each symbol (32K: within each stored half): FEC-block-major, and within a
@@ -1325,22 +1380,28 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
   // block per workgroup, one contiguous run per symbol (half) instead of 10-byte TI-row runs
   // scattered over the symbol (its per-cell deltas take any order inside a run).
   // (blocks numbered PLP-major: PLP k's block r is g0_k + r, so each symbol half's slots are PLP-major too)
-  // (a TIME_IL_TYPE 1 PLP's blocks by the first T2 frame of its interleaving frame: its other frames' cells
-  // come from the same blocks, at the same positions when the frame boundary falls between TI rows)
-  std::vector<int32_t> blk_of(fp.S), plp_of_blk;
-  for (int k = 0, g0 = 0; k < fp.nplp; g0 += fp.plp[k].F, k++)
-    for (int r = 0; r < fp.plp[k].F; r++) {
+  // (a TIME_IL_TYPE 1 PLP's blocks by the first T2 frame of the launch unit in this class that carries it: its
+  // other frames' cells come from the same blocks, at the same positions when the frame boundary falls between
+  // TI rows)
+  std::vector<int32_t> blk_of(S), plp_of_blk;
+  for (int k = 0, g0 = 0; k < fp.nplp; g0 += fp.plp[k].F, k++) {
+    const PlpPlan &pl = fp.plp[k];
+    int ph = cls;   // the first frame of class cls in the unit (k present there iff present in the class)
+    const int off = ph % pl.cycle();
+    for (int r = 0; r < pl.F; r++) {
       plp_of_blk.push_back(k);
-      for (int t = 0; t < fp.plp[k].cs; t++) {
-        const CellDest cd = cell_dest(fp, k, r, t);
-        if (cd.phase == 0) blk_of[cd.pos] = g0 + r;
+      if (!fc.present[k]) continue;
+      for (int t = 0; t < pl.cs; t++) {
+        const CellDest cd = cell_dest(fp, k, r, t, ph - off);
+        if (cd.off == off) blk_of[cd.pos] = g0 + r;
       }
     }
+  }
   const int P = fp.nplp;
   cl.plp_bnd.assign((size_t)2 * pp.Nsym * (P + 1), 0);
   const bool split = ofdm_split(pp.N);
   const int half = pp.N / 2;
-  cl.part.assign(fp.S, 0);
+  cl.part.assign(S, 0);
   std::vector<int32_t> order;
   for (int j = 0; j < pp.Nsym; j++) {
     const int d0 = cl.sym_d0[j], n = cl.sym_n[j];
@@ -1377,8 +1438,8 @@ int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl
         if (plp_of_blk[blk_of[order[k]]] > plp_of_blk[blk_of[order[k + 1]]]) return -1;
     }
   }
-  std::vector<uint16_t> inv2(fp.S);
-  for (int s = 0; s < fp.S; s++) inv2[cl.part[s]] = cl.inv[s];
+  std::vector<uint16_t> inv2(S);
+  for (int s = 0; s < S; s++) inv2[cl.part[s]] = cl.inv[s];
   cl.inv.swap(inv2);
   for (auto &c : cl.cmap)
     if (c >= 0) c = cl.part[c];

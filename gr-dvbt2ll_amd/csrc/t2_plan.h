@@ -76,13 +76,18 @@ struct FmParams {
 //  - Type-1 PLPs occupy one run of S data cells each, back to back in PLP_ID order after the L1
 //    signalling (PLP_START = start); then the Type-2 PLPs, sub-sliced: sub-slice j (S / nss cells) of
 //    every Type-2 PLP in PLP_ID order, then sub-slice j + 1 (SUB_SLICE_INTERVAL ssi, TYPE_2_START t2start).
+//  - FRAME_INTERVAL I_JUMP (7.2.3.1): the PLP occurs only in the T2 frames f with f mod I_JUMP = FIRST_FRAME_IDX;
+//    its interleaving frame spans P_I of those.  The frames then differ in which PLPs they carry: frame
+//    class c = f mod ncls (ncls = lcm of the I_JUMPs) has its own placement (FrameClass).
 struct PlpParams {
   int framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband;
-  int plp_type = 1, ti_type = 0, ti_frames = 1;
+  int plp_type = 1, ti_type = 0, ti_frames = 1, frame_interval = 1, first_frame = 0;
 };
 struct PlpPlan {
   int cs = 0, F = 0, S = 0, start = 0;   // F: FEC blocks per interleaving frame; S: cells per T2 frame
   int S_if = 0, P = 1;                   // cells per interleaving frame (F cs), its T2 frames (P_I)
+  int I = 1, FF = 0;                     // FRAME_INTERVAL, FIRST_FRAME_IDX
+  int cycle() const { return P * I; }    // T2 frames from one interleaving frame's first frame to the next's
   int type2 = 0, ss = 0, ss_off = 0;     // Type 2: sub-slice cells, offset within a sub-slice group
   int in_off = 0;                        // framemapper block: the PLP's interleaving frame in its input buffer
   int ti_on = 0, ti_small = 1, ti_big = 1, ti_nsmall = 0;
@@ -112,7 +117,8 @@ struct L1PostPlan {
   int ncols = 0, rows = 0;         // 16/64QAM bit interleaver geometry
   int q = 0, pbits = 0;            // LDPC: 25, 9000
   uint32_t crc_k = 0;              // CRC-32 of the all-zero message (the 0xFFFFFFFF init's share)
-  std::vector<uint32_t> tmpl;      // ceil(nsig / 32) words, MSB first; FRAME_IDX and CRC fields 0
+  std::vector<uint32_t> tmpl;      // per frame class ceil(nsig / 32) words, MSB first; FRAME_IDX and CRC fields 0
+  int ncls = 1;
   std::vector<uint32_t> crc_c;     // nsig - 32: CRC-32 contribution of message bit i
   std::vector<uint32_t> scr;       // ceil(nsig / 32) words of L1 scrambler PRBS, empty when off
   std::vector<uint16_t> sig_pos;   // nsig: position of signal bit i in the 7032-bit BCH info word
@@ -125,11 +131,21 @@ struct L1PostPlan {
   cf32 lut[64] = {};
 };
 
-// The single-PLP fields (cs, F, ci_perm, ci_shift, ti_*) are PLP 0's; S is the total over the PLPs.
+// The T2 frames f with f mod ncls = c: which PLPs they carry and where (8.3.6.3 over the present PLPs).
+struct FrameClass {
+  int S = 0, D = 0, ssi = 0, t2start = 0;   // data cells, dummy cells, SUB_SLICE_INTERVAL, TYPE_2_START
+  std::vector<uint8_t> present;             // per PLP
+  std::vector<int32_t> start, ss_off;       // per PLP: PLP_START (0 when absent), Type 2: offset in a sub-slice group
+  std::vector<int32_t> gather_d;            // M: mapped cell -> frame data index (< S) | aux
+};
+// The single-PLP fields (cs, F, ci_perm, ci_shift, ti_*) are PLP 0's; S is the total over the PLPs (the
+// largest of the frame classes'), D the most dummy cells of any class.
 struct FramePlan {
   int nplp = 1;
   int nss = 1, ssi = 0, t2start = 0;     // SUB_SLICES_PER_FRAME, SUB_SLICE_INTERVAL, TYPE_2_START
-  int unit = 1;                          // T2 frames per launch unit: lcm of the PLPs' P_I (the frame phases)
+  int unit = 1;                          // T2 frames per launch unit: lcm of the PLPs' P_I x I_JUMP (frame phases)
+  int ncls = 1;                          // frame classes: lcm of the PLPs' I_JUMP (frame f has class f mod ncls)
+  std::vector<FrameClass> cls;
   int S_in = 0;                          // framemapper block input: every PLP's interleaving frame (sum S_if)
   std::vector<PlpParams> plp_in;         // the PLPs' parameters
   std::vector<PlpPlan> plp;
@@ -158,8 +174,8 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps, Fram
                      int nss = 1);
 // fp.l1 from the parameters and fp's L1 geometry (called by build_frame)
 int build_l1post_plan(const FmParams &p, FramePlan &fp);
-// the L1-post signalling bits before the CRC-32 (one per byte) of FRAME_IDX frame_idx; *fidx_pos: FRAME_IDX's
-// first bit (framemapper:1553-1691 with the frame's PLP loops)
+// the L1-post signalling bits before the CRC-32 (one per byte) of FRAME_IDX frame_idx (a frame of class
+// frame_idx mod ncls); *fidx_pos: FRAME_IDX's first bit (framemapper:1553-1691 with the frame's PLP loops)
 std::vector<uint8_t> l1post_signal(const FmParams &p, const FramePlan &fp, int frame_idx, int *fidx_pos);
 // one FRAME_IDX variant's Lp L1-post cells, encoded bit by bit on the host (tests only)
 int l1post_host(const FmParams &p, const FramePlan &fp, int frame_idx, cf32 *dst);
@@ -216,7 +232,8 @@ struct ChainLayout {
   // group's slots are PLP-major, so slot s of the group belongs to the PLP p with bnd[p] <= s < bnd[p + 1]
   std::vector<int32_t> plp_bnd;
 };
-int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl);
+// the layout of the T2 frames of class cls
+int build_chain_layout(const FramePlan &fp, const PilotPlan &pp, ChainLayout &cl, int cls = 0);
 
 // Non-data bins of the fused chain as compact per-(symbol, half) lists, group g = 2 j + h
 // (h = 0 when N is not split), bins relative to the half.  The OFDM kernel zero-fills its
@@ -243,17 +260,21 @@ int build_aux_lists(const ChainLayout &cl, int N, int Nsym, const std::vector<cf
 // time-interleaver output index (within the interleaving frame, [0, S_if)) of cell-interleaved cell t of FEC
 // block r of PLP plp (framemapper:1999-2028)
 int64_t ti_index(const FramePlan &fp, int plp, int r, int t);
-// frame data-region index of cell c (< S) of PLP plp in a T2 frame (8.3.6.3: Type-1 run or Type-2 sub-slices)
-int32_t plp_cell_pos(const FramePlan &fp, int plp, int c);
-// where cell t of FEC block r of PLP plp lands: T2 frame `phase` of its interleaving frame, data index `pos`
+// frame data-region index of cell c (< S) of PLP plp in a T2 frame of class cls (8.3.6.3: Type-1 run or Type-2
+// sub-slices)
+int32_t plp_cell_pos(const FramePlan &fp, int plp, int c, int cls = 0);
+// where cell t of FEC block r of PLP plp lands when its interleaving frame starts at T2 frame f0 (a multiple of
+// the PLP's cycle): T2 frame f0 + off (off = FIRST_FRAME_IDX + I_JUMP i for the interleaving frame's i-th frame),
+// frame data index pos
 struct CellDest {
-  int phase;
+  int off;
   int32_t pos;
 };
-inline CellDest cell_dest(const FramePlan &fp, int plp, int r, int t) {
+inline CellDest cell_dest(const FramePlan &fp, int plp, int r, int t, int64_t f0 = 0) {
+  const PlpPlan &pl = fp.plp[plp];
   const int64_t u = ti_index(fp, plp, r, t);
-  const int S = fp.plp[plp].S;
-  return CellDest{(int)(u / S), plp_cell_pos(fp, plp, (int)(u % S))};
+  const int off = pl.FF + pl.I * (int)(u / pl.S);
+  return CellDest{off, plp_cell_pos(fp, plp, (int)(u % pl.S), (int)((f0 + off) % fp.ncls))};
 }
 
 // framemapper cell counts {N_P2, C_P2, C_DATA, N_FC, C_FC} (framemapper:290-356, 425-915); -1 if invalid

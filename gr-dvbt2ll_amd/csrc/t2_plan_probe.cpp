@@ -12,8 +12,8 @@ using namespace t2;
 // {carriermode, fftsize, guardinterval, l1constellation, pilotpattern, t2frames, numdatasyms, paprmode,
 // version, preamble, reservedbiasbits, l1scrambled}, nplp, then MAX_PLP x 12 per-PLP fields {framesize,
 // rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, tsrate, plp_type, ti_type,
-// ti_frames}, then num_subslices
-constexpr int PLP_INTS = 12;
+// ti_frames, frame_interval, first_frame_idx}, then num_subslices
+constexpr int PLP_INTS = 14;
 static bool parse_mplp(const int *a, FmParams &f, std::vector<PlpParams> &plps, int *nss) {
   const int n = a[12];
   if (n < 1 || n > MAX_PLP) return false;
@@ -23,7 +23,7 @@ static bool parse_mplp(const int *a, FmParams &f, std::vector<PlpParams> &plps, 
   plps.clear();
   for (int k = 0; k < n; k++) {
     const int *q = a + 13 + PLP_INTS * k;
-    plps.push_back(PlpParams{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[9], q[10], q[11]});
+    plps.push_back(PlpParams{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7], q[9], q[10], q[11], q[12], q[13]});
   }
   *nss = a[13 + PLP_INTS * MAX_PLP];
   return true;
@@ -71,7 +71,7 @@ int t2probe_chain_mplp(const int *mp, const int *pg3, int *info, int32_t *cmap, 
   PilotPlan pp;
   ChainLayout cl;
   if (build_frame_mplp(f, plps, fp, false, nss) || build_pilot(g, pp) || build_chain_layout(fp, pp, cl)) return -1;
-  info[0] = pp.Nsym; info[1] = pp.N; info[2] = fp.S; info[3] = ofdm_split(pp.N) ? 1 : 0; info[4] = fp.nplp;
+  info[0] = pp.Nsym; info[1] = pp.N; info[2] = fp.cls[0].S; info[3] = ofdm_split(pp.N) ? 1 : 0; info[4] = fp.nplp;
   if (cmap) memcpy(cmap, cl.cmap.data(), cl.cmap.size() * 4);
   if (inv) memcpy(inv, cl.inv.data(), cl.inv.size() * 2);
   if (d0) memcpy(d0, cl.sym_d0.data(), cl.sym_d0.size() * 4);

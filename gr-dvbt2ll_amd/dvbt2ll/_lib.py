@@ -51,7 +51,7 @@ MAX_PLP = 8   # DVBT2LL_MAX_PLP
 class _PlpParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "framesize", "rate", "constellation", "rotation", "fecblocks", "tiblocks", "inputmode", "inband", "tsrate",
-        "plp_type", "ti_type", "ti_frames")]
+        "plp_type", "ti_type", "ti_frames", "frame_interval", "first_frame_idx")]
 
 
 PLP_INTS = len(_PlpParams._fields_)
@@ -101,7 +101,7 @@ EXPORTS += ["dvbt2ll_framemapperfint_stream_items", "dvbt2ll_pilotgenp1insert_ac
 EXPORTS += ["dvbt2ll_bbheaderbch_set_isi"]
 EXPORTS += ["dvbt2ll_framemapper_mplp_" + f for f in ("create", "output_multiple", "stream_items", "forecast",
                                                       "general_work", "destroy")]
-EXPORTS += ["dvbt2ll_chain_" + f for f in ("host_submit", "host_wait", "run_host_pipelined")]
+EXPORTS += ["dvbt2ll_chain_" + f for f in ("host_submit", "host_wait", "run_host_pipelined", "run_plps_host")]
 EXPORTS += ["dvbt2ll_host_alloc", "dvbt2ll_host_free"]
 EXPORTS += ["dvbt2ll_chain_" + f for f in ("create_mplp", "num_plps", "unit_frames", "get_plp_info", "run_plps",
                                            "debug_plp_codewords", "debug_keep_codewords")]
@@ -141,6 +141,8 @@ def lib():
     L.dvbt2ll_chain_set_output.argtypes = [vp, ctypes.c_float, ci]
     L.dvbt2ll_chain_host_submit.argtypes = [vp, vp, i64, i64, i64, ci, vp, ctypes.POINTER(i64)]
     L.dvbt2ll_chain_host_wait.argtypes = [vp, i64]
+    L.dvbt2ll_chain_run_plps_host.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(i64), ctypes.POINTER(i64), i64,
+                                              ci, vp]
     L.dvbt2ll_chain_run_host_pipelined.argtypes = [vp, vp, i64, i64, i64, ci, vp, ci]
     L.dvbt2ll_host_alloc.restype = vp
     L.dvbt2ll_host_alloc.argtypes = [ctypes.c_size_t]

@@ -89,7 +89,7 @@ CONFIGS = {
 }
 
 MAX_PLP = 8   # DVBT2LL_MAX_PLP
-PLP_INTS = 12   # ints of dvbt2ll_plp_params
+PLP_INTS = 14   # ints of dvbt2ll_plp_params
 
 
 @dataclass(frozen=True)
@@ -111,11 +111,17 @@ class PlpConfig:
     plp_type: int = 1
     ti_type: int = 0
     ti_frames: int = 1
+    frame_interval: int = 1
+    first_frame_idx: int = 0
 
     @property
     def if_frames(self):
-        """T2 frames per interleaving frame (P_I)"""
-        return self.ti_frames if self.ti_type else 1
+        """T2 frames from one interleaving frame's first T2 frame to the next's (P_I x FRAME_INTERVAL)"""
+        return (self.ti_frames if self.ti_type else 1) * self.frame_interval
+
+    def starts_if(self, frame):
+        """whether an interleaving frame of this PLP starts at T2 frame `frame`"""
+        return frame % self.if_frames == self.first_frame_idx
 
     def bb_args(self):
         return (self.framesize, self.rate, self.inputmode, self.inband, self.fecblocks, self.tsrate)
@@ -126,7 +132,8 @@ class PlpConfig:
     def plp_args(self):
         """the dvbt2ll_plp_params layout (include/dvbt2ll_hip.h)"""
         return (self.framesize, self.rate, self.constellation, self.rotation, self.fecblocks, self.tiblocks,
-                self.inputmode, self.inband, self.tsrate, self.plp_type, self.ti_type, self.ti_frames)
+                self.inputmode, self.inband, self.tsrate, self.plp_type, self.ti_type, self.ti_frames,
+                self.frame_interval, self.first_frame_idx)
 
 
 @dataclass(frozen=True)
@@ -328,6 +335,23 @@ def _if_configs():
             _plp(c1, rate=E.C1_2, constellation=E.MOD_QPSK, rotation=E.ROTATION_OFF, fecblocks=1, tiblocks=1),
             _plp(c1, rate=E.C3_5, constellation=E.MOD_16QAM, fecblocks=1, tiblocks=1, plp_type=2,
                  inputmode=E.INPUTMODE_HIEFF)]).with_(num_subslices=6),
+        # FRAME_INTERVAL: cfg3's frame with a 256-QAM PLP in every T2 frame and a 64-QAM PLP in the odd ones only
+        # (I_JUMP 2, FIRST_FRAME_IDX 1): the even frames carry dummy cells in its place
+        "ij2_32k": mplp_from(c3, "ij2-32kext-every+odd", [
+            _plp(c3, fecblocks=100),
+            _plp(c3, rate=E.C2_3, constellation=E.MOD_64QAM, rotation=E.ROTATION_OFF, fecblocks=70, tiblocks=2,
+                 frame_interval=2, first_frame_idx=1)]),
+        # one 4K short PLP every other T2 frame (I_JUMP 2): frames 1, 3, .. carry no data cells at all
+        "ij2_4k_single": mplp_from(c1, "ij2-4k-short-single", [_plp(c1, frame_interval=2)]),
+        # 8K, four frame classes: a Type-2 16-QAM PLP every 2nd frame, a Type-1 QPSK TIME_IL_TYPE 1 PLP (P_I = 2)
+        # every 4th frame from frame 3 (interleaving frames of frames 3 + 8 m, 7 + 8 m), a Type-2 64-QAM PLP in
+        # every frame; 10 sub-slices, superframe of 8 T2 frames
+        "ij_mix_8k": mplp_from(c4, "ij-mix-8k", [
+            _plp(c4, fecblocks=12, tiblocks=2, plp_type=2, frame_interval=2),
+            _plp(c4, rate=E.C3_4, constellation=E.MOD_QPSK, rotation=E.ROTATION_ON, fecblocks=4, tiblocks=1,
+                 ti_type=1, ti_frames=2, frame_interval=4, first_frame_idx=3),
+            _plp(c4, rate=E.C2_3, constellation=E.MOD_64QAM, fecblocks=6, tiblocks=1, plp_type=2)]).with_(
+                t2frames=8, num_subslices=10),
         # 32K, two PLPs with different interleaving-frame lengths (P_I = 2 and 4: launch unit 4 frames)
         "ti1_32k_p2p4": mplp_from(c5, "ti1-32k-PI2+PI4", [
             _plp(c5, fecblocks=120, tiblocks=1, ti_type=1, ti_frames=2),

@@ -159,9 +159,9 @@ typedef struct {
   int64_t iq_samples_per_frame;
   int cell_size, stream_items, mapped_items, num_symbols, fft_size, guard_interval;
   int64_t cw_stride_bytes;     /* packed codeword stride in the internal buffer */
-  /* T2 frames per interleaving frame of the PLP (1, or P_I for TIME_IL_TYPE 1, dvbt2ll_plp_params);
-   * fec_blocks_per_frame and ts_bytes_per_frame then count one interleaving frame; stream_items stays
-   * the cells per T2 frame */
+  /* T2 frames from one interleaving frame of the PLP to the next: 1 for the reference's PLP, P_I x
+   * FRAME_INTERVAL in general (dvbt2ll_plp_params); fec_blocks_per_frame and ts_bytes_per_frame then count
+   * one interleaving frame; stream_items stays the cells per T2 frame carrying the PLP */
   int frames_per_if;
 } dvbt2ll_chain_info;
 int dvbt2ll_chain_create(const dvbt2ll_chain_params *p, int device, dvbt2ll_chain **out);
@@ -226,7 +226,8 @@ int dvbt2ll_chain_host_wait(dvbt2ll_chain *h, int64_t ticket);
  * frame f's IQ at iq + (f - first_frame) * iq_samples_per_frame samples; synchronous */
 int dvbt2ll_chain_run_host_pipelined(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                                      int64_t first_frame, int nframes, void *iq, int chunk_frames);
-/* page-locked host memory for the streaming path (hipHostMalloc); NULL on failure */
+/* page-locked host memory for the streaming path (page-aligned heap memory, hipHostRegister'ed); NULL on
+ * failure.  Free with dvbt2ll_host_free. */
 void *dvbt2ll_host_alloc(size_t bytes);
 void dvbt2ll_host_free(void *p);
 /* IQ output of the chain (default: gain 1, DVBT2LL_IQ_CF32 = pilotgenp1insert_cc's own complex64
@@ -285,9 +286,13 @@ typedef struct {
    *             FEC blocks per interleaving frame, spread over ti_frames = P_I consecutive T2 frames
    *             (TIME_IL_LENGTH = P_I, FRAME_INTERVAL 1): T2 frame i of interleaving frame m (frames
    *             m P_I + i) carries TI output cells [i D, (i + 1) D), D = fecblocks x cell size / P_I;
-   *   ti_frames P_I (0 is read as 1; must be 1 for ti_type 0; fecblocks x cell size divisible by it).
+   *   ti_frames P_I (0 is read as 1; must be 1 for ti_type 0; fecblocks x cell size divisible by it);
+   *   frame_interval  FRAME_INTERVAL = I_JUMP (7.2.3.1; 0 is read as 1): the PLP occurs only in the T2 frames f
+   *             with f mod I_JUMP = first_frame_idx (FIRST_FRAME_IDX < I_JUMP), its interleaving frame spanning
+   *             P_I of them; t2frames must be a multiple of P_I x I_JUMP.  A T2 frame carries only its PLPs
+   *             (the others' L1-post PLP_START and PLP_NUM_BLOCKS are 0), dummy cells fill the rest.
    * fecblocks is then PLP_NUM_BLOCKS: the FEC blocks of one interleaving frame. */
-  int plp_type, ti_type, ti_frames;
+  int plp_type, ti_type, ti_frames, frame_interval, first_frame_idx;
 } dvbt2ll_plp_params;
 typedef struct {
   /* the common (frame, L1, OFDM) fields of framemapperfint_cc::make */
@@ -298,8 +303,8 @@ typedef struct {
   /* SUB_SLICES_PER_FRAME of the Type-2 PLPs (0 is read as 1; must be 1 without Type-2 PLPs): the frame's
    * data cells are the Type-1 PLPs back to back in PLP_ID order, then sub-slice 0 of every Type-2 PLP
    * (PLP_ID order), sub-slice 1 of every Type-2 PLP, ...; each Type-2 PLP's cells per T2 frame divisible
-   * by it.  A chain whose PLPs have interleaving frames of several T2 frames runs whole launch units:
-   * first_frame and nframes multiples of the least common multiple of the PLPs' P_I
+   * by it.  A chain whose PLPs have interleaving frames of several T2 frames or FRAME_INTERVAL > 1 runs whole
+   * launch units: first_frame and nframes multiples of the least common multiple of the PLPs' P_I x I_JUMP
    * (dvbt2ll_chain_unit_frames). */
   int num_subslices;
 } dvbt2ll_mplp_params;
@@ -333,8 +338,8 @@ typedef struct {
 } dvbt2ll_mplp_chain_params;
 int dvbt2ll_chain_create_mplp(const dvbt2ll_mplp_chain_params *p, int device, dvbt2ll_chain **out);
 int dvbt2ll_chain_num_plps(const dvbt2ll_chain *h);
-/* T2 frames of the chain's launch unit: the least common multiple of its PLPs' interleaving-frame lengths
- * (1 for TIME_IL_TYPE 0 PLPs).  Every run's first_frame and nframes are multiples of it (else
+/* T2 frames of the chain's launch unit: the least common multiple of its PLPs' P_I x FRAME_INTERVAL
+ * (1 for the reference's PLPs).  Every run's first_frame and nframes are multiples of it (else
  * DVBT2LL_EINVAL); create fails when max_frames is smaller. */
 int dvbt2ll_chain_unit_frames(const dvbt2ll_chain *h);
 /* PLP plp's FEC blocks, payload and TS bytes per frame, cell size, cells per frame (stream_items) and
@@ -345,6 +350,9 @@ int dvbt2ll_chain_get_plp_info(const dvbt2ll_chain *h, int plp, dvbt2ll_chain_in
  * one-PLP chain == run_plps with one entry. */
 int dvbt2ll_chain_run_plps(dvbt2ll_chain *h, const void *const *ts_dev, const int64_t *ts_base,
                            const int64_t *ts_len, int64_t first_frame, int nframes, void *iq_dev, void *stream);
+/* run_plps with host buffers (each PLP's TS copied to the device, IQ copied back), synchronous */
+int dvbt2ll_chain_run_plps_host(dvbt2ll_chain *h, const void *const *ts, const int64_t *ts_base, const int64_t *ts_len,
+                                int64_t first_frame, int nframes, void *iq);
 /* test hook: PLP plp's packed codewords of the last run's frame 0 (as dvbt2ll_chain_debug_codewords) */
 int dvbt2ll_chain_debug_plp_codewords(dvbt2ll_chain *h, int plp, void *out, int64_t bytes);
 

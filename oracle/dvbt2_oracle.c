@@ -552,18 +552,21 @@ int orc_im_work(orc_im *h, int nout, const uint8_t *in, float *out, int *consume
  *    blocks in ti_blocks TI blocks) per T2 frame; TIME_IL_TYPE 1: one TI block of fec_blocks FEC blocks
  *    per interleaving frame, spread over P_I = ti_frames consecutive T2 frames, T2 frame i of the
  *    interleaving frame carrying the TI output cells [i D, (i + 1) D), D = fec_blocks cell_size / P_I
- *    (FRAME_INTERVAL 1: the PLP is in every T2 frame; interleaving frame m = T2 frames m P_I ..);
+ *    FRAME_INTERVAL I_JUMP (7.2.3.1): the PLP occurs in the T2 frames f with f mod I_JUMP = FIRST_FRAME_IDX
+ *    only (the superframe holds whole I_JUMP P_I cycles), an interleaving frame spanning P_I of those;
  *  - 8.3.6.3 mapping: Type-1 PLPs first, back to back in PLP_ID order, each one run of D cells at its
  *    PLP_START; then the Type-2 PLPs, each cut into N_subslices sub-slices of D / N_subslices cells,
  *    sub-slice j of every Type-2 PLP (PLP_ID order) before sub-slice j + 1 of any
- *    (SUB_SLICE_INTERVAL = the Type-2 cells per T2 frame / N_subslices, TYPE_2_START = the Type-1 cells). */
+ *    (SUB_SLICE_INTERVAL = the Type-2 cells per T2 frame / N_subslices, TYPE_2_START = the Type-1 cells), over
+ *    the PLPs present in the T2 frame; an absent PLP signals PLP_START = PLP_NUM_BLOCKS = 0. */
 #define ORC_MAX_PLP 16
-#define ORC_PLP_INTS 11
+#define ORC_PLP_INTS 13
 typedef struct {
   int cell_size, stream_items, start, pn_degree;   /* stream_items: cells per T2 frame (D) */
   int ti_blocks, fec_blocks, small_fec, big_fec, n_big, n_small;
   int plp_cod, plp_mod, rotation, fec_type, inband_b, plp_mode;
   int plp_type, ti_type, ti_frames, if_items, phase;   /* if_items = fec_blocks cell_size */
+  int frame_interval, first_frame, present;            /* I_JUMP, FIRST_FRAME_IDX; in the current T2 frame */
   int ss, ss_off;                                      /* Type 2: sub-slice cells, offset in a sub-slice group */
   int *permutations;
   cf *time_interleave, *ti_out;                        /* CI output, TI output of the interleaving frame */
@@ -573,6 +576,7 @@ struct orc_fm {
   int nplp, ksig_post;               /* ksig_post: L1-post signalling bits incl. CRC (KSIG_POST = 350 for one PLP) */
   orc_plp plp[ORC_MAX_PLP];
   int nss, ssi, t2start, ntype2;     /* SUB_SLICES_PER_FRAME, SUB_SLICE_INTERVAL, TYPE_2_START, Type-2 PLPs */
+  long frame;                        /* absolute T2 frame of the next work call */
   int stream_items, mapped_items, l1_constellation, eta_mod, t2_frames, t2_frame_num;
   int l1_scrambled, N_P2, C_P2, N_FC, C_FC, C_DATA, N_post, N_punc, num_data_symbols;
   /* L1 fields that are not constant (framemapper ctor :114-250) */
@@ -671,14 +675,14 @@ static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
     put_bits(info, &o, 3, 5);                /* PLP_PAYLOAD_TYPE: TS */
     info[o++] = 0;                           /* FF_FLAG */
     put_bits(info, &o, 0, 3);                /* FIRST_RF_IDX */
-    put_bits(info, &o, 0, 8);                /* FIRST_FRAME_IDX */
+    put_bits(info, &o, (unsigned)q->first_frame, 8);   /* FIRST_FRAME_IDX */
     put_bits(info, &o, 1, 8);                /* PLP_GROUP_ID */
     put_bits(info, &o, (unsigned)q->plp_cod, 3);
     put_bits(info, &o, (unsigned)q->plp_mod, 3);
     info[o++] = (uint8_t)q->rotation;
     put_bits(info, &o, (unsigned)q->fec_type, 2);
     put_bits(info, &o, (unsigned)q->fec_blocks, 10);   /* PLP_NUM_BLOCKS_MAX */
-    put_bits(info, &o, 1, 8);                /* FRAME_INTERVAL (I_JUMP) */
+    put_bits(info, &o, (unsigned)q->frame_interval, 8);   /* FRAME_INTERVAL (I_JUMP) */
     /* TIME_IL_LENGTH: N_TI (type 0) or P_I (type 1), EN 302 755 7.2.3.1 */
     put_bits(info, &o, (unsigned)(q->ti_type ? q->ti_frames : q->ti_blocks), 8);
     info[o++] = (uint8_t)q->ti_type;         /* TIME_IL_TYPE */
@@ -700,8 +704,9 @@ static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
   for (int p = 0; p < h->nplp; p++) {
     /* PLP_ID (dynamic): the reference's plp_id_dynamic is never set, i.e. 0 for its one PLP */
     put_bits(info, &o, (unsigned)p, 8);
-    put_bits(info, &o, (unsigned)h->plp[p].start, 22);       /* PLP_START (cell address after L1) */
-    put_bits(info, &o, (unsigned)h->plp[p].fec_blocks, 10);  /* PLP_NUM_BLOCKS (of the interleaving frame) */
+    const int in = h->plp[p].present;
+    put_bits(info, &o, in ? (unsigned)h->plp[p].start : 0u, 22);        /* PLP_START (cell address after L1) */
+    put_bits(info, &o, in ? (unsigned)h->plp[p].fec_blocks : 0u, 10);   /* PLP_NUM_BLOCKS (of the interleaving frame) */
     put_bits(info, &o, (unsigned)h->post_reserved4, 8);
   }
   put_bits(info, &o, (unsigned)h->post_reserved5, 8);
@@ -815,9 +820,38 @@ static void active_counts(int fft, int carriermode, int pp, int papr, int gi, in
   }
 }
 
+/* 8.3.6.3 placement over the PLPs present in T2 frame `frame`: Type-1 runs back to back in PLP_ID order, then
+ * the Type-2 sub-slices; returns the frame's data cells */
+static int frame_layout(orc_fm *h, long frame) {
+  int cells = 0;
+  for (int p = 0; p < h->nplp; p++) {
+    orc_plp *d = &h->plp[p];
+    d->present = frame % d->frame_interval == d->first_frame;
+    d->start = 0;
+  }
+  for (int p = 0; p < h->nplp; p++)
+    if (h->plp[p].present && h->plp[p].plp_type == 1) {
+      h->plp[p].start = cells;                   /* PLP_START: the cells before it */
+      cells += h->plp[p].stream_items;
+    }
+  int any2 = 0, off = 0;
+  for (int p = 0; p < h->nplp; p++) any2 |= h->plp[p].present && h->plp[p].plp_type == 2;
+  h->t2start = any2 ? cells : 0;
+  for (int p = 0; p < h->nplp; p++) {
+    orc_plp *d = &h->plp[p];
+    if (!d->present || d->plp_type != 2) continue;
+    d->ss_off = off;
+    d->start = cells + off;                      /* PLP_START: its first sub-slice */
+    off += d->ss;
+  }
+  h->ssi = off;                                  /* SUB_SLICE_INTERVAL (0 without Type-2 PLPs) */
+  return cells + off * h->nss;
+}
+
 /* framemapperfint ctor (framemapper:41-1190) for nplp data PLPs; plp: nplp x ORC_PLP_INTS ints per PLP
  * {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, plp_type (1, 2),
- * ti_type (0, 1), ti_frames (P_I)}; num_subslices: SUB_SLICES_PER_FRAME (1 without Type-2 PLPs) */
+ * ti_type (0, 1), ti_frames (P_I), frame_interval (I_JUMP), first_frame_idx}; num_subslices:
+ * SUB_SLICES_PER_FRAME (1 without Type-2 PLPs) */
 orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int num_subslices, int carriermode, int fftsize,
                            int guardinterval, int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
                            int paprmode, int version, int preamble, int reservedbiasbits, int l1scrambled) {
@@ -842,6 +876,10 @@ orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int num_subslices, int carr
     d->plp_type = q[8];
     d->ti_type = q[9];
     d->ti_frames = q[10];
+    d->frame_interval = q[11];
+    d->first_frame = q[12];
+    if (d->frame_interval < 1 || d->first_frame < 0 || d->first_frame >= d->frame_interval ||
+        t2frames % (d->frame_interval * d->ti_frames)) { orc_fm_destroy(h); return NULL; }
     /* type 1 interleaving: one TI block spread over P_I >= 1 frames; type 0: P_I = 1 */
     if ((d->plp_type != 1 && d->plp_type != 2) || (d->ti_type != 0 && d->ti_type != 1) || d->ti_frames < 1 ||
         (d->ti_type == 0 && d->ti_frames != 1) || (d->ti_type == 1 && d->ti_blocks != 1) ||
@@ -992,26 +1030,20 @@ orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int num_subslices, int carr
     d->time_interleave = (cf *)calloc((size_t)d->if_items, sizeof(cf));
     d->ti_out = (cf *)calloc((size_t)d->if_items, sizeof(cf));
   }
-  /* 8.3.6.3: Type-1 PLPs back to back in PLP_ID order, then the sub-sliced Type-2 PLPs */
+  /* 8.3.6.3: Type-1 PLPs back to back in PLP_ID order, then the sub-sliced Type-2 PLPs (frame_layout); the
+   * most data cells any T2 frame of the superframe carries must fit */
   if (!h->ntype2 && num_subslices != 1) { orc_fm_destroy(h); return NULL; }
-  for (int p = 0; p < nplp; p++)
-    if (h->plp[p].plp_type == 1) {
-      h->plp[p].start = h->stream_items;         /* PLP_START: the cells before it */
-      h->stream_items += h->plp[p].stream_items;
-    }
-  h->t2start = h->ntype2 ? h->stream_items : 0;
-  for (int p = 0, off = 0; p < nplp; p++) {
+  for (int p = 0; p < nplp; p++) {
     orc_plp *d = &h->plp[p];
     if (d->plp_type != 2) continue;
     if (d->stream_items % num_subslices) { orc_fm_destroy(h); return NULL; }
     d->ss = d->stream_items / num_subslices;
-    d->ss_off = off;
-    d->start = h->stream_items + off;           /* PLP_START: its first sub-slice */
-    off += d->ss;
-    h->ssi = off;                               /* SUB_SLICE_INTERVAL */
   }
-  for (int p = 0; p < nplp; p++)
-    if (h->plp[p].plp_type == 2) h->stream_items += h->plp[p].stream_items;
+  for (long f = 0; f < t2frames; f++) {
+    const int c = frame_layout(h, f);
+    if (c > h->stream_items) h->stream_items = c;
+  }
+  frame_layout(h, 0);
   if (h->N_FC == 0) { h->mapped_items = h->N_P2 * h->C_P2 + numdatasyms * h->C_DATA; h->num_data_symbols = numdatasyms; }
   else { h->mapped_items = h->N_P2 * h->C_P2 + (numdatasyms - 1) * h->C_DATA + h->N_FC; h->num_data_symbols = numdatasyms - 1; }
   int fixed = h->stream_items + 1840 + h->N_post / h->eta_mod + (h->N_FC - h->C_FC);
@@ -1019,7 +1051,8 @@ orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int num_subslices, int carr
   h->cell_out = (cf *)calloc((size_t)h->mapped_items, sizeof(cf));
   h->frame_out = (cf *)calloc((size_t)h->mapped_items, sizeof(cf));
   h->zigzag = (cf *)calloc((size_t)h->mapped_items, sizeof(cf));
-  int ndummy = h->mapped_items - fixed;
+  /* dummy cells of a T2 frame with no data cells at all (a frame without its PLPs, FRAME_INTERVAL > 1) */
+  int ndummy = h->mapped_items - (fixed - h->stream_items);
   h->dummy = (cf *)calloc((size_t)ndummy + 1, sizeof(cf));
   /* init_dummy_randomizer (framemapper:1912-1926) */
   int sr = 0x4A80;
@@ -1040,7 +1073,7 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
                       int paprmode, int version, int preamble, int inputmode,
                       int reservedbiasbits, int l1scrambled, int inband) {
   const int plp[ORC_PLP_INTS] = {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband,
-                                 1, 0, 1};
+                                 1, 0, 1, 1, 0};
   return orc_fm_create_mplp(1, plp, 1, carriermode, fftsize, guardinterval, l1constellation, pilotpattern, t2frames,
                             numdatasyms, paprmode, version, preamble, reservedbiasbits, l1scrambled);
 }
@@ -1058,12 +1091,18 @@ void orc_fm_destroy(orc_fm *h) {
 
 void orc_fm_seek(orc_fm *h, long frame) {
   h->t2_frame_num = (int)(frame % h->t2_frames);
-  for (int p = 0; p < h->nplp; p++) h->plp[p].phase = (int)(frame % h->plp[p].ti_frames);
+  h->frame = frame;
+  for (int p = 0; p < h->nplp; p++) {   /* the PLP's T2 frames before `frame`, mod P_I */
+    const orc_plp *d = &h->plp[p];
+    const long before = frame > d->first_frame ? (frame - d->first_frame + d->frame_interval - 1) / d->frame_interval : 0;
+    h->plp[p].phase = (int)(before % d->ti_frames);
+  }
 }
 
 int orc_fm_consume(const orc_fm *h, int plp) {
   if (plp < 0 || plp >= h->nplp) return 0;
-  return h->plp[plp].phase == 0 ? h->plp[plp].if_items : 0;
+  const orc_plp *d = &h->plp[plp];
+  return h->frame % d->frame_interval == d->first_frame && d->phase == 0 ? d->if_items : 0;
 }
 
 /* general_work (framemapper:1948-2151), exactly one T2 frame: in = the cells each PLP consumes this
@@ -1071,11 +1110,13 @@ int orc_fm_consume(const orc_fm *h, int plp) {
 int orc_fm_work(orc_fm *h, const float *inf, float *outf) {
   const cf *in = (const cf *)inf;
   cf *out = (cf *)outf;
-  int M = h->mapped_items, S = h->stream_items;
+  const int S = frame_layout(h, h->frame);   /* this T2 frame's PLPs and their placement */
+  int M = h->mapped_items;
   int Lp = h->N_post / h->eta_mod;
   for (int p = 0; p < h->nplp; p++) {
     orc_plp *d = &h->plp[p];
     int cs = d->cell_size;
+    if (!d->present) continue;
     if (d->phase == 0) {   /* a new interleaving frame: cell + time interleave it (framemapper:1973-2028) */
       /* cell interleaver :1973-1998 */
       int cell_index = 0;
@@ -1125,6 +1166,7 @@ int orc_fm_work(orc_fm *h, const float *inf, float *outf) {
   for (int j = 0; j < 1840; j++) dst[o++] = h->l1pre_cache[j];
   add_l1post(h, dst + o, h->t2_frame_num);
   h->t2_frame_num = (h->t2_frame_num + 1) % h->t2_frames;
+  h->frame++;
   o += Lp;
   for (int j = 0; j < S; j++) dst[o++] = h->cell_out[j];
   int ndummy = M - S - 1840 - Lp - (h->N_FC - h->C_FC);

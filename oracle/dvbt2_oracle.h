@@ -62,12 +62,13 @@ orc_fm *orc_fm_create(int framesize, int rate, int constellation, int rotation, 
                       int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
                       int paprmode, int version, int preamble, int inputmode,
                       int reservedbiasbits, int l1scrambled, int inband);
-/* nplp data PLPs in one T2 frame (EN 302 755 6.5, 8.3.6.3; the reference carries one Type-1 PLP with
- * TIME_IL_TYPE 0, framemapper:152-250; PARITY UNPINNED beyond that frame): plp = nplp x
+/* nplp data PLPs in one T2 frame (EN 302 755 6.5, 7.2.3.1, 8.3.6.3; the reference carries one Type-1 PLP
+ * with TIME_IL_TYPE 0 in every frame, framemapper:152-250; PARITY UNPINNED beyond that frame): plp = nplp x
  * {framesize, rate, constellation, rotation, fecblocks, tiblocks, inputmode, inband, plp_type (1 | 2),
  * ti_type (TIME_IL_TYPE 0 | 1), ti_frames (P_I: 1 for type 0; type 1: one TI block, tiblocks = 1, of
- * fecblocks FEC blocks spread over P_I T2 frames)}; num_subslices = SUB_SLICES_PER_FRAME of the Type-2
- * PLPs (1 without any); the other arguments are the common fields. */
+ * fecblocks FEC blocks spread over P_I T2 frames), frame_interval (I_JUMP), first_frame_idx (< I_JUMP)};
+ * num_subslices = SUB_SLICES_PER_FRAME of the Type-2 PLPs (1 without any); the other arguments are the
+ * common fields. */
 orc_fm *orc_fm_create_mplp(int nplp, const int *plp, int num_subslices, int carriermode, int fftsize,
                            int guardinterval, int l1constellation, int pilotpattern, int t2frames, int numdatasyms,
                            int paprmode, int version, int preamble, int reservedbiasbits, int l1scrambled);

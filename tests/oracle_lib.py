@@ -158,8 +158,8 @@ class FMM(FM):
     Type-1 PLP): work() takes the cells every PLP consumes this T2 frame (consume(k): a whole interleaving
     frame on its first T2 frame, else none), PLP 0 first"""
     def __init__(self, mcfg):
-        plp = np.array([list(p.plp_args()[:8]) + [p.plp_type, p.ti_type, p.ti_frames] for p in mcfg.plps],
-                       np.int32).reshape(-1)
+        plp = np.array([list(p.plp_args()[:8]) + [p.plp_type, p.ti_type, p.ti_frames, p.frame_interval,
+                                                   p.first_frame_idx] for p in mcfg.plps], np.int32).reshape(-1)
         self._plp = plp
         self.h = lib().orc_fm_create_mplp(mcfg.nplp, _p(plp), mcfg.num_subslices, *mcfg.common_args())
         assert self.h, "oracle multi-PLP framemapper create failed"
@@ -192,7 +192,7 @@ def mplp_cells(mcfg, first_frame, nframes):
         ts, base = ts_for_frames(p, 0, first_frame + nframes, seed=k + 1)
         off = 0
         bits_k, cw_k = [], []
-        for f in range(0, first_frame + nframes, P):
+        for f in range(p.first_frame_idx, first_frame + nframes, P):   # its interleaving frames' first T2 frames
             bits, c = bb.work(ts[off:], F)
             off += c
             if f >= first_frame:

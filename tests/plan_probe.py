@@ -247,7 +247,8 @@ def chain_layout_mplp(mcfg):
     info = np.zeros(5, np.int32)
     fr = frame_plan_mplp(mcfg)
     pl = pilot_plan(mcfg.pg_args())
-    Nsym, N, S, P = pl["Nsym"], pl["N"], fr["S"], fr["nplp"]
+    assert lib().t2probe_chain_mplp(_p(a), _p(pg3), _p(info), *([None] * 7)) == 0
+    Nsym, N, S, P = pl["Nsym"], pl["N"], int(info[2]), fr["nplp"]   # frame class 0's data cells
     cmap = np.zeros(Nsym * N, np.int32)
     inv = np.zeros(S, np.uint16)
     d0, dn, dn0 = (np.zeros(Nsym, np.int32) for _ in range(3))

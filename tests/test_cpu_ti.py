@@ -37,12 +37,12 @@ def test_if_frame_matches_oracle(name):
     fm = O.FMM(m)
     assert fr is not None and fr["unit"] == m.unit_frames
     assert (fr["M"], fr["S"], fr["Lp"]) == (fm.mapped_items, fm.stream_items, fm.l1post_cells)
-    cur = [None] * m.nplp
+    cur = [np.zeros(p.fecblocks * c, np.complex64) for p, c in zip(m.plps, fr["cs"])]   # before a PLP's first
     for f in range(2 * fr["unit"]):
         fresh = []
         for k, p in enumerate(m.plps):
             n = fm.consume(k)
-            assert n == (p.fecblocks * fr["cs"][k] if f % p.if_frames == 0 else 0)
+            assert n == (p.fecblocks * fr["cs"][k] if p.starts_if(f) else 0)
             if n:
                 cur[k] = _rand(n)
                 fresh.append(cur[k])
@@ -57,6 +57,23 @@ def _field(bits, pos, n):
     return int("".join(str(int(b)) for b in bits[pos:pos + n]), 2)
 
 
+def _placement(m, frame, per):
+    """8.3.6.3 restated independently: the PLPs present in T2 frame `frame` (f mod I_JUMP = FIRST_FRAME_IDX),
+    Type-1 runs back to back in PLP_ID order, then the Type-2 sub-slices; returns (present, PLP_START per PLP
+    (0 when absent), TYPE_2_START, SUB_SLICE_INTERVAL, cells)"""
+    present = [frame % p.frame_interval == p.first_frame_idx for p in m.plps]
+    start, cells = [0] * m.nplp, 0
+    for k, p in enumerate(m.plps):
+        if present[k] and p.plp_type == 1:
+            start[k], cells = cells, cells + per[k]
+    t2 = [k for k, p in enumerate(m.plps) if present[k] and p.plp_type == 2]
+    ssi = 0
+    for k in t2:
+        start[k] = cells + ssi
+        ssi += per[k] // m.num_subslices
+    return present, start, (cells if t2 else 0), ssi, cells + ssi * m.num_subslices
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_if_l1post_fields(name):
     """the L1-post (EN 302 755 7.2.3): SUB_SLICES_PER_FRAME, per PLP PLP_TYPE, PLP_NUM_BLOCKS_MAX,
@@ -65,31 +82,32 @@ def test_if_l1post_fields(name):
     bits at the standard's field offsets"""
     m = IF_CONFIGS[name]
     fr = PP.frame_plan_mplp(m)
-    bits = PP.l1post_bits_mplp(m, 1)
-    assert _field(bits, 0, 15) == m.num_subslices and _field(bits, 15, 8) == m.nplp
-    o = 15 + 8 + 4 + 8 + 3 + 32
-    for k, p in enumerate(m.plps):
-        assert _field(bits, o, 8) == k                          # PLP_ID
-        assert _field(bits, o + 8, 3) == p.plp_type             # PLP_TYPE
-        q = o + 8 + 3 + 5 + 1 + 3
-        assert _field(bits, q, 8) == 0                          # FIRST_FRAME_IDX
-        q += 8 + 8 + 3 + 3 + 1 + 2
-        assert _field(bits, q, 10) == p.fecblocks               # PLP_NUM_BLOCKS_MAX
-        assert _field(bits, q + 10, 8) == 1                     # FRAME_INTERVAL
-        assert _field(bits, q + 18, 8) == (p.ti_frames if p.ti_type else p.tiblocks)   # TIME_IL_LENGTH
-        assert _field(bits, q + 26, 1) == p.ti_type             # TIME_IL_TYPE
-        o += 89
-    o += 2 + 30
-    assert _field(bits, o, 8) == 1                              # FRAME_IDX
-    ntype2 = sum(p.plp_type == 2 for p in m.plps)
-    assert _field(bits, o + 8, 22) == (fr["ssi"] if ntype2 else 0)       # SUB_SLICE_INTERVAL
-    assert _field(bits, o + 30, 22) == (fr["t2start"] if ntype2 else 0)  # TYPE_2_START
-    o += 8 + 22 + 22 + 8 + 3 + 8
-    for k, p in enumerate(m.plps):
-        assert _field(bits, o, 8) == k
-        assert _field(bits, o + 8, 22) == fr["start"][k]       # PLP_START
-        assert _field(bits, o + 30, 10) == p.fecblocks          # PLP_NUM_BLOCKS
-        o += 48
+    for fidx in range(m.t2frames):
+        bits = PP.l1post_bits_mplp(m, fidx)
+        present, start, t2start, ssi, _ = _placement(m, fidx, fr["plp_S"])
+        assert _field(bits, 0, 15) == m.num_subslices and _field(bits, 15, 8) == m.nplp
+        o = 15 + 8 + 4 + 8 + 3 + 32
+        for k, p in enumerate(m.plps):
+            assert _field(bits, o, 8) == k                          # PLP_ID
+            assert _field(bits, o + 8, 3) == p.plp_type             # PLP_TYPE
+            q = o + 8 + 3 + 5 + 1 + 3
+            assert _field(bits, q, 8) == p.first_frame_idx          # FIRST_FRAME_IDX
+            q += 8 + 8 + 3 + 3 + 1 + 2
+            assert _field(bits, q, 10) == p.fecblocks               # PLP_NUM_BLOCKS_MAX
+            assert _field(bits, q + 10, 8) == p.frame_interval      # FRAME_INTERVAL
+            assert _field(bits, q + 18, 8) == (p.ti_frames if p.ti_type else p.tiblocks)   # TIME_IL_LENGTH
+            assert _field(bits, q + 26, 1) == p.ti_type             # TIME_IL_TYPE
+            o += 89
+        o += 2 + 30
+        assert _field(bits, o, 8) == fidx                           # FRAME_IDX
+        assert _field(bits, o + 8, 22) == ssi                       # SUB_SLICE_INTERVAL
+        assert _field(bits, o + 30, 22) == t2start                  # TYPE_2_START
+        o += 8 + 22 + 22 + 8 + 3 + 8
+        for k, p in enumerate(m.plps):
+            assert _field(bits, o, 8) == k
+            assert _field(bits, o + 8, 22) == start[k]             # PLP_START (0 when absent)
+            assert _field(bits, o + 30, 10) == (p.fecblocks if present[k] else 0)   # PLP_NUM_BLOCKS
+            o += 48
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -99,17 +117,11 @@ def test_if_geometry(name):
     TIME_IL_TYPE 1 PLP carries fecblocks x cell size / P_I cells per T2 frame"""
     m = IF_CONFIGS[name]
     fr = PP.frame_plan_mplp(m)
-    per = [p.fecblocks * c // p.if_frames for p, c in zip(m.plps, fr["cs"])]
+    per = [p.fecblocks * c * p.frame_interval // p.if_frames for p, c in zip(m.plps, fr["cs"])]
     assert fr["plp_S"] == per
-    t1 = [k for k, p in enumerate(m.plps) if p.plp_type == 1]
-    t2 = [k for k, p in enumerate(m.plps) if p.plp_type == 2]
-    assert [fr["start"][k] for k in t1] == list(np.cumsum([0] + [per[k] for k in t1])[:-1])
-    if t2:
-        assert fr["t2start"] == sum(per[k] for k in t1)
-        assert fr["ssi"] * m.num_subslices == sum(per[k] for k in t2)
-        assert [fr["start"][k] for k in t2] == list(fr["t2start"] + np.cumsum([0] + [per[k] // m.num_subslices
-                                                                                    for k in t2])[:-1])
-    assert fr["S"] == sum(per)
+    present, start, t2start, ssi, cells = _placement(m, 0, per)   # the frame class of T2 frame 0
+    assert fr["start"] == start and fr["t2start"] == t2start and fr["ssi"] == ssi
+    assert fr["S"] == max(_placement(m, f, per)[4] for f in range(m.t2frames))
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -119,9 +131,13 @@ def test_if_chain_layout(name):
     m = IF_CONFIGS[name]
     cl = PP.chain_layout_mplp(m)
     fr = cl["frame"]
-    P, S = cl["nplp"], cl["S"]
+    P = cl["nplp"]
+    present, _, _, _, S = _placement(m, 0, fr["plp_S"])   # class 0's layout
+    assert cl["S"] == S
     plp_of_cell = np.full(S, -1, np.int64)
     for k, p in enumerate(m.plps):
+        if not present[k]:
+            continue
         c = np.arange(fr["plp_S"][k])
         if p.plp_type == 1:
             pos = fr["start"][k] + c
@@ -163,8 +179,8 @@ def test_if_rejects_invalid():
     assert PP.frame_plan_mplp(s.with_(num_subslices=11)) is None            # 756000 % 11 != 0
     assert PP.frame_plan_mplp(_bad(m, plp_type=3)) is None
     for bad in (_bad(m, tiblocks=2), m.with_(num_subslices=2)):
-        plp = np.array([list(p.plp_args()[:8]) + [p.plp_type, p.ti_type, p.ti_frames] for p in bad.plps],
-                       np.int32).reshape(-1)
+        plp = np.array([list(p.plp_args()[:8]) + [p.plp_type, p.ti_type, p.ti_frames, p.frame_interval,
+                                                   p.first_frame_idx] for p in bad.plps], np.int32).reshape(-1)
         assert not O.lib().orc_fm_create_mplp(bad.nplp, O._p(plp), bad.num_subslices, *bad.common_args())
 
 

@@ -45,3 +45,13 @@ def test_tx_fails_cleanly_without_device(tmp_path):
         pytest.skip("a GPU is visible")
     r = run("--in", "/dev/null", "--out", str(tmp_path / "iq.bin"))
     assert r.returncode == 1 and "chain create" in r.stderr
+
+
+@pytest.mark.parametrize("name", ["mplp3_4k", "mix_4k"])
+def test_tx_mplp_presets_match_configs(name):
+    """the transmitter's multi-PLP presets resolve to exactly configs.py's frames (dvbt2ll_mplp_params ints)"""
+    from dvbt2ll.configs import MPLP_CONFIGS, IF_CONFIGS
+    m = {**MPLP_CONFIGS, **IF_CONFIGS}[name]
+    r = subprocess.run([str(TOOL), "--mplp", name, "--print-params"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert [int(x) for x in r.stdout.split()] == m.mplp_array()

@@ -1,5 +1,6 @@
-"""TIME_IL_TYPE 1 interleaving frames (one TI block over P_I T2 frames) and sub-sliced Type-2 PLPs on the GPU
-(EN 302 755 6.5, 8.3.6.3): the fused chain and the drop-in blocks, bit-exact against the
+"""TIME_IL_TYPE 1 interleaving frames (one TI block over P_I T2 frames), FRAME_INTERVAL > 1 (PLPs in every
+I_JUMP-th T2 frame only: frame classes) and sub-sliced Type-2 PLPs on the GPU (EN 302 755
+6.5, 7.2.3.1, 8.3.6.3): the fused chain and the drop-in blocks, bit-exact against the
 oracle's framemapper generalised to both (test_cpu_ti.py pins the planner to it on the CPU).
 
 PARITY UNPINNED: the reference implements TIME_IL_TYPE 0 Type-1 PLPs only (lib/framemapperfint_cc_impl.cc:159,
@@ -63,7 +64,7 @@ def test_if_chain_codewords(gpu, name):
         assert bad.size == 0, (name, "plp", k, bad.tolist())
 
 
-@pytest.mark.parametrize("name", ["ti1_8k_p4", "mix_4k", "ti1_32k_p2p4"])
+@pytest.mark.parametrize("name", ["ti1_8k_p4", "mix_4k", "ti1_32k_p2p4", "ij_mix_8k", "ij2_4k_single"])
 def test_if_chain_units_independent(gpu, name):
     """the sharding unit: launch unit 1 (frames u .. 2u - 1) encoded alone equals the same frames of a
     two-unit batch; runs that do not start or end on a unit boundary are refused"""
@@ -108,7 +109,7 @@ def test_if_chain_rejects_bad_config(gpu):
         dvbt2ll.Chain(m.with_(num_subslices=3), max_frames=4)
 
 
-@pytest.mark.parametrize("name", ["mix_4k", "ti1_8k_p4"])
+@pytest.mark.parametrize("name", ["mix_4k", "ti1_8k_p4", "ij_mix_8k"])
 def test_if_blocks(gpu, name):
     """the drop-in path: per PLP bbheaderbch (set_isi) -> ldpc -> interleavermod once per interleaving
     frame, the multi-PLP framemapper (a TIME_IL_TYPE 1 port delivers its interleaving frame on the first of
@@ -131,7 +132,7 @@ def test_if_blocks(gpu, name):
         want_in = fmb.forecast(fmb.output_multiple())
         ports = []
         for k, (p, (bb, ld, im, ts)) in enumerate(zip(m.plps, chains)):
-            if f % p.if_frames:
+            if not p.starts_if(f):
                 assert want_in[k] == 0
                 ports.append(np.zeros(0, np.complex64))
                 continue
@@ -174,3 +175,28 @@ def test_if_chain_large_batch(gpu):
         one = _run(ch, m, first, 2)
         got = iq[first * per:(first + 2) * per].cpu().numpy().view(np.complex64).reshape(-1)
         np.testing.assert_array_equal(one.view(np.uint32), got.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["mix_4k", "mplp3_4k"])
+def test_tx_tool_mplp(gpu, tmp_path, name):
+    """dvbt2ll_tx --mplp (one TS file per PLP, batches of whole launch units, dvbt2ll_chain_run_plps_host)
+    writes exactly the chain's IQ"""
+    import subprocess
+    from pathlib import Path
+    from dvbt2ll.configs import MPLP_CONFIGS
+    m = {**MPLP_CONFIGS, **IF_CONFIGS}[name]
+    n = 4 * m.unit_frames
+    args = []
+    for k, p in enumerate(m.plps):
+        ts, base = ts_for_frames(p, 0, n, seed=k + 1)
+        assert base == 0
+        (tmp_path / ("p%d.ts" % k)).write_bytes(ts.tobytes())
+        args += ["--in", str(tmp_path / ("p%d.ts" % k))]
+    tool = Path(__file__).resolve().parents[1] / "gr-dvbt2ll_amd" / "dvbt2ll" / "dvbt2ll_tx"
+    r = subprocess.run([str(tool), "--mplp", name, *args, "--out", str(tmp_path / "iq.bin"), "--batch",
+                        str(2 * m.unit_frames), "--frames", str(n)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    ch = dvbt2ll.Chain(m, max_frames=n)
+    want = _run(ch, m, 0, n)
+    got = np.frombuffer((tmp_path / "iq.bin").read_bytes(), dtype=np.complex64)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -2,8 +2,10 @@
 under ASan).  `make -C gr-dvbt2ll_amd/csrc asan-host` (build container) instruments the host code of
 libdvbt2ll_hip.so (handles, planner, launch wrappers; -Xarch_host, device code untouched) and of its two
 native drivers:
-  - dvbt2ll_tx, the CLI transmitter: the chain (dvbt2ll_chain_create / run_host: H2D of the TS, the
-    kernels, D2H of the IQ), cf32 and sc16 with the output gain, batches of frames;
+  - dvbt2ll_tx, the CLI transmitter: the chain (dvbt2ll_chain_create / the streaming host ring: H2D of the
+    TS, the kernels, D2H of the IQ), cf32 and sc16 with the output gain, batches of frames; and its --mplp
+    mode (dvbt2ll_chain_create_mplp with its quad tables and per-PLP layouts, run_plps_host) for a 3-PLP
+    frame and a frame with TIME_IL_TYPE 1 and sub-sliced Type-2 PLPs (ADVICE r4: multi-PLP host code);
   - gr_flowgraph, the GR-style scheduler over the header-only adapters: every block's make /
     output_multiple / forecast / general_work with ragged noutput_items and TS chunks / consume_each.
 Each run's IQ must equal, byte for byte, the same command with the uninstrumented build (whose IQ the
@@ -16,12 +18,17 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "gr-dvbt2ll_amd"))
-from dvbt2ll.configs import CONFIGS, ts_for_frames  # noqa: E402  (numpy only: no GPU, no library load)
+from dvbt2ll.configs import CONFIGS, MPLP_CONFIGS, IF_CONFIGS, ts_for_frames  # noqa: E402  (numpy only)
 
 PLAIN = {"tx": ROOT / "gr-dvbt2ll_amd" / "dvbt2ll" / "dvbt2ll_tx", "fg": ROOT / "tests" / "adapter" / "gr_flowgraph"}
 ASAN = {"tx": ROOT / "build" / "asan_host" / "dvbt2ll_tx", "fg": ROOT / "build" / "asan_host" / "gr_flowgraph"}
+# quarantine_size_mb: large enough that the quarantine never recycles during the HIP runtime's teardown at
+# exit -- recycling a freed device-allocator chunk after the device runtime has unloaded trips the ROCm ASan
+# runtime's own CHECK (sanitizer_allocator_device.h "!dev_runtime_unloaded_", seen once a run frees ~100 MB
+# of device buffers, e.g. the streaming ring's); a larger quarantine only widens use-after-free detection
 ENV = dict(os.environ,
-           ASAN_OPTIONS="protect_shadow_gap=0:detect_leaks=0:verify_asan_link_order=0:halt_on_error=1",
+           ASAN_OPTIONS="protect_shadow_gap=0:detect_leaks=0:verify_asan_link_order=0:halt_on_error=1:"
+                        "quarantine_size_mb=4096",
            UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
 
 
@@ -57,6 +64,18 @@ def main():
         if name != "cfg3":
             cases.append(("fg", "%s_flowgraph" % name,
                           lambda o, t=tsf, c=cfg, k=nfr: [str(t), o, str(k), "7"] + fg_params(c)))
+    for name in ("mplp3_4k", "mix_4k"):
+        m = {**MPLP_CONFIGS, **IF_CONFIGS}[name]
+        n = 4 * m.unit_frames
+        ins = []
+        for k, p in enumerate(m.plps):
+            ts, base = ts_for_frames(p, 0, n, seed=k + 1)
+            f = outdir / ("%s_p%d.ts" % (name, k))
+            f.write_bytes(ts.tobytes())
+            ins += ["--in", str(f)]
+        cases.append(("tx", "%s_mplp" % name,
+                      lambda o, nm=name, i=ins, k=n, u=m.unit_frames:
+                      ["--mplp", nm, *i, "--out", o, "--batch", str(2 * u), "--frames", str(k)]))
     for tool in ASAN.values():   # the instrumented drivers really load the sanitizer runtime and library
         deps = subprocess.run(["ldd", str(tool)], capture_output=True, text=True, check=True).stdout
         assert "libclang_rt.asan" in deps and str(ROOT / "build" / "asan_host" / "libdvbt2ll_hip.so") in deps, deps
