@@ -1430,7 +1430,15 @@ hipError_t launch_ldpc_map(const FecDev &fd, const FecIO &fio, const MapDev &md,
 }
 
 // ============================================================================ OFDM kernels
-constexpr int OFDM_SQ16 = 8;   // data-slot quads per thread per scatter round (N <= 16K)
+constexpr int OFDM_SQ16 = 4;   // data-slot quads per thread per scatter round (N <= 16K: one round)
+// the first scatter round of a unit's data slots, loaded while the previous unit's transform runs
+struct SlotPre {
+  uint2 b[OFDM_SQ16], c[OFDM_SQ16];
+  int aux;            // the first round of direct aux quads below is loaded (quad tid)
+  int4 gr;            // the unit's aux group
+  uint2 ab;           // quad tid's bins and values
+  float4 av0, av1;
+};
 // exp(+2 pi i k / 32): exact at multiples of pi/2
 __device__ constexpr float kCos32[32] = {
     1.0f, 0.98078528040323043f, 0.92387953251128674f, 0.83146961230254524f, 0.70710678118654757f,
@@ -1645,19 +1653,42 @@ struct NoWork {
 // of data-slot loads is in flight (after the loop when the run has no slots)
 template <int NT, int SQ, class Mid>
 __device__ __forceinline__ void scatter_slots(float2 *lds, const BinSource &src, uint32_t r0, uint32_t rn,
-                                              uint32_t dummy, int tid, const Mid &mid, uint32_t lb);
+                                              uint32_t dummy, int tid, const Mid &mid, uint32_t lb,
+                                              const SlotPre *pre = nullptr);
 // MULTI (a kernel instantiation of its own, so the one-PLP kernels keep their register allocation):
 // the data slots of a multi-PLP frame, streamed PLP by PLP (a group's slots are PLP-major), each
 // PLP's run looked up in its own constellation table
 template <int NT, int SQ, bool MULTI = false, class Mid = NoWork>
 __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src, int g, uint32_t r0, uint32_t rn,
-                                              uint32_t dummy, int tid, const Mid &mid = Mid()) {
-  const int4 gr = src.agrp[g];
+                                              uint32_t dummy, int tid, const Mid &mid = Mid(),
+                                              const SlotPre *pre = nullptr) {
+  // the prefetched values copied out first: a select between a load of them and a global load
+  // would become a load through a select of the two pointers, and put SlotPre in scratch
+  bool pa = false;
+  int4 gr;
+  uint2 pab = make_uint2(0u, 0u);
+  float4 pv0 = make_float4(0.f, 0.f, 0.f, 0.f), pv1 = pv0;
+  if (pre) {
+    pa = pre->aux != 0;
+    gr = pre->gr;
+    pab = pre->ab;
+    pv0 = pre->av0;
+    pv1 = pre->av1;
+  }
+  if (!pa) gr = src.agrp[g];
   for (uint32_t q = (uint32_t)tid; q < ((uint32_t)gr.y >> 2); q += NT) {
     const uint32_t e0 = (uint32_t)gr.x + 4u * q;
-    const uint2 b = ld_off((const uint2 *)src.abin, e0 * 2u);
-    const float4 v01 = ld_off((const float4 *)src.aval, e0 * 8u);
-    const float4 v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
+    uint2 b;
+    float4 v01, v23;
+    if (pa && q == (uint32_t)tid) {
+      b = pab;
+      v01 = pv0;
+      v23 = pv1;
+    } else {
+      b = ld_off((const uint2 *)src.abin, e0 * 2u);
+      v01 = ld_off((const float4 *)src.aval, e0 * 8u);
+      v23 = ld_off((const float4 *)src.aval, e0 * 8u + 16u);
+    }
     const uint32_t k0 = b.x & 0xFFFFu, k1 = b.x >> 16, k2 = b.y & 0xFFFFu, k3 = b.y >> 16;
     lds[k0 != 0xFFFFu ? k0 : dummy] = make_float2(v01.x, v01.y);   // bins stored padded
     lds[k1 != 0xFFFFu ? k1 : dummy] = make_float2(v01.z, v01.w);
@@ -1676,7 +1707,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
       if (b > a) scatter_slots<NT, SQ>(lds, src, a, b - a, dummy, tid, NoWork(), (uint32_t)src.qbase[p]);
     }
   } else {
-    scatter_slots<NT, SQ>(lds, src, r0, rn, dummy, tid, mid, 0u);
+    scatter_slots<NT, SQ>(lds, src, r0, rn, dummy, tid, mid, 0u, pre);
   }
 }
 
@@ -1684,7 +1715,8 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
 // table at lb of qre / qim (QAM + rotated-Q delay) and written to their bins
 template <int NT, int SQ, class Mid>
 __device__ __forceinline__ void scatter_slots(float2 *lds, const BinSource &src, uint32_t r0, uint32_t rn,
-                                              uint32_t dummy, int tid, const Mid &mid, uint32_t lb) {
+                                              uint32_t dummy, int tid, const Mid &mid, uint32_t lb,
+                                              const SlotPre *pre) {
   if (SQ == 4) {
     // 32K kernel: slots in aligned octets, one 16-byte load of bins and one of index pairs per
     // octet (half the load instructions of quads; the pair rows are padded to a multiple of 8)
@@ -1732,11 +1764,19 @@ __device__ __forceinline__ void scatter_slots(float2 *lds, const BinSource &src,
   const uint32_t lastq = nq - 1u;
   for (uint32_t g0 = 0; g0 < nq; g0 += (uint32_t)SQ * NT) {
     uint2 b[SQ], c[SQ];
+    if (SQ == OFDM_SQ16 && pre && g0 == 0) {   // loaded by slot_prefetch
 #pragma unroll
-    for (int u = 0; u < SQ; u++) {
-      const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
-      b[u] = ld_off((const uint2 *)src.inv, s * 2u);
-      c[u] = ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u);
+      for (int u = 0; u < SQ; u++) {
+        b[u] = pre->b[u];
+        c[u] = pre->c[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < SQ; u++) {
+        const uint32_t s = q0 + 4u * min(g0 + (uint32_t)(tid + NT * u), lastq);
+        b[u] = ld_off((const uint2 *)src.inv, s * 2u);
+        c[u] = ld_off((const uint2 *)src.pairs, (src.cbase + s) * 2u);
+      }
     }
 #pragma unroll
     for (int u = 0; u < SQ; u += 2) {
@@ -1761,11 +1801,41 @@ __device__ __forceinline__ void scatter_slots(float2 *lds, const BinSource &src,
   }
 }
 
+// the loads of scatter_slots' first round for the slots [r0, r0 + rn) of bins inv, pairs at cbase
+template <int NT>
+__device__ __forceinline__ void slot_prefetch(SlotPre &p, const uint16_t *inv, const uint16_t *pairs, uint32_t cbase,
+                                              uint32_t r0, uint32_t rn, int tid, bool aux = false,
+                                              const int4 *agrp = nullptr, const uint16_t *abin = nullptr,
+                                              const float2 *aval = nullptr) {
+  p.aux = aux;
+  if (aux) {
+    p.gr = agrp[0];
+    const uint32_t q = (uint32_t)tid;
+    if (q < ((uint32_t)p.gr.y >> 2)) {
+      const uint32_t e0 = (uint32_t)p.gr.x + 4u * q;
+      p.ab = ld_off((const uint2 *)abin, e0 * 2u);
+      p.av0 = ld_off((const float4 *)aval, e0 * 8u);
+      p.av1 = ld_off((const float4 *)aval, e0 * 8u + 16u);
+    }
+  }
+  if (rn == 0) return;   // (uniform) scatter_slots runs no round
+  const uint32_t q0 = r0 & ~3u, lastq = ((r0 + rn - q0 + 3u) >> 2) - 1u;
+#pragma unroll
+  for (int u = 0; u < OFDM_SQ16; u++) {
+    const uint32_t s = q0 + 4u * min((uint32_t)(tid + NT * u), lastq);
+    p.b[u] = ld_off((const uint2 *)inv, s * 2u);
+    p.c[u] = ld_off((const uint2 *)pairs, (cbase + s) * 2u);
+  }
+}
+
 // One NSUB-point transform (N <= 16K) by NT = NSUB/V threads, ending with
 // v[u*RL + r] = y[t + NT*(u + (V/RL)*r)].  Also stores the kernel's constant tables (`stage`) to LDS.
-template <int NSUB, int V, bool MULTI, class Stage>
+// pre: the scatter's first round, loaded before (null: loaded here); after_scatter: run once the
+// scatter is in LDS (the next unit's slot_prefetch)
+template <int NSUB, int V, bool MULTI, class Stage, class After = NoWork>
 __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource &src, const float *isinc,
-                                         const float2 *tw, int tid, const Stage &stage) {
+                                         const float2 *tw, int tid, const Stage &stage, const SlotPre *pre = nullptr,
+                                         const After &after_scatter = After(), bool nobar = false) {
   constexpr int NT = NSUB / V, N = NSUB;
   constexpr int PS = FftPlan<NSUB, V>::PS;
   if (src.inv) {
@@ -1773,11 +1843,16 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
       const int2 zr = src.azr[0];
       for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
     }
-    stage.store((unsigned char *)lds, true, tid);
-    __syncthreads();
+    // nobar: the tables are in LDS already (stored once by the kernel), and the zero run, the
+    // scatter's bins and its dummy slots are disjoint, so the scatter needs no barrier after the fill
+    if (!nobar) {
+      stage.store((unsigned char *)lds, true, tid);
+      __syncthreads();
+    }
     const uint32_t dummy = (uint32_t)(NSUB + (NSUB >> PS)) + (uint32_t)(tid & 63);
-    scatter_group<NT, OFDM_SQ16, MULTI>(lds, src, 0, src.d0, src.dn, dummy, tid);
+    scatter_group<NT, OFDM_SQ16, MULTI>(lds, src, 0, src.d0, src.dn, dummy, tid, NoWork(), pre);
     __syncthreads();
+    after_scatter();
     StockhamPass<NSUB, NT, V, 1, PS>::load_lds(v, lds, tid);
     __syncthreads();
   } else {
@@ -1817,9 +1892,11 @@ struct OfdmShape {
   static constexpr int NT = N / V;
   static constexpr int PS = FftPlan<N, V>::PS;
   static constexpr int FFT_LDS = (N + (N >> PS) + 64) * 8;           // padded buffer + 64 dummy slots
+  // the next unit's first direct aux quad is prefetched with its data slots where the registers allow
+  // it (4K, 8K: 1K, 2K and 16K would spill at the 128-VGPR cap)
+  static constexpr bool AUX_PRE = N == 4096;
   static constexpr int TW_ENTRIES = 128 + N / 128;                   // two-level twiddle table
   static constexpr int QAM_OFF = FFT_LDS + TW_ENTRIES * 8;
-  static constexpr int LDS_BYTES = QAM_OFF + 256 * 8;                // + constellation re[256], im[256]
   // with the constellation tables of nq entries (multi-PLP frames: every PLP's table, re[nq] then im[nq])
   static constexpr int lds_bytes(int nq) { return QAM_OFF + nq * 8; }
 };
@@ -1918,21 +1995,30 @@ struct TableStage {
 
 // OFDM symbols of N <= 16K points: one workgroup of N / 16 threads per (symbol, frame), the
 // symbol's bins in LDS, radix-16 Stockham passes, normalisation, GI copy, IQ store
+// the slot run of unit u (symbol u / nframes of frame u % nframes) in the chain's scatter mode
+struct UnitSlots {
+  const uint16_t *inv;
+  uint32_t cbase, r0, rn;
+  const int4 *agrp;
+};
+__device__ __forceinline__ UnitSlots unit_slots(const OfdmDev &d, const OfdmIO &io, int u) {
+  const int j = u / io.nframes, f = u - j * io.nframes;
+  const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);
+  const int c = d.ncls > 1 ? (int)(frame % d.ncls) : 0, jc = c * d.Nsym + j;
+  return UnitSlots{d.inv + d.cls_inv[c], io.cell_off + (uint32_t)f * io.cell_stride, (uint32_t)d.sym_d0[jc],
+                   (uint32_t)d.sym_n[jc], d.agrp + 2 * jc};
+}
+
+// pf (one-PLP chain frames): in, this unit's first scatter round (loaded by the previous unit or
+// the kernel); out, unit un's (un < 0: none)
 template <int N, int FMT, bool MULTI>
-__global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmIO io) {
+__device__ __forceinline__ void ofdm_unit(const OfdmDev &d, const OfdmIO &io, int u, unsigned char *smem,
+                                          const TableStage<N> &tabs, int tid, SlotPre *pf = nullptr, int un = -1) {
   using Sh = OfdmShape<N>;
   constexpr int NT = Sh::NT, V = Sh::V, RL = FftPlan<N, V>::RL, UL = V / RL;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float2 *lds = (float2 *)smem;
   float2 *twl = (float2 *)(smem + Sh::FFT_LDS);
-  const int tid = threadIdx.x;
   float *qre = (float *)(smem + Sh::QAM_OFF), *qim = qre + d.nq;
-  // constant tables: loaded into registers here, stored to LDS after the zero fill
-  TableStage<N> tabs;
-  tabs.load(d, tid);
-  // one workgroup per (symbol, frame); XCD-major so each XCD walks a contiguous run of symbols
-  // for all frames of the launch at once and reads each bin_map row from its own L2
-  const int u = xcd_major(blockIdx.x, gridDim.x);
   const int j = u / io.nframes;                   // symbol
   const int f = u - j * io.nframes;               // frame within launch
   const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);   // stream-major batch
@@ -1981,7 +2067,18 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
   const IqOut<FMT> o{(char *)io.out + ((int64_t)f * io.out_stride + 2048 + (int64_t)j * (N + G)) * SB, d.gain};
   const float nrm = d.norm;
   float2 v[V];
-  sub_ifft<N, V, MULTI>(v, lds, src, d.isinc, twl, tid, tabs);
+  if (pf) {
+    auto next = [&]() {
+      if (un >= 0) {
+        const UnitSlots ns = unit_slots(d, io, un);
+        slot_prefetch<NT>(*pf, ns.inv, io.pairs, ns.cbase, ns.r0, ns.rn, tid, OfdmShape<N>::AUX_PRE, ns.agrp, d.abin,
+                          d.aval);
+      }
+    };
+    sub_ifft<N, V, MULTI>(v, lds, src, d.isinc, twl, tid, tabs, pf, next, true);
+  } else {
+    sub_ifft<N, V, MULTI>(v, lds, src, d.isinc, twl, tid, tabs);
+  }
   if ((((uintptr_t)o.base + (uint32_t)G * SB) & (2u * SB - 1u)) == 0) {
     // two consecutive samples per lane and store: lanes t, t ^ 1 swap half of their values
     // (as o32_store_pairs), so the even lane stores (t, t + 1) of every even m and the odd lane
@@ -2011,6 +2108,48 @@ __global__ __launch_bounds__(OfdmShape<N>::NT) void ofdm_kernel(OfdmDev d, OfdmI
         o.put((uint32_t)G + n, a);
         if (n >= (uint32_t)(N - G)) o.put(n - (uint32_t)(N - G), a);
       }
+  }
+}
+
+// OFDM symbols of N <= 16K points: N / 16 threads per workgroup, each workgroup a run of consecutive
+// (symbol, frame) units u = symbol * nframes + frame (the same symbol of consecutive frames: the same
+// slot bins and aux lists), so the constant tables are loaded once per run and one unit's IQ stores
+// drain while the next unit's bins are loaded.  Runs are XCD-major, so each XCD walks a contiguous
+// range of symbols for all frames of the launch and reads each symbol's tables from its own L2.
+template <int N, int FMT, bool MULTI>
+__global__ __launch_bounds__(OfdmShape<N>::NT, 4) void ofdm_kernel(OfdmDev d, OfdmIO io) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  // constant tables: loaded into registers here, stored to LDS once (one-PLP chain frames) or after
+  // every unit's zero fill
+  TableStage<N> tabs;
+  tabs.load(d, tid);
+  const int units = d.Nsym * io.nframes, per = (units + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int u0 = xcd_major(blockIdx.x, gridDim.x) * per, u1 = min(u0 + per, units);
+  // one-PLP chain frames: each unit's first scatter round is loaded during the previous unit
+  const bool pre = !MULTI && d.inv && !io.carriers_only;
+  SlotPre pf;
+  if (pre && u0 < u1) {
+    const UnitSlots ns = unit_slots(d, io, u0);
+    slot_prefetch<OfdmShape<N>::NT>(pf, ns.inv, io.pairs, ns.cbase, ns.r0, ns.rn, tid, OfdmShape<N>::AUX_PRE,
+                                    ns.agrp, d.abin, d.aval);
+    tabs.store(smem, true, tid);
+    __syncthreads();
+  }
+#pragma nounroll
+  for (int u = u0; u < u1; u++) {
+    // the previous unit's last reads of the transform buffer came before its final barrier; in the
+    // chain's scatter mode the next unit writes nothing else (the tables stay), elsewhere the table
+    // store rewrites them, so wait for every wave there
+    if (u > u0 && !pre) __syncthreads();
+    // opaque per unit: otherwise every per-thread address of the unit's passes is hoisted out of the
+    // loop and held in registers across it
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    if (pre)
+      ofdm_unit<N, FMT, MULTI>(d, io, u, smem, tabs, t, &pf, u + 1 < u1 ? u + 1 : -1);
+    else
+      ofdm_unit<N, FMT, MULTI>(d, io, u, smem, tabs, t);
   }
 }
 
@@ -2331,7 +2470,11 @@ static hipError_t launch_ofdm_f(const OfdmDev &d, const OfdmIO &io, hipStream_t 
   const int lds = Sh::lds_bytes(d.inv ? d.nq : 256);
   hipError_t e = lds_limit((const void *)ofdm_kernel<NN, FMT, MULTI>, Sh::lds_bytes(OFDM_MAX_QAM));   // the largest launch
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((ofdm_kernel<NN, FMT, MULTI>), dim3(d.Nsym * io.nframes), dim3(Sh::NT), lds, s, d, io);
+  const int units = d.Nsym * io.nframes;
+  // units per workgroup: 4 for 8K / 16K, 2 below (cfg4 8K: 2.09 -> 1.81 ms with the slot prefetch; runs
+  // of 8 or more leave a grid tail at cfg1's 4K launch sizes, profiles/r5_ofdm_runs.txt)
+  const int run = NN >= 8192 ? 4 : 2;
+  hipLaunchKernelGGL((ofdm_kernel<NN, FMT, MULTI>), dim3((units + run - 1) / run), dim3(Sh::NT), lds, s, d, io);
   return hipGetLastError();
 }
 template <int N, int FMT>
