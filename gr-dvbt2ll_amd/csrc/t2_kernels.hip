@@ -2471,9 +2471,10 @@ static hipError_t launch_ofdm_f(const OfdmDev &d, const OfdmIO &io, hipStream_t 
   hipError_t e = lds_limit((const void *)ofdm_kernel<NN, FMT, MULTI>, Sh::lds_bytes(OFDM_MAX_QAM));   // the largest launch
   if (e != hipSuccess) return e;
   const int units = d.Nsym * io.nframes;
-  // units per workgroup: 4 for 8K / 16K, 2 below (cfg4 8K: 2.09 -> 1.81 ms with the slot prefetch; runs
-  // of 8 or more leave a grid tail at cfg1's 4K launch sizes, profiles/r5_ofdm_runs.txt)
-  const int run = NN >= 8192 ? 4 : 2;
+  // units per workgroup: up to 4 for 8K / 16K, 2 below (cfg4 8K: 2.09 -> 1.81 ms with the slot
+  // prefetch; runs of 8 or more leave a grid tail at cfg1's 4K launch sizes, profiles/r5_ofdm_runs.txt),
+  // and one per workgroup for small launches (a one-frame call keeps its latency)
+  const int run = std::max(1, std::min(NN >= 8192 ? 4 : 2, units / 8192));
   hipLaunchKernelGGL((ofdm_kernel<NN, FMT, MULTI>), dim3((units + run - 1) / run), dim3(Sh::NT), lds, s, d, io);
   return hipGetLastError();
 }
