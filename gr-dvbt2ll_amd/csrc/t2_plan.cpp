@@ -1013,23 +1013,27 @@ const uint16_t *reserved_tones(int N, bool tr, int *n) {
 }
 
 // complex IDFT in double (radix-2, unnormalised, e^{+j})
-void idft_double(std::vector<double> &re, std::vector<double> &im) {
-  size_t n = re.size();
-  for (size_t i = 1, j = 0; i < n; i++) {
-    size_t bit = n >> 1;
-    for (; j & bit; bit >>= 1) j ^= bit;
-    j ^= bit;
-    if (i < j) { std::swap(re[i], re[j]); std::swap(im[i], im[j]); }
+// the P1 symbol's 1024-point inverse DFT in double, term by term in the order of the oracle's
+// restatement (oracle/dvbt2_oracle.c cdft_double: angle 2 pi ((j k) mod n) / n, sums over j), so the
+// planner's P1 samples equal the oracle's bit for bit; the cosine / sine of each of the n angles are
+// computed once, as the same double expression
+void p1_idft(const std::vector<double> &x, cf32 *y) {
+  const int n = (int)x.size();
+  std::vector<double> c(n), sn(n);
+  for (int m = 0; m < n; m++) {
+    const double a = 1 * 2.0 * M_PI * (double)m / n;
+    c[m] = std::cos(a);
+    sn[m] = std::sin(a);
   }
-  for (size_t len = 2; len <= n; len <<= 1) {
-    for (size_t i = 0; i < n; i += len)
-      for (size_t k = 0; k < len / 2; k++) {
-        double a = 2.0 * M_PI * (double)k / (double)len, wr = std::cos(a), wi = std::sin(a);
-        double br = re[i + k + len / 2], bi = im[i + k + len / 2];
-        double tr = br * wr - bi * wi, ti = br * wi + bi * wr;
-        re[i + k + len / 2] = re[i + k] - tr; im[i + k + len / 2] = im[i + k] - ti;
-        re[i + k] += tr; im[i + k] += ti;
-      }
+  for (int k = 0; k < n; k++) {
+    double sr = 0, si = 0;
+    for (int j = 0; j < n; j++) {
+      const int m = (int)((long)j * k % n);
+      const double xr = x[j], xi = 0.0;
+      sr += xr * c[m] - xi * sn[m];
+      si += xr * sn[m] + xi * c[m];
+    }
+    y[k] = cf32{(float)sr, (float)si};
   }
 }
 }  // namespace
@@ -1209,14 +1213,14 @@ int build_pilot(const PgParams &p, PilotPlan &pp) {
     float inv = (float)std::sqrt(384.0);
     std::vector<cf32> t0(1024), t1(1024);
     for (int pass = 0; pass < 2; pass++) {
-      std::vector<double> re(1024), im(1024, 0.0);
+      std::vector<double> re(1024);
       for (int i = 0; i < 1024; i++) {
         int src = (i + 512) % 1024;                    // fftshift
         re[i] = pass == 0 ? fr[src] : fr[(src + 1023) % 1024];   // 1-bin shifted copy
       }
-      idft_double(re, im);
       std::vector<cf32> &t = pass == 0 ? t0 : t1;
-      for (int i = 0; i < 1024; i++) t[i] = cf32{(float)re[i] / inv, (float)im[i] / inv};
+      p1_idft(re, t.data());
+      for (int i = 0; i < 1024; i++) t[i] = cf32{t[i].re / inv, t[i].im / inv};
     }
     int k = 0;
     for (int j = 0; j < 542; j++) pp.p1[k++] = t1[j];

@@ -7,6 +7,7 @@ oracle still reproduces them, and the GPU suite checks the HIP blocks against th
 
     python tests/golden/make_golden.py
 """
+import hashlib
 import sys
 from pathlib import Path
 
@@ -18,7 +19,10 @@ sys.path[:0] = [str(HERE.parent), str(HERE.parents[1] / "gr-dvbt2ll_amd")]
 from dvbt2ll.configs import CONFIGS, ts_for_frames  # noqa: E402
 import oracle_lib as O  # noqa: E402
 
-CASES = {"cfg1": (2, True), "cfg1q": (2, True), "cfg4": (1, False)}   # name: (frames, keep carriers)
+# name: (frames, what is kept): "all" every stage; "bits" the TS and bit stages, digests of the float
+# stages; "digest" digests only (the 32K configs: the benched frame shapes)
+CASES = {"cfg1": (2, "all"), "cfg1q": (2, "all"), "cfg4": (1, "bits"), "cfg2": (1, "digest"), "cfg3": (1, "digest"),
+         "cfg5": (1, "digest")}
 
 
 def stages(cfg, nframes):
@@ -45,16 +49,25 @@ def stages(cfg, nframes):
     res["ts_consumed"] = np.int64(off)
     res["p1"] = pg.p1()
     res["normalization"] = np.float64(pg.normalization)
+    # each frame's IQ as the GPU writes it: the oracle's carriers through oracle/ifft_model.c (the OFDM
+    # kernels' operation order) after the oracle's P1
+    res["iq"] = np.stack([O.model_frame(c, pg.guard, pg.normalization, res["p1"]) for c in res["carriers"]])
     return res
 
 
+def digest(a):
+    return np.frombuffer(hashlib.sha256(np.ascontiguousarray(a).tobytes()).digest(), np.uint8)
+
+
 def main():
-    import hashlib
     for name, (nframes, keep) in CASES.items():
         st = stages(CONFIGS[name], nframes)
-        if not keep:   # large: keep only digests of the bit-exact float stages
-            for k in ("cells", "mapped", "carriers"):
-                st[k + "_sha256"] = np.frombuffer(hashlib.sha256(st.pop(k).tobytes()).digest(), np.uint8)
+        st["iq_sha256"] = digest(st.pop("iq"))
+        st["nframes"] = np.int64(nframes)
+        big = ("cells", "mapped", "carriers") + (("ts", "bbbits", "codeword") if keep == "digest" else ())
+        if keep != "all":   # large: keep only digests of these stages
+            for k in big:
+                st[k + "_sha256"] = digest(st.pop(k))
         np.savez_compressed(HERE / ("%s.npz" % name), **st)
         print("wrote", name)
 

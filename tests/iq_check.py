@@ -68,13 +68,25 @@ def check_frame(iq, carriers, N, G, norm, p1, ctx=""):
     return worst
 
 
+_P1 = {}
+
+
+def _oracle_p1(pg_args):
+    """the oracle's P1 samples for these pilotgen arguments (cached: the oracle evaluates its DFT term by term)"""
+    key = tuple(pg_args)
+    if key not in _P1:
+        import oracle_lib as O
+        _P1[key] = O.PG(*pg_args).p1()
+    return _P1[key]
+
+
 def check_frame_exact(iq, carriers, pg_args, G, norm, ctx="", gain=1.0, fmt=0):
     """SURVEY 8(c)'s bit-exact bar between the CPU restatement and the GPU: the frame equals, bit for
     bit, the oracle's carriers put through oracle/ifft_model.c (the OFDM kernels' operation order)
-    with the planner's P1 samples (the GPU copies them).  Returns the number of samples compared."""
+    with the oracle's P1 samples (the planner's, which the GPU copies, are bit-equal to them:
+    test_cpu_plan).  Returns the number of samples compared."""
     import oracle_lib as O
-    import plan_probe as PP
-    want = O.model_frame(carriers, G, norm, PP.pilot_plan(pg_args)["p1"], gain, fmt)
+    want = O.model_frame(carriers, G, norm, _oracle_p1(pg_args), gain, fmt)
     got = np.asarray(iq)
     assert got.shape == want.shape, (ctx, got.shape, want.shape)
     a, b = got.view(np.uint32).reshape(-1), want.view(np.uint32).reshape(-1)

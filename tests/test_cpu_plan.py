@@ -209,7 +209,10 @@ def test_pilot_map_matches_oracle(name, over):
             bins = (bins.view(np.float32).reshape(-1, 2) * plan["isinc"][:, None]).view(np.complex64).reshape(-1)
         np.testing.assert_array_equal(bins.view(np.uint32), want[j].view(np.uint32), err_msg="symbol %d" % j)
     assert abs(plan["norm"] - pg.normalization) == 0
-    assert np.abs(plan["p1"] - pg.p1()).max() < 2e-6
+    # the planner's P1 samples (the GPU copies them) are the oracle's, bit for bit (both evaluate the
+    # 1024-point inverse DFT term by term in double in the same order)
+    np.testing.assert_array_equal(np.asarray(plan["p1"], np.complex64).view(np.uint32),
+                                  np.asarray(pg.p1(), np.complex64).view(np.uint32))
 
 
 @pytest.mark.parametrize("name", ["cfg1", "cfg1q", "cfg2", "cfg3", "cfg4", "cfg5"])
