@@ -21,6 +21,6 @@ step bench && timeout -k 10 900 python -u bench.py $BENCH_ARGS > "$O/bench.json"
   && cat "$O/bench.json" || { rc=$?; tail -20 "$O/bench.err"; exit $rc; }
 [ -n "$NOTRACE" ] && exit 0
 step trace && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace" -o trace -f csv -- \
-     python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --no-blocks --no-mplp --slots 1 --steps 10 --warmup 2 \
+     python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --no-blocks --no-mplp --no-host --slots 1 --steps 10 --warmup 2 \
      > "$O/trace_bench.json" 2> "$O/trace.err" \
   && echo "=== done ($(date +%T))"

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/$1; shift; mkdir -p "$O"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/trace" -o trace -f csv -- \
-  python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --no-blocks --slots 1 --steps 10 --warmup 2 "$@" \
+  python bench.py --no-pmc --no-cpu-baseline --no-latency --no-sc16 --no-blocks --no-host --slots 1 --steps 10 --warmup 2 "$@" \
   > "$O/trace_bench.json" 2> "$O/trace.err" || { tail -20 "$O/trace.err"; exit 1; }
 f=$(find "$O/trace" -name '*kernel_stats.csv' | head -1)
 python - "$f" <<'PY'
