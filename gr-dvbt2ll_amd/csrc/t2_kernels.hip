@@ -57,6 +57,21 @@ __device__ __forceinline__ float2 cscale(float2 a, float sc) {
   return make_float2(r.x, r.y);
 }
 
+// a read-only table entry at a wave-uniform index through the constant address space: a scalar (SMEM)
+// load, counted by lgkmcnt, so its wait never waits for the wave's outstanding vector stores (vmcnt
+// retires loads and stores in order).  Only for tables the host writes before the launch.
+template <class T>
+__device__ __forceinline__ T kc(const T *p, int64_t i) {
+  static_assert(sizeof(T) % 4 == 0, "whole dwords");
+  const __attribute__((address_space(4))) uint32_t *q = (const __attribute__((address_space(4))) uint32_t *)(p + i);
+  uint32_t w[sizeof(T) / 4];
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) w[k] = q[k];
+  T r;
+  __builtin_memcpy(&r, w, sizeof(T));
+  return r;
+}
+
 // uniform (SGPR) base + 32-bit unsigned byte offset: lets the compiler use the global
 // saddr form (one VGPR per address instead of a 64-bit VGPR pair per element)
 template <class T>
@@ -72,6 +87,16 @@ __device__ __forceinline__ void st_off(T *base, uint32_t byte_off, T v) {
 __device__ __forceinline__ void st_nt(float2 *base, uint32_t byte_off, float2 v) {
   float2 *p = (float2 *)((char *)base + byte_off);
   __builtin_nontemporal_store(__builtin_bit_cast(uint64_t, v), (uint64_t *)p);
+}
+
+// workgroup barrier that orders LDS accesses only (the OFDM kernels): the fence of __syncthreads also
+// covers global memory, and in the OFDM kernels (whose units end in IQ stores) it measured slower
+// (session r5s: cfg4 OFDM 1.833 -> 1.775 ms, cfg3 7.655 -> 7.59 ms with this barrier and the scalar
+// table loads, kc).  Never for global memory communicated between threads.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 __device__ __forceinline__ uint32_t rd_lane_u32(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -1595,11 +1620,11 @@ struct StockhamTail<NSUB, NT, PS, NS, R, Rs...> {
   __device__ __forceinline__ static void run(float2 *v, float2 *lds, const float2 *tw, uint32_t tws, int tid) {
     using P = StockhamPass<NSUB, NT, R, NS, PS>;
     P::load_lds(v, lds, tid);
-    __syncthreads();
+    lds_barrier();
     P::compute(v, tw, tws, tid);
     if (sizeof...(Rs) > 0) {
       P::store_lds(v, lds, tid);
-      __syncthreads();
+      lds_barrier();
       StockhamTail<NSUB, NT, PS, NS * R, Rs...>::run(v, lds, tw, tws, tid);
     }
   }
@@ -1675,7 +1700,7 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
     pv0 = pre->av0;
     pv1 = pre->av1;
   }
-  if (!pa) gr = src.agrp[g];
+  if (!pa) gr = kc(src.agrp, g);
   for (uint32_t q = (uint32_t)tid; q < ((uint32_t)gr.y >> 2); q += NT) {
     const uint32_t e0 = (uint32_t)gr.x + 4u * q;
     uint2 b;
@@ -1703,8 +1728,8 @@ __device__ __forceinline__ void scatter_group(float2 *lds, const BinSource &src,
     mid();
     const int P = src.nplp;
     for (int p = 0; p < P; p++) {   // (uniform)
-      const uint32_t a = (uint32_t)src.bnd[g * (P + 1) + p], b = (uint32_t)src.bnd[g * (P + 1) + p + 1];
-      if (b > a) scatter_slots<NT, SQ>(lds, src, a, b - a, dummy, tid, NoWork(), (uint32_t)src.qbase[p]);
+      const uint32_t a = (uint32_t)kc(src.bnd, g * (P + 1) + p), b = (uint32_t)kc(src.bnd, g * (P + 1) + p + 1);
+      if (b > a) scatter_slots<NT, SQ>(lds, src, a, b - a, dummy, tid, NoWork(), (uint32_t)kc(src.qbase, p));
     }
   } else {
     scatter_slots<NT, SQ>(lds, src, r0, rn, dummy, tid, mid, 0u, pre);
@@ -1809,7 +1834,7 @@ __device__ __forceinline__ void slot_prefetch(SlotPre &p, const uint16_t *inv, c
                                               const float2 *aval = nullptr) {
   p.aux = aux;
   if (aux) {
-    p.gr = agrp[0];
+    p.gr = kc(agrp, 0);
     const uint32_t q = (uint32_t)tid;
     if (q < ((uint32_t)p.gr.y >> 2)) {
       const uint32_t e0 = (uint32_t)p.gr.x + 4u * q;
@@ -1840,21 +1865,21 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   constexpr int PS = FftPlan<NSUB, V>::PS;
   if (src.inv) {
     {
-      const int2 zr = src.azr[0];
+      const int2 zr = kc(src.azr, 0);
       for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
     }
     // nobar: the tables are in LDS already (stored once by the kernel), and the zero run, the
     // scatter's bins and its dummy slots are disjoint, so the scatter needs no barrier after the fill
     if (!nobar) {
       stage.store((unsigned char *)lds, true, tid);
-      __syncthreads();
+      lds_barrier();
     }
     const uint32_t dummy = (uint32_t)(NSUB + (NSUB >> PS)) + (uint32_t)(tid & 63);
     scatter_group<NT, OFDM_SQ16, MULTI>(lds, src, 0, src.d0, src.dn, dummy, tid, NoWork(), pre);
-    __syncthreads();
+    lds_barrier();
     after_scatter();
     StockhamPass<NSUB, NT, V, 1, PS>::load_lds(v, lds, tid);
-    __syncthreads();
+    lds_barrier();
   } else {
     stage.store((unsigned char *)lds, false, tid);
 #pragma unroll
@@ -1882,7 +1907,7 @@ __device__ __forceinline__ void sub_ifft(float2 *v, float2 *lds, const BinSource
   __builtin_amdgcn_sched_barrier(0);
   Dft<V>::run(v);
   StockhamPass<NSUB, NT, V, 1, PS>::store_lds(v, lds, tid);
-  __syncthreads();
+  lds_barrier();
   FftPlan<NSUB, V>::Tail::run(v, lds, tw, 1u, tid);
 }
 
@@ -2005,8 +2030,8 @@ __device__ __forceinline__ UnitSlots unit_slots(const OfdmDev &d, const OfdmIO &
   const int j = u / io.nframes, f = u - j * io.nframes;
   const int64_t frame = io.first_frame + (io.frames_per_stream ? f % io.frames_per_stream : f);
   const int c = d.ncls > 1 ? (int)(frame % d.ncls) : 0, jc = c * d.Nsym + j;
-  return UnitSlots{d.inv + d.cls_inv[c], io.cell_off + (uint32_t)f * io.cell_stride, (uint32_t)d.sym_d0[jc],
-                   (uint32_t)d.sym_n[jc], d.agrp + 2 * jc};
+  return UnitSlots{d.inv + kc(d.cls_inv, c), io.cell_off + (uint32_t)f * io.cell_stride, (uint32_t)kc(d.sym_d0, jc),
+                   (uint32_t)kc(d.sym_n, jc), d.agrp + 2 * jc};
 }
 
 // pf (one-PLP chain frames): in, this unit's first scatter round (loaded by the previous unit or
@@ -2031,12 +2056,12 @@ __device__ __forceinline__ void ofdm_unit(const OfdmDev &d, const OfdmIO &io, in
   if (d.inv) {
     // the frame's class (FRAME_INTERVAL > 1): its rows of the per-symbol tables, its slots' bins
     const int c = d.ncls > 1 ? (int)(frame % d.ncls) : 0, jc = c * d.Nsym + j;
-    src.inv = d.inv + d.cls_inv[c];
+    src.inv = d.inv + kc(d.cls_inv, c);
     src.data = io.l1;                              // indirect entries: this frame's L1-post cells
     src.abase = (uint32_t)f * io.l1_stride - 1u;
-    src.d0 = (uint32_t)d.sym_d0[jc];
-    src.dn = (uint32_t)d.sym_n[jc];
-    src.dn0 = (uint32_t)d.sym_n0[jc];
+    src.d0 = (uint32_t)kc(d.sym_d0, jc);
+    src.dn = (uint32_t)kc(d.sym_n, jc);
+    src.dn0 = (uint32_t)kc(d.sym_n0, jc);
     src.agrp = d.agrp + 2 * jc;
     src.azr = d.azr + 2 * jc;
     src.nplp = d.nplp;
@@ -2134,14 +2159,14 @@ __global__ __launch_bounds__(OfdmShape<N>::NT, 4) void ofdm_kernel(OfdmDev d, Of
     slot_prefetch<OfdmShape<N>::NT>(pf, ns.inv, io.pairs, ns.cbase, ns.r0, ns.rn, tid, OfdmShape<N>::AUX_PRE,
                                     ns.agrp, d.abin, d.aval);
     tabs.store(smem, true, tid);
-    __syncthreads();
+    lds_barrier();
   }
 #pragma nounroll
   for (int u = u0; u < u1; u++) {
     // the previous unit's last reads of the transform buffer came before its final barrier; in the
     // chain's scatter mode the next unit writes nothing else (the tables stay), elsewhere the table
     // store rewrites them, so wait for every wave there
-    if (u > u0 && !pre) __syncthreads();
+    if (u > u0 && !pre) lds_barrier();
     // opaque per unit: otherwise every per-thread address of the unit's passes is hoisted out of the
     // loop and held in registers across it
     int t = tid;
@@ -2213,7 +2238,7 @@ template <int SPLIT>
 __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t tid, uint32_t a, uint32_t b) {
 #pragma unroll
   for (uint32_t h = 0; h < 2; h++) {
-    __syncthreads();
+    lds_barrier();
     const bool mine = ((tid >> SPLIT) & 1u) == h;
     if (mine) {
 #pragma unroll
@@ -2223,7 +2248,7 @@ __device__ __forceinline__ void o32_exchange(float2 *v, float2 *lds, uint32_t ti
         lds[o32_x(e)] = v[r];
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (mine) {
       if (SPLIT == 8) {
         // values r, r + 1 are adjacent, 16-byte aligned slots: one ds_read_b128 per pair (lanes
@@ -2387,8 +2412,8 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     const float2 tq = tid < d.nq ? d.qam[tid] : make_float2(0.f, 0.f);   // nq <= OFDM_MAX_QAM = O32_NT
     // the frame's class (FRAME_INTERVAL > 1): its rows of the per-symbol tables, its slots' bins
     const int c = d.ncls > 1 ? (int)(frame % d.ncls) : 0, jc = c * d.Nsym + j;
-    BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv + d.cls_inv[c], io.pairs, qre, qim,
-                  (uint32_t)d.sym_d0[jc], (uint32_t)d.sym_n[jc], (uint32_t)d.sym_n0[jc], d.abin, d.aval, d.aind,
+    BinSource src{map, io.l1, cbase, (uint32_t)f * io.l1_stride - 1u, d.inv + kc(d.cls_inv, c), io.pairs, qre, qim,
+                  (uint32_t)kc(d.sym_d0, jc), (uint32_t)kc(d.sym_n, jc), (uint32_t)kc(d.sym_n0, jc), d.abin, d.aval, d.aind,
                   d.agrp + 2 * jc, d.azr + 2 * jc, d.nplp,
                   d.plp_bnd ? d.plp_bnd + 2 * jc * (d.nplp + 1) : nullptr, d.plp_qbase};
     const uint32_t dummy = (uint32_t)(O32_H + (O32_H >> O32_PS)) + (uint32_t)(tid & 63);
@@ -2396,7 +2421,7 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
     // first half is written, in one batch or half 1 behind half 0's arrival: +11 % kernel time)
     float2 ev[16], od[16];                        // stage-A inputs m2 = 2 r, 2 r + 1
     {
-      const int2 zr = src.azr[0];
+      const int2 zr = kc(src.azr, 0);
       for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
       if (tid < d.nq) {
         qre[tid] = tq.x;
@@ -2404,15 +2429,15 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
       }
       tw1k[tid] = t1k;
       if (tid < 384) tw2[tid] = t2;
-      __syncthreads();                            // constellation visible to the scatter
+      lds_barrier();                            // constellation visible to the scatter
       scatter_group<NT, 4, MULTI>(lds, src, 0, src.d0, src.dn0, dummy, tid);
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (uint32_t r = 0; r < 16; r++) ev[r] = lds[o32_bin(kin + 1024u * r)];
     }
-    __syncthreads();                              // half 0 read back before half 1 overwrites it
+    lds_barrier();                              // half 0 read back before half 1 overwrites it
     {
-      const int2 zr = src.azr[1];
+      const int2 zr = kc(src.azr, 1);
       for (int i = zr.x + tid; i < zr.y; i += NT) lds[i] = make_float2(0.f, 0.f);
       auto dft_even = [&]() {
         eq(ev, 16, 2u, 0u);
@@ -2420,7 +2445,7 @@ __global__ __launch_bounds__(O32_NT) void ofdm32_kernel(OfdmDev d, OfdmIO io) {
         Dft<16>::run(ev);
       };
       scatter_group<NT, 4, MULTI>(lds, src, 1, src.d0 + src.dn0, src.dn - src.dn0, dummy, tid, dft_even);
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (uint32_t r = 0; r < 16; r++) od[r] = lds[o32_bin(kin + 1024u * r)];
     }
