@@ -1055,7 +1055,7 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const int b = 4 * qd + i;
-          const int2 cw = d.col[b];   // scalar loads at the point of use
+          const int2 cw = kc(d.col, b);   // scalar (SMEM) loads at the point of use
           const int c0 = cw.x;
           win[i] = 0u;
           if (c0 < 0) continue;
