@@ -1099,7 +1099,7 @@ __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t fr
   const uint2 *qs = d.slot_quad + (int64_t)r * d.slot_stride;
   const uint16_t *qo = d.slot_qoff + (int64_t)r * d.slot_stride;
   const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
-  const int nqd = d.slot_nq[r];
+  const int nqd = kc(d.slot_nq, r);
   constexpr int MQ = 9, NW = NT / 64;
   const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
   // (idx[j], idx[j - 1] under rotation, else idx[j]) without branches, so a quad's eight byte reads
@@ -1118,7 +1118,7 @@ __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t fr
     for (int u = 0; u < MQ; u++) {
       const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
       e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
-      qa[u] = (uint32_t)qb[c] + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
+      qa[u] = (uint32_t)kc(qb, c) + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
     }
 #pragma unroll
     for (int u = 0; u < MQ; u++) {
