@@ -1254,16 +1254,24 @@ static const uint16_t *papr_map(int fft, int tr, int *n) {
 }
 
 static void cdft_double(const cf *x, cf *y, int n, int sign) {
+  /* the n angles' cosines / sines once (each the same double expression as a term-by-term evaluation) */
+  double *ct = (double *)malloc(sizeof(double) * 2 * (size_t)n), *st = ct + n;
+  for (int m = 0; m < n; m++) {
+    double a = sign * 2.0 * M_PI * (double)m / n;
+    ct[m] = cos(a);
+    st[m] = sin(a);
+  }
   for (int k = 0; k < n; k++) {
     double sr = 0, si = 0;
     for (int j = 0; j < n; j++) {
-      double a = sign * 2.0 * M_PI * (double)((long)j * k % n) / n;
-      double c = cos(a), s = sin(a);
+      const int m = (int)((long)j * k % n);
+      double c = ct[m], s = st[m];
       sr += x[j].re * c - x[j].im * s;
       si += x[j].re * s + x[j].im * c;
     }
     y[k].re = (float)sr; y[k].im = (float)si;
   }
+  free(ct);
 }
 
 orc_pg *orc_pg_create(int carriermode, int fftsize, int pilotpattern, int guardinterval,
