@@ -977,11 +977,12 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
     // interleaving frames m' < fp.unit / cycle and their FEC blocks r
     const int nif = fp.unit / pp.cycle(), Fu = pp.F * nif;
     md.F = Fu;
+    if (pp.cs > 0x7FFF) return DVBT2LL_EINVAL;   // 15-bit cell indices in the quad table (<= 32400)
     // the LDPC + map kernel's cell interleaver + TI store in stored-slot order (layout.part: frame data slot
     // of each frame data index; a TIME_IL_TYPE 1 PLP's block r writes the P_I T2 frames of its interleaving
     // frame, frame i's slots at i * pair_stride), in aligned quads of four slots: block r's quads sorted by
     // slot, each with the cell-interleaver input index of the cell landing in each of its four slots (j with
-    // (ci_perm[j] + ci_shift[r]) mod cs = t, framemapper:1973-1998; 0xFFFF: a slot of another block, at a
+    // (ci_perm[j] + ci_shift[r]) mod cs = t, framemapper:1973-1998; 0x8000: a slot of another block, at a
     // run's edge), its offset from its 64-quad chunk's first quad, each chunk's first quad and the block's
     // quad count.  A full quad is one 8-byte store, so a store instruction writes 512 B of one or two
     // contiguous runs (the block's cells in a symbol (half) are one run, bank-balanced inside, t2_plan
@@ -1016,7 +1017,7 @@ static int chain_build(dvbt2ll_chain *h, const FmParams &fm, const std::vector<P
       qmax = std::max(qmax, n + 1);
     }
     const int qst = (qmax + 63) & ~63, nchk = qst / 64;
-    std::vector<uint32_t> qsrc((size_t)Fu * qst * 2 + 2, 0xFFFFFFFFu);
+    std::vector<uint32_t> qsrc((size_t)Fu * qst * 2 + 2, 0x80008000u);
     std::vector<uint16_t> qoff((size_t)Fu * qst + 4, 0);
     std::vector<int32_t> qb((size_t)Fu * nchk + 1, 0), qn(Fu, 0);
     for (int rr = 0; rr < Fu; rr++) {

@@ -92,7 +92,7 @@ struct MapDev {
   int F;                   // chain: FEC blocks per frame (launch block b is FEC block b mod F of frame b / F)
   // chain: block r's cell interleaver + time-interleaver store in aligned quads of four frame slots,
   // sorted by slot (map_store_quads): quad n at r * slot_stride + n holds the cell-interleaver input
-  // index of each of its slots (0xFFFF: another block's slot) and its quad index minus
+  // index j < 0x8000 of each of its slots (0x8000: another block's slot) and its quad index minus
   // slot_qbase[r * slot_stride / 64 + n / 64]; slot_nq[r] quads
   const uint2 *slot_quad;
   const uint16_t *slot_qoff;

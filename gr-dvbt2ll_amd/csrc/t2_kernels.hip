@@ -1080,37 +1080,37 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
   }
 }
 
-// chain: cell interleaver (framemapper:1973-1998) of block blk's (index, previous index) pairs through
-// LDS (stage, 2 cs bytes), then the time-interleaver (framemapper:1999-2028) store into the frame
-// data region out_pairs + (blk / F) frame_stride
-// Chain: the cell interleaver and the time-interleaver store in one pass, in stored-slot order, in
-// aligned quads of four frame slots (MapDev::slot_quad): wave w takes 64-quad chunks c = c0 + u NT / 64
-// + w and lane l quad 64 c + l, whose four slots list the cell-interleaver INPUT index j of the cell
-// landing there (the chain composes j = CI^-1(t) for the block's shift); the slot gets (idx[j],
-// idx[j - 1]) (the rotated constellation's Q delay; the QAM lookup is fused into the OFDM kernel's bin
-// scatter).  One 8-byte store per full quad (2-byte stores for a quad at a run's edge, whose other
-// slots belong to neighbouring blocks), so a store instruction writes 512 B of one or two contiguous
-// runs; no stage array and no cell-interleaver pass through LDS
-template <int NT>
+// Chain: the cell interleaver (framemapper:1973-1998) and the time-interleaver store (:1999-2028) in one
+// pass, in stored-slot order, in aligned quads of four frame slots (MapDev::slot_quad): wave w takes
+// 64-quad chunks c = c0 + u NT / 64 + w and lane l quad 64 c + l, whose four slots list the
+// cell-interleaver INPUT index j of the cell landing there (the chain composes j = CI^-1(t) for the
+// block's shift); the slot gets (idx[j], idx[j - 1]) under rotation (the rotated constellation's Q
+// delay; the QAM lookup is fused into the OFDM kernel's bin scatter), else (idx[j], idx[j]).  One
+// 8-byte store per full quad (2-byte stores for a quad at a run's edge, whose other slots belong to
+// neighbouring blocks), so a store instruction writes 512 B of one or two contiguous runs.
+// idx[-1] holds a copy of idx[cs - 1] under rotation (the caller's), so idx[j - 1] needs no wrap: both
+// bytes are one address and two offsets, and a slot of another block is a flag bit of its entry rather
+// than a sentinel index (three VALU per slot instead of ~11).
+template <int NT, bool ROT>
 __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
                                 int blk, int tid) {
-  const int cs = d.cs, r = blk % d.F;
+  const int r = blk % d.F;
   uint16_t *dst = out_pairs + (int64_t)(blk / d.F) * frame_stride;   // frame data region
   const uint2 *qs = d.slot_quad + (int64_t)r * d.slot_stride;
   const uint16_t *qo = d.slot_qoff + (int64_t)r * d.slot_stride;
   const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
   const int nqd = kc(d.slot_nq, r);
-  constexpr int MQ = 9, NW = NT / 64;
+  constexpr int NW = NT / 64;
   const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
-  // (idx[j], idx[j - 1] under rotation, else idx[j]) without branches, so a quad's eight byte reads
-  // go out together (a branch per read had put an LDS wait after each); j = 0xFFFF (another block's
-  // slot) reads idx[0], and the caller drops it
-  const uint32_t rmask = d.rotation ? 0xFFFFFFFFu : 0u;
+  const uint8_t *ib = idx - 1;   // ib[j + 1] = idx[j], ib[j] = idx[j - 1]
+  // entry bits 0..14: j; bit 15: another block's slot (j = 0 then, read and dropped)
   auto pair_of = [&](uint32_t j) -> uint32_t {
-    j = j == 0xFFFFu ? 0u : j;
-    const uint32_t jm = j == 0 ? (uint32_t)cs - 1u : j - 1u, jh = (jm & rmask) | (j & ~rmask);
-    return (uint32_t)idx[j] | ((uint32_t)idx[jh] << 8);
+    const uint8_t *p = ib + j;
+    return ROT ? (uint32_t)p[1] | ((uint32_t)p[0] << 8) : (uint32_t)p[1] * 0x101u;
   };
+  // rounds of MQ chunks per wave (chunk c0 + u NW + wv): one round for a normal block (<= 36 chunks; the
+  // wave-uniform clamp repeats a chunk without storing it), its table loads all in flight together
+  constexpr int MQ = 9;
   for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
     uint2 e[MQ];
     uint32_t qa[MQ];
@@ -1123,16 +1123,17 @@ __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t fr
 #pragma unroll
     for (int u = 0; u < MQ; u++) {
       const int c = c0 + u * NW + wv;
-      const uint32_t j0 = e[u].x & 0xFFFFu, j1 = e[u].x >> 16, j2 = e[u].y & 0xFFFFu, j3 = e[u].y >> 16;
-      const uint32_t p0 = pair_of(j0), p1 = pair_of(j1), p2 = pair_of(j2), p3 = pair_of(j3);
+      const uint32_t j0 = e[u].x & 0x7FFFu, j1 = (e[u].x >> 16) & 0x7FFFu, j2 = e[u].y & 0x7FFFu,
+                     j3 = (e[u].y >> 16) & 0x7FFFu;
+      const uint2 v = make_uint2(pair_of(j0) | (pair_of(j1) << 16), pair_of(j2) | (pair_of(j3) << 16));
       if (c < nch && 64 * c + lane < nqd) {
-        if (j0 != 0xFFFFu && j1 != 0xFFFFu && j2 != 0xFFFFu && j3 != 0xFFFFu) {
-          st_off((uint2 *)dst, qa[u] * 8u, make_uint2(p0 | (p1 << 16), p2 | (p3 << 16)));
+        if (!((e[u].x | e[u].y) & 0x80008000u)) {
+          st_off((uint2 *)dst, qa[u] * 8u, v);
         } else {
-          if (j0 != 0xFFFFu) st_off(dst, (4u * qa[u] + 0u) * 2u, (uint16_t)p0);
-          if (j1 != 0xFFFFu) st_off(dst, (4u * qa[u] + 1u) * 2u, (uint16_t)p1);
-          if (j2 != 0xFFFFu) st_off(dst, (4u * qa[u] + 2u) * 2u, (uint16_t)p2);
-          if (j3 != 0xFFFFu) st_off(dst, (4u * qa[u] + 3u) * 2u, (uint16_t)p3);
+          if (!(e[u].x & 0x8000u)) st_off(dst, (4u * qa[u] + 0u) * 2u, (uint16_t)v.x);
+          if (!(e[u].x & 0x80000000u)) st_off(dst, (4u * qa[u] + 1u) * 2u, (uint16_t)(v.x >> 16));
+          if (!(e[u].y & 0x8000u)) st_off(dst, (4u * qa[u] + 2u) * 2u, (uint16_t)v.y);
+          if (!(e[u].y & 0x80000000u)) st_off(dst, (4u * qa[u] + 3u) * 2u, (uint16_t)(v.y >> 16));
         }
       }
     }
@@ -1426,7 +1427,13 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void ldpc_map_kern
   __syncthreads();
   map_cells<FEC_THREADS>(md, cww, idx, tid);
   __syncthreads();
-  map_store_quads<FEC_THREADS>(md, mio.out_pairs, mio.frame_stride, idx, blk, tid);
+  if (md.rotation) {   // idx[-1] (the codeword's dead slack word) = idx[cs - 1] for map_store_quads
+    if (tid == 0) idx[-1] = idx[md.cs - 1];
+    __syncthreads();
+    map_store_quads<FEC_THREADS, true>(md, mio.out_pairs, mio.frame_stride, idx, blk, tid);
+  } else {
+    map_store_quads<FEC_THREADS, false>(md, mio.out_pairs, mio.frame_stride, idx, blk, tid);
+  }
 }
 
 hipError_t launch_ldpc_map(const FecDev &fd, const FecIO &fio, const MapDev &md, const MapIO &mio, hipStream_t s,
