@@ -411,6 +411,12 @@ struct BbGeom {
   int64_t J0, pos0, w0;
   int npay, padding, count0, delta, nq;
 };
+// x mod 188 for x >= 0 from 32-bit remainders (2^32 = 136 mod 188): a 64-bit remainder by a constant is
+// a long 64-bit multiply chain on the scalar unit, and the BB pass evaluates the geometry per block
+__device__ __forceinline__ int mod188(int64_t x) {
+  const uint32_t hi = (uint32_t)((uint64_t)x >> 32), lo = (uint32_t)x;
+  return (int)(((hi % 188u) * 136u + lo % 188u) % 188u);
+}
 __device__ __forceinline__ BbGeom bb_geom(const FecDev &d, const FecIO &io, int64_t B) {
   BbGeom g;
   const int pay_full = (d.kbch - 80) >> 3;
@@ -424,8 +430,8 @@ __device__ __forceinline__ BbGeom bb_geom(const FecDev &d, const FecIO &io, int6
   g.J0 = B * pay_full - 13 * npad_before;
   g.pos0 = payload_pos(g.J0, d.hem);
   // TS packet position of the next input byte at block start
-  if (d.hem) g.count0 = g.J0 == 0 ? 0 : (int)((payload_pos(g.J0 - 1, 1) + 1) % 188);
-  else g.count0 = (int)(g.pos0 % 188);
+  if (d.hem) g.count0 = g.J0 == 0 ? 0 : mod188(payload_pos(g.J0 - 1, 1) + 1);
+  else g.count0 = mod188(g.pos0);
   const int64_t rel = g.pos0 - 188 - io.ts_base;        // >= -188
   g.w0 = (rel >= 0 ? rel : rel - 15) / 16;              // floor
   g.delta = (int)(rel - 16 * g.w0);
@@ -444,9 +450,12 @@ __device__ __forceinline__ uint4 bb_raw_unit(const FecIO &io, const uint8_t *tin
 }
 constexpr int FEC_PRE = 2;   // raw units per thread a BB pass workgroup prefetches for its next block (nq <= 512)
 
-template <bool CRC_RESIDENT, bool PRE>
+// GOUT (the chain's BB pass): the BBFRAME words go straight to the block's codeword row outw, not through
+// the LDS frame and a copy (fec 1.553 -> 1.539 ms per 1280 cfg3 frames)
+template <bool CRC_RESIDENT, bool PRE, bool GOUT = false>
 __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv, unsigned char *smem, int64_t B,
-                            const uint8_t *tin, int tid, const uint4 *pre = nullptr) {
+                            const uint8_t *tin, int tid, const uint4 *pre = nullptr, const BbGeom *gp = nullptr,
+                            uint32_t *outw = nullptr) {
   const int lane = tid & 63, wave = tid >> 6;
   const int L = d.kbch >> 3;
   uint8_t *frame = smem + cv.frame, *phase = smem + cv.phase;
@@ -454,7 +463,7 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
   const uint8_t *crcsl = smem + cv.crcsl;   // BB pass (CRC_RESIDENT): T^2 | T^3 | T^4
   const uint8_t *hcrc8 = smem + cv.hcrc;
   uint8_t *syncv = smem + cv.sync;
-  const BbGeom g = bb_geom(d, io, B);
+  const BbGeom g = gp ? *gp : bb_geom(d, io, B);
   const int npay = g.npay, padding = g.padding, count0 = g.count0;
   const int64_t J0 = g.J0, pos0 = g.pos0;
   // NM: stage the raw stream bytes once (PRE: the units this thread prefetched, unit tid + 256 k in
@@ -572,7 +581,7 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
   };
   // BBFRAME words = header | payload (each sync slot carries the CRC-8 of the previous packet,
   // bbheader:701-719) | in-band field, BB-scrambled (:694-696, :724-726)
-  uint32_t *framew = (uint32_t *)frame;
+  uint32_t *framew = GOUT ? outw : (uint32_t *)frame;
   // (the BB pass keeps the PRBS in LDS: a global load per word here was waited for with vmcnt(0),
   // which also waited for the next block's prefetched TS units)
   const uint32_t *prbsw = CRC_RESIDENT ? (const uint32_t *)(smem + cv.prbs) : (const uint32_t *)d.prbs;
@@ -707,29 +716,34 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel
     }
   }
   __syncthreads();
-  const uint4 *framq = (const uint4 *)(smem + cv.frame);
-  // NM: each block's raw TS units are requested one block ahead (in flight during the previous block)
+  // NM: each block's raw TS units are requested one block ahead (in flight during the previous block),
+  // with its geometry, which the block then reuses (the per-block geometry is scalar 64-bit arithmetic)
   uint4 pre[FEC_PRE];
+  BbGeom gpre{};
+  const uint8_t *tpre = io.in;
+  int64_t bpre = 0;
   auto prefetch = [&](int b) {
-    const uint8_t *tn;
-    const BbGeom gn = bb_geom(d, io, fec_block_of(io, b, tn));
+    bpre = fec_block_of(io, b, tpre);
+    gpre = bb_geom(d, io, bpre);
 #pragma unroll
     for (int k = 0; k < FEC_PRE; k++)
-      pre[k] = tid + FEC_THREADS * k < gn.nq ? bb_raw_unit(io, tn, gn.w0, tid + FEC_THREADS * k) : make_uint4(0u, 0u, 0u, 0u);
+      pre[k] = tid + FEC_THREADS * k < gpre.nq ? bb_raw_unit(io, tpre, gpre.w0, tid + FEC_THREADS * k) : make_uint4(0u, 0u, 0u, 0u);
   };
   if (!d.hem && (int)blockIdx.x < io.nblocks) prefetch(blockIdx.x);
   for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
-    const uint8_t *tin;
-    const int64_t B = fec_block_of(io, bi, tin);
+    const uint8_t *tin = tpre;
+    int64_t B = bpre;
+    BbGeom g = gpre;
+    if (d.hem) {
+      B = fec_block_of(io, bi, tin);
+      g = bb_geom(d, io, B);
+    }
     uint4 cur[FEC_PRE];
 #pragma unroll
     for (int k = 0; k < FEC_PRE; k++) cur[k] = pre[k];
     if (!d.hem && bi + (int)gridDim.x < io.nblocks) prefetch(bi + gridDim.x);
-    fec_bbframe<true, true>(d, io, cv, smem, B, tin, tid, cur);
-    uint4 *dst = (uint4 *)(io.out + (int64_t)bi * io.cw_stride);
-    for (int i = tid; i < (L + 15) >> 4; i += FEC_THREADS) dst[i] = framq[i];
+    fec_bbframe<true, true, true>(d, io, cv, smem, B, tin, tid, cur, &g, (uint32_t *)(io.out + (int64_t)bi * io.cw_stride));
     if (tid < BCH_PART_WORDS) io.bch_part[(int64_t)bi * BCH_PART_WORDS + tid] = 0u;   // the BCH pass XORs into it
-    __syncthreads();   // the frame is rebuilt by the next block
   }
 }
 
