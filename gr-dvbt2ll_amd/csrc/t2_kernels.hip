@@ -1134,6 +1134,10 @@ __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t fr
       e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
       qa[u] = (uint32_t)kc(qb, c) + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
     }
+    // every table load lands here, before the first store: a load the compiler sinks into a store
+    // branch is waited for with vmcnt(0), which also drains every store issued before it
+#pragma unroll
+    for (int u = 0; u < MQ; u++) asm volatile("" : "+v"(e[u].x), "+v"(e[u].y), "+v"(qa[u]));
 #pragma unroll
     for (int u = 0; u < MQ; u++) {
       const int c = c0 + u * NW + wv;
