@@ -163,11 +163,11 @@ __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int 
   c.w = o; o += ldpc ? 48 : 0;             // 12 column-parity words
   c.rowp = o; o += ldpc ? 192 : 0;         // q + 1 <= 91 LDPC row pointers
   c.frame = (o + 15) & ~15;
-  c.phase = c.frame + ((nbch / 8 + 15) & ~15);
+  c.phase = c.frame + (kind == CARVE_BB ? 0 : ((nbch / 8 + 15) & ~15));   // the BB pass stores its frame to HBM
   c.crc8 = c.phase + ((188 + (kbch - 80) / 8 + 32 + 15) & ~15);   // + slack: 16-byte staging start
   c.crcsh = c.crc8 + 256;
-  c.crcsl = c.crcsh + 2048;                // BB pass: T^2, T^3, T^4 of the CRC-8 byte table (slicing by 4)
-  c.prbs = c.crcsl + (kind == CARVE_BB ? 768 : 0);   // BB pass: the BB-scrambler PRBS words
+  c.crcsl = c.crcsh + 2048;                // BB pass: T^1 .. T^24 of the CRC-8 byte table T
+  c.prbs = c.crcsl + (kind == CARVE_BB ? 24 * 256 : 0);   // BB pass: the BB-scrambler PRBS words
   const int bb_end = c.prbs + (kind == CARVE_BB ? ((kbch / 8 + 15) & ~15) : 0), ldpc_end = c.phase + 4 * ((kind == CARVE_LDPC ? FEC_DW_PASS : FEC_DW) * (nbch / 360) + 12 * q);
   c.total = kind == CARVE_BB ? bb_end : kind == CARVE_LDPC ? ldpc_end : (bb_end > ldpc_end ? bb_end : ldpc_end);
   return c;
@@ -460,7 +460,7 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
   const int L = d.kbch >> 3;
   uint8_t *frame = smem + cv.frame, *phase = smem + cv.phase;
   uint8_t *crc8 = smem + cv.crc8, *crcsh = smem + cv.crcsh;
-  const uint8_t *crcsl = smem + cv.crcsl;   // BB pass (CRC_RESIDENT): T^2 | T^3 | T^4
+  const uint8_t *crcsl = smem + cv.crcsl;   // BB pass (CRC_RESIDENT): T^1 | T^2 | .. | T^24
   const uint8_t *hcrc8 = smem + cv.hcrc;
   uint8_t *syncv = smem + cv.sync;
   const BbGeom g = gp ? *gp : bb_geom(d, io, B);
@@ -500,18 +500,14 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
         const int n = k == 7 ? 19 : 24;            // 187 = 7 x 24 + 19
         uint32_t c = 0;
         if (CRC_RESIDENT) {
-          // slicing by 4 (the BB pass keeps T^2, T^3, T^4 in LDS; T is linear):
-          // c <- T^4[c ^ b0] ^ T^3[b1] ^ T^2[b2] ^ T[b3], six dependent lookups per 24 bytes instead of
-          // 24; the 19-byte last chunk is front-padded with zero bytes, which leave c = 0
+          // T is linear, so the register after bytes b_0 .. b_23 from c = 0 is the XOR of T^(24 - i)[b_i]:
+          // 24 independent lookups (the BB pass keeps T^1 .. T^24 in LDS) instead of a chain of dependent
+          // ones (slicing by 4 had six LDS round trips in a row: the CRC phase was ~0.18 ms of the pass);
+          // the 19-byte last chunk is front-padded with zero bytes, T^k[0] = 0
           const int pad = 24 - n;
           const uint8_t *b0 = raw + (p - 187 + 24 * k - rs) - pad;
-          uint32_t by[24];
 #pragma unroll
-          for (int i = 0; i < 24; i++) by[i] = i >= pad ? (uint32_t)b0[i] : 0u;
-#pragma unroll
-          for (int g = 0; g < 6; g++)
-            c = (uint32_t)crcsl[512 + (c ^ by[4 * g])] ^ (uint32_t)crcsl[256 + by[4 * g + 1]] ^
-                (uint32_t)crcsl[by[4 * g + 2]] ^ (uint32_t)crc8[by[4 * g + 3]];
+          for (int i = 0; i < 24; i++) c ^= (uint32_t)crcsl[(23 - i) * 256 + (i >= pad ? (uint32_t)b0[i] : 0u)];
         } else {
           const uint8_t *b0 = raw + (p - 187 + 24 * k - rs);
           uint8_t by[24];
@@ -705,14 +701,15 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel
   for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)(smem + cv.crcsh))[i] = ((const uint32_t *)d.crc8_shift)[i];
   __syncthreads();
   for (int i = tid; i < (L + 3) >> 2; i += FEC_THREADS) ((uint32_t *)(smem + cv.prbs))[i] = ((const uint32_t *)d.prbs)[i];
-  {   // slicing-by-4 tables T^2, T^3, T^4 of the CRC-8 byte table T
+  {   // the powers T^1 .. T^24 of the CRC-8 byte table T (T^(k+1)[x] = T[T^k[x]])
     const uint8_t *t1 = smem + cv.crc8;
     uint8_t *sl = smem + cv.crcsl;
     if (tid < 256) {
-      const uint8_t a2 = t1[t1[tid]], a3 = t1[a2], a4 = t1[a3];
-      sl[tid] = a2;
-      sl[256 + tid] = a3;
-      sl[512 + tid] = a4;
+      uint32_t v = (uint32_t)tid;
+      for (int k = 0; k < 24; k++) {
+        v = t1[v];
+        sl[k * 256 + tid] = (uint8_t)v;
+      }
     }
   }
   __syncthreads();
