@@ -162,12 +162,14 @@ __host__ __device__ inline FecCarve fec_carve(int kind, int kbch, int nbch, int 
   c.sync = o; o += bb ? 48 : 0;            // <= 36 sync-slot CRC-8s
   c.w = o; o += ldpc ? 48 : 0;             // 12 column-parity words
   c.rowp = o; o += ldpc ? 192 : 0;         // q + 1 <= 91 LDPC row pointers
+  // BB pass: T^1 .. T^24 of the CRC-8 byte table T at a compile-time offset (the lookups' addresses are
+  // the byte itself plus an immediate), before the code-dependent areas
+  c.crcsl = o; o += kind == CARVE_BB ? 24 * 256 : 0;
   c.frame = (o + 15) & ~15;
   c.phase = c.frame + (kind == CARVE_BB ? 0 : ((nbch / 8 + 15) & ~15));   // the BB pass stores its frame to HBM
   c.crc8 = c.phase + ((188 + (kbch - 80) / 8 + 32 + 15) & ~15);   // + slack: 16-byte staging start
   c.crcsh = c.crc8 + 256;
-  c.crcsl = c.crcsh + 2048;                // BB pass: T^1 .. T^24 of the CRC-8 byte table T
-  c.prbs = c.crcsl + (kind == CARVE_BB ? 24 * 256 : 0);   // BB pass: the BB-scrambler PRBS words
+  c.prbs = c.crcsh + 2048;                 // BB pass: the BB-scrambler PRBS words
   const int bb_end = c.prbs + (kind == CARVE_BB ? ((kbch / 8 + 15) & ~15) : 0), ldpc_end = c.phase + 4 * ((kind == CARVE_LDPC ? FEC_DW_PASS : FEC_DW) * (nbch / 360) + 12 * q);
   c.total = kind == CARVE_BB ? bb_end : kind == CARVE_LDPC ? ldpc_end : (bb_end > ldpc_end ? bb_end : ldpc_end);
   return c;
@@ -504,10 +506,32 @@ __device__ void fec_bbframe(const FecDev &d, const FecIO &io, const FecCarve &cv
           // 24 independent lookups (the BB pass keeps T^1 .. T^24 in LDS) instead of a chain of dependent
           // ones (slicing by 4 had six LDS round trips in a row: the CRC phase was ~0.18 ms of the pass);
           // the 19-byte last chunk is front-padded with zero bytes, T^k[0] = 0
+          // the chunk's bytes as six aligned dwords (seven dword reads and a byte align each) instead of
+          // 24 byte reads
           const int pad = 24 - n;
-          const uint8_t *b0 = raw + (p - 187 + 24 * k - rs) - pad;
+          const uint8_t *bp = raw + (p - 187 + 24 * k - rs) - pad;
+          const uint32_t sh = (uint32_t)((uintptr_t)bp & 3u);
+          const uint32_t *bw = (const uint32_t *)(bp - sh);
+          uint32_t w7[7], t[24];
 #pragma unroll
-          for (int i = 0; i < 24; i++) c ^= (uint32_t)crcsl[(23 - i) * 256 + (i >= pad ? (uint32_t)b0[i] : 0u)];
+          for (int j = 0; j < 7; j++) w7[j] = bw[j];
+#pragma unroll
+          for (int j = 0; j < 6; j++) {
+            const uint32_t a = __builtin_amdgcn_alignbyte(w7[j + 1], w7[j], sh);
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              const int i = 4 * j + e;
+              uint32_t by = (a >> (8 * e)) & 0xFFu;
+              if (i < 5) by = i >= pad ? by : 0u;   // pad is 0 or 5
+              t[i] = crcsl[(23 - i) * 256 + by];
+            }
+          }
+          // all 24 lookups in flight, then an XOR tree (a running XOR had the compiler wait per pair)
+#pragma unroll
+          for (int h = 12; h >= 3; h >>= 1)
+#pragma unroll
+            for (int i = 0; i < h; i++) t[i] ^= t[i + h];
+          c = t[0] ^ t[1] ^ t[2];
         } else {
           const uint8_t *b0 = raw + (p - 187 + 24 * k - rs);
           uint8_t by[24];
