@@ -1054,12 +1054,23 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
       if (d.mode == 1) {                         // two cells per row: pack >> mod, pack & (2^mod - 1)
         const uint32_t lo_mask = (1u << mod) - 1u;
         uint32_t wq[4];
+        if (mod == 8) {
+          // 256-QAM: the row's two cells are byte k of hi and byte k of lo, so each word of four cells
+          // is one byte permute of a half of hi and a half of lo (v_perm: selector bytes 4..7 pick
+          // the first operand's bytes, 0..3 the second's)
+          const uint32_t lh = (uint32_t)(lo >> 32), hh = (uint32_t)(hi >> 32), ll = (uint32_t)lo, hl = (uint32_t)hi;
+          wq[0] = __builtin_amdgcn_perm(hh, lh, 0x02060307u);
+          wq[1] = __builtin_amdgcn_perm(hh, lh, 0x00040105u);
+          wq[2] = __builtin_amdgcn_perm(hl, ll, 0x02060307u);
+          wq[3] = __builtin_amdgcn_perm(hl, ll, 0x00040105u);
+        } else {
 #pragma unroll
-        for (int qd = 0; qd < 4; qd++) {
-          const int k0 = 2 * qd;
-          const uint32_t p0 = (uint32_t)((lo >> (8 * (7 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (7 - k0))) & 0xFFu) << 8);
-          const uint32_t p1 = (uint32_t)((lo >> (8 * (6 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (6 - k0))) & 0xFFu) << 8);
-          wq[qd] = (p0 >> mod) | ((p0 & lo_mask) << 8) | ((p1 >> mod) << 16) | ((p1 & lo_mask) << 24);
+          for (int qd = 0; qd < 4; qd++) {
+            const int k0 = 2 * qd;
+            const uint32_t p0 = (uint32_t)((lo >> (8 * (7 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (7 - k0))) & 0xFFu) << 8);
+            const uint32_t p1 = (uint32_t)((lo >> (8 * (6 - k0))) & 0xFFu) | (uint32_t)(((hi >> (8 * (6 - k0))) & 0xFFu) << 8);
+            wq[qd] = (p0 >> mod) | ((p0 & lo_mask) << 8) | ((p1 >> mod) << 16) | ((p1 & lo_mask) << 24);
+          }
         }
         // one 16-byte LDS write of the group's four words (four b32 writes at a lane stride of 8 words
         // were 8-way bank conflicts); the last group's rows past R bytewise-guarded
