@@ -193,6 +193,16 @@ extern "C" const char *dvbt2ll_strerror(int status) {
   }
 }
 extern "C" const char *dvbt2ll_version(void) { return "dvbt2ll-mi355x 0.1 (gfx950)"; }
+extern "C" int dvbt2ll_abi_version(void) { return DVBT2LL_ABI_VERSION; }
+extern "C" int dvbt2ll_abi_check(int abi_version, size_t sizeof_chain_params, size_t sizeof_chain_info,
+                                 size_t sizeof_plp_params, size_t sizeof_mplp_params, size_t sizeof_mplp_chain_params) {
+  return abi_version == DVBT2LL_ABI_VERSION && sizeof_chain_params == sizeof(dvbt2ll_chain_params) &&
+                 sizeof_chain_info == sizeof(dvbt2ll_chain_info) && sizeof_plp_params == sizeof(dvbt2ll_plp_params) &&
+                 sizeof_mplp_params == sizeof(dvbt2ll_mplp_params) &&
+                 sizeof_mplp_chain_params == sizeof(dvbt2ll_mplp_chain_params)
+             ? DVBT2LL_OK
+             : DVBT2LL_EINVAL;
+}
 extern "C" int dvbt2ll_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -719,7 +729,16 @@ struct HostRing {
     }
     return 0;
   }
+  hipError_t synchronize() const {
+    for (hipStream_t st : {in, comp, out})
+      if (st) {
+        hipError_t r = hipStreamSynchronize(st);
+        if (r != hipSuccess) return r;
+      }
+    return hipSuccess;
+  }
   ~HostRing() {
+    (void)synchronize();   // no copy or kernel of a submission may outlive the entries' buffers
     for (auto &x : e)
       for (hipEvent_t ev : {x.h2d, x.kern, x.d2h})
         if (ev) (void)hipEventDestroy(ev);
@@ -930,6 +949,11 @@ struct dvbt2ll_chain {
     return 0;
   }
   ~dvbt2ll_chain() {
+    // every run still in flight (the ring's streams, the slots' last runs on caller streams) ends before
+    // the slot buffers and ring entries are freed
+    (void)host.synchronize();
+    for (int k = 0; k < DVBT2LL_CHAIN_MAX_SLOTS; k++)
+      if (slot_used[k] && slot_done[k]) (void)hipEventSynchronize(slot_done[k]);
     graphs.clear();
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (auto &e : evpool)
@@ -1444,8 +1468,10 @@ extern "C" int dvbt2ll_chain_run_plps_host(dvbt2ll_chain *h, const void *const *
 
 extern "C" int dvbt2ll_chain_host_submit(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                                          int64_t first_frame, int nframes, void *iq, int64_t *ticket) {
+  // every argument check precedes the first asynchronous operation, so a refused submission leaves no copy
+  // of the caller's buffers in flight (the unit check is repeated by chain_run, after the copy-in is queued)
   if (!h || !ts || !iq || !ticket || h->nplp != 1 || nframes < 1 || nframes > h->max_frames || first_frame < 0 ||
-      ts_base < 0 || ts_base % 188)
+      ts_base < 0 || ts_base % 188 || first_frame % h->frame.unit || nframes % h->frame.unit)
     return DVBT2LL_EINVAL;
   const ChainPlp &pl = *h->plps[0];
   int64_t lo, end;
@@ -1465,7 +1491,12 @@ extern "C" int dvbt2ll_chain_host_submit(dvbt2ll_chain *h, const void *ts, int64
                          R.in));
   HIP_TRY(hipEventRecord(x.h2d, R.in));
   HIP_TRY(hipStreamWaitEvent(R.comp, x.h2d, 0));
-  if ((r = dvbt2ll_chain_run_device(h, x.ts.p, lo, end - lo, first_frame, nframes, x.iq.p, R.comp))) return r;
+  if ((r = dvbt2ll_chain_run_device(h, x.ts.p, lo, end - lo, first_frame, nframes, x.iq.p, R.comp))) {
+    // unreachable after the checks above unless the device fails; the copy-in must still end before the
+    // caller may reuse ts
+    (void)hipStreamSynchronize(R.in);
+    return r;
+  }
   HIP_TRY(hipEventRecord(x.kern, R.comp));
   HIP_TRY(hipStreamWaitEvent(R.out, x.kern, 0));
   HIP_TRY(hipMemcpyAsync(iq, x.iq.p, iq_bytes, hipMemcpyDeviceToHost, R.out));
@@ -1487,14 +1518,28 @@ extern "C" int dvbt2ll_chain_host_wait(dvbt2ll_chain *h, int64_t ticket) {
 
 extern "C" int dvbt2ll_chain_run_host_pipelined(dvbt2ll_chain *h, const void *ts, int64_t ts_base, int64_t ts_len,
                                                 int64_t first_frame, int nframes, void *iq, int chunk_frames) {
-  if (!h || nframes < 1 || chunk_frames < 0) return DVBT2LL_EINVAL;
-  const int c = chunk_frames ? std::min(chunk_frames, h->max_frames) : h->max_frames;
+  if (!h || !ts || !iq || nframes < 1 || chunk_frames < 0 || h->nplp != 1) return DVBT2LL_EINVAL;
+  const int U = h->frame.unit;
+  // chunks of whole launch units; every chunk is checked before the first one is submitted
+  int c = chunk_frames ? std::min(chunk_frames, h->max_frames) : h->max_frames;
+  c -= c % U;
+  if (c < U || first_frame < 0 || first_frame % U || nframes % U || ts_base < 0 || ts_base % 188)
+    return DVBT2LL_EINVAL;
+  {
+    int64_t lo, end;
+    ts_span(*h->plps[0], first_frame, nframes, &lo, &end);   // the union of the chunks' spans
+    if (ts_base > lo || ts_base + ts_len < end) return DVBT2LL_EINVAL;
+  }
   const size_t per = (size_t)h->iq_per_frame * (h->ofdm.dev.fmt == DVBT2LL_IQ_SC16 ? 4 : 8);
   int64_t t = -1;
   for (int f = 0; f < nframes; f += c) {
     const int n = std::min(c, nframes - f);
     int r = dvbt2ll_chain_host_submit(h, ts, ts_base, ts_len, first_frame + f, n, (char *)iq + (size_t)f * per, &t);
-    if (r) return r;
+    if (r) {
+      // the chunks already submitted still copy into iq: drain them before the caller sees the error
+      if (t >= 0) (void)dvbt2ll_chain_host_wait(h, t);
+      return r;
+    }
   }
   return dvbt2ll_chain_host_wait(h, t);
 }
@@ -1599,6 +1644,11 @@ extern "C" int dvbt2ll_chain_synchronize(dvbt2ll_chain *h) {
   if (!h) return DVBT2LL_EINVAL;
   HIP_TRY(hipSetDevice(h->ctx.device));
   HIP_TRY(hipStreamSynchronize(h->ctx.stream));
+  // the streaming host path's three streams (dvbt2ll_chain_host_submit) and the slots' last runs on
+  // caller streams
+  HIP_TRY(h->host.synchronize());
+  for (int k = 0; k < DVBT2LL_CHAIN_MAX_SLOTS; k++)
+    if (h->slot_used[k] && h->slot_done[k]) HIP_TRY(hipEventSynchronize(h->slot_done[k]));
   return DVBT2LL_OK;
 }
 extern "C" void dvbt2ll_chain_destroy(dvbt2ll_chain *h) { delete h; }

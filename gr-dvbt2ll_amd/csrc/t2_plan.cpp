@@ -550,10 +550,15 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
 
   // ---- per PLP: cell interleaver (framemapper:1973-1998: per-TI-block running n, skip shifts >= cs) and
   //      time interleaver geometry (:1108-1119); PLP p's cells are data cells [start, start + S)
+  // the accumulated fields start afresh, so a plan built twice is the plan built once
   fp.S = 0;
+  fp.S_in = 0;
+  fp.ncls = 1;
+  fp.unit = 1;
   for (int k = 0; k < nplp; k++) {
     const PlpParams &q = plps[k];
     PlpPlan &pl = fp.plp[k];
+    pl.ci_shift.clear();
     pl.cs = cell_size_of(q.framesize == 1, q.constellation);
     if (!pl.cs || q.fecblocks < 1 || (q.framesize != 0 && q.framesize != 1)) return -1;
     // tiblocks > fecblocks is accepted like the reference (framemapper:1114-1119): the surplus TI

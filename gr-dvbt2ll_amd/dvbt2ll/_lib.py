@@ -46,6 +46,7 @@ class _ChainParams(ctypes.Structure):
 
 
 MAX_PLP = 8   # DVBT2LL_MAX_PLP
+ABI_VERSION = 2   # DVBT2LL_ABI_VERSION
 
 
 class _PlpParams(ctypes.Structure):
@@ -92,7 +93,7 @@ PARAMS = {"bbheaderbch": _BbParams, "ldpc": _LdpcParams, "interleavermod": _ImPa
           "framemapperfint": _FmParams, "pilotgenp1insert": _PgParams}
 
 # every symbol include/dvbt2ll_hip.h declares (checked by the CPU test suite)
-EXPORTS = ["dvbt2ll_strerror", "dvbt2ll_version", "dvbt2ll_device_count"]
+EXPORTS = ["dvbt2ll_strerror", "dvbt2ll_version", "dvbt2ll_device_count", "dvbt2ll_abi_version", "dvbt2ll_abi_check"]
 for _b in BLOCKS:
     EXPORTS += ["dvbt2ll_%s_%s" % (_b, f) for f in
                 ("create", "output_multiple", "forecast", "general_work", "destroy")]
@@ -123,6 +124,13 @@ def lib():
     L.dvbt2ll_strerror.argtypes = [ci]
     L.dvbt2ll_version.restype = ctypes.c_char_p
     L.dvbt2ll_device_count.restype = ci
+    L.dvbt2ll_abi_version.restype = ci
+    L.dvbt2ll_abi_check.argtypes = [ci] + [ctypes.c_size_t] * 5
+    # this mirror's struct layouts must be the library's (include/dvbt2ll_hip.h DVBT2LL_ABI_VERSION)
+    if L.dvbt2ll_abi_check(ABI_VERSION, ctypes.sizeof(_ChainParams), ctypes.sizeof(_ChainInfo),
+                           ctypes.sizeof(_PlpParams), ctypes.sizeof(_MplpParams), ctypes.sizeof(_MplpChainParams)):
+        raise DVBT2Error("%s: ABI version %d with other struct layouts than this mirror's (ABI %d)"
+                         % (LIB_PATH, L.dvbt2ll_abi_version(), ABI_VERSION))
     for b in BLOCKS:
         getattr(L, "dvbt2ll_%s_create" % b).argtypes = [ctypes.POINTER(PARAMS[b]), ci, ctypes.POINTER(vp)]
         getattr(L, "dvbt2ll_%s_output_multiple" % b).argtypes = [vp]

@@ -31,7 +31,9 @@ inline int check(int status, const char *what) {
   return status;
 }
 
+// every adapter constructor calls this before its create: the library's struct layouts must be this header's
 inline int device() {
+  check(DVBT2LL_ABI_CHECK(), "libdvbt2ll_hip.so ABI version / struct layouts differ from dvbt2ll_hip.h");
   const char *e = std::getenv("DVBT2LL_DEVICE");
   return e ? std::atoi(e) : 0;
 }

@@ -356,6 +356,25 @@ int dvbt2ll_chain_run_plps_host(dvbt2ll_chain *h, const void *const *ts, const i
 /* test hook: PLP plp's packed codewords of the last run's frame 0 (as dvbt2ll_chain_debug_codewords) */
 int dvbt2ll_chain_debug_plp_codewords(dvbt2ll_chain *h, int plp, void *out, int64_t bytes);
 
+/* ---------------------------------------------------------------------------
+ * ABI version.  The parameter and info structs are passed by pointer with no size field, so a caller
+ * compiled against another layout would be read or written past its struct.  Version history:
+ *   1  rounds 1-4: dvbt2ll_plp_params = the first nine ints, no num_subslices, no frames_per_if;
+ *   2  round 5: dvbt2ll_plp_params + plp_type .. first_frame_idx (which moves every field of
+ *      dvbt2ll_mplp_params / dvbt2ll_mplp_chain_params after plp[0]), dvbt2ll_mplp_params.num_subslices,
+ *      dvbt2ll_chain_info.frames_per_if.
+ * dvbt2ll_abi_check(DVBT2LL_ABI_VERSION, sizeof ...) (or the DVBT2LL_ABI_CHECK() macro) returns DVBT2LL_OK when the
+ * caller's header is this library's, DVBT2LL_EINVAL otherwise; the adapters and the Python mirror call it
+ * before their first create.
+ * ------------------------------------------------------------------------- */
+#define DVBT2LL_ABI_VERSION 2
+int dvbt2ll_abi_version(void);
+int dvbt2ll_abi_check(int abi_version, size_t sizeof_chain_params, size_t sizeof_chain_info,
+                      size_t sizeof_plp_params, size_t sizeof_mplp_params, size_t sizeof_mplp_chain_params);
+#define DVBT2LL_ABI_CHECK()                                                                                      \
+  dvbt2ll_abi_check(DVBT2LL_ABI_VERSION, sizeof(dvbt2ll_chain_params), sizeof(dvbt2ll_chain_info),               \
+                    sizeof(dvbt2ll_plp_params), sizeof(dvbt2ll_mplp_params), sizeof(dvbt2ll_mplp_chain_params))
+
 #ifdef __cplusplus
 }
 #endif

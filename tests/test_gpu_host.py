@@ -77,3 +77,33 @@ def test_host_submit_rejects(gpu):
     m = dvbt2ll.Chain(MPLP_CONFIGS["mplp3_4k"], max_frames=1)
     with pytest.raises(dvbt2ll.DVBT2Error):           # single-PLP chains only
         m.host_submit(tsp.data_ptr(), base, len(ts), 0, 1, iq.data_ptr())
+
+
+def test_host_paths_unit_checks_before_any_copy(gpu):
+    """a chain whose launch unit is 2 T2 frames (FRAME_INTERVAL 2, ij2_4k_single): submissions and pipelined
+    calls off the unit grid are refused before any copy is queued (a refused call must leave no DMA
+    into or out of the caller's buffers); pipelined chunks are rounded down to whole units and the output equals
+    the device path's"""
+    import torch
+    from dvbt2ll.configs import IF_CONFIGS
+    from test_gpu_mplp import _run
+    m = IF_CONFIGS["ij2_4k_single"]
+    assert m.unit_frames == 2
+    n = 6
+    ch = dvbt2ll.Chain(m, max_frames=4)
+    ts, base = ts_for_frames(m.plps[0], 0, n, seed=1)
+    tsp = torch.from_numpy(ts).pin_memory()
+    iq = torch.zeros((n * ch.iq_per_frame, 2), dtype=torch.float32).pin_memory()
+    for first, nf in ((1, 2), (0, 3)):
+        with pytest.raises(dvbt2ll.DVBT2Error):
+            ch.host_submit(tsp.data_ptr(), base, len(ts), first, nf, iq.data_ptr())
+    out = np.zeros(n * ch.iq_per_frame, np.complex64)
+    with pytest.raises(dvbt2ll.DVBT2Error):          # 5 frames: the last chunk would not be a whole unit
+        ch.run_host_pipelined(ts, base, 0, 5, out, 2)
+    with pytest.raises(dvbt2ll.DVBT2Error):          # a chunk smaller than the unit
+        ch.run_host_pipelined(ts, base, 0, n, out, 1)
+    assert not out.any()                            # nothing was copied out by the refused calls
+    ch.run_host_pipelined(ts, base, 0, n, out, 3)   # chunks of 3 -> 2 frames
+    want = _run(dvbt2ll.Chain(m, max_frames=n), m, 0, n)
+    np.testing.assert_array_equal(out.view(np.uint32), want.view(np.uint32))
+    ch.synchronize()
