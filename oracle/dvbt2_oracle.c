@@ -659,8 +659,8 @@ static void add_l1pre(orc_fm *h, cf *out) {
 
 /* add_l1post (framemapper:1536-1910); the PLP loops of the configurable (:1577-1639) and dynamic
  * (:1672-1687) parts run over the frame's PLPs */
-static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
-  uint8_t info[FRAME_SIZE_SHORT], t[FRAME_SIZE_SHORT], map[KBCH_1_2];
+/* the L1-post signalling bits before the CRC-32 (:1546-1691) into info; returns their count */
+static int l1post_info(const orc_fm *h, uint8_t *info, int t2_frame_num) {
   int o = 0;
   put_bits(info, &o, (unsigned)h->nss, 15);  /* SUB_SLICES_PER_FRAME (1 without Type-2 PLPs) */
   put_bits(info, &o, (unsigned)h->nplp, 8);  /* NUM_PLP */
@@ -710,6 +710,12 @@ static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
     put_bits(info, &o, (unsigned)h->post_reserved4, 8);
   }
   put_bits(info, &o, (unsigned)h->post_reserved5, 8);
+  return o;
+}
+
+static void add_l1post(orc_fm *h, cf *out, int t2_frame_num) {
+  uint8_t info[FRAME_SIZE_SHORT], t[FRAME_SIZE_SHORT], map[KBCH_1_2];
+  int o = l1post_info(h, info, t2_frame_num);
   uint32_t crc = orc_crc32_bits(info, o);
   put_bits(info, &o, crc, 32);
   if (h->l1_scrambled) for (int n = 0; n < o; n++) info[n] ^= h->l1_randomize[n];
@@ -1087,6 +1093,17 @@ void orc_fm_destroy(orc_fm *h) {
   }
   free(h->Heven); free(h->Hodd); free(h->HevenP2); free(h->HoddP2); free(h->HevenFC); free(h->HoddFC);
   free(h->cell_out); free(h->frame_out); free(h->zigzag); free(h->dummy); free(h);
+}
+
+/* test hook: the L1-post signalling bits (one per byte, before the CRC-32) of absolute T2 frame `frame` as
+ * orc_fm_work would build them there; returns the bit count (0 when cap is too small) */
+int orc_fm_l1post_bits(orc_fm *h, long frame, uint8_t *out, int cap) {
+  uint8_t info[FRAME_SIZE_SHORT];
+  (void)frame_layout(h, frame);   /* orc_fm_work recomputes the placement of its own frame */
+  const int o = l1post_info(h, info, (int)(frame % h->t2_frames));
+  if (o > cap) return 0;
+  memcpy(out, info, (size_t)o);
+  return o;
 }
 
 void orc_fm_seek(orc_fm *h, long frame) {

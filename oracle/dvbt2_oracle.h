@@ -82,6 +82,8 @@ int orc_fm_consume(const orc_fm *h, int plp);
 /* the state at absolute T2 frame `frame` (t2_frame_num = frame mod t2frames; every PLP at frame mod P_I of
  * its interleaving frame -- the next work call must start interleaving frames of the PLPs it consumes) */
 void orc_fm_seek(orc_fm *h, long frame);
+/* test hook: T2 frame `frame`'s L1-post signalling bits before the CRC-32, one per byte; returns the count */
+int orc_fm_l1post_bits(orc_fm *h, long frame, uint8_t *out, int cap);
 /* one T2 frame: the consumed cells of every PLP (PLP 0 first) in -> mapped_items cells out; returns
  * mapped_items */
 int orc_fm_work(orc_fm *h, const float *in, float *out);

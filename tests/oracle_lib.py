@@ -36,6 +36,7 @@ def lib():
         L.orc_fm_consume.argtypes = [vp, ci]
         L.orc_fm_seek.argtypes = [vp, ctypes.c_long]
         L.orc_fm_l1post_cells.argtypes = [vp]
+        L.orc_fm_l1post_bits.argtypes = [vp, ctypes.c_long, vp, ci]
         L.orc_ldpc_create.restype = vp
         L.orc_ldpc_create.argtypes = [ci, ci]
         L.orc_ldpc_work.argtypes = [vp, ci, vp, vp]
@@ -173,6 +174,13 @@ class FMM(FM):
     def seek(self, frame):
         """start at absolute T2 frame `frame` (a launch unit boundary)"""
         lib().orc_fm_seek(self.h, int(frame))
+
+    def l1post_bits(self, frame):
+        """the L1-post signalling bits (before the CRC-32, one per byte) the oracle builds for T2 frame `frame`"""
+        out = np.zeros(4096, np.uint8)
+        n = lib().orc_fm_l1post_bits(self.h, int(frame), _p(out), len(out))
+        assert n > 0
+        return out[:n]
 
 
 def mplp_cells(mcfg, first_frame, nframes):

@@ -31,7 +31,10 @@ def run_driver(tmp_path, cfg, nframes, ts, seed):
     return np.fromfile(tmp_path / "iq.bin", np.complex64), r
 
 
-@pytest.mark.parametrize("name,nframes,seed", [("cfg1", 4, 1), ("cfg1q", 3, 2), ("cfg4", 3, 3), ("cfg1", 3, 4)])
+# the 32K configurations too (verdict r5 item 5): cfg3 is the headline config (32K-ext 256-QAM 3/5 PP4 rotated),
+# cfg2 32K 64-QAM 2/3 PP7, cfg5 32K 256-QAM 5/6; two frames each through the C++ adapters with ragged calls
+@pytest.mark.parametrize("name,nframes,seed", [("cfg1", 4, 1), ("cfg1q", 3, 2), ("cfg4", 3, 3), ("cfg1", 3, 4),
+                                               ("cfg3", 2, 5), ("cfg2", 2, 6), ("cfg5", 2, 7)])
 def test_gr_adapter_flowgraph(gpu, tmp_path, name, nframes, seed):
     cfg = CONFIGS[name]
     ts, base = ts_for_frames(cfg, 0, nframes + 1)
