@@ -779,6 +779,8 @@ struct dvbt2ll_chain {
   bool keep_cw = false;
   bool cw_kept[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   bool slot_used[DVBT2LL_CHAIN_MAX_SLOTS] = {};
+  // a run on the slot failed after its FEC pass may have run: its BCH partial parities are not known to be zero
+  bool bpart_dirty[DVBT2LL_CHAIN_MAX_SLOTS] = {};
   int nslots = 1, next_slot = 0, last_slot = 0;
   // hipGraph mode (dvbt2ll_chain_set_graph)
   bool use_graph = false;
@@ -843,8 +845,8 @@ struct dvbt2ll_chain {
     if (e == hipSuccess) e = launch_ofdm(ofdm.dev, oio, s);
     return e;
   }
-  // kernel nodes per run: 2 FEC passes and an LDPC + map kernel per PLP, one OFDM
-  int graph_nodes() const { return 3 * nplp + 1; }
+  // kernel nodes per run: the fused BB + BCH pass and the LDPC + map kernel per PLP, one OFDM
+  int graph_nodes() const { return 2 * nplp + 1; }
   int graph_launch(const L1IO &lio, const FecIO *fio, const MapIO *mio, const OfdmIO &oio, int nframes, int slot,
                    hipStream_t s) {
     const int nk = graph_nodes();
@@ -923,8 +925,7 @@ struct dvbt2ll_chain {
       fd[k] = plps[k]->fec.dev;
       md[k] = plps[k]->map.dev;
     }
-    for (int k = 0; k < nplp; k++)
-      for (int pass = 0; pass < 2; pass++) args.push_back({&fd[k], &fi[k]});
+    for (int k = 0; k < nplp; k++) args.push_back({&fd[k], &fi[k]});
     for (int k = 0; k < nplp; k++) args.push_back({&fd[k], &fi[k], &md[k], &mi[k], k ? &ld0 : &ld, k ? &li0 : &li});
     args.push_back({&od, &oi});
     for (int k = 0; k < nk; k++) {
@@ -939,10 +940,15 @@ struct dvbt2ll_chain {
     return 0;
   }
   int alloc_slot(int k) {
-    for (auto &pl : plps)
-      if (pl->cw[k].ensure((size_t)pl->blocks(max_frames) * pl->cw_stride) ||
+    for (auto &pl : plps) {
+      // one spare row past the largest launch: the fused FEC pass stores its dead lanes' pieces there
+      if (pl->cw[k].ensure((size_t)(pl->blocks(max_frames) + 1) * pl->cw_stride) ||
           pl->bpart[k].ensure((size_t)pl->blocks(max_frames) * BCH_PART_WORDS * sizeof(uint32_t)))
         return DVBT2LL_ENOMEM;
+      // the BCH partial parities start at zero (bbch_kernel XORs into them, ldpc_map_kernel zeroes what it reads)
+      HIP_TRY(hipMemset(pl->bpart[k].p, 0, pl->bpart[k].n));
+    }
+    bpart_dirty[k] = false;
     if (pairs[k].ensure((size_t)pair_stride * max_frames * 2) || l1buf[k].ensure((size_t)l1_stride * max_frames * 8))
       return DVBT2LL_ENOMEM;
     if (!slot_done[k]) HIP_TRY(hipEventCreateWithFlags(&slot_done[k], hipEventDisableTiming));
@@ -1322,6 +1328,10 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
   const int slot = h->next_slot;
   if (h->slot_used[slot] && h->slot_stream[slot] != s) HIP_TRY(hipStreamWaitEvent(s, h->slot_done[slot], 0));
   DevBuf &pairs = h->pairs[slot];
+  if (h->bpart_dirty[slot]) {
+    for (auto &pl : h->plps) HIP_TRY(hipMemsetAsync(pl->bpart[slot].p, 0, pl->bpart[slot].n, s));
+    h->bpart_dirty[slot] = false;
+  }
   hipEvent_t ev[dvbt2ll_chain::NEV] = {};
   if (h->timing && !h->use_graph) {   // per-stage events only on the direct launch path
     if (h->evused + dvbt2ll_chain::NEV > 4096 && h->fold_timing()) return DVBT2LL_EDEVICE;
@@ -1374,9 +1384,16 @@ static int chain_run(dvbt2ll_chain *h, const void *const *ts, const int64_t *bas
   oio.l1_stride = h->l1_stride;
   if (h->use_graph) {
     int r = h->graph_launch(lio, fio, mio, oio, nf, slot, s);
-    if (r) return r;
+    if (r) {
+      h->bpart_dirty[slot] = true;
+      return r;
+    }
   } else {
-    HIP_TRY(h->launch_chain(lio, fio, mio, oio, s, ev[1], ev[2]));
+    const hipError_t e = h->launch_chain(lio, fio, mio, oio, s, ev[1], ev[2]);
+    if (e != hipSuccess) {
+      h->bpart_dirty[slot] = true;
+      HIP_TRY(e);
+    }
     if (h->timing) HIP_TRY(hipEventRecord(ev[3], s));
   }
   HIP_TRY(hipEventRecord(h->slot_done[slot], s));

@@ -7,16 +7,16 @@ namespace t2 {
 
 // ---------------------------------------------------------------- FEC (BB + BCH + LDPC)
 enum FecMode {
-  FEC_TS_TO_BBFRAME = 0, // chain: TS bytes -> BBFRAME rows + BCH partial parities (BB pass, matrix-core
-                         // BCH pass); launch_ldpc_map continues from them
+  FEC_TS_TO_BBFRAME = 0, // chain: TS bytes -> BBFRAME rows + BCH partial parities (one fused pass: the BBFRAME
+                         // built in registers, BCH on the matrix cores); launch_ldpc_map continues from them
   FEC_TS_TO_BITS = 1,    // bbheaderbch block: TS bytes -> unpacked nbch bits
   FEC_BITS_TO_BITS = 2,  // ldpc block: unpacked nbch bits -> unpacked nldpc bits (natural)
 };
 
-// the chain's BCH pass (bch_gemm_kernel): K slices (slice = blockIdx % 2: the even XCDs take slice 0,
-// the odd ones slice 1, so each XCD's L2 holds half the generator table; 2 slices measured 2 % faster
-// than 8 and 1 % faster than 4 or 1: fewer tile-segment prologues, epilogues and atomics); parity words
-// per block (the slices XOR their partial parities into them)
+// the chain's BCH (bbch_kernel): K slices (slice = blockIdx % 2: the even XCDs take slice 0, the odd ones
+// slice 1, so each XCD's L2 holds half the generator table; 2 slices measured 2 % faster than 8 and 1 %
+// faster than 4 or 1 in round 4: fewer tile-segment prologues, epilogues and atomics); parity words per
+// block (the slices XOR their partial parities into them)
 constexpr int BCH_KS = 2;
 constexpr int BCH_PART_WORDS = 8;
 
@@ -52,9 +52,9 @@ struct FecIO {
   // b / blocks_per_stream, whose TS bytes start at in + stream * ts_stride (same ts_base, ts_len)
   int blocks_per_stream;
   int64_t ts_stride;
-  // chain (FEC_TS_TO_BBFRAME): BCH parity of launch block b at bch_part + b * BCH_PART_WORDS (zeroed by
-  // the BB pass, XOR-accumulated by the K slices of the matrix-core pass, read by launch_ldpc_map;
-  // room for bch_part_blocks >= nblocks)
+  // chain (FEC_TS_TO_BBFRAME): BCH parity of launch block b at bch_part + b * BCH_PART_WORDS (zero before the
+  // launch, XOR-accumulated by the K slices of the fused BB + BCH pass, read and zeroed again by
+  // launch_ldpc_map; room for bch_part_blocks >= nblocks).  out has a spare row at nblocks (dead lanes' stores).
   uint32_t *bch_part;
   int64_t bch_part_blocks;
   // launch_ldpc_map (test hook): 1 = also store each block's interleaver-input codeword into its row

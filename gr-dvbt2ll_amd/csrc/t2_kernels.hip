@@ -712,127 +712,398 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_WG_PER_CU) void fec_kernel(FecDev 
   }
 }
 
-// chain pass 1: the BBFRAME of every launch block into its codeword row (bytes [0, L); bytes past L
-// of the last 16-byte unit are don't-care: the BCH pass multiplies them by zero rows, the LDPC stage
-// rewrites them)
-__global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void fec_bb_kernel(FecDev d, FecIO io) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x;
-  const int L = d.kbch >> 3;
-  const FecCarve cv = fec_carve(CARVE_BB, d.kbch, d.nbch, d.q);
-  for (int i = tid; i < 72; i += FEC_THREADS) smem[cv.hcrc + i] = d.hcrc_bits[i];
-  for (int i = tid; i < 64; i += FEC_THREADS) ((uint32_t *)(smem + cv.crc8))[i] = ((const uint32_t *)d.crc8_tab)[i];
-  for (int i = tid; i < 512; i += FEC_THREADS) ((uint32_t *)(smem + cv.crcsh))[i] = ((const uint32_t *)d.crc8_shift)[i];
-  __syncthreads();
-  for (int i = tid; i < (L + 3) >> 2; i += FEC_THREADS) ((uint32_t *)(smem + cv.prbs))[i] = ((const uint32_t *)d.prbs)[i];
-  {   // the powers T^1 .. T^24 of the CRC-8 byte table T (T^(k+1)[x] = T[T^k[x]])
-    const uint8_t *t1 = smem + cv.crc8;
-    uint8_t *sl = smem + cv.crcsl;
-    if (tid < 256) {
-      uint32_t v = (uint32_t)tid;
-      for (int k = 0; k < 24; k++) {
-        v = t1[v];
-        sl[k * 256 + tid] = (uint8_t)v;
-      }
-    }
-  }
-  __syncthreads();
-  // NM: each block's raw TS units are requested one block ahead (in flight during the previous block),
-  // with its geometry, which the block then reuses (the per-block geometry is scalar 64-bit arithmetic)
-  uint4 pre[FEC_PRE];
-  BbGeom gpre{};
-  const uint8_t *tpre = io.in;
-  int64_t bpre = 0;
-  auto prefetch = [&](int b) {
-    bpre = fec_block_of(io, b, tpre);
-    gpre = bb_geom(d, io, bpre);
-#pragma unroll
-    for (int k = 0; k < FEC_PRE; k++)
-      pre[k] = tid + FEC_THREADS * k < gpre.nq ? bb_raw_unit(io, tpre, gpre.w0, tid + FEC_THREADS * k) : make_uint4(0u, 0u, 0u, 0u);
-  };
-  if (!d.hem && (int)blockIdx.x < io.nblocks) prefetch(blockIdx.x);
-  for (int bi = blockIdx.x; bi < io.nblocks; bi += gridDim.x) {
-    const uint8_t *tin = tpre;
-    int64_t B = bpre;
-    BbGeom g = gpre;
-    if (d.hem) {
-      B = fec_block_of(io, bi, tin);
-      g = bb_geom(d, io, B);
-    }
-    uint4 cur[FEC_PRE];
-#pragma unroll
-    for (int k = 0; k < FEC_PRE; k++) cur[k] = pre[k];
-    if (!d.hem && bi + (int)gridDim.x < io.nblocks) prefetch(bi + gridDim.x);
-    fec_bbframe<true, true, true>(d, io, cv, smem, B, tin, tid, cur, &g, (uint32_t *)(io.out + (int64_t)bi * io.cw_stride));
-    if (tid < BCH_PART_WORDS) io.bch_part[(int64_t)bi * BCH_PART_WORDS + tid] = 0u;   // the BCH pass XORs into it
-  }
-}
-
 // ---- chain pass 2: BCH as a GF(2) matrix product on the matrix cores
 typedef int bch_v8i __attribute__((ext_vector_type(8)));
 typedef float bch_v16f __attribute__((ext_vector_type(16)));
 
-// Persistent workgroups, BCH_WG_PER_CU per CU.  Workgroup i serves K slice i % BCH_KS (by its XCD: that
-// XCD's L2 holds 1 / BCH_KS of the generator table) and a contiguous, equal share of the slice's
-// (tile, chunk) units, tile-major: a tile is 128 FEC blocks (wave w: blocks 32 w .. 32 w + 31, one per
-// A row) x all bch_nt parity tiles, a chunk 32 message bytes = four K-steps of 64 bits.  Per chunk
-// the B fragments (t2_plan build_bch_mfma) are staged in LDS (double-buffered LDS-DMA, one barrier per
-// chunk), each lane loads 16 message bytes of its block and masks each 32-bit word into an A
-// fragment, and each wave issues 4 x NT v_mfma_scale_f32_32x32x64_f8f6f4 (fp4 A and B; E8M0 scales 2
-// for A, 1 for B).  Sums are exact small integers in f32; at the end of each tile segment the partial
-// parity ((int) sum & 1) is packed by wave ballots into 8 words per block (bytes in transmission
-// order) and XORed into bch_part[b * 8] (zeroed by the BB pass).
-constexpr int BCH_WG_PER_CU = 3;
-// s_waitcnt immediate for vmcnt(0) alone on gfx9: vmcnt [3:0] + [15:14] = 0, expcnt [6:4] = 7, lgkmcnt [11:8] = 15
-constexpr int BCH_WAIT_VMCNT0 = 0x0F70;
-template <int NT>
-__global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(FecDev d, FecIO io) {
+// ---- chain FEC, fused (round 6): the BB pass and the matrix-core BCH as one kernel, bbch_kernel
+// The BB pass wrote each BBFRAME to HBM and the BCH pass read it back (1.7 x the FEC stage's minimal bytes).
+// Here each lane builds its own A-fragment piece -- BBFRAME bytes [P0, P0 + 16), P0 = 32 q + 16 h, of its block
+// (h = lane >> 5) -- straight from the TS in registers: the payload bytes of the stream with each sync slot
+// replaced by the CRC-8 of the packet before it (bbheader:701-719; HEM: the sync bytes dropped, :673-680), the
+// BBHEADER in chunk 0 (:272-325), the in-band type B field after the payload (:327-355), BB scrambling
+// (:694-696, 724-726).  The piece is stored to the block's codeword row (the LDPC + map kernel reads the BBFRAME
+// there) and multiplied as in bch_gemm_kernel.
+// Sync-slot CRC-8s are streamed.  The CRC register is linear, so a 16-byte piece b_0..b_15 moves it as
+// s' = T^16[s] ^ G, G = XOR_i T^(16-i)[b_i]: 16 independent lookups in the power tables T^1..T^16 (LDS).  A piece
+// with a sync position at offset e gives the slot T^e[s] ^ P_e (P_e = T^-(16-e)[X_e], X_e = XOR_{i<e} of G's
+// terms, through the inverse power tables) and restarts the register after it (s' = G ^ X_e ^ t_e).  The two
+// lanes of a row hand the register to each other once per piece.  A tile segment starting at chunk q0 first
+// streams the CRC through the BBCH_PRO chunks (192 stream bytes) before it, so a sync position (one every 188
+// bytes) has restarted the register before the first slot it fills.
+constexpr int BBCH_WG_PER_CU = 2;   // ~210 VGPRs: two waves per SIMD
+constexpr int BBCH_PRO = 6;         // CRC prologue chunks (6 x 32 >= 188 + 4)
+constexpr int BBCH_TAB = 16 * 256 * 2 + 9 * 256 + 16;   // T^k, T^-k, BBHEADER CRC per byte, in-band bytes
+constexpr int BBCH_PRBS = 32 * 216;                      // BB-scrambler PRBS bytes, whole chunks (>= 6750 B)
+static_assert(BBCH_TAB % 16 == 0, "the PRBS bytes after the tables are read as 16-byte units");
+__host__ __device__ constexpr int bbch_lds(int nt) { return 2 * 4 * nt * 64 * 16 + BBCH_TAB + BBCH_PRBS; }
+
+// 32 stream bytes: the 16-byte aligned unit holding tin + rel and the next; o = (tin + rel) & 15.  ts_fetch always
+// issues the two 16-byte loads (from a safe address inside [tin, tin + len) when the window is not: edge) and
+// returns without waiting for them; ts_slow redoes an edge window bytewise with zeros outside the buffer.  (A
+// fast / slow branch merged inside the fetch made the compiler wait for the loads right there, vmcnt(0).)
+struct TsWin {
+  uint32_t w[8];
+  uint32_t o;
+  bool edge;
+};
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4 *g4ptr;   // global, not flat: a flat load may read LDS, so
+typedef const __attribute__((address_space(1))) uint8_t *g1ptr;  // the compiler would wait for every LDS write first
+__device__ __forceinline__ TsWin ts_fetch(const uint8_t *tin, int64_t len, int64_t rel) {
+  TsWin r;
+  const uintptr_t t0 = (uintptr_t)tin, a = t0 + (uintptr_t)rel, a0 = a & ~(uintptr_t)15;
+  r.o = (uint32_t)(a & 15);
+  r.edge = !(a0 >= t0 && a0 + 32 <= t0 + (uintptr_t)len);
+  const uintptr_t src = r.edge ? (t0 + 15) & ~(uintptr_t)15 : a0;   // len >= 64 (fec_chain_args_ok)
+  const u32x4 x = *(g4ptr)src, y = *(g4ptr)(src + 16);
+  r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
+  r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+  return r;
+}
+__device__ __forceinline__ void ts_slow(const uint8_t *tin, int64_t len, int64_t rel, uint32_t *w) {
+  const uintptr_t t0 = (uintptr_t)tin, a0 = (t0 + (uintptr_t)rel) & ~(uintptr_t)15;
+  uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // named halves, not an indexed array (that would live in scratch)
+#pragma unroll 1
+  for (int b = 0; b < 32; b++) {
+    const uintptr_t p = a0 + b;
+    const uint64_t v = p >= t0 && p < t0 + (uintptr_t)len ? (uint64_t)*(g1ptr)p << (8 * (b & 7)) : 0ull;
+    q0 |= b < 8 ? v : 0ull;
+    q1 |= b >= 8 && b < 16 ? v : 0ull;
+    q2 |= b >= 16 && b < 24 ? v : 0ull;
+    q3 |= b >= 24 ? v : 0ull;
+  }
+  w[0] = (uint32_t)q0; w[1] = (uint32_t)(q0 >> 32); w[2] = (uint32_t)q1; w[3] = (uint32_t)(q1 >> 32);
+  w[4] = (uint32_t)q2; w[5] = (uint32_t)(q2 >> 32); w[6] = (uint32_t)q3; w[7] = (uint32_t)(q3 >> 32);
+}
+// the 16 bytes at offset o (0 .. 16) of a window, as four little-endian dwords.  Selects between named 64-bit
+// values, never an indexed array: a select chain over an array's elements is folded into a dynamically
+// indexed load, which lives in scratch memory.
+__device__ __forceinline__ uint64_t fsh64(uint64_t lo, uint64_t hi, uint32_t ob) {   // bytes ob .. ob + 7 of hi:lo
+  return ob ? (lo >> (8 * ob)) | (hi << (64 - 8 * ob)) : lo;
+}
+__device__ __forceinline__ void win_bytes(const uint32_t *w, uint32_t o, uint32_t *d) {
+  const uint64_t q0 = ((uint64_t)w[1] << 32) | w[0], q1 = ((uint64_t)w[3] << 32) | w[2];
+  const uint64_t q2 = ((uint64_t)w[5] << 32) | w[4], q3 = ((uint64_t)w[7] << 32) | w[6];
+  const uint32_t qi = o >> 3, ob = o & 7;
+  const uint64_t A = qi == 0 ? q0 : qi == 1 ? q1 : q2, B = qi == 0 ? q1 : qi == 1 ? q2 : q3,
+                 C = qi == 0 ? q2 : qi == 1 ? q3 : 0ull;
+  const uint64_t lo = fsh64(A, B, ob), hi = fsh64(B, C, ob);
+  d[0] = (uint32_t)lo;
+  d[1] = (uint32_t)(lo >> 32);
+  d[2] = (uint32_t)hi;
+  d[3] = (uint32_t)(hi >> 32);
+}
+__device__ __forceinline__ uint32_t byte_of(const uint32_t *d, int i) {   // i dynamic, 0 .. 15
+  const uint64_t lo = ((uint64_t)d[1] << 32) | d[0], hi = ((uint64_t)d[3] << 32) | d[2];
+  return (uint32_t)(((i & 8) ? hi : lo) >> (8 * (i & 7))) & 0xFFu;
+}
+__device__ __forceinline__ void set_byte(uint32_t *d, int i, uint32_t b) {   // i dynamic, 0 .. 15
+  uint64_t lo = ((uint64_t)d[1] << 32) | d[0], hi = ((uint64_t)d[3] << 32) | d[2];
+  const uint64_t m = 0xFFull << (8 * (i & 7)), v = (uint64_t)b << (8 * (i & 7));
+  const uint64_t lo2 = (lo & ~m) | v, hi2 = (hi & ~m) | v;
+  lo = (i & 8) ? lo : lo2;
+  hi = (i & 8) ? hi2 : hi;
+  d[0] = (uint32_t)lo;
+  d[1] = (uint32_t)(lo >> 32);
+  d[2] = (uint32_t)hi;
+  d[3] = (uint32_t)(hi >> 32);
+}
+
+// one row's BB state over the chunks: the block's geometry and, per lane, its stream cursor
+struct BbchRow {
+  const uint8_t *tin;
+  uint8_t *row;
+  BbGeom g;
+  int64_t rel;   // NM: TS offset of this lane's piece in the current chunk (BBFRAME byte P0 -> stream pos0 + P0 - 10)
+  int m;         // NM: that stream position mod 188
+  int64_t sh;    // HEM: stream position of payload byte J0 + P0 - 10 (the tracked chunk's piece)
+  int r;         // HEM: (J0 + P0 - 10) mod 187
+  bool live;
+};
+
+// NM CRC of one piece: its terms t_i = T^(16-i)[b_i] (16 independent lookups) folded into G, the prefix X_e of the
+// terms before the sync position e and t_e
+struct CrcTerms {
+  uint32_t g, x, te;
+};
+__device__ __forceinline__ CrcTerms crc_terms(const uint8_t *tp, const uint32_t *d, int e) {
+  uint32_t t[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) t[i] = tp[(15 - i) * 256 + ((d[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
+  // prefixes as masked XORs (a select "i == e ? t[i]" would be folded into a dynamically indexed load)
+  CrcTerms c{0u, 0u, 0u};
+  uint32_t x1 = 0u;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    c.g ^= t[i];
+    c.x ^= t[i] & (i < e ? 0xFFu : 0u);
+    x1 ^= t[i] & (i <= e ? 0xFFu : 0u);
+  }
+  c.te = c.x ^ x1;
+  return c;
+}
+// the register after the piece from s_in, and the sync slot's value where the piece holds a sync position (e < 16):
+// T^e[s_in] ^ P_e, P_e = T^-(16-e)[X_e] (T^k at tp + (k-1) 256, T^-k at tq + (k-1) 256); after the sync position
+// the register restarts from 0 and takes the terms after it, G ^ X_e ^ t_e
+__device__ __forceinline__ uint32_t crc_step(const uint8_t *tp, const uint8_t *tq, const CrcTerms &c, int e,
+                                             uint32_t s_in, uint32_t &slot) {
+  const bool sync = e < 16;
+  const uint32_t pe = e > 0 && sync ? (uint32_t)tq[(15 - e) * 256 + c.x] : 0u;
+  slot = (e > 0 && sync ? (uint32_t)tp[(e - 1) * 256 + s_in] : s_in) ^ pe;
+  return sync ? c.g ^ c.x ^ c.te : (uint32_t)tp[15 * 256 + s_in] ^ c.g;
+}
+// the row's register through one chunk: lane 0's piece, then lane 1's (two lane exchanges); slot: this lane's
+// sync slot value; returns the register at the next chunk (both lanes)
+__device__ __forceinline__ uint32_t crc_chunk(const uint8_t *tp, const uint8_t *tq, const uint32_t *d, int e, int h,
+                                              uint32_t s, uint32_t &slot) {
+  const CrcTerms c = crc_terms(tp, d, e);
+  uint32_t sl;
+  const uint32_t o0 = crc_step(tp, tq, c, e, s, sl);   // lane 0: the register after its piece
+  // every lane runs both exchanges (a lane exchange under a condition would read inactive lanes)
+  const uint32_t y = (uint32_t)__shfl_xor((int)o0, 32);
+  const uint32_t s_in = h ? y : s;
+  const uint32_t o1 = crc_step(tp, tq, c, e, s_in, slot);
+  const uint32_t z = (uint32_t)__shfl_xor((int)o1, 32);
+  return h ? o1 : z;
+}
+
+template <int NT, bool HEM>
+__global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) uint4 bsm[];
   constexpr int PER = 4 * NT * 64;                   // uint4 per chunk buffer
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int slice = (int)blockIdx.x % BCH_KS, per_slice = (int)gridDim.x / BCH_KS, k = (int)blockIdx.x / BCH_KS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int L = d.kbch >> 3, nprbs = (L + 3) >> 2;
+  const uint32_t *prbsw = (const uint32_t *)d.prbs;
+  uint8_t *tp = (uint8_t *)(bsm + 2 * PER), *tq = tp + 4096, *hd = tq + 4096, *ibb = hd + 9 * 256;
+  uint8_t *prb = tp + BBCH_TAB;   // 16-byte aligned: BBCH_TAB is a multiple of 16
+  // ---- tables, once per workgroup: T^1..T^16 and their inverses (NM), the BBHEADER CRC-8 per header byte
+  // (add_crc8_bits :247-270: XOR of the per-bit contributions hcrc_bits, bit 8 b + j = bit 7 - j of byte b), the
+  // in-band type B bytes (:327-355: 01, 65 zero bits, the TS rate in 27 bits, 10 zero bits)
+  if (!HEM && tid < 256) {
+    uint32_t v = (uint32_t)tid;
+    for (int k = 0; k < 16; k++) {
+      v = d.crc8_tab[v];
+      tp[k * 256 + tid] = (uint8_t)v;
+    }
+  }
+  for (int i = tid; i < 9 * 256; i += FEC_THREADS) {
+    const int b = i >> 8, x = i & 255;
+    uint32_t v = 0;
+    for (int j = 0; j < 8; j++)
+      if ((x >> (7 - j)) & 1) v ^= d.hcrc_bits[8 * b + j];
+    hd[i] = (uint8_t)v;
+  }
+  for (int i = tid; i < BBCH_PRBS / 4; i += FEC_THREADS) ((uint32_t *)prb)[i] = i < nprbs ? prbsw[i] : 0u;
+  if (tid < 13) {
+    uint32_t v = tid == 0 ? 0x40u : 0u;
+    for (int e = 0; e < 8; e++) {
+      const int bit = 8 * tid + e;
+      if (bit >= 67 && bit < 94 && ((d.ts_rate >> (26 - (bit - 67))) & 1)) v |= 1u << (7 - e);
+    }
+    ibb[tid] = (uint8_t)v;
+  }
+  __syncthreads();
+  if (!HEM && tid < 256)
+    for (int k = 0; k < 16; k++) tq[k * 256 + tp[k * 256 + tid]] = (uint8_t)tid;
+  __syncthreads();
+
+  const int slice = (int)blockIdx.x % BCH_KS, per_slice = (int)gridDim.x / BCH_KS, kq = (int)blockIdx.x / BCH_KS;
   const int qs0 = slice * d.bch_nq / BCH_KS, nc = (slice + 1) * d.bch_nq / BCH_KS - qs0;   // chunks per tile
   const int64_t units = (int64_t)((io.nblocks + BCH_ROWS - 1) / BCH_ROWS) * nc;
-  const int64_t u1 = units * (k + 1) / per_slice;
-  // chunk q's B fragments into LDS buffer buf by LDS-DMA (16 bytes per lane, no VGPR staging): each
-  // wave-instruction fills 1 KB at a wave-uniform base, lane l at + 16 l (the table is lane-linear)
-  auto stage = [&](int q, int buf) {
+  const int64_t u1 = units * (kq + 1) / per_slice;
+  // chunk q's B fragments (t2_plan build_bch_mfma, lane-linear): loaded into registers a chunk ahead, written to
+  // LDS buffer buf after the chunk's MFMAs.  Not LDS-DMA: the compiler cannot tell which LDS bytes a DMA writes,
+  // so it waits for every outstanding DMA with vmcnt(0) before any LDS read.  (In round 5's bch_gemm_kernel that
+  // wait sat right after the next chunk's DMA, so its double buffer never overlapped a DMA with the MFMAs; here
+  // vmcnt(0) would also drain the BBFRAME stores.)
+  // (a vector value, not a uint4 array: the array was kept in scratch memory, a store and a reload per chunk)
+  typedef uint32_t bfr_t __attribute__((ext_vector_type(4 * NT)));
+  auto bload = [&](int q) -> bfr_t {
+    bfr_t v;
 #pragma unroll
     for (int j = 0; j < NT; j++) {
-      const uint4 *src = d.bch_mfma + (size_t)q * PER + FEC_THREADS * j + tid;
-      uint4 *dst = bsm + buf * PER + FEC_THREADS * j + 64 * wave;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
-                                       (__attribute__((address_space(3))) void *)dst, 16, 0, 0);
+      const uint4 x = d.bch_mfma[(size_t)q * PER + FEC_THREADS * j + tid];
+      v[4 * j] = x.x;
+      v[4 * j + 1] = x.y;
+      v[4 * j + 2] = x.z;
+      v[4 * j + 3] = x.w;
     }
+    return v;
   };
-  for (int64_t u = units * k / per_slice; u < u1;) {
-    // one tile segment: chunks [q0, q1) of tile `tile`
+  auto bstore = [&](int buf, const bfr_t &v) {
+#pragma unroll
+    for (int j = 0; j < NT; j++)
+      bsm[buf * PER + FEC_THREADS * j + tid] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+  };
+
+  for (int64_t u = units * kq / per_slice; u < u1;) {
     const int tile = (int)(u / nc), q0 = qs0 + (int)(u % nc);
     const int q1 = q0 + (int)min((int64_t)(qs0 + nc - q0), u1 - u);
     u += q1 - q0;
-    const int row0 = tile * BCH_ROWS + wave * 32;
-    const int blk = row0 + (lane & 31);
-    const bool live = blk < io.nblocks;
-    const uint4 *msg = (const uint4 *)(io.out + (int64_t)(live ? blk : 0) * io.cw_stride) + (lane >> 5);
+    const int row0 = tile * BCH_ROWS + wave * 32, blk = row0 + (lane & 31);
+    BbchRow R{};
+    R.live = blk < io.nblocks;
+    R.tin = io.in;
+    if (R.live) {
+      const int64_t B = fec_block_of(io, blk, R.tin);
+      R.g = bb_geom(d, io, B);
+    }
+    R.row = io.out + (int64_t)(R.live ? blk : 0) * io.cw_stride;
+    const int npay = R.g.npay;
+    uint32_t crc = 0;   // NM: the CRC register at the start of this lane's row's current chunk (both lanes)
+    // ---- per-lane cursors at the first chunk this segment streams
+    if (!HEM) {
+      const int qa = q0 - BBCH_PRO;
+      const int64_t S = R.g.pos0 + 32 * qa + 16 * h - 10;   // >= pos0 - 208
+      R.rel = S - io.ts_base;
+      R.m = mod188(S + 376);
+      // the CRC prologue: the register through the BBCH_PRO chunks before q0 (no slots, no stores)
+      for (int q = qa; q < q0; q++) {
+        uint32_t pd[4] = {0u, 0u, 0u, 0u};
+        TsWin w = ts_fetch(R.tin, io.ts_len, R.rel);
+        if (R.live && w.edge) ts_slow(R.tin, io.ts_len, R.rel, w.w);
+        if (R.live) win_bytes(w.w, w.o, pd);
+        const int e = R.m == 0 ? 0 : 188 - R.m;
+        uint32_t slot;
+        crc = crc_chunk(tp, tq, pd, e, h, crc, slot);
+        R.rel += 32;
+        R.m += 32;
+        R.m -= R.m >= 188 ? 188 : 0;
+      }
+    } else {
+      // HEM: the tracked piece is chunk q0's, or chunk 1's where chunk 0's lane-0 piece holds the header
+      const int qa = (q0 == 0 && h == 0) ? 1 : q0;
+      const int64_t J = R.g.J0 + 32 * qa + 16 * h - 10;
+      R.r = (int)(J % 187);
+      R.sh = 188 * (J / 187) + 1 + R.r;
+    }
+    // ---- the piece of chunk q in four dwords; stores nothing
+    auto build = [&](int q, TsWin w, uint32_t *pd) {
+      const int P0 = 32 * q + 16 * h;
+      if (w.edge && R.live && P0 < L && P0 - 10 < npay && (P0 >= 10 || !HEM))
+        ts_slow(R.tin, io.ts_len, HEM ? R.sh - io.ts_base : R.rel, w.w);
+      uint32_t raw[4];
+      if (!HEM) {
+        win_bytes(w.w, w.o, raw);
+        const int e = R.m == 0 ? 0 : 188 - R.m;
+        uint32_t slot;
+        crc = crc_chunk(tp, tq, raw, e, h, crc, slot);
+#pragma unroll
+        for (int k = 0; k < 4; k++) pd[k] = raw[k];
+        const int j = P0 + e - 10;   // payload byte at the sync position
+        if (e < 16 && j >= 0 && j < npay && R.live) {
+          if (io.sync_err && byte_of(raw, e) != 0x47u) atomicAdd(io.sync_err, 1u);   // bbheader:703-705
+          set_byte(pd, e, slot);
+        }
+        R.rel += 32;
+        R.m += 32;
+        R.m -= R.m >= 188 ? 188 : 0;
+      } else if (P0 >= 10) {
+        // payload bytes with the sync byte before payload byte J' (J' mod 187 = 0) dropped: bytes e.. shift by one
+        uint32_t b1[4];
+        win_bytes(w.w, w.o, raw);
+        win_bytes(w.w, w.o + 1, b1);
+        const int es = 187 - R.r;   // the next packet's first payload byte is J + es (its sync byte before it)
+        const int e = es < 16 ? es : 16;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int t = min(max(e - 4 * k, 0), 4);
+          const uint32_t m = t >= 4 ? 0u : 0xFFFFFFFFu << (8 * t);   // bytes i >= e
+          pd[k] = (raw[k] & ~m) | (b1[k] & m);
+        }
+        // the sync byte consumed before payload byte J' = J + es (bbheader:675-677), counted here for es in
+        // [1, 16] (the window holds it: window byte o + es); J' = J itself was the previous piece's es = 16 (or
+        // the header piece's)
+        if (io.sync_err && R.live && es <= 16 && P0 - 10 + es < npay &&
+            (es < 16 ? byte_of(raw, es) : byte_of(b1, 15)) != 0x47u)
+          atomicAdd(io.sync_err, 1u);
+        R.sh += 32;
+        R.r += 32;
+        if (R.r >= 187) {
+          R.r -= 187;
+          R.sh += 1;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) pd[k] = 0u;
+      }
+      // the BBHEADER (bbheader:272-325): bytes 0 .. 7 = MATYPE, UPL, DFL, SYNC, SYNCD high (big-endian), byte 8 =
+      // SYNCD low, byte 9 = its CRC-8 (the register's LSB first)
+      if (P0 == 0) {
+        const uint32_t upl = HEM ? 0u : 188u * 8u, dfl = (uint32_t)(d.kbch - 80 - R.g.padding);
+        const uint32_t syncb = HEM ? 0u : 0x47u, syncd = R.g.count0 == 0 ? 0u : (uint32_t)(188 - R.g.count0) * 8u;
+        const uint64_t hw = ((uint64_t)(uint32_t)d.matype << 48) | ((uint64_t)upl << 32) | ((uint64_t)dfl << 16) |
+                            ((uint64_t)syncb << 8) | (uint64_t)(syncd >> 8);
+        uint32_t c = HEM ? 0x80u : 0u;
+#pragma unroll
+        for (int b = 0; b < 8; b++) c ^= hd[b * 256 + ((hw >> (56 - 8 * b)) & 0xFF)];
+        c ^= hd[8 * 256 + (syncd & 0xFF)];
+        pd[0] = __builtin_bswap32((uint32_t)(hw >> 32));
+        pd[1] = __builtin_bswap32((uint32_t)hw);
+        pd[2] = (pd[2] & 0xFFFF0000u) | (syncd & 0xFFu) | ((__builtin_bitreverse32(c) >> 24) << 8);
+        if (HEM) {   // payload bytes 0 .. 5 from the stream; the sync bytes before payload bytes J0 .. J0 + 6 (the
+                     // tracked pieces count from J0 + 7 on)
+#pragma unroll 1
+          for (int i = 10; i < 17; i++) {
+            const int64_t J = R.g.J0 + (i - 10);
+            if (i < 16) set_byte(pd, i, R.live && i - 10 < npay ? (uint32_t)R.tin[payload_pos(J, 1) - io.ts_base] : 0u);
+            if (io.sync_err && R.live && i - 10 < npay && J % 187 == 0 && R.tin[188 * (J / 187) - io.ts_base] != 0x47)
+              atomicAdd(io.sync_err, 1u);
+          }
+        }
+      }
+      // past the payload: the in-band type B field (first BBFRAME of an interleaving frame), then zeros
+      if (P0 + 16 > 10 + npay) {
+#pragma unroll 1
+        for (int i = max(0, 10 + npay - P0); i < 16; i++) {
+          const int k = P0 + i - 10 - npay;
+          set_byte(pd, i, R.g.padding && k < 13 ? (uint32_t)ibb[k] : 0u);
+        }
+      }
+      // BB scrambling: the piece's 16 PRBS bytes from LDS (the two halves of a wave read two addresses)
+      if (P0 < L) {
+        const uint4 pr = *(const uint4 *)(prb + P0);
+        pd[0] ^= pr.x;
+        pd[1] ^= pr.y;
+        pd[2] ^= pr.z;
+        pd[3] ^= pr.w;
+      }
+      if (!R.live) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) pd[k] = 0u;
+      }
+    };
+    // the window the piece of chunk q needs (requested a chunk ahead)
+    auto fetch = [&](int q) -> TsWin {   // every lane loads (dead rows from a safe address): no branch to merge
+      return ts_fetch(R.tin, io.ts_len, HEM ? R.sh - io.ts_base : R.rel);
+    };
+
     bch_v16f acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = bch_v16f{};
-    __syncthreads();   // the previous segment's epilogue has read its parity words out of buffer 0
-    stage(q0, 0);
-    uint4 a = live ? msg[2 * q0] : make_uint4(0u, 0u, 0u, 0u);
-    // every wave retires its own LDS-DMA before the barrier, so after it all slices have landed (the
-    // workgroup-scope fence of __syncthreads does not promise a vmcnt(0) on gfx950)
-    __builtin_amdgcn_s_waitcnt(BCH_WAIT_VMCNT0);
+    uint32_t a[4];
+    {
+      const bfr_t bs = bload(q0);
+      const TsWin w = fetch(q0);
+      build(q0, w, a);
+      __syncthreads();   // the previous segment's epilogue has read its parity words out of buffer 0
+      bstore(0, bs);
+    }
     __syncthreads();
     for (int q = q0; q < q1; q++) {
-      const int cur = (q - q0) & 1;
-      uint4 an = make_uint4(0u, 0u, 0u, 0u);
-      if (q + 1 < q1) {   // the other buffer was last read before the previous barrier
-        stage(q + 1, cur ^ 1);
-        if (live) an = msg[2 * (q + 1)];
-      }
+      const int cur = (q - q0) & 1, qn = min(q + 1, q1 - 1);
+      // the next chunk's B fragments and TS window, unconditionally (the last chunk's repeated, unused): an array
+      // assigned under a condition and kept across it is not promoted to registers
+      const bfr_t bs = bload(qn);
+      const TsWin wn = fetch(qn);
+      // this chunk's piece to the codeword row, after the next chunk's loads: vmcnt retires in order, so waiting
+      // for those loads (the build of q + 1, the B writes) does not drain this store.  Every lane stores (dead rows
+      // into the spare row nblocks of the buffer): a store the wave may branch around would make the compiler's
+      // wait for the B loads a vmcnt(0) that drains it.
+      const int P0 = 32 * q + 16 * h;
+      *(uint4 *)((R.live ? R.row : io.out + (int64_t)io.nblocks * io.cw_stride) + P0) = make_uint4(a[0], a[1], a[2], a[3]);
       const uint4 *bq = bsm + cur * PER;
-      // B fragments of K-step s + 1 requested before the MFMAs of step s (two steps' fragments live)
       uint4 bc[NT], bx[NT];
 #pragma unroll
       for (int t = 0; t < NT; t++) bc[t] = bq[t * 64 + lane];
@@ -842,9 +1113,7 @@ __global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(Fe
 #pragma unroll
           for (int t = 0; t < NT; t++) bx[t] = bq[((s + 1) * NT + t) * 64 + lane];
         }
-        // A fragment: dword e = bits e, e + 4, .. of the message word as fp4 nibbles 0x1 (0.5; the A
-        // scale 2^1 makes them 1.0): two VALU ops per dword
-        const uint32_t w = s == 0 ? a.x : s == 1 ? a.y : s == 2 ? a.z : a.w;
+        const uint32_t w = a[s];
         const bch_v8i A = {(int)(w & 0x11111111u), (int)((w >> 1) & 0x11111111u), (int)((w >> 2) & 0x11111111u),
                            (int)((w >> 3) & 0x11111111u), 0, 0, 0, 0};
 #pragma unroll
@@ -856,13 +1125,15 @@ __global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(Fe
 #pragma unroll
         for (int t = 0; t < NT; t++) bc[t] = bx[t];
       }
-      __builtin_amdgcn_s_waitcnt(BCH_WAIT_VMCNT0);   // chunk q + 1's DMA, as above
+      // the MFMAs stay here, before the next piece's build: left alone, the compiler sinks them below it and
+      // hoists every B-fragment read above it (all 4 K-steps' fragments live across the build: ~80 VGPRs)
+#pragma unroll
+      for (int t = 0; t < NT; t++) asm volatile("" : "+v"(acc[t]));
+      if (q + 1 < q1) build(q + 1, wn, a);
+      bstore(cur ^ 1, bs);   // the other buffer was last read before the previous barrier
       __syncthreads();
-      a = an;
     }
-    // partial parities: accumulator register r of lane l is block row (r & 3) + 8 (r >> 2) + 4 (l >> 5),
-    // parity column l & 31 of its tile; one ballot per (tile, register) gives 32 parities of two rows,
-    // bit c -> byte c / 8, bit 7 - c % 8 of the row's tile word (bswap o bitreverse)
+    // partial parities (as bch_gemm_kernel)
     uint32_t *pw = (uint32_t *)bsm + wave * 32 * BCH_PART_WORDS;   // after the loop's last barrier
 #pragma unroll
     for (int t = 0; t < NT; t++)
@@ -891,38 +1162,35 @@ __global__ __launch_bounds__(FEC_THREADS, BCH_WG_PER_CU) void bch_gemm_kernel(Fe
 // BBFRAME and BCH parity bytes from frame, then the LDPC parity rows cur (fec_ldpc), parity-interleaved
 // (byte m = byte m mod 45 of row m / 45) by byte-aligning two row words where the code has the parity
 // interleaver, bit by bit otherwise; zero past the codeword
-__device__ __forceinline__ uint32_t ldpc_out_word(const FecDev &d, const uint8_t *frame, const uint32_t *cur, int i) {
+// The rows come without the column-parity correction (fec_ldpc<.., false>): word w of every row is XORed with
+// Wv[w] here, where it is read, instead of by a read-modify-write pass over all q x 12 row words.
+__device__ __forceinline__ uint32_t ldpc_out_word(const FecDev &d, const uint8_t *frame, const uint32_t *cur,
+                                                  const uint32_t *Wv, int i) {
   const int NB = d.nbch >> 3, cwb = d.nldpc >> 3, q = d.q;
   auto parity_byte = [&](int m) -> uint32_t {
     if (d.parity_il) {
       const int a = m / 45, k = m - 45 * a;
-      return (cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu;
+      return ((cur[a * 12 + (k >> 2)] ^ Wv[k >> 2]) >> (24 - 8 * (k & 3))) & 0xFFu;
     }
     uint32_t v = 0;
     for (int e = 0; e < 8; e++) {
       const int j = 8 * m + e, a = j % q, c = j / q;
-      v |= ((cur[a * 12 + (c >> 5)] >> (31 - (c & 31))) & 1u) << (7 - e);
+      v |= (((cur[a * 12 + (c >> 5)] ^ Wv[c >> 5]) >> (31 - (c & 31))) & 1u) << (7 - e);
     }
     return v;
   };
   if (4 * i + 4 <= NB) return ((const uint32_t *)frame)[i];
   uint32_t v = 0;
   if (d.parity_il && 4 * i >= NB && 4 * i + 4 <= cwb) {
-    // four parity bytes m .. m + 3 = bytes k .. k + 3 of row a (m = 45 a + k; rows of 12 big-endian
-    // words): one byte align of two row words, or bytewise where they cross into row a + 1
-    int a = (4 * i - NB) / 45, k = 4 * i - NB - 45 * a;
-    if (k <= 41) {
-      const uint32_t w0 = cur[a * 12 + (k >> 2)], w1 = cur[a * 12 + (k >> 2) + 1];
-      return __builtin_bswap32((k & 3) ? __builtin_amdgcn_alignbyte(w0, w1, (uint32_t)(4 - (k & 3))) : w0);
-    }
-    for (int e = 0; e < 4; e++) {
-      v |= ((cur[a * 12 + (k >> 2)] >> (24 - 8 * (k & 3))) & 0xFFu) << (8 * e);
-      if (++k == 45) {
-        k = 0;
-        a++;
-      }
-    }
-    return v;
+    // four parity bytes m .. m + 3 = bytes k .. k + 3 of row a (m = 45 a + k; rows of 12 big-endian words,
+    // bytes 45 .. 47 zero): one byte align of two row words, plus, for k >= 42, the first 45 - k .. 3 bytes
+    // of row a + 1 shifted in (no per-byte loop: 3 of the 45 offsets cross a row, so nearly every wave has a
+    // lane there)
+    const int a = (4 * i - NB) / 45, k = 4 * i - NB - 45 * a, c = k >> 2;
+    const uint32_t w0 = cur[a * 12 + c] ^ Wv[c], w1 = c < 11 ? cur[a * 12 + c + 1] ^ Wv[c + 1] : 0u;
+    uint32_t x = (k & 3) ? __builtin_amdgcn_alignbyte(w0, w1, (uint32_t)(4 - (k & 3))) : w0;
+    if (k >= 42 && a + 1 < q) x |= (cur[(a + 1) * 12] ^ Wv[0]) >> (8 * (45 - k));
+    return __builtin_bswap32(x);
   }
   for (int e = 0; e < 4; e++) {
     const int bidx = 4 * i + e;
@@ -964,32 +1232,29 @@ static hipError_t fec_launch_persistent(const void *fn, int kind, int cap, const
 }
 
 template <int NT>
-static hipError_t bch_launch(const FecDev &d, const FecIO &io, hipStream_t s) {
-  const int lds = 2 * 4 * NT * 64 * 16;
-  hipError_t e = lds_limit((const void *)bch_gemm_kernel<NT>, lds);
+static hipError_t bbch_launch(const FecDev &d, const FecIO &io, hipStream_t s) {
+  const int lds = bbch_lds(NT);
+  const void *fn = d.hem ? (const void *)bbch_kernel<NT, true> : (const void *)bbch_kernel<NT, false>;
+  hipError_t e = lds_limit(fn, lds);
   if (e != hipSuccess) return e;
-  // persistent: BCH_WG_PER_CU workgroups per CU, a multiple of BCH_KS (slices by XCD)
-  const int per_slice = (fec_grid(1 << 30, BCH_WG_PER_CU) + BCH_KS - 1) / BCH_KS;
-  hipLaunchKernelGGL(bch_gemm_kernel<NT>, dim3(per_slice * BCH_KS), dim3(FEC_THREADS), lds, s, d, io);
-  return hipGetLastError();
+  // persistent: BBCH_WG_PER_CU workgroups per CU, a multiple of BCH_KS (slices by XCD)
+  const int per_slice = (fec_grid(1 << 30, BBCH_WG_PER_CU) + BCH_KS - 1) / BCH_KS;
+  void *args[2] = {(void *)&d, (void *)&io};
+  return hipLaunchKernel(fn, dim3(per_slice * BCH_KS), dim3(FEC_THREADS), args, lds, s);
 }
 
 static bool fec_chain_args_ok(const FecDev &d, const FecIO &io) {
-  return d.bch_mfma && io.bch_part && io.bch_part_blocks >= io.nblocks && d.bch_nt >= 4 && d.bch_nt <= 6 &&
+  return d.bch_mfma && io.bch_part && io.bch_part_blocks >= io.nblocks && d.bch_nt >= 4 && d.bch_nt <= 6 && io.ts_len >= 64 &&
          d.bch_nq >= 1 && d.bch_nq * 32 <= io.cw_stride;
 }
 
 hipError_t launch_fec(int mode, const FecDev &d, const FecIO &io, hipStream_t s) {
   if (io.nblocks <= 0) return hipSuccess;
   if (!fec_plan_fits(d)) return hipErrorInvalidValue;
-  hipError_t e;
   switch (mode) {
-    case FEC_TS_TO_BBFRAME:   // the chain: BB pass, BCH on the matrix cores (the LDPC follows in launch_ldpc_map)
+    case FEC_TS_TO_BBFRAME:   // the chain: BB + BCH on the matrix cores in one pass (the LDPC follows in launch_ldpc_map)
       if (!fec_chain_args_ok(d, io)) return hipErrorInvalidValue;
-      e = fec_launch_persistent((const void *)fec_bb_kernel, CARVE_BB, FEC_PASS_WG_PER_CU, d, io, s);
-      if (e == hipSuccess)
-        e = d.bch_nt == 6 ? bch_launch<6>(d, io, s) : d.bch_nt == 5 ? bch_launch<5>(d, io, s) : bch_launch<4>(d, io, s);
-      return e;
+      return d.bch_nt == 6 ? bbch_launch<6>(d, io, s) : d.bch_nt == 5 ? bbch_launch<5>(d, io, s) : bbch_launch<4>(d, io, s);
     case FEC_TS_TO_BITS:
       return fec_launch_persistent((const void *)fec_kernel<FEC_TS_TO_BITS>, CARVE_FUSED, FEC_WG_PER_CU, d, io, s);
     default:
@@ -1433,6 +1698,8 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void ldpc_map_kern
     for (int k = 0; k < FEC_PRE; k++)
       u[k] = tid + FEC_THREADS * k < nqi ? rowq[tid + FEC_THREADS * k] : make_uint4(0u, 0u, 0u, 0u);
     const uint32_t par = tid < (PB + 3) >> 2 ? fio.bch_part[(int64_t)blk * BCH_PART_WORDS + tid] : 0u;
+    // consumed: zero the words for the next run on this buffer slot (bbch_kernel XOR-accumulates into them)
+    if (tid < BCH_PART_WORDS) fio.bch_part[(int64_t)blk * BCH_PART_WORDS + tid] = 0u;
     for (int i = tid; i < fd.nent; i += FEC_THREADS) ents[i] = fd.ldpc_ent[i];
     for (int i = tid; i <= q; i += FEC_THREADS) rowp[i] = fd.ldpc_rowptr[i];
 #pragma unroll
@@ -1450,12 +1717,13 @@ __global__ __launch_bounds__(FEC_THREADS, FEC_PASS_WG_PER_CU) void ldpc_map_kern
                                                       ldpc_group_val(frame, g, k0 + 2), ldpc_group_val(frame, g, k0 + 3));
   }
   __syncthreads();
-  const uint32_t *cur = fec_ldpc<FEC_DW_PASS>(fd, D, ngroups, ents, rowp, Wv, tid);
+  // rows without the column-parity correction: ldpc_out_word applies Wv as it reads them
+  const uint32_t *cur = fec_ldpc<FEC_DW_PASS, false>(fd, D, ngroups, ents, rowp, Wv, tid);
   uint32_t w[LM_WORDS];
 #pragma unroll
   for (int k = 0; k < LM_WORDS; k++) {
     const int i = tid + FEC_THREADS * k;
-    w[k] = i < nw ? ldpc_out_word(fd, frame, cur, i) : 0u;
+    w[k] = i < nw ? ldpc_out_word(fd, frame, cur, Wv, i) : 0u;
   }
   if (fio.keep_cw) {   // test hook: the row as the three-pass FEC stored it (words below L / 4 hold the BBFRAME)
     uint32_t *dstw = (uint32_t *)row;
