@@ -731,69 +731,71 @@ typedef float bch_v16f __attribute__((ext_vector_type(16)));
 // lanes of a row hand the register to each other once per piece.  A tile segment starting at chunk q0 first
 // streams the CRC through the BBCH_PRO chunks (192 stream bytes) before it, so a sync position (one every 188
 // bytes) has restarted the register before the first slot it fills.
-constexpr int BBCH_WG_PER_CU = 2;   // ~210 VGPRs: two waves per SIMD
+constexpr int BBCH_THREADS = 256;   // 4 waves: a tile of 128 FEC blocks per workgroup, two workgroups per CU (~220
+constexpr int BBCH_ROWS = 128;      // VGPRs: two waves per SIMD)
+constexpr int BBCH_WG_PER_CU = 2;
 constexpr int BBCH_PRO = 6;         // CRC prologue chunks (6 x 32 >= 188 + 4)
 constexpr int BBCH_TAB = 16 * 256 * 2 + 9 * 256 + 16;   // T^k, T^-k, BBHEADER CRC per byte, in-band bytes
-constexpr int BBCH_PRBS = 32 * 216;                      // BB-scrambler PRBS bytes, whole chunks (>= 6750 B)
-static_assert(BBCH_TAB % 16 == 0, "the PRBS bytes after the tables are read as 16-byte units");
-__host__ __device__ constexpr int bbch_lds(int nt) { return 2 * 4 * nt * 64 * 16 + BBCH_TAB + BBCH_PRBS; }
+// the BBFRAME pieces of 4 chunks per row are staged in LDS (row stride 144 B: conflict-free 16-byte writes) and
+// stored as whole 128-byte lines: a wave's store instruction then writes 8 full lines instead of 32 rows x 32 B
+constexpr int BBCH_STG_STRIDE = 144;
+constexpr int BBCH_STG = BBCH_ROWS * BBCH_STG_STRIDE;
+static_assert(BBCH_TAB % 16 == 0, "the staging area after the tables is read as 16-byte units");
+__host__ __device__ constexpr int bbch_lds(int nt) { return 2 * 4 * nt * 64 * 16 + BBCH_TAB + BBCH_STG; }
 
-// 32 stream bytes: the 16-byte aligned unit holding tin + rel and the next; o = (tin + rel) & 15.  ts_fetch always
-// issues the two 16-byte loads (from a safe address inside [tin, tin + len) when the window is not: edge) and
-// returns without waiting for them; ts_slow redoes an edge window bytewise with zeros outside the buffer.  (A
-// fast / slow branch merged inside the fetch made the compiler wait for the loads right there, vmcnt(0).)
+// The stream bytes of a piece: a = bytes [rel, rel + 16) of the TS buffer, and for HEM also b = [rel + 1, rel + 17),
+// each one unaligned 16-byte load (gfx9 global loads need no alignment; the compiler emits one dwordx4 for an
+// align-1 pointer).  ts_fetch always issues the loads (from the buffer start when the bytes are not all inside
+// [tin, tin + len): edge) and returns without waiting for them; ts_slow redoes an edge piece bytewise with zeros
+// outside the buffer.  (A fast / slow branch merged inside the fetch made the compiler wait for the loads right
+// there, vmcnt(0).)
 struct TsWin {
-  uint32_t w[8];
-  uint32_t o;
+  uint32_t a[4], b[4];
   bool edge;
 };
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(1))) u32x4 *g4ptr;   // global, not flat: a flat load may read LDS, so
-typedef const __attribute__((address_space(1))) uint8_t *g1ptr;  // the compiler would wait for every LDS write first
+struct __attribute__((packed, aligned(1))) U32x4Unaligned {
+  u32x4 v;
+};
+typedef const __attribute__((address_space(1))) U32x4Unaligned *g4uptr;   // global, not flat: a flat load may read
+typedef const __attribute__((address_space(1))) uint8_t *g1ptr;          // LDS, so the compiler would wait for LDS
+template <bool HEM>
 __device__ __forceinline__ TsWin ts_fetch(const uint8_t *tin, int64_t len, int64_t rel) {
   TsWin r;
-  const uintptr_t t0 = (uintptr_t)tin, a = t0 + (uintptr_t)rel, a0 = a & ~(uintptr_t)15;
-  r.o = (uint32_t)(a & 15);
-  r.edge = !(a0 >= t0 && a0 + 32 <= t0 + (uintptr_t)len);
-  const uintptr_t src = r.edge ? (t0 + 15) & ~(uintptr_t)15 : a0;   // len >= 64 (fec_chain_args_ok)
-  const u32x4 x = *(g4ptr)src, y = *(g4ptr)(src + 16);
-  r.w[0] = x.x; r.w[1] = x.y; r.w[2] = x.z; r.w[3] = x.w;
-  r.w[4] = y.x; r.w[5] = y.y; r.w[6] = y.z; r.w[7] = y.w;
+  const uintptr_t t0 = (uintptr_t)tin, a = t0 + (uintptr_t)rel;
+  r.edge = !(rel >= 0 && rel + 17 <= len);
+  const uintptr_t src = r.edge ? t0 : a;   // len >= 64 (fec_chain_args_ok)
+  const u32x4 x = ((g4uptr)src)->v;
+#pragma unroll
+  for (int k = 0; k < 4; k++) r.a[k] = x[k];
+  if (HEM) {
+    const u32x4 y = ((g4uptr)(src + 1))->v;
+#pragma unroll
+    for (int k = 0; k < 4; k++) r.b[k] = y[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) r.b[k] = 0u;
+  }
   return r;
 }
-__device__ __forceinline__ void ts_slow(const uint8_t *tin, int64_t len, int64_t rel, uint32_t *w) {
-  const uintptr_t t0 = (uintptr_t)tin, a0 = (t0 + (uintptr_t)rel) & ~(uintptr_t)15;
-  uint64_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;   // named halves, not an indexed array (that would live in scratch)
+// bytes [rel, rel + 17) bytewise, zeros outside the buffer, into a (first 16) and b (from rel + 1)
+__device__ __forceinline__ void ts_slow(const uint8_t *tin, int64_t len, int64_t rel, TsWin &w) {
+  uint64_t q0 = 0, q1 = 0, q2 = 0;   // named halves, not an indexed array (that would live in scratch)
 #pragma unroll 1
-  for (int b = 0; b < 32; b++) {
-    const uintptr_t p = a0 + b;
-    const uint64_t v = p >= t0 && p < t0 + (uintptr_t)len ? (uint64_t)*(g1ptr)p << (8 * (b & 7)) : 0ull;
+  for (int b = 0; b < 17; b++) {
+    const int64_t p = rel + b;
+    const uint64_t v = p >= 0 && p < len ? (uint64_t)*(g1ptr)(tin + p) << (8 * (b & 7)) : 0ull;
     q0 |= b < 8 ? v : 0ull;
     q1 |= b >= 8 && b < 16 ? v : 0ull;
-    q2 |= b >= 16 && b < 24 ? v : 0ull;
-    q3 |= b >= 24 ? v : 0ull;
+    q2 |= b >= 16 ? v : 0ull;
   }
-  w[0] = (uint32_t)q0; w[1] = (uint32_t)(q0 >> 32); w[2] = (uint32_t)q1; w[3] = (uint32_t)(q1 >> 32);
-  w[4] = (uint32_t)q2; w[5] = (uint32_t)(q2 >> 32); w[6] = (uint32_t)q3; w[7] = (uint32_t)(q3 >> 32);
+  w.a[0] = (uint32_t)q0; w.a[1] = (uint32_t)(q0 >> 32); w.a[2] = (uint32_t)q1; w.a[3] = (uint32_t)(q1 >> 32);
+  const uint64_t r0 = (q0 >> 8) | (q1 << 56), r1 = (q1 >> 8) | (q2 << 56);
+  w.b[0] = (uint32_t)r0; w.b[1] = (uint32_t)(r0 >> 32); w.b[2] = (uint32_t)r1; w.b[3] = (uint32_t)(r1 >> 32);
 }
-// the 16 bytes at offset o (0 .. 16) of a window, as four little-endian dwords.  Selects between named 64-bit
-// values, never an indexed array: a select chain over an array's elements is folded into a dynamically
-// indexed load, which lives in scratch memory.
-__device__ __forceinline__ uint64_t fsh64(uint64_t lo, uint64_t hi, uint32_t ob) {   // bytes ob .. ob + 7 of hi:lo
-  return ob ? (lo >> (8 * ob)) | (hi << (64 - 8 * ob)) : lo;
-}
-__device__ __forceinline__ void win_bytes(const uint32_t *w, uint32_t o, uint32_t *d) {
-  const uint64_t q0 = ((uint64_t)w[1] << 32) | w[0], q1 = ((uint64_t)w[3] << 32) | w[2];
-  const uint64_t q2 = ((uint64_t)w[5] << 32) | w[4], q3 = ((uint64_t)w[7] << 32) | w[6];
-  const uint32_t qi = o >> 3, ob = o & 7;
-  const uint64_t A = qi == 0 ? q0 : qi == 1 ? q1 : q2, B = qi == 0 ? q1 : qi == 1 ? q2 : q3,
-                 C = qi == 0 ? q2 : qi == 1 ? q3 : 0ull;
-  const uint64_t lo = fsh64(A, B, ob), hi = fsh64(B, C, ob);
-  d[0] = (uint32_t)lo;
-  d[1] = (uint32_t)(lo >> 32);
-  d[2] = (uint32_t)hi;
-  d[3] = (uint32_t)(hi >> 32);
-}
+// byte i (dynamic) of four little-endian dwords, and its replacement; selects between named 64-bit values, never
+// an indexed array (a select chain over an array's elements is folded into a dynamically indexed load, which
+// lives in scratch memory)
 __device__ __forceinline__ uint32_t byte_of(const uint32_t *d, int i) {   // i dynamic, 0 .. 15
   const uint64_t lo = ((uint64_t)d[1] << 32) | d[0], hi = ((uint64_t)d[3] << 32) | d[2];
   return (uint32_t)(((i & 8) ? hi : lo) >> (8 * (i & 7))) & 0xFFu;
@@ -869,32 +871,31 @@ __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *tp, const uint8_t *
 }
 
 template <int NT, bool HEM>
-__global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDev d, FecIO io) {
+__global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDev d, FecIO io) {
   extern __shared__ __attribute__((aligned(16))) uint4 bsm[];
   constexpr int PER = 4 * NT * 64;                   // uint4 per chunk buffer
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int L = d.kbch >> 3, nprbs = (L + 3) >> 2;
-  const uint32_t *prbsw = (const uint32_t *)d.prbs;
+  const int L = d.kbch >> 3;
+  const uint4 *prbs16 = (const uint4 *)d.prbs;   // zero-padded to whole chunks (t2_plan FecPlan::prbs_bytes)
   uint8_t *tp = (uint8_t *)(bsm + 2 * PER), *tq = tp + 4096, *hd = tq + 4096, *ibb = hd + 9 * 256;
-  uint8_t *prb = tp + BBCH_TAB;   // 16-byte aligned: BBCH_TAB is a multiple of 16
+  uint8_t *stg = tp + BBCH_TAB;   // 16-byte aligned: BBCH_TAB is a multiple of 16
   // ---- tables, once per workgroup: T^1..T^16 and their inverses (NM), the BBHEADER CRC-8 per header byte
   // (add_crc8_bits :247-270: XOR of the per-bit contributions hcrc_bits, bit 8 b + j = bit 7 - j of byte b), the
   // in-band type B bytes (:327-355: 01, 65 zero bits, the TS rate in 27 bits, 10 zero bits)
-  if (!HEM && tid < 256) {
+  if (!HEM && tid < 256) {   // (BBCH_THREADS >= 256)
     uint32_t v = (uint32_t)tid;
     for (int k = 0; k < 16; k++) {
       v = d.crc8_tab[v];
       tp[k * 256 + tid] = (uint8_t)v;
     }
   }
-  for (int i = tid; i < 9 * 256; i += FEC_THREADS) {
+  for (int i = tid; i < 9 * 256; i += BBCH_THREADS) {
     const int b = i >> 8, x = i & 255;
     uint32_t v = 0;
     for (int j = 0; j < 8; j++)
       if ((x >> (7 - j)) & 1) v ^= d.hcrc_bits[8 * b + j];
     hd[i] = (uint8_t)v;
   }
-  for (int i = tid; i < BBCH_PRBS / 4; i += FEC_THREADS) ((uint32_t *)prb)[i] = i < nprbs ? prbsw[i] : 0u;
   if (tid < 13) {
     uint32_t v = tid == 0 ? 0x40u : 0u;
     for (int e = 0; e < 8; e++) {
@@ -910,7 +911,7 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
 
   const int slice = (int)blockIdx.x % BCH_KS, per_slice = (int)gridDim.x / BCH_KS, kq = (int)blockIdx.x / BCH_KS;
   const int qs0 = slice * d.bch_nq / BCH_KS, nc = (slice + 1) * d.bch_nq / BCH_KS - qs0;   // chunks per tile
-  const int64_t units = (int64_t)((io.nblocks + BCH_ROWS - 1) / BCH_ROWS) * nc;
+  const int64_t units = (int64_t)((io.nblocks + BBCH_ROWS - 1) / BBCH_ROWS) * nc;
   const int64_t u1 = units * (kq + 1) / per_slice;
   // chunk q's B fragments (t2_plan build_bch_mfma, lane-linear): loaded into registers a chunk ahead, written to
   // LDS buffer buf after the chunk's MFMAs.  Not LDS-DMA: the compiler cannot tell which LDS bytes a DMA writes,
@@ -918,12 +919,14 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
   // wait sat right after the next chunk's DMA, so its double buffer never overlapped a DMA with the MFMAs; here
   // vmcnt(0) would also drain the BBFRAME stores.)
   // (a vector value, not a uint4 array: the array was kept in scratch memory, a store and a reload per chunk)
-  typedef uint32_t bfr_t __attribute__((ext_vector_type(4 * NT)));
+  constexpr int BJ = (PER + BBCH_THREADS - 1) / BBCH_THREADS;   // uint4 per thread (the last one partial for odd NT)
+  typedef uint32_t bfr_t __attribute__((ext_vector_type(4 * BJ)));
   auto bload = [&](int q) -> bfr_t {
     bfr_t v;
 #pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const uint4 x = d.bch_mfma[(size_t)q * PER + FEC_THREADS * j + tid];
+    for (int j = 0; j < BJ; j++) {
+      const int i = BBCH_THREADS * j + tid;
+      const uint4 x = i < PER ? d.bch_mfma[(size_t)q * PER + i] : make_uint4(0u, 0u, 0u, 0u);
       v[4 * j] = x.x;
       v[4 * j + 1] = x.y;
       v[4 * j + 2] = x.z;
@@ -933,15 +936,17 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
   };
   auto bstore = [&](int buf, const bfr_t &v) {
 #pragma unroll
-    for (int j = 0; j < NT; j++)
-      bsm[buf * PER + FEC_THREADS * j + tid] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    for (int j = 0; j < BJ; j++) {
+      const int i = BBCH_THREADS * j + tid;
+      if (i < PER) bsm[buf * PER + i] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    }
   };
 
   for (int64_t u = units * kq / per_slice; u < u1;) {
     const int tile = (int)(u / nc), q0 = qs0 + (int)(u % nc);
     const int q1 = q0 + (int)min((int64_t)(qs0 + nc - q0), u1 - u);
     u += q1 - q0;
-    const int row0 = tile * BCH_ROWS + wave * 32, blk = row0 + (lane & 31);
+    const int row0 = tile * BBCH_ROWS + wave * 32, blk = row0 + (lane & 31);
     BbchRow R{};
     R.live = blk < io.nblocks;
     R.tin = io.in;
@@ -960,10 +965,11 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
       R.m = mod188(S + 376);
       // the CRC prologue: the register through the BBCH_PRO chunks before q0 (no slots, no stores)
       for (int q = qa; q < q0; q++) {
-        uint32_t pd[4] = {0u, 0u, 0u, 0u};
-        TsWin w = ts_fetch(R.tin, io.ts_len, R.rel);
-        if (R.live && w.edge) ts_slow(R.tin, io.ts_len, R.rel, w.w);
-        if (R.live) win_bytes(w.w, w.o, pd);
+        TsWin w = ts_fetch<false>(R.tin, io.ts_len, R.rel);
+        if (R.live && w.edge) ts_slow(R.tin, io.ts_len, R.rel, w);
+        uint32_t pd[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) pd[k] = R.live ? w.a[k] : 0u;
         const int e = R.m == 0 ? 0 : 188 - R.m;
         uint32_t slot;
         crc = crc_chunk(tp, tq, pd, e, h, crc, slot);
@@ -982,10 +988,11 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
     auto build = [&](int q, TsWin w, uint32_t *pd) {
       const int P0 = 32 * q + 16 * h;
       if (w.edge && R.live && P0 < L && P0 - 10 < npay && (P0 >= 10 || !HEM))
-        ts_slow(R.tin, io.ts_len, HEM ? R.sh - io.ts_base : R.rel, w.w);
+        ts_slow(R.tin, io.ts_len, HEM ? R.sh - io.ts_base : R.rel, w);
       uint32_t raw[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) raw[k] = w.a[k];
       if (!HEM) {
-        win_bytes(w.w, w.o, raw);
         const int e = R.m == 0 ? 0 : 188 - R.m;
         uint32_t slot;
         crc = crc_chunk(tp, tq, raw, e, h, crc, slot);
@@ -1001,9 +1008,7 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
         R.m -= R.m >= 188 ? 188 : 0;
       } else if (P0 >= 10) {
         // payload bytes with the sync byte before payload byte J' (J' mod 187 = 0) dropped: bytes e.. shift by one
-        uint32_t b1[4];
-        win_bytes(w.w, w.o, raw);
-        win_bytes(w.w, w.o + 1, b1);
+        const uint32_t *b1 = w.b;
         const int es = 187 - R.r;   // the next packet's first payload byte is J + es (its sync byte before it)
         const int e = es < 16 ? es : 16;
 #pragma unroll
@@ -1061,13 +1066,13 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
           set_byte(pd, i, R.g.padding && k < 13 ? (uint32_t)ibb[k] : 0u);
         }
       }
-      // BB scrambling: the piece's 16 PRBS bytes from LDS (the two halves of a wave read two addresses)
+      // BB scrambling: the chunk's 32 PRBS bytes as two uniform scalar loads, this half's 16
       if (P0 < L) {
-        const uint4 pr = *(const uint4 *)(prb + P0);
-        pd[0] ^= pr.x;
-        pd[1] ^= pr.y;
-        pd[2] ^= pr.z;
-        pd[3] ^= pr.w;
+        const uint4 p0 = kc(prbs16, 2 * q), p1 = kc(prbs16, 2 * q + 1);
+        pd[0] ^= h ? p1.x : p0.x;
+        pd[1] ^= h ? p1.y : p0.y;
+        pd[2] ^= h ? p1.z : p0.z;
+        pd[3] ^= h ? p1.w : p0.w;
       }
       if (!R.live) {
 #pragma unroll
@@ -1076,17 +1081,24 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
     };
     // the window the piece of chunk q needs (requested a chunk ahead)
     auto fetch = [&](int q) -> TsWin {   // every lane loads (dead rows from a safe address): no branch to merge
-      return ts_fetch(R.tin, io.ts_len, HEM ? R.sh - io.ts_base : R.rel);
+      return ts_fetch<HEM>(R.tin, io.ts_len, HEM ? R.sh - io.ts_base : R.rel);
+    };
+    // the piece one chunk after the cursor's (the cursor is at the next chunk to build)
+    auto fetch2 = [&]() -> TsWin {
+      const int64_t rel = HEM ? R.sh + 32 + (R.r + 32 >= 187 ? 1 : 0) - io.ts_base : R.rel + 32;
+      return ts_fetch<HEM>(R.tin, io.ts_len, rel);
     };
 
     bch_v16f acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = bch_v16f{};
     uint32_t a[4];
+    TsWin wn1;
     {
       const bfr_t bs = bload(q0);
       const TsWin w = fetch(q0);
       build(q0, w, a);
+      wn1 = fetch(q0 + 1);
       __syncthreads();   // the previous segment's epilogue has read its parity words out of buffer 0
       bstore(0, bs);
     }
@@ -1096,13 +1108,29 @@ __global__ __launch_bounds__(FEC_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecDe
       // the next chunk's B fragments and TS window, unconditionally (the last chunk's repeated, unused): an array
       // assigned under a condition and kept across it is not promoted to registers
       const bfr_t bs = bload(qn);
-      const TsWin wn = fetch(qn);
-      // this chunk's piece to the codeword row, after the next chunk's loads: vmcnt retires in order, so waiting
-      // for those loads (the build of q + 1, the B writes) does not drain this store.  Every lane stores (dead rows
-      // into the spare row nblocks of the buffer): a store the wave may branch around would make the compiler's
-      // wait for the B loads a vmcnt(0) that drains it.
-      const int P0 = 32 * q + 16 * h;
-      *(uint4 *)((R.live ? R.row : io.out + (int64_t)io.nblocks * io.cw_stride) + P0) = make_uint4(a[0], a[1], a[2], a[3]);
+      const TsWin wn = wn1;
+      wn1 = fetch2();
+      // this chunk's piece into the staging lines; after every 4th chunk (and the segment's last) each wave stores
+      // its 32 rows' staged bytes as whole 128-byte lines, after the next chunk's loads: vmcnt retires in order,
+      // so waiting for those loads (the build of q + 1, the B writes) does not drain these stores.  Every lane
+      // stores (dead rows into the spare row nblocks of the buffer, masked parts to their own bytes again): a store
+      // the wave may branch around would make the compiler's wait for the B loads a vmcnt(0) that drains it.
+      *(uint4 *)(stg + (wave * 32 + (lane & 31)) * BBCH_STG_STRIDE + (q & 3) * 32 + h * 16) =
+          make_uint4(a[0], a[1], a[2], a[3]);
+      if ((q & 3) == 3 || q == q1 - 1) {
+        const int qa = max(q0, q & ~3);   // the group's first chunk this segment wrote
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int r = 8 * k + (lane >> 3), part = lane & 7;   // 8 lanes per row, 16 bytes each
+          const uint4 v = *(const uint4 *)(stg + (wave * 32 + r) * BBCH_STG_STRIDE + part * 16);
+          const int c = (q & ~3) + (part >> 1);                  // the chunk of this part
+          const int rb = row0 + r;
+          const bool ok = rb < io.nblocks && c >= qa && c <= q && 32 * c + 16 * (part & 1) < L;
+          uint8_t *dst = (ok ? io.out + (int64_t)rb * io.cw_stride : io.out + (int64_t)io.nblocks * io.cw_stride) +
+                         (int64_t)32 * (q & ~3) + 16 * part;
+          *(uint4 *)dst = v;
+        }
+      }
       const uint4 *bq = bsm + cur * PER;
       uint4 bc[NT], bx[NT];
 #pragma unroll
@@ -1240,7 +1268,7 @@ static hipError_t bbch_launch(const FecDev &d, const FecIO &io, hipStream_t s) {
   // persistent: BBCH_WG_PER_CU workgroups per CU, a multiple of BCH_KS (slices by XCD)
   const int per_slice = (fec_grid(1 << 30, BBCH_WG_PER_CU) + BCH_KS - 1) / BCH_KS;
   void *args[2] = {(void *)&d, (void *)&io};
-  return hipLaunchKernel(fn, dim3(per_slice * BCH_KS), dim3(FEC_THREADS), args, lds, s);
+  return hipLaunchKernel(fn, dim3(per_slice * BCH_KS), dim3(BBCH_THREADS), args, lds, s);
 }
 
 static bool fec_chain_args_ok(const FecDev &d, const FecIO &io) {

@@ -193,7 +193,7 @@ int build_fec(int framesize, int rate, int constellation, FecPlan &fp) {
   // BB scrambler bytes (init_bb_randomiser, bbheader:357-369)
   std::vector<uint8_t> bits(fp.kbch);
   prbs15(bits.data(), fp.kbch);
-  fp.prbs_bytes.assign((L + 7) & ~3, 0);   // zero-padded: the FEC kernel reads whole words
+  fp.prbs_bytes.assign(((L + 31) & ~31) + 32, 0);   // zero-padded: the FEC kernels read whole words / chunks
   for (int i = 0; i < fp.kbch; i++) fp.prbs_bytes[i >> 3] |= bits[i] << (7 - (i & 7));
   // CRC-8 (x^8+x^7+x^6+x^4+x^2+1, MSB first) table and zero-byte extension tables
   fp.crc8_tab.assign(256, 0);
