@@ -104,7 +104,7 @@ def algorithmic_bytes(cfg, info):
 
 def minimal_bytes(cfg, info, iq_bytes=8):
     """per-frame bytes each kernel stage of the fused chain must move through HBM at least:
-    fec (BB + matrix-core BCH passes) reads the TS payload and writes the BBFRAMEs and their BCH parity;
+    fec (the fused BB + BCH pass) reads the TS payload and writes the BBFRAMEs and their BCH parity;
     map (the LDPC + map kernel) reads those and writes one 2-byte constellation index pair per cell;
     ofdm reads the pairs and writes the IQ samples (per-symbol tables are shared by every frame of a
     launch and are not counted)"""
@@ -120,9 +120,10 @@ def minimal_bytes(cfg, info, iq_bytes=8):
 
 
 KERNELS = ("fec", "map", "ofdm")
-# the kernels each stage launches per step: fec = the BB pass and the BCH matrix-core pass, map = the LDPC +
-# map kernel (LDPC parity, bit interleaver, cell + time interleaver; with the frames' L1-post workgroups)
-STAGE_KERNELS = {"fec": ("fec_bb", "bch_gemm"), "map": ("ldpc_map",), "ofdm": ("ofdm",)}
+# the kernels each stage launches per step: fec = the fused BB + BCH pass (BBFRAME from the TS, BCH parity on the
+# matrix cores), map = the LDPC + map kernel (LDPC parity, bit interleaver, cell + time interleaver; with the
+# frames' L1-post workgroups)
+STAGE_KERNELS = {"fec": ("bbch",), "map": ("ldpc_map",), "ofdm": ("ofdm",)}
 # rocprofv3 FETCH_SIZE / WRITE_SIZE (KiB) -> bytes.  gfx950 tallies 128-B read requests at 64 B
 # (MI355X_MICROARCH.md, HBM): x2 on the read side, calibrated per access width by tools/fetch_calib
 # (profiles/r2_fetch_calib.json); the kernels' dominant access widths: fec 16-B TS staging / BBFRAME
@@ -168,11 +169,10 @@ def pmc_passes(args):
                 for row in csv.DictReader(fh):
                     kn = row.get("Kernel_Name", "")
                     names.add(kn[:60])
-                    m = re.search(r"\b(fec_bb|bch_gemm|ldpc_map|fec|map|ofdm)(32)?_kernel", kn)
+                    m = re.search(r"\b(bbch|ldpc_map|fec|map|ofdm)(32)?_kernel", kn)
                     if m and row.get("Counter_Name") in ctrs:
                         vals.setdefault((m.group(1), row["Counter_Name"]), []).append(float(row["Counter_Value"]))
-        # per-launch means; the chain's FEC stage is two kernels launched once each per step (BB pass,
-        # BCH on the matrix cores): their means add up
+        # per-launch means (a stage with several kernels adds their means)
         for (kn, c), v in vals.items():
             k = next((st for st, kns in STAGE_KERNELS.items() if kn in kns), kn)
             res[k][c] = res[k].get(c, 0.0) + sum(v) / len(v)
@@ -911,7 +911,7 @@ def main():
             stages[name] = {"avg_launch_ms": avg_ms, "algorithmic_bytes_per_launch": ab[name] * B,
                             "achieved_GBs": ab[name] * B / t / 1e9 if t > 0 else None}
             kname = ("ofdm32_kernel" if name == "ofdm" and info["fft_size"] == 32768 else
-                     "fec_bb_kernel + bch_gemm_kernel" if name == "fec" else
+                     "bbch_kernel (BB + BCH)" if name == "fec" else
                      "ldpc_map_kernel (+ L1-post workgroups)" if name == "map" else name + "_kernel")
             e = {"kernel": kname, "bound": "hbm", "avg_launch_ms": avg_ms, "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "min_bytes_per_launch": mb[name] * B,
@@ -977,6 +977,28 @@ def main():
             "roofline": roof,
             "rooflines": rooflines,
         }
+        # chain level (per GPU): the bytes the step cannot avoid (TS payload in, IQ out) and the bytes the PMC
+        # passes counted (each stage's calibrated FETCH + WRITE per launch x its launches per step), over the
+        # pipelined step time; the serial kernel sum beside the pipelined step is what the slots overlap
+        from dvbt2ll.configs import KBCH
+        ts_in = info["fec_blocks_per_frame"] * ((KBCH[(cfg.framesize, cfg.rate)] - 80) // 8)
+        mand = B * (ts_in + 8 * per)
+        t_step = elapsed / args.steps
+        chain_f = {"mandatory_bytes_per_step": mand,
+                   "mandatory_bytes_frac": mand / t_step / 1e9 / HBM_PEAK_GBS,
+                   "serial_kernel_ms_per_step": sum(stage_ms) / args.steps,
+                   "pipelined_ms_per_step": t_step * 1e3,
+                   "overlap_ms_per_step": sum(stage_ms) / args.steps - t_step * 1e3,
+                   "note": "per GPU: mandatory = TS payload in + complex64 IQ out per step; pmc = calibrated "
+                           "FETCH_SIZE + WRITE_SIZE of every kernel launch of a step; fracs over ms_per_step and "
+                           "8 TB/s; overlap = serial kernel sum - pipelined step (profiles/r6_overlap_trace.txt)"}
+        if traffic is not None and all(rooflines[k].get("traffic") for k in KERNELS):
+            pb = sum(rooflines[k]["traffic"] * launches[i] / args.steps for i, k in enumerate(KERNELS))
+            chain_f["pmc_bytes_per_step"] = pb
+            chain_f["pmc_bytes_frac"] = pb / t_step / 1e9 / HBM_PEAK_GBS
+        else:
+            chain_f["pmc_bytes_per_step"] = None
+        out["chain"] = chain_f
         if sc16:
             out["iq_sc16_x0.2"] = {
                 "value": samples_total / sc16["elapsed"] / 1e6, "unit": "Msamples/s",

@@ -5,7 +5,7 @@
 //                division, chunk remainders moved by per-lane nibble tables) + LDPC as a
 //                quasi-cyclic array of 360-bit rotations with a bit-packed accumulate scan.
 //                Reference: lib/bbheaderbch_bb_impl.cc:648-742 (+ ldpc_calculate :625-646).
-//   chain FEC     fec_bb_kernel, bch_gemm_kernel (the BCH as a GF(2) product on the matrix cores),
+//   chain FEC     bbch_kernel (BBFRAME from the TS + the BCH as a GF(2) product on the matrix cores),
 //                 ldpc_map_kernel (LDPC, then the bit interleaver, cell and time interleaver of the
 //                 block's constellation index pairs; extra workgroups generate the L1-post cells).
 //                 Reference: bbheaderbch :625-742, lib/interleavermod_bc_impl.cc:270-704,
@@ -122,14 +122,14 @@ static hipError_t lds_limit(const void *fn, int bytes) {
 
 // ============================================================================ FEC kernels
 // Block API (bbheaderbch / ldpc blocks): fec_kernel<MODE>, one fused pass per FEC block (BBFRAME,
-// BCH on one wave, LDPC).  The chain runs three launches instead (launch_fec FEC_TS_TO_BBFRAME, then
+// BCH on one wave, LDPC).  The chain runs two launches per PLP instead (launch_fec FEC_TS_TO_BBFRAME, then
 // launch_ldpc_map):
-//   fec_bb_kernel    TS -> BBFRAME bytes in the codeword row (header, CRC-8 sync replacement,
-//                    in-band field, BB scrambling)
-//   bch_gemm_kernel  BCH parity of every block as a GF(2) matrix product on the matrix cores
-//                    (blocks x message bits x parity bits, fp4 0/1 operands, exact f32 sums, parity
-//                    = sum & 1), K split into slices (each XCD's L2 holds its slices' share of
-//                    the generator table) whose partial parities are XORed by the LDPC stage
+//   bbch_kernel      TS -> BBFRAME bytes (header, CRC-8 sync replacement, in-band field, BB scrambling)
+//                    built in registers and stored into the codeword row, and the BCH parity of every
+//                    block as a GF(2) matrix product on the matrix cores on the same pieces (blocks x
+//                    message bits x parity bits, fp4 0/1 operands, exact f32 sums, parity = sum & 1),
+//                    K split into slices (each XCD's L2 holds its slices' share of the generator
+//                    table) whose partial parities are XORed by the LDPC stage
 //   ldpc_map_kernel  info bytes + XOR of the partials -> LDPC parity -> interleaver-input codeword in
 //                    LDS -> the map (column twist, demux, cell + time interleaver), see below
 constexpr int FEC_THREADS = 256;
@@ -141,7 +141,6 @@ constexpr int FEC_WG_PER_CU = 7;        // fused kernel: resident workgroups per
 constexpr int FEC_PASS_WG_PER_CU = 8;   // chain BB pass, LDPC + map kernel (64-VGPR budget, 32 waves per CU)
 constexpr int FEC_BCH_JB = 2;           // nibble-table lookups in flight per lane in the BCH combine
 constexpr int FEC_LDPC_BYTES = 4 * (FEC_DW_PASS * 150 + 12 * 30); // max over codes of 64 ngroups + 48 q
-constexpr int BCH_ROWS = 128;           // bch_gemm_kernel: FEC blocks per workgroup (4 waves x 32)
 
 // dynamic LDS carve (bytes) of each FEC kernel kind: persistent tables (staged once; the
 // workgroups loop over FEC blocks), then the per-block area, reused by phase:
@@ -723,14 +722,14 @@ typedef float bch_v16f __attribute__((ext_vector_type(16)));
 // replaced by the CRC-8 of the packet before it (bbheader:701-719; HEM: the sync bytes dropped, :673-680), the
 // BBHEADER in chunk 0 (:272-325), the in-band type B field after the payload (:327-355), BB scrambling
 // (:694-696, 724-726).  The piece is stored to the block's codeword row (the LDPC + map kernel reads the BBFRAME
-// there) and multiplied as in bch_gemm_kernel.
+// there) and multiplied on the matrix cores.
 // Sync-slot CRC-8s are streamed.  The CRC register is linear, so a 16-byte piece b_0..b_15 moves it as
 // s' = T^16[s] ^ G, G = XOR_i T^(16-i)[b_i]: 16 independent lookups in the power tables T^1..T^16 (LDS).  A piece
-// with a sync position at offset e gives the slot T^e[s] ^ P_e (P_e = T^-(16-e)[X_e], X_e = XOR_{i<e} of G's
-// terms, through the inverse power tables) and restarts the register after it (s' = G ^ X_e ^ t_e).  The two
-// lanes of a row hand the register to each other once per piece.  A tile segment starting at chunk q0 first
-// streams the CRC through the BBCH_PRO chunks (192 stream bytes) before it, so a sync position (one every 188
-// bytes) has restarted the register before the first slot it fills.
+// with a sync position at offset e restarts the register after it (s' = the same lookups over bytes e+1..15) and
+// its slot is recovered from s' through the inverse power tables (crc_chunk).  The two lanes of a row hand the
+// register to each other once per piece.  A tile segment starting at chunk q0 first streams the CRC through the
+// BBCH_PRO chunks (192 stream bytes) before it, so a sync position (one every 188 bytes) has restarted the
+// register before the first slot it fills.
 constexpr int BBCH_THREADS = 256;   // 4 waves: a tile of 128 FEC blocks per workgroup, two workgroups per CU (~220
 constexpr int BBCH_ROWS = 128;      // VGPRs: two waves per SIMD)
 constexpr int BBCH_WG_PER_CU = 2;
@@ -824,48 +823,45 @@ struct BbchRow {
   bool live;
 };
 
-// NM CRC of one piece: its terms t_i = T^(16-i)[b_i] (16 independent lookups) folded into G, the prefix X_e of the
-// terms before the sync position e and t_e
-struct CrcTerms {
-  uint32_t g, x, te;
-};
-__device__ __forceinline__ CrcTerms crc_terms(const uint8_t *tp, const uint32_t *d, int e) {
-  uint32_t t[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) t[i] = tp[(15 - i) * 256 + ((d[i >> 2] >> (8 * (i & 3))) & 0xFFu)];
-  // prefixes as masked XORs (a select "i == e ? t[i]" would be folded into a dynamically indexed load)
-  CrcTerms c{0u, 0u, 0u};
-  uint32_t x1 = 0u;
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    c.g ^= t[i];
-    c.x ^= t[i] & (i < e ? 0xFFu : 0u);
-    x1 ^= t[i] & (i <= e ? 0xFFu : 0u);
-  }
-  c.te = c.x ^ x1;
-  return c;
+// NM CRC of a row's chunk (two 16-byte pieces, lane h = 0 then h = 1).  The register is linear: from s, a piece
+// b_0..b_15 leads to s_full = T^16[s] ^ G, G = XOR_i t_i, t_i = T^(16-i)[b_i] (16 independent lookups, T^k at
+// tp + (k-1) 256).  A piece with a sync position e < 16 restarts the register after it: A = XOR_{i>e} t_i = G ^ P,
+// P = XOR_{i<=e} t_i, and its slot value is the register before byte e: s_full = T^(16-e)[slot ^ b_e] ^ A, so
+// slot = T^-(16-e)[s_full ^ A] ^ b_e (T^-k at tq + (k-1) 256).  The terms are packed four to a dword, so G and
+// the prefix P under a per-lane bound e are two 128-bit XOR folds, one of them masked (a per-term masked prefix
+// cost ~4 VALU per term).
+__device__ __forceinline__ uint32_t fold8(uint64_t x) {
+  const uint32_t y = (uint32_t)x ^ (uint32_t)(x >> 32);
+  return (y ^ (y >> 8) ^ (y >> 16) ^ (y >> 24)) & 0xFFu;
 }
-// the register after the piece from s_in, and the sync slot's value where the piece holds a sync position (e < 16):
-// T^e[s_in] ^ P_e, P_e = T^-(16-e)[X_e] (T^k at tp + (k-1) 256, T^-k at tq + (k-1) 256); after the sync position
-// the register restarts from 0 and takes the terms after it, G ^ X_e ^ t_e
-__device__ __forceinline__ uint32_t crc_step(const uint8_t *tp, const uint8_t *tq, const CrcTerms &c, int e,
-                                             uint32_t s_in, uint32_t &slot) {
-  const bool sync = e < 16;
-  const uint32_t pe = e > 0 && sync ? (uint32_t)tq[(15 - e) * 256 + c.x] : 0u;
-  slot = (e > 0 && sync ? (uint32_t)tp[(e - 1) * 256 + s_in] : s_in) ^ pe;
-  return sync ? c.g ^ c.x ^ c.te : (uint32_t)tp[15 * 256 + s_in] ^ c.g;
-}
-// the row's register through one chunk: lane 0's piece, then lane 1's (two lane exchanges); slot: this lane's
-// sync slot value; returns the register at the next chunk (both lanes)
+// the register at the next chunk (both lanes) from s; slot: this lane's sync slot value (e < 16)
 __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *tp, const uint8_t *tq, const uint32_t *d, int e, int h,
                                               uint32_t s, uint32_t &slot) {
-  const CrcTerms c = crc_terms(tp, d, e);
-  uint32_t sl;
-  const uint32_t o0 = crc_step(tp, tq, c, e, s, sl);   // lane 0: the register after its piece
+  const bool sync = e < 16;
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    w[k] = 0u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int i = 4 * k + j;
+      w[k] |= (uint32_t)tp[(15 - i) * 256 + ((d[k] >> (8 * j)) & 0xFFu)] << (8 * j);
+    }
+  }
+  const uint64_t lo = ((uint64_t)w[1] << 32) | w[0], hi = ((uint64_t)w[3] << 32) | w[2];
+  const int kb = e + 1;   // terms 0 .. e (1 .. 17 of them)
+  const uint64_t mlo = kb >= 8 ? ~0ull : (1ull << (8 * kb)) - 1ull;
+  const uint64_t mhi = kb <= 8 ? 0ull : kb >= 16 ? ~0ull : (1ull << (8 * (kb - 8))) - 1ull;
+  const uint32_t g = fold8(lo ^ hi), A = g ^ fold8((lo & mlo) ^ (hi & mhi));
+  const uint32_t o0 = sync ? A : (uint32_t)tp[15 * 256 + s] ^ g;   // lane 0's register after its piece
   // every lane runs both exchanges (a lane exchange under a condition would read inactive lanes)
   const uint32_t y = (uint32_t)__shfl_xor((int)o0, 32);
   const uint32_t s_in = h ? y : s;
-  const uint32_t o1 = crc_step(tp, tq, c, e, s_in, slot);
+  const uint32_t sf = (uint32_t)tp[15 * 256 + s_in] ^ g;
+  const uint64_t dlo = ((uint64_t)d[1] << 32) | d[0], dhi = ((uint64_t)d[3] << 32) | d[2];
+  const uint32_t be = (uint32_t)(((e & 8) ? dhi : dlo) >> (8 * (e & 7))) & 0xFFu;
+  slot = (uint32_t)tq[(15 - min(e, 15)) * 256 + (sf ^ A)] ^ be;
+  const uint32_t o1 = sync ? A : sf;
   const uint32_t z = (uint32_t)__shfl_xor((int)o1, 32);
   return h ? o1 : z;
 }
@@ -1161,7 +1157,7 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
       bstore(cur ^ 1, bs);   // the other buffer was last read before the previous barrier
       __syncthreads();
     }
-    // partial parities (as bch_gemm_kernel)
+    // partial parities
     uint32_t *pw = (uint32_t *)bsm + wave * 32 * BCH_PART_WORDS;   // after the loop's last barrier
 #pragma unroll
     for (int t = 0; t < NT; t++)
@@ -1895,10 +1891,15 @@ __device__ __forceinline__ float2 tw_at(const float2 *tw, uint32_t i) {
   return cmulf(tw[128 + (i >> 7)], tw[i & 127]);
 }
 
-// v[r] *= w^(r * e) for r = 1..R-1 (R <= 32): one table lookup for w^e, the other powers by
-// products of depth <= 5 (w^2e, w^3e, w^4e, w^8e, w^12e, w^16e, then top * hi * lo)
+// v[r] *= w^(r * e) for r = 1..R-1 (R <= 16): w^e and w^(4e) from the table (tw_at), lo = w^(l e) and
+// hi = w^(4 h e) (l, h < 4) as their powers, w^(r e) = hi * lo.  (Round 5 built every power from w^e alone by
+// products of depth <= 5: a relative phase error d of w^e becomes k d in w^(k e), and that IFFT was 2.3-4.2 x
+// pocketfft's float32 error at 1K-16K; with the second base the powers are <= 3 and it is 1.4-1.8 x.  Six bases
+// (w^(k e), k = 1, 2, 3, 4, 8, 12, as the 32K kernel) measured 1.1-1.3 x but 2-4 % slower OFDM, from the extra
+// table reads.)
 template <int R>
 __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32_t e) {
+  static_assert(R <= 16, "bases for r < 16");
   if (R == 1) return;
   float2 lo[4], hi[4];
   lo[1] = tw_at(tw, e);
@@ -1906,18 +1907,15 @@ __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32
     lo[2] = cmulf(lo[1], lo[1]);
     lo[3] = cmulf(lo[2], lo[1]);
   }
-  if (R > 4) hi[1] = cmulf(lo[2], lo[2]);
+  if (R > 4) hi[1] = tw_at(tw, 4 * e);
   if (R > 8) {
     hi[2] = cmulf(hi[1], hi[1]);
     hi[3] = cmulf(hi[2], hi[1]);
   }
-  float2 top = make_float2(1.f, 0.f);
-  if (R > 16) top = cmulf(hi[2], hi[2]);                  // w^16e
 #pragma unroll
   for (int r = 1; r < R; r++) {
-    const int t = r >> 4, h = (r >> 2) & 3, l = r & 3;
-    float2 w = h == 0 ? lo[l] : (l == 0 ? hi[h] : cmulf(hi[h], lo[l]));
-    if (t) w = (h == 0 && l == 0) ? top : cmulf(top, w);
+    const int h = (r >> 2) & 3, l = r & 3;
+    const float2 w = h == 0 ? lo[l] : (l == 0 ? hi[h] : cmulf(hi[h], lo[l]));
     v[r] = cmulf(v[r], w);
   }
 }
