@@ -1089,23 +1089,26 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = bch_v16f{};
     uint32_t a[4];
-    TsWin wn1;
+    // the TS windows two chunks deep in two named slots, the chunk loop unrolled by two so that they trade roles
+    // (one slot and a copy at the loop's end: the copy waited for the window's load with vmcnt(0), draining the
+    // BBFRAME stores issued after it)
+    TsWin w0, w1;
     {
       const bfr_t bs = bload(q0);
-      const TsWin w = fetch(q0);
-      build(q0, w, a);
-      wn1 = fetch(q0 + 1);
+      w0 = fetch(q0);
+      build(q0, w0, a);
+      w1 = fetch(q0 + 1);
       __syncthreads();   // the previous segment's epilogue has read its parity words out of buffer 0
       bstore(0, bs);
     }
     __syncthreads();
-    for (int q = q0; q < q1; q++) {
+    // chunk q: wn holds the window of chunk q + 1 (loaded a chunk ago), wl receives chunk q + 2's
+    auto chunk = [&](int q, const TsWin &wn, TsWin &wl) {
       const int cur = (q - q0) & 1, qn = min(q + 1, q1 - 1);
       // the next chunk's B fragments and TS window, unconditionally (the last chunk's repeated, unused): an array
       // assigned under a condition and kept across it is not promoted to registers
       const bfr_t bs = bload(qn);
-      const TsWin wn = wn1;
-      wn1 = fetch2();
+      wl = fetch2();
       // this chunk's piece into the staging lines; after every 4th chunk (and the segment's last) each wave stores
       // its 32 rows' staged bytes as whole 128-byte lines, after the next chunk's loads: vmcnt retires in order,
       // so waiting for those loads (the build of q + 1, the B writes) does not drain these stores.  Every lane
@@ -1156,7 +1159,13 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
       if (q + 1 < q1) build(q + 1, wn, a);
       bstore(cur ^ 1, bs);   // the other buffer was last read before the previous barrier
       __syncthreads();
+    };
+    int q = q0;
+    for (; q + 1 < q1; q += 2) {
+      chunk(q, w1, w0);
+      chunk(q + 1, w0, w1);
     }
+    if (q < q1) chunk(q, w1, w0);
     // partial parities
     uint32_t *pw = (uint32_t *)bsm + wave * 32 * BCH_PART_WORDS;   // after the loop's last barrier
 #pragma unroll
