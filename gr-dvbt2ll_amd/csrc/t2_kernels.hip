@@ -734,7 +734,8 @@ constexpr int BBCH_THREADS = 256;   // 4 waves: a tile of 128 FEC blocks per wor
 constexpr int BBCH_ROWS = 128;      // VGPRs: two waves per SIMD)
 constexpr int BBCH_WG_PER_CU = 2;
 constexpr int BBCH_PRO = 6;         // CRC prologue chunks (6 x 32 >= 188 + 4)
-constexpr int BBCH_TAB = 16 * 256 * 2 + 9 * 256 + 16;   // T^k, T^-k, BBHEADER CRC per byte, in-band bytes
+// T^k, T^-k, BBHEADER CRC per byte, in-band bytes, the CRC prefix masks (17 x 16 bytes)
+constexpr int BBCH_TAB = 16 * 256 * 2 + 9 * 256 + 16 + 17 * 16;
 // the BBFRAME pieces of 4 chunks per row are staged in LDS (row stride 144 B: conflict-free 16-byte writes) and
 // stored as whole 128-byte lines: a wave's store instruction then writes 8 full lines instead of 32 rows x 32 B
 constexpr int BBCH_STG_STRIDE = 144;
@@ -750,6 +751,7 @@ __host__ __device__ constexpr int bbch_lds(int nt) { return 2 * 4 * nt * 64 * 16
 // there, vmcnt(0).)
 struct TsWin {
   uint32_t a[4], b[4];
+  uint32_t p[4];   // the chunk's BB-scrambling bytes for this lane's half (loaded with the window)
   bool edge;
 };
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -835,8 +837,8 @@ __device__ __forceinline__ uint32_t fold8(uint64_t x) {
   return (y ^ (y >> 8) ^ (y >> 16) ^ (y >> 24)) & 0xFFu;
 }
 // the register at the next chunk (both lanes) from s; slot: this lane's sync slot value (e < 16)
-__device__ __forceinline__ uint32_t crc_chunk(const uint8_t *tp, const uint8_t *tq, const uint32_t *d, int e, int h,
-                                              uint32_t s, uint32_t &slot) {
+__device__ __forceinline__ uint32_t crc_chunk(const uint8_t *tp, const uint8_t *tq, const uint4 *pmask, const uint32_t *d,
+                                              int e, int h, uint32_t s, uint32_t &slot) {
   const bool sync = e < 16;
   uint32_t w[4];
 #pragma unroll
@@ -849,10 +851,9 @@ __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *tp, const uint8_t *
     }
   }
   const uint64_t lo = ((uint64_t)w[1] << 32) | w[0], hi = ((uint64_t)w[3] << 32) | w[2];
-  const int kb = e + 1;   // terms 0 .. e (1 .. 17 of them)
-  const uint64_t mlo = kb >= 8 ? ~0ull : (1ull << (8 * kb)) - 1ull;
-  const uint64_t mhi = kb <= 8 ? 0ull : kb >= 16 ? ~0ull : (1ull << (8 * (kb - 8))) - 1ull;
-  const uint32_t g = fold8(lo ^ hi), A = g ^ fold8((lo & mlo) ^ (hi & mhi));
+  const uint4 m = pmask[min(e, 16)];   // terms 0 .. e
+  const uint32_t g = fold8(lo ^ hi);
+  const uint32_t A = g ^ fold8((((uint64_t)(w[1] & m.y) << 32) | (w[0] & m.x)) ^ (((uint64_t)(w[3] & m.w) << 32) | (w[2] & m.z)));
   const uint32_t o0 = sync ? A : (uint32_t)tp[15 * 256 + s] ^ g;   // lane 0's register after its piece
   // every lane runs both exchanges (a lane exchange under a condition would read inactive lanes)
   const uint32_t y = (uint32_t)__shfl_xor((int)o0, 32);
@@ -874,6 +875,7 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
   const int L = d.kbch >> 3;
   const uint4 *prbs16 = (const uint4 *)d.prbs;   // zero-padded to whole chunks (t2_plan FecPlan::prbs_bytes)
   uint8_t *tp = (uint8_t *)(bsm + 2 * PER), *tq = tp + 4096, *hd = tq + 4096, *ibb = hd + 9 * 256;
+  uint4 *pmask = (uint4 *)(ibb + 16);   // pmask[e]: bytes 0 .. e of a piece (e = 16: all)
   uint8_t *stg = tp + BBCH_TAB;   // 16-byte aligned: BBCH_TAB is a multiple of 16
   // ---- tables, once per workgroup: T^1..T^16 and their inverses (NM), the BBHEADER CRC-8 per header byte
   // (add_crc8_bits :247-270: XOR of the per-bit contributions hcrc_bits, bit 8 b + j = bit 7 - j of byte b), the
@@ -891,6 +893,10 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
     for (int j = 0; j < 8; j++)
       if ((x >> (7 - j)) & 1) v ^= d.hcrc_bits[8 * b + j];
     hd[i] = (uint8_t)v;
+  }
+  if (tid < 17 * 4) {   // prefix masks
+    const int e = tid >> 2, k = tid & 3, n = min(max(e + 1 - 4 * k, 0), 4);
+    ((uint32_t *)pmask)[tid] = n >= 4 ? 0xFFFFFFFFu : (1u << (8 * n)) - 1u;
   }
   if (tid < 13) {
     uint32_t v = tid == 0 ? 0x40u : 0u;
@@ -922,7 +928,8 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
 #pragma unroll
     for (int j = 0; j < BJ; j++) {
       const int i = BBCH_THREADS * j + tid;
-      const uint4 x = i < PER ? d.bch_mfma[(size_t)q * PER + i] : make_uint4(0u, 0u, 0u, 0u);
+      // (j + 1) THREADS <= PER: the compiler does not know tid < THREADS, and a condition it cannot fold makes a branch
+      const uint4 x = (BBCH_THREADS * (j + 1) <= PER || i < PER) ? d.bch_mfma[(size_t)q * PER + i] : make_uint4(0u, 0u, 0u, 0u);
       v[4 * j] = x.x;
       v[4 * j + 1] = x.y;
       v[4 * j + 2] = x.z;
@@ -934,7 +941,7 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
 #pragma unroll
     for (int j = 0; j < BJ; j++) {
       const int i = BBCH_THREADS * j + tid;
-      if (i < PER) bsm[buf * PER + i] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+      if (BBCH_THREADS * (j + 1) <= PER || i < PER) bsm[buf * PER + i] = make_uint4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
     }
   };
 
@@ -968,7 +975,7 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
         for (int k = 0; k < 4; k++) pd[k] = R.live ? w.a[k] : 0u;
         const int e = R.m == 0 ? 0 : 188 - R.m;
         uint32_t slot;
-        crc = crc_chunk(tp, tq, pd, e, h, crc, slot);
+        crc = crc_chunk(tp, tq, pmask, pd, e, h, crc, slot);
         R.rel += 32;
         R.m += 32;
         R.m -= R.m >= 188 ? 188 : 0;
@@ -991,7 +998,7 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
       if (!HEM) {
         const int e = R.m == 0 ? 0 : 188 - R.m;
         uint32_t slot;
-        crc = crc_chunk(tp, tq, raw, e, h, crc, slot);
+        crc = crc_chunk(tp, tq, pmask, raw, e, h, crc, slot);
 #pragma unroll
         for (int k = 0; k < 4; k++) pd[k] = raw[k];
         const int j = P0 + e - 10;   // payload byte at the sync position
@@ -1064,11 +1071,8 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
       }
       // BB scrambling: the chunk's 32 PRBS bytes as two uniform scalar loads, this half's 16
       if (P0 < L) {
-        const uint4 p0 = kc(prbs16, 2 * q), p1 = kc(prbs16, 2 * q + 1);
-        pd[0] ^= h ? p1.x : p0.x;
-        pd[1] ^= h ? p1.y : p0.y;
-        pd[2] ^= h ? p1.z : p0.z;
-        pd[3] ^= h ? p1.w : p0.w;
+#pragma unroll
+        for (int k = 0; k < 4; k++) pd[k] ^= w.p[k];
       }
       if (!R.live) {
 #pragma unroll
@@ -1076,13 +1080,24 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
       }
     };
     // the window the piece of chunk q needs (requested a chunk ahead)
+    // (the PRBS half as a vector load with the window: two uniform scalar loads and a per-lane select cost 12
+    // VALU per chunk; the chunk index is clamped to the segment, the windows past it are never built)
+    auto prbs = [&](int c, TsWin &w) {
+      const u32x4 v = ((const __attribute__((address_space(1))) u32x4 *)(uintptr_t)prbs16)[2 * min(c, q1 - 1) + h];
+#pragma unroll
+      for (int k = 0; k < 4; k++) w.p[k] = v[k];
+    };
     auto fetch = [&](int q) -> TsWin {   // every lane loads (dead rows from a safe address): no branch to merge
-      return ts_fetch<HEM>(R.tin, io.ts_len, HEM ? R.sh - io.ts_base : R.rel);
+      TsWin w = ts_fetch<HEM>(R.tin, io.ts_len, HEM ? R.sh - io.ts_base : R.rel);
+      prbs(q, w);
+      return w;
     };
     // the piece one chunk after the cursor's (the cursor is at the next chunk to build)
-    auto fetch2 = [&]() -> TsWin {
+    auto fetch2 = [&](int c) -> TsWin {   // c = the chunk after the cursor's
       const int64_t rel = HEM ? R.sh + 32 + (R.r + 32 >= 187 ? 1 : 0) - io.ts_base : R.rel + 32;
-      return ts_fetch<HEM>(R.tin, io.ts_len, rel);
+      TsWin w = ts_fetch<HEM>(R.tin, io.ts_len, rel);
+      prbs(c, w);
+      return w;
     };
 
     bch_v16f acc[NT];
@@ -1108,7 +1123,7 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
       // the next chunk's B fragments and TS window, unconditionally (the last chunk's repeated, unused): an array
       // assigned under a condition and kept across it is not promoted to registers
       const bfr_t bs = bload(qn);
-      wl = fetch2();
+      wl = fetch2(q + 2);
       // this chunk's piece into the staging lines; after every 4th chunk (and the segment's last) each wave stores
       // its 32 rows' staged bytes as whole 128-byte lines, after the next chunk's loads: vmcnt retires in order,
       // so waiting for those loads (the build of q + 1, the B writes) does not drain these stores.  Every lane
@@ -1125,7 +1140,8 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
           const int c = (q & ~3) + (part >> 1);                  // the chunk of this part
           const int rb = row0 + r;
           const bool ok = rb < io.nblocks && c >= qa && c <= q && 32 * c + 16 * (part & 1) < L;
-          uint8_t *dst = (ok ? io.out + (int64_t)rb * io.cw_stride : io.out + (int64_t)io.nblocks * io.cw_stride) +
+          // (row x stride as one 32 x 32 -> 64-bit multiply)
+          uint8_t *dst = io.out + (uint64_t)(uint32_t)(ok ? rb : io.nblocks) * (uint32_t)io.cw_stride +
                          (int64_t)32 * (q & ~3) + 16 * part;
           *(uint4 *)dst = v;
         }
