@@ -1143,7 +1143,9 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
           // (row x stride as one 32 x 32 -> 64-bit multiply)
           uint8_t *dst = io.out + (uint64_t)(uint32_t)(ok ? rb : io.nblocks) * (uint32_t)io.cw_stride +
                          (int64_t)32 * (q & ~3) + 16 * part;
-          *(uint4 *)dst = v;
+          // nontemporal: 1.2 GB of BBFRAME lines per 1280 cfg3 frames written through L2 evicted the generator-table
+          // slices (FETCH_SIZE 1.145e6 -> 0.897e6 KiB per launch with these stores; FEC 1.283 -> 1.254 ms)
+          __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4 *)dst);
         }
       }
       const uint4 *bq = bsm + cur * PER;
