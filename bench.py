@@ -403,10 +403,21 @@ def one_frame_latency(chain, ts_dev, ts_meta, iq, streams, per):
         chain.run_device(ts_dev[0].data_ptr(), base, n, first, 1, iq[0].data_ptr(), streams[0].cuda_stream)
         streams[0].synchronize()
         lat.append((time.perf_counter() - t0) * 1e3)
-    chain.set_graph(False)
     lat = sorted(lat[5:])
     latency["graph_median_ms"] = lat[len(lat) // 2]
     latency["graph_p90_ms"] = lat[int(len(lat) * 0.9)]
+    # a different frame each call: the graph's kernel arguments change, so every call rewrites its nodes
+    # (hipGraphExecKernelNodeSetParams); the calls above repeat one frame and skip that
+    lat = []
+    for k in range(25):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        chain.run_device(ts_dev[0].data_ptr(), base, n, first + k, 1, iq[0].data_ptr(), streams[0].cuda_stream)
+        streams[0].synchronize()
+        lat.append((time.perf_counter() - t0) * 1e3)
+    chain.set_graph(False)
+    lat = sorted(lat[5:])
+    latency["graph_new_args_median_ms"] = lat[len(lat) // 2]
     return latency
 
 

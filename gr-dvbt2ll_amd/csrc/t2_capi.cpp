@@ -694,6 +694,9 @@ struct ChainGraph {
   hipGraphExec_t exec[DVBT2LL_CHAIN_GRAPH_RING] = {};
   hipEvent_t done[DVBT2LL_CHAIN_GRAPH_RING] = {};
   bool used[DVBT2LL_CHAIN_GRAPH_RING] = {};
+  // the argument bytes each instantiation's kernel nodes hold: a call whose arguments match skips
+  // hipGraphExecKernelNodeSetParams (one per node, the bulk of a graph call's host time)
+  std::vector<std::vector<uint8_t>> held[DVBT2LL_CHAIN_GRAPH_RING];
   int next = 0;
   ~ChainGraph() {
     for (auto &e : exec)
@@ -928,11 +931,25 @@ struct dvbt2ll_chain {
     for (int k = 0; k < nplp; k++) args.push_back({&fd[k], &fi[k]});
     for (int k = 0; k < nplp; k++) args.push_back({&fd[k], &fi[k], &md[k], &mi[k], k ? &ld0 : &ld, k ? &li0 : &li});
     args.push_back({&od, &oi});
+    std::vector<std::vector<size_t>> sizes;
+    for (int k = 0; k < nplp; k++) sizes.push_back({sizeof(FecDev), sizeof(FecIO)});
+    for (int k = 0; k < nplp; k++)
+      sizes.push_back({sizeof(FecDev), sizeof(FecIO), sizeof(MapDev), sizeof(MapIO), sizeof(L1Dev), sizeof(L1IO)});
+    sizes.push_back({sizeof(OfdmDev), sizeof(OfdmIO)});
+    if (g->held[r].size() != (size_t)nk) g->held[r].assign(nk, {});
     for (int k = 0; k < nk; k++) {
+      std::vector<uint8_t> bytes;
+      for (size_t a = 0; a < args[k].size(); a++) {
+        const uint8_t *b = (const uint8_t *)args[k][a];
+        bytes.insert(bytes.end(), b, b + sizes[k][a]);
+      }
+      if (bytes == g->held[r][k]) continue;
       hipKernelNodeParams p = g->base[k];
       p.kernelParams = args[k].data();
       p.extra = nullptr;
+      g->held[r][k].clear();   // unknown until the update succeeds
       HIP_TRY(hipGraphExecKernelNodeSetParams(g->exec[r], g->node[k], &p));
+      g->held[r][k] = std::move(bytes);
     }
     HIP_TRY(hipGraphLaunch(g->exec[r], s));
     HIP_TRY(hipEventRecord(g->done[r], s));

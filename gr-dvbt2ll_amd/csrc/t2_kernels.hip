@@ -1453,14 +1453,35 @@ __device__ void map_cells(const MapDev &d, const uint32_t *cww, uint8_t *idx, in
 // idx[-1] holds a copy of idx[cs - 1] under rotation (the caller's), so idx[j - 1] needs no wrap: both
 // bytes are one address and two offsets, and a slot of another block is a flag bit of its entry rather
 // than a sentinel index (three VALU per slot instead of ~11).
-template <int NT, bool ROT>
-__device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
-                                int blk, int tid) {
+// rounds of MQ chunks per wave (chunk c0 + u NW + wv): one round for a normal block (<= 36 chunks; the
+// wave-uniform clamp repeats a chunk without storing it), its table loads all in flight together
+constexpr int MQ = 9;
+struct QuadRound {
+  uint2 e[MQ];
+  uint32_t qa[MQ];
+};
+template <int NT>
+__device__ __forceinline__ void map_quads_load(const MapDev &d, int blk, int tid, int c0, QuadRound &R) {
   const int r = blk % d.F;
-  uint16_t *dst = out_pairs + (int64_t)(blk / d.F) * frame_stride;   // frame data region
   const uint2 *qs = d.slot_quad + (int64_t)r * d.slot_stride;
   const uint16_t *qo = d.slot_qoff + (int64_t)r * d.slot_stride;
   const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
+  const int nqd = kc(d.slot_nq, r);
+  constexpr int NW = NT / 64;
+  const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
+#pragma unroll
+  for (int u = 0; u < MQ; u++) {
+    const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
+    R.e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
+    R.qa[u] = (uint32_t)kc(qb, c) + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
+  }
+}
+// pre: the first round's table entries, loaded by the caller earlier (map_quads_load with c0 = 0), or null
+template <int NT, bool ROT>
+__device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t frame_stride, const uint8_t *idx,
+                                int blk, int tid, const QuadRound *pre = nullptr) {
+  const int r = blk % d.F;
+  uint16_t *dst = out_pairs + (int64_t)(blk / d.F) * frame_stride;   // frame data region
   const int nqd = kc(d.slot_nq, r);
   constexpr int NW = NT / 64;
   const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
@@ -1470,36 +1491,30 @@ __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t fr
     const uint8_t *p = ib + j;
     return ROT ? (uint32_t)p[1] | ((uint32_t)p[0] << 8) : (uint32_t)p[1] * 0x101u;
   };
-  // rounds of MQ chunks per wave (chunk c0 + u NW + wv): one round for a normal block (<= 36 chunks; the
-  // wave-uniform clamp repeats a chunk without storing it), its table loads all in flight together
-  constexpr int MQ = 9;
   for (int c0 = 0; c0 < nch; c0 += MQ * NW) {
-    uint2 e[MQ];
-    uint32_t qa[MQ];
-#pragma unroll
-    for (int u = 0; u < MQ; u++) {
-      const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
-      e[u] = ld_off(qs, (uint32_t)(64 * c + lane) * 8u);
-      qa[u] = (uint32_t)kc(qb, c) + (uint32_t)ld_off(qo, (uint32_t)(64 * c + lane) * 2u);
-    }
+    QuadRound R;
+    if (c0 == 0 && pre)
+      R = *pre;
+    else
+      map_quads_load<NT>(d, blk, tid, c0, R);
     // every table load lands here, before the first store: a load the compiler sinks into a store
     // branch is waited for with vmcnt(0), which also drains every store issued before it
 #pragma unroll
-    for (int u = 0; u < MQ; u++) asm volatile("" : "+v"(e[u].x), "+v"(e[u].y), "+v"(qa[u]));
+    for (int u = 0; u < MQ; u++) asm volatile("" : "+v"(R.e[u].x), "+v"(R.e[u].y), "+v"(R.qa[u]));
 #pragma unroll
     for (int u = 0; u < MQ; u++) {
       const int c = c0 + u * NW + wv;
-      const uint32_t j0 = e[u].x & 0x7FFFu, j1 = (e[u].x >> 16) & 0x7FFFu, j2 = e[u].y & 0x7FFFu,
-                     j3 = (e[u].y >> 16) & 0x7FFFu;
+      const uint2 e = R.e[u];
+      const uint32_t j0 = e.x & 0x7FFFu, j1 = (e.x >> 16) & 0x7FFFu, j2 = e.y & 0x7FFFu, j3 = (e.y >> 16) & 0x7FFFu;
       const uint2 v = make_uint2(pair_of(j0) | (pair_of(j1) << 16), pair_of(j2) | (pair_of(j3) << 16));
       if (c < nch && 64 * c + lane < nqd) {
-        if (!((e[u].x | e[u].y) & 0x80008000u)) {
-          st_off((uint2 *)dst, qa[u] * 8u, v);
+        if (!((e.x | e.y) & 0x80008000u)) {
+          st_off((uint2 *)dst, R.qa[u] * 8u, v);
         } else {
-          if (!(e[u].x & 0x8000u)) st_off(dst, (4u * qa[u] + 0u) * 2u, (uint16_t)v.x);
-          if (!(e[u].x & 0x80000000u)) st_off(dst, (4u * qa[u] + 1u) * 2u, (uint16_t)(v.x >> 16));
-          if (!(e[u].y & 0x8000u)) st_off(dst, (4u * qa[u] + 2u) * 2u, (uint16_t)v.y);
-          if (!(e[u].y & 0x80000000u)) st_off(dst, (4u * qa[u] + 3u) * 2u, (uint16_t)(v.y >> 16));
+          if (!(e.x & 0x8000u)) st_off(dst, (4u * R.qa[u] + 0u) * 2u, (uint16_t)v.x);
+          if (!(e.x & 0x80000000u)) st_off(dst, (4u * R.qa[u] + 1u) * 2u, (uint16_t)(v.x >> 16));
+          if (!(e.y & 0x8000u)) st_off(dst, (4u * R.qa[u] + 2u) * 2u, (uint16_t)v.y);
+          if (!(e.y & 0x80000000u)) st_off(dst, (4u * R.qa[u] + 3u) * 2u, (uint16_t)(v.y >> 16));
         }
       }
     }
