@@ -319,6 +319,53 @@ def cpu_baseline(cfg, seconds, all_configs=True):
     return out
 
 
+def iq_accuracy(names):
+    """IQ error of one T2 frame per config against a float64 IFFT of the oracle's carriers, for the
+    GPU chain, the oracle's own float32 radix-2 IFFT (its restatement of pilotgen's FFTW path) and numpy's float32
+    pocketfft (an FFTW-class float FFT); max and mean over the frame's symbols of ||y - x|| / ||x||.  Runs only
+    with the CPU baseline (the oracle is the checker here, never the measured path)."""
+    import numpy as np
+    import torch
+    import dvbt2ll
+    from dvbt2ll.configs import CONFIGS, ts_for_frames
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib as O
+    import iq_check
+    res = {}
+    for name in names:
+        cfg = CONFIGS[name]
+        ch = dvbt2ll.Chain(cfg, max_frames=1)
+        ts, base = ts_for_frames(cfg, 0, 1)
+        ts_d = torch.from_numpy(ts).cuda()
+        iq_d = torch.empty((ch.iq_per_frame, 2), dtype=torch.float32, device="cuda")
+        ch.run_device(ts_d.data_ptr(), base, len(ts), 0, 1, iq_d.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        iq = iq_d.cpu().numpy().view(np.complex64).reshape(-1)
+        F = cfg.fecblocks
+        bits, _ = O.BB(*cfg.bb_args()).work(ts, F)
+        cells = O.IM(*cfg.im_args()).work(O.LDPC(cfg.framesize, cfg.rate).work(bits, F), F)
+        pg = O.PG(*cfg.pg_args())
+        mapped = O.FM(*cfg.fm_args()).work(cells)
+        car, oiq = pg.carriers(mapped), pg.work(mapped)
+        N, G, norm = pg.vlength, pg.guard, pg.normalization
+        g, o, f = [], [], []
+        for j in range(car.shape[0]):
+            lo, hi = 2048 + j * (N + G), 2048 + (j + 1) * (N + G)
+            want = iq_check.symbol_reference(car[j], N, G, norm)
+            g.append(iq_check.errors(iq[lo:hi], want)[0])
+            o.append(iq_check.errors(oiq[lo:hi], want)[0])
+            f.append(iq_check.f32_reference_errors(car[j], N, G, norm, want)[0])
+        res[name] = {"fft_size": N, "symbols": len(g), "gpu_rel_rms_max": max(g), "gpu_rel_rms_mean": sum(g) / len(g),
+                     "oracle_f32_radix2_rel_rms_max": max(o), "oracle_f32_radix2_rel_rms_mean": sum(o) / len(o),
+                     "pocketfft_f32_rel_rms_max": max(f), "pocketfft_f32_rel_rms_mean": sum(f) / len(f),
+                     "gpu_over_pocketfft_mean": (sum(g) / len(g)) / (sum(f) / len(f))}
+        del ch
+    return {"per_config": res,
+            "note": "rel RMS error of one T2 frame's symbols against a float64 IFFT of the oracle's carriers: the GPU "
+                    "chain, the oracle's own float32 radix-2 IFFT and numpy's float32 pocketfft (SURVEY 8(c) bound "
+                    "1e-6)"}
+
+
 def per_block_rate(cfg, frames=6, pinned=False):
     """the drop-in path GNU Radio would drive: the five blocks' C-ABI general_work calls on host
     buffers (pageable numpy, or page-locked with `pinned`: the DMA then reads / writes the caller's
@@ -1031,6 +1078,7 @@ def main():
             # the box's CPU share is 16 threads (os.cpu_count() reports the whole machine)
             threads = min(16, os.cpu_count() or 1)
             out["cpu_baseline"]["whole_host"] = cpu_host_replicas(cfg, args.cpu_seconds / 2, threads)
+            out["iq_accuracy"] = iq_accuracy(sorted({args.config, "cfg1", "cfg4"}))
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
