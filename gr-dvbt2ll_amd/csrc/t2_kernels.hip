@@ -1933,12 +1933,12 @@ __device__ __forceinline__ float2 tw_at(const float2 *tw, uint32_t i) {
   return cmulf(tw[128 + (i >> 7)], tw[i & 127]);
 }
 
-// v[r] *= w^(r * e) for r = 1..R-1 (R <= 16): w^e and w^(4e) from the table (tw_at), lo = w^(l e) and
-// hi = w^(4 h e) (l, h < 4) as their powers, w^(r e) = hi * lo.  (Round 5 built every power from w^e alone by
-// products of depth <= 5: a relative phase error d of w^e becomes k d in w^(k e), and that IFFT was 2.3-4.2 x
-// pocketfft's float32 error at 1K-16K; with the second base the powers are <= 3 and it is 1.4-1.8 x.  Six bases
-// (w^(k e), k = 1, 2, 3, 4, 8, 12, as the 32K kernel) measured 1.1-1.3 x but 2-4 % slower OFDM, from the extra
-// table reads.)
+// v[r] *= w^(r * e) for r = 1..R-1 (R <= 16): w^e, w^(4e) and (R = 16) w^(8e) from the table (tw_at), the
+// other lo = w^(l e) and hi = w^(4 h e) (l, h < 4) as products of those, w^(r e) = hi * lo.  (Round 5 built every
+// power from w^e alone by products of depth <= 5: a relative phase error d of w^e becomes k d in w^(k e), and
+// that IFFT was 2.3-4.2 x pocketfft's float32 error at 1K-16K; with these bases it is 1.3-1.6 x on random
+// symbols.  Six bases (w^(k e), k = 1, 2, 3, 4, 8, 12, as the 32K kernel) measured 1.1-1.3 x but 2-4 % slower
+// OFDM, from the extra table reads.)
 template <int R>
 __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32_t e) {
   static_assert(R <= 16, "bases for r < 16");
@@ -1951,7 +1951,7 @@ __device__ __forceinline__ void twiddle_unit(float2 *v, const float2 *tw, uint32
   }
   if (R > 4) hi[1] = tw_at(tw, 4 * e);
   if (R > 8) {
-    hi[2] = cmulf(hi[1], hi[1]);
+    hi[2] = tw_at(tw, 8 * e);
     hi[3] = cmulf(hi[2], hi[1]);
   }
 #pragma unroll

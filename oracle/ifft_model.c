@@ -12,7 +12,7 @@
  *   a + i b, a - i b (a.x - b.y, a.y + b.x), (a.x + b.y, a.y - b.x)
  *   in-register DFT  bit reversal, then radix-2 stages with the kCos32 / kSin32 constants (Dft<R>)
  *   N <= 16K         Stockham passes 16 x 16 x {4, 8, 16, 16 x 2, 16 x 4} (FftPlan), twiddles
- *                    w^(r e) from the table bases w^e, w^(4e) (twiddle_unit)
+ *                    w^(r e) from the table bases w^e, w^(4e), w^(8e) (twiddle_unit)
  *   32K              32 x 32 x 32 with the seven-lookup twiddle bases (o32_fft, o32_twiddle)
  *   store            (y * norm) * gain, then (sc16) saturate(rint(x * 32767))
  * Built with -ffp-contract=off: every product is rounded before the add unless fmaf says so.
@@ -97,8 +97,8 @@ static void dft(c32 *x, int R) {
 /* two-level table lookup w^i = hi[i >> 7] * lo[i & 127] (tw_at) */
 static c32 tw_at(const c32 *tw, uint32_t i) { return cmulf(tw[128 + (i >> 7)], tw[i & 127]); }
 
-/* twiddle_unit<R> (R <= 16): v[r] *= w^(r e); bases w^e and w^(4e) from the table, lo = w^(l e), hi = w^(4 h e)
- * as their powers (l, h < 4), w^(r e) = hi * lo */
+/* twiddle_unit<R> (R <= 16): v[r] *= w^(r e); bases w^e, w^(4e) and (R = 16) w^(8e) from the table, the other
+ * lo = w^(l e), hi = w^(4 h e) (l, h < 4) as products of those, w^(r e) = hi * lo */
 static void twiddle_unit(c32 *v, int R, const c32 *tw, uint32_t e) {
   c32 lo[4], hi[4];
   lo[1] = tw_at(tw, e);
@@ -108,7 +108,7 @@ static void twiddle_unit(c32 *v, int R, const c32 *tw, uint32_t e) {
   }
   if (R > 4) hi[1] = tw_at(tw, 4 * e);
   if (R > 8) {
-    hi[2] = cmulf(hi[1], hi[1]);
+    hi[2] = tw_at(tw, 8 * e);
     hi[3] = cmulf(hi[2], hi[1]);
   }
   for (int r = 1; r < R; r++) {
