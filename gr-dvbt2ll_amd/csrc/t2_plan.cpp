@@ -577,6 +577,9 @@ int build_frame_mplp(const FmParams &p, const std::vector<PlpParams> &plps_in, F
     pl.FF = q.first_frame;
     fp.ncls = std::lcm(fp.ncls, pl.I);
     pl.S_if = pl.cs * pl.F;
+    // TIME_IL_TYPE 1: the TI block's output cells, in order, split into P_I equal runs [i S, (i + 1) S), run i in
+    // the i-th T2 frame the PLP appears in (EN 302 755 6.5: "one TI-block ... mapped to P_I T2-frames"; the
+    // reference has TIME_IL_TYPE 0 only, so this reading is shared by the planner and the oracle: PARITY UNPINNED)
     pl.S = pl.S_if / pl.P;
     pl.type2 = q.plp_type == 2;
     pl.in_off = fp.S_in;
@@ -822,7 +825,10 @@ std::vector<uint8_t> l1post_signal(const FmParams &p, const FramePlan &fp, int f
   b.put((uint64_t)frame_idx, 8); b.put((uint64_t)fc.ssi, 22); b.put((uint64_t)fc.t2start, 22); b.put(0, 8);
   b.put(0, 3); b.put(resv ? 0xff : 0, 8);
   for (int k = 0; k < fp.nplp; k++) {
-    // PLP_ID, PLP_START, PLP_NUM_BLOCKS (both 0 for a PLP absent from this T2 frame)
+    // PLP_ID, PLP_START, PLP_NUM_BLOCKS (EN 302 755 7.2.3.2, L1-post dynamic); both 0 for a PLP absent from this
+    // T2 frame (FRAME_INTERVAL > 1: it carries no cells here).  The reference signals one PLP in every frame, so
+    // this value is the planner's and the oracle's shared reading: PARITY UNPINNED
+    // (tests/test_cpu_ti_kat.py KAT_B holds the hand-derived bit strings)
     b.put((uint64_t)k, 8); b.put(fc.present[k] ? (uint64_t)fc.start[k] : 0, 22);
     b.put(fc.present[k] ? (uint64_t)fp.plp[k].F : 0, 10);
     b.put(resv ? 0xff : 0, 8);
