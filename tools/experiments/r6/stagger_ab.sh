@@ -1,5 +1,6 @@
 #!/bin/bash
-# same-box A/B of the staggered slots (env DVBT2LL_STAGGER) on the default bench, two rounds
+# same-box A/B of the staggered slots (env DVBT2LL_STAGGER, read by an experiment build of t2_capi.cpp that was
+# reverted: profiles/r6_overlap_trace.txt) on the default bench, two rounds
 set -o pipefail
 cd "$(dirname "$0")" 2>/dev/null; cd $GRAFT_REPO_ROOT
 O=gpurun_out/r6x; mkdir -p $O
