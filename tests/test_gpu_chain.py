@@ -218,6 +218,31 @@ def test_chain_graph_mode(gpu, name):
     np.testing.assert_array_equal(ch.run(6, 1), ref.run(6, 1))
 
 
+@pytest.mark.parametrize("name", ["cfg1", "cfg3"])
+def test_chain_graph_reused_buffers(gpu, name):
+    """graph mode with the caller's device buffers reused: a ring instantiation whose held kernel arguments
+    equal a call's skips the node re-arms (t2_capi.cpp graph_launch); calls that repeat a frame and calls
+    that change it, cycling the ring (4 instantiations) on one slot, each give the direct launch's IQ"""
+    import torch
+    cfg = CONFIGS[name]
+    ts, base = ts_for_frames(cfg, 0, 4)
+    ts_d = torch.from_numpy(ts).cuda()
+    ch = dvbt2ll.Chain(cfg, max_frames=1)
+    iq_d = torch.empty((ch.iq_per_frame, 2), dtype=torch.float32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run(frame):
+        ch.run_device(ts_d.data_ptr(), base, len(ts), frame, 1, iq_d.data_ptr(), st)
+        torch.cuda.synchronize()
+        return iq_d.cpu().numpy().copy()
+
+    want = {f: run(f) for f in range(4)}      # direct launches
+    ch.set_graph(True)
+    for k, f in enumerate((0, 0, 1, 0, 1, 1, 2, 0, 0, 0, 0, 0, 3, 3, 0)):
+        np.testing.assert_array_equal(run(f).view(np.uint32), want[f].view(np.uint32), err_msg="call %d frame %d" % (k, f))
+    ch.set_graph(False)
+
+
 def _stream_batch(cfg, S, first, B, graph=False, sc16=False):
     """S independent TS streams (seeds 1..S) in one dvbt2ll_chain_run_streams launch; returns the
     per-stream IQ and a single-stream reference handle's IQ of each stream's own TS"""
