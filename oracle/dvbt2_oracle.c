@@ -347,26 +347,71 @@ int orc_bb_work(orc_bb *h, int nout, const uint8_t *in, uint8_t *out, int *consu
 /* ========================================================================= */
 /* LDPC                                                                      */
 /* ========================================================================= */
-struct orc_ldpc { const t2_ldpc_code_t *c; int nbch, nldpc; };
+/* The block restates ldpc_calculate in its gather form (bbheader:625-646): per parity bit the XOR of the info
+ * bits listed for it (the reference's ldpc_lut, built by ldpc_lookup_generate :533-598 from the same address
+ * tables), then the accumulate.  The lists are built once per handle from the scatter form of ldpc_encode, so
+ * both forms give the same bits (the L1 codes keep ldpc_encode).  The gather form also prices the CPU baseline
+ * like the reference: one pass over the edge lists per block, no modulo per edge. */
+struct orc_ldpc { const t2_ldpc_code_t *c; int nbch, nldpc; int *lut_off, *lut; };
 
 orc_ldpc *orc_ldpc_create(int framesize, int rate) {
   fec_par fp;
   if (fec_params(framesize, rate, &fp)) return NULL;
   orc_ldpc *h = (orc_ldpc *)calloc(1, sizeof(orc_ldpc));
+  if (!h) return NULL;
   h->c = ldpc_code(framesize == FECFRAME_NORMAL, rate);
   h->nbch = fp.nbch;
   h->nldpc = framesize == FECFRAME_NORMAL ? FRAME_SIZE_NORMAL : FRAME_SIZE_SHORT;
+  const t2_ldpc_code_t *c = h->c;
+  const int pbits = h->nldpc - h->nbch;
+  h->lut_off = (int *)calloc((size_t)pbits + 1, sizeof(int));
+  if (!h->lut_off) { free(h); return NULL; }
+  /* two passes over the scatter form: count each parity bit's edges, then fill them in info-bit order */
+  for (int pass = 0; pass < 2; pass++) {
+    int *fill = NULL;
+    if (pass == 1) {
+      for (int i = 0; i < pbits; i++) h->lut_off[i + 1] += h->lut_off[i];
+      h->lut = (int *)malloc(sizeof(int) * (size_t)(h->lut_off[pbits] ? h->lut_off[pbits] : 1));
+      fill = (int *)malloc(sizeof(int) * (size_t)pbits);
+      if (!h->lut || !fill) { free(fill); orc_ldpc_destroy(h); return NULL; }
+      memcpy(fill, h->lut_off, sizeof(int) * (size_t)pbits);
+    }
+    int im = 0, off = c->addr_off;
+    for (int row = 0; row < c->nrows; row++) {
+      const int cnt = T2_LDPC_ROWLEN[c->row_off + row];
+      for (int n = 0; n < 360; n++, im++)
+        for (int col = 0; col < cnt; col++) {
+          const int x = (T2_LDPC_ADDR[off + col] + n * c->q) % pbits;
+          if (pass == 0) h->lut_off[x + 1]++;
+          else h->lut[fill[x]++] = im;
+        }
+      off += cnt;
+    }
+    free(fill);
+  }
   return h;
 }
 int orc_ldpc_work(orc_ldpc *h, int nblocks, const uint8_t *in, uint8_t *out) {
+  const int pbits = h->nldpc - h->nbch;
   for (int b = 0; b < nblocks; b++) {
     uint8_t *cw = out + (size_t)b * h->nldpc;
     memcpy(cw, in + (size_t)b * h->nbch, (size_t)h->nbch);
-    ldpc_encode(h->c, h->nbch, h->nldpc, cw);
+    uint8_t *p = cw + h->nbch;
+    for (int i = 0; i < pbits; i++) {
+      uint8_t v = 0;
+      for (int e = h->lut_off[i]; e < h->lut_off[i + 1]; e++) v ^= cw[h->lut[e]];
+      p[i] = v;
+    }
+    for (int j = 1; j < pbits; j++) p[j] ^= p[j - 1];
   }
   return nblocks * h->nldpc;
 }
-void orc_ldpc_destroy(orc_ldpc *h) { free(h); }
+void orc_ldpc_destroy(orc_ldpc *h) {
+  if (!h) return;
+  free(h->lut_off);
+  free(h->lut);
+  free(h);
+}
 
 /* ========================================================================= */
 /* interleavermod_bc                                                          */
