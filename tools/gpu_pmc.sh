@@ -1,12 +1,12 @@
 # PMC counter passes over bench.py --pmc-child (one rocprofv3 run per counter set, each time-limited)
-#   bash tools/gpu_pmc.sh <tag> "<set1>" "<set2>" ...
+#   [PMC_ARGS="--config cfg4"] bash tools/gpu_pmc.sh <tag> "<set1>" "<set2>" ...
 set -o pipefail
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 TAG=$1; shift
 for set in "$@"; do
   t=$(echo $set | tr ' ' '_' | cut -c1-40)
-  timeout -s KILL 120 rocprofv3 --pmc $set -T -f csv -d gpurun_out/prof/pmc_${TAG}_$t -o pmc -- python3 bench.py --pmc-child --no-sc16 --steps 2 --warmup 1 > /dev/null 2> gpurun_out/prof/pmc_${TAG}_$t.err
+  timeout -s KILL 120 rocprofv3 --pmc $set -T -f csv -d gpurun_out/prof/pmc_${TAG}_$t -o pmc -- python3 bench.py --pmc-child $PMC_ARGS --no-sc16 --steps 2 --warmup 1 > /dev/null 2> gpurun_out/prof/pmc_${TAG}_$t.err
   rc=$?; echo "PMC $t EXIT $rc"
   [ $rc = 0 ] || exit $rc
 done
