@@ -8,7 +8,8 @@ cd "$(dirname "$0")/.."
 make -s -C oracle asan
 make -s -C gr-dvbt2ll_amd/csrc asan
 export DVBT2LL_SANITIZED=1
-export LD_PRELOAD="$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)"
+# the sanitizer runtimes first, anything already preloaded kept after them
+export LD_PRELOAD="$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)${LD_PRELOAD:+:$LD_PRELOAD}"
 export ASAN_OPTIONS=detect_leaks=0:halt_on_error=1:abort_on_error=1
 export UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1
 args=("$@")
