@@ -1158,13 +1158,16 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
 #pragma unroll
           for (int t = 0; t < NT; t++) bx[t] = bq[((s + 1) * NT + t) * 64 + lane];
         }
+        // the message bits in place where fp4 allows (dword d = bits d of each nibble: 0.5, 1.0, 2.0; bit 3 is
+        // the sign, so d = 3 moves down one), B's set entries 2.0, 1.0, 0.5, 0.5 (t2_plan build_bch_mfma): five
+        // VALU per K-step instead of seven
         const uint32_t w = a[s];
-        const bch_v8i A = {(int)(w & 0x11111111u), (int)((w >> 1) & 0x11111111u), (int)((w >> 2) & 0x11111111u),
-                           (int)((w >> 3) & 0x11111111u), 0, 0, 0, 0};
+        const bch_v8i A = {(int)(w & 0x11111111u), (int)(w & 0x22222222u), (int)(w & 0x44444444u),
+                           (int)((w >> 1) & 0x44444444u), 0, 0, 0, 0};
 #pragma unroll
         for (int t = 0; t < NT; t++) {
           const bch_v8i Bv = {(int)bc[t].x, (int)bc[t].y, (int)bc[t].z, (int)bc[t].w, 0, 0, 0, 0};
-          acc[t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, Bv, acc[t], 4, 4, 0, 128, 0, 127);
+          acc[t] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(A, Bv, acc[t], 4, 4, 0, 127, 0, 127);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

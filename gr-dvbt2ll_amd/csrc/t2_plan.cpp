@@ -231,14 +231,16 @@ int build_bch_mfma(FecPlan &fp) {
   if (!fp.kbch) return -1;
   const int P = fp.nparity, L = fp.kbch / 8;
   Poly192 g = bch_generator(fp.normal, P);
-  // BCH as a GF(2) matrix product for the chain's MFMA pass (bch_gemm_kernel): parity bit p (p = 0
+  // BCH as a GF(2) matrix product for the chain's MFMA pass (bbch_kernel): parity bit p (p = 0
   // the x^(P-1) coefficient, sent first) of message bit i is coefficient P-1-p of x^(kbch-1-i) x^P
   // mod g.  fp4 (e2m1) B fragments of v_mfma_scale_f32_32x32x64_f8f6f4: 32-byte message chunk q,
   // K-step u (the little-endian message word w of bytes 32 q + 16 (l >> 5) + 4 u .. + 3), parity tile
-  // t, lane l, dword d, nibble e <-> bit 4 e + d of w (the A fragment's dword d is (w >> d) & 0x11111111),
-  // i.e. message byte b = 32 q + 16 (l >> 5) + 4 u + (4 e + d) / 8, bit (4 e + d) % 8 (LSB first:
-  // i = 8 b + 7 - (4 e + d) % 8), parity p = 32 t + (l & 31); nibble 0x2 (1.0) where G[i][p] = 1.
-  // Bits past kbch and parities past P are zero.
+  // t, lane l, dword d, nibble e <-> bit 4 e + d of w, i.e. message byte b = 32 q + 16 (l >> 5) + 4 u +
+  // (4 e + d) / 8, bit (4 e + d) % 8 (LSB first: i = 8 b + 7 - (4 e + d) % 8), parity p = 32 t + (l & 31).
+  // The A fragment's dword d is the message bits left in place where it can be: w & 0x11111111 << d for
+  // d = 0, 1, 2 (nibbles 0001 = 0.5, 0010 = 1.0, 0100 = 2.0) and (w >> 1) & 0x44444444 for d = 3 (bit 3 of
+  // a nibble is the sign), scale 1; so B's set entries are 2.0, 1.0, 0.5, 0.5 (nibbles 0x4, 0x2, 0x1, 0x1)
+  // for d = 0 .. 3 and every product of set bits is exactly 1.  Bits past kbch and parities past P are zero.
   fp.bch_nq = (L + 31) / 32;
   fp.bch_nt = (P + 31) / 32;
   std::vector<Poly192> col(fp.kbch);
@@ -259,7 +261,7 @@ int build_bch_mfma(FecPlan &fp) {
           for (int d = 0; d < 4; d++)
             for (int e = 0; e < 8; e++) {
               const int wb = 4 * e + d, b = 32 * q + 16 * (l >> 5) + 4 * u + wb / 8, i = 8 * b + 7 - wb % 8;
-              if (i < fp.kbch && p < P && col[i].bit(P - 1 - p)) e4[d] |= 2u << (4 * e);
+              if (i < fp.kbch && p < P && col[i].bit(P - 1 - p)) e4[d] |= (d == 0 ? 4u : d == 1 ? 2u : 1u) << (4 * e);
             }
         }
   return 0;

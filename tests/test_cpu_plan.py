@@ -344,7 +344,7 @@ def test_bch_lane_shift_tables(framesize, rate):
 
 @pytest.mark.parametrize("framesize,rate", [(1, r) for r in range(6)] + [(0, r) for r in range(8)])
 def test_bch_matrix_core_table(framesize, rate):
-    """The chain's BCH pass (t2_kernels.hip bch_gemm_kernel) computes every block's parity as a GF(2)
+    """The chain's BCH (t2_kernels.hip bbch_kernel) computes every block's parity as a GF(2)
     matrix product on the matrix cores: fp4 A fragments masked from the message words, fp4 B fragments
     from the planner table (build_bch_mfma), exact sums, parity = sum & 1, K split into slices whose
     partial parities are XORed (BCH_KS = 8).  Replayed here with the kernel's operand pairing (lane half h,
@@ -367,8 +367,13 @@ def test_bch_matrix_core_table(framesize, rate):
     nq, nt = tab.shape[0], tab.shape[2]
     assert nq == (L + 31) // 32 and nt == (P + 31) // 32
     nib = (tab[..., None] >> (4 * np.arange(8, dtype=np.uint32))) & 0xF    # (nq, 4, nt, 64, 4, 8)
-    assert set(np.unique(nib)) <= {0, 2}
-    tb = (nib == 2).astype(np.int64).reshape(nq, 4, nt, 2, 32, 4, 8)       # lane = 32 h + c
+    # B's set entries per A dword d: fp4 2.0, 1.0, 0.5, 0.5 against the kernel's A values 0.5, 1.0, 2.0, 2.0
+    # (dword d keeps bit d of each nibble in place, d = 3 moved down one): every product of set bits is 1
+    code, fp4 = np.array([4, 2, 1, 1]), {0: 0.0, 1: 0.5, 2: 1.0, 4: 2.0}
+    for d in range(4):
+        assert set(np.unique(nib[..., d, :])) <= {0, int(code[d])}
+        assert fp4[int(code[d])] * [0.5, 1.0, 2.0, 2.0][d] == 1.0
+    tb = (nib != 0).astype(np.int64).reshape(nq, 4, nt, 2, 32, 4, 8)       # lane = 32 h + c
     rng = np.random.default_rng(2000 + 10 * framesize + rate)
     for _ in range(2):
         msg = rng.integers(0, 256, 32 * nq, dtype=np.uint8)                # garbage past L
