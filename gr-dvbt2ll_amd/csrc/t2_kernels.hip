@@ -801,16 +801,15 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t *d, int i) {   // i d
   const uint64_t lo = ((uint64_t)d[1] << 32) | d[0], hi = ((uint64_t)d[3] << 32) | d[2];
   return (uint32_t)(((i & 8) ? hi : lo) >> (8 * (i & 7))) & 0xFFu;
 }
-__device__ __forceinline__ void set_byte(uint32_t *d, int i, uint32_t b) {   // i dynamic, 0 .. 15
-  uint64_t lo = ((uint64_t)d[1] << 32) | d[0], hi = ((uint64_t)d[3] << 32) | d[2];
-  const uint64_t m = 0xFFull << (8 * (i & 7)), v = (uint64_t)b << (8 * (i & 7));
-  const uint64_t lo2 = (lo & ~m) | v, hi2 = (hi & ~m) | v;
-  lo = (i & 8) ? lo : lo2;
-  hi = (i & 8) ? hi2 : hi;
-  d[0] = (uint32_t)lo;
-  d[1] = (uint32_t)(lo >> 32);
-  d[2] = (uint32_t)hi;
-  d[3] = (uint32_t)(hi >> 32);
+__device__ __forceinline__ void set_byte(uint32_t *d, int i, uint32_t b) {   // i dynamic, 0 .. 15; b < 256
+  // one byte permute per dword: the identity selector (bytes 4 .. 7 pick d's bytes) with byte i's selector 0
+  // (b's byte 0); the four selectors as two 64-bit halves
+  const uint64_t id = 0x0706050407060504ull, m = 0xFFull << (8 * (i & 7));
+  const uint64_t slo = (i & 8) ? id : id & ~m, shi = (i & 8) ? id & ~m : id;
+  d[0] = __builtin_amdgcn_perm(d[0], b, (uint32_t)slo);
+  d[1] = __builtin_amdgcn_perm(d[1], b, (uint32_t)(slo >> 32));
+  d[2] = __builtin_amdgcn_perm(d[2], b, (uint32_t)shi);
+  d[3] = __builtin_amdgcn_perm(d[3], b, (uint32_t)(shi >> 32));
 }
 
 // one row's BB state over the chunks: the block's geometry and, per lane, its stream cursor
