@@ -835,9 +835,10 @@ __device__ __forceinline__ uint32_t fold8(uint64_t x) {
   const uint32_t y = (uint32_t)x ^ (uint32_t)(x >> 32);
   return (y ^ (y >> 8) ^ (y >> 16) ^ (y >> 24)) & 0xFFu;
 }
-// the register at the next chunk (both lanes) from s; slot: this lane's sync slot value (e < 16)
+// the register at the next chunk (both lanes) from s; slot: this lane's sync slot value, be: the piece's byte
+// at the sync position (e < 16)
 __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *tp, const uint8_t *tq, const uint4 *pmask, const uint32_t *d,
-                                              int e, int h, uint32_t s, uint32_t &slot) {
+                                              int e, int h, uint32_t s, uint32_t &slot, uint32_t &be) {
   const bool sync = e < 16;
   uint32_t w[4];
 #pragma unroll
@@ -859,7 +860,7 @@ __device__ __forceinline__ uint32_t crc_chunk(const uint8_t *tp, const uint8_t *
   const uint32_t s_in = h ? y : s;
   const uint32_t sf = (uint32_t)tp[15 * 256 + s_in] ^ g;
   const uint64_t dlo = ((uint64_t)d[1] << 32) | d[0], dhi = ((uint64_t)d[3] << 32) | d[2];
-  const uint32_t be = (uint32_t)(((e & 8) ? dhi : dlo) >> (8 * (e & 7))) & 0xFFu;
+  be = (uint32_t)(((e & 8) ? dhi : dlo) >> (8 * (e & 7))) & 0xFFu;
   slot = (uint32_t)tq[(15 - min(e, 15)) * 256 + (sf ^ A)] ^ be;
   const uint32_t o1 = sync ? A : sf;
   const uint32_t z = (uint32_t)__shfl_xor((int)o1, 32);
@@ -973,8 +974,8 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
 #pragma unroll
         for (int k = 0; k < 4; k++) pd[k] = R.live ? w.a[k] : 0u;
         const int e = R.m == 0 ? 0 : 188 - R.m;
-        uint32_t slot;
-        crc = crc_chunk(tp, tq, pmask, pd, e, h, crc, slot);
+        uint32_t slot, be;
+        crc = crc_chunk(tp, tq, pmask, pd, e, h, crc, slot, be);
         R.rel += 32;
         R.m += 32;
         R.m -= R.m >= 188 ? 188 : 0;
@@ -996,13 +997,13 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
       for (int k = 0; k < 4; k++) raw[k] = w.a[k];
       if (!HEM) {
         const int e = R.m == 0 ? 0 : 188 - R.m;
-        uint32_t slot;
-        crc = crc_chunk(tp, tq, pmask, raw, e, h, crc, slot);
+        uint32_t slot, be;
+        crc = crc_chunk(tp, tq, pmask, raw, e, h, crc, slot, be);
 #pragma unroll
         for (int k = 0; k < 4; k++) pd[k] = raw[k];
         const int j = P0 + e - 10;   // payload byte at the sync position
         if (e < 16 && j >= 0 && j < npay && R.live) {
-          if (io.sync_err && byte_of(raw, e) != 0x47u) atomicAdd(io.sync_err, 1u);   // bbheader:703-705
+          if (io.sync_err && be != 0x47u) atomicAdd(io.sync_err, 1u);   // bbheader:703-705
           set_byte(pd, e, slot);
         }
         R.rel += 32;
