@@ -1074,10 +1074,7 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
 #pragma unroll
         for (int k = 0; k < 4; k++) pd[k] ^= w.p[k];
       }
-      if (!R.live) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) pd[k] = 0u;
-      }
+      // (a dead row's piece is garbage: it goes to the spare row, and its own accumulator rows are never written out)
     };
     // the window the piece of chunk q needs (requested a chunk ahead)
     // (the PRBS half as a vector load with the window: two uniform scalar loads and a per-lane select cost 12
