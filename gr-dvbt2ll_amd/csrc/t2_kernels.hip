@@ -1070,10 +1070,9 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
         }
       }
       // BB scrambling: the chunk's 32 PRBS bytes as two uniform scalar loads, this half's 16
-      if (P0 < L) {
+      // (unconditional: past the BBFRAME the PRBS padding is zero, t2_plan FecPlan::prbs_bytes)
 #pragma unroll
-        for (int k = 0; k < 4; k++) pd[k] ^= w.p[k];
-      }
+      for (int k = 0; k < 4; k++) pd[k] ^= w.p[k];
       // (a dead row's piece is garbage: it goes to the spare row, and its own accumulator rows are never written out)
     };
     // the window the piece of chunk q needs (requested a chunk ahead)
