@@ -730,8 +730,8 @@ typedef float bch_v16f __attribute__((ext_vector_type(16)));
 // register to each other once per piece.  A tile segment starting at chunk q0 first streams the CRC through the
 // BBCH_PRO chunks (192 stream bytes) before it, so a sync position (one every 188 bytes) has restarted the
 // register before the first slot it fills.
-constexpr int BBCH_THREADS = 256;   // 4 waves: a tile of 128 FEC blocks per workgroup, two workgroups per CU (~220
-constexpr int BBCH_ROWS = 128;      // VGPRs: two waves per SIMD)
+constexpr int BBCH_THREADS = 256;   // 4 waves: a tile of 128 FEC blocks per workgroup, two workgroups per CU (up
+constexpr int BBCH_ROWS = 128;      // to 256 VGPRs: two waves per SIMD)
 constexpr int BBCH_WG_PER_CU = 2;
 constexpr int BBCH_PRO = 6;         // CRC prologue chunks (6 x 32 >= 188 + 4)
 // T^k, T^-k, BBHEADER CRC per byte, in-band bytes, the CRC prefix masks (17 x 16 bytes)
@@ -1069,8 +1069,8 @@ __global__ __launch_bounds__(BBCH_THREADS, BBCH_WG_PER_CU) void bbch_kernel(FecD
           set_byte(pd, i, R.g.padding && k < 13 ? (uint32_t)ibb[k] : 0u);
         }
       }
-      // BB scrambling: the chunk's 32 PRBS bytes as two uniform scalar loads, this half's 16
-      // (unconditional: past the BBFRAME the PRBS padding is zero, t2_plan FecPlan::prbs_bytes)
+      // BB scrambling: this half's 16 PRBS bytes, loaded with the window (unconditional: past the BBFRAME the PRBS
+      // padding is zero, t2_plan FecPlan::prbs_bytes)
 #pragma unroll
       for (int k = 0; k < 4; k++) pd[k] ^= w.p[k];
       // (a dead row's piece is garbage: it goes to the spare row, and its own accumulator rows are never written out)
