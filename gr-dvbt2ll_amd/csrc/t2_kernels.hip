@@ -1467,7 +1467,9 @@ __device__ __forceinline__ void map_quads_load(const MapDev &d, int blk, int tid
   const int32_t *qb = d.slot_qbase + (int64_t)r * (d.slot_stride >> 6);
   const int nqd = kc(d.slot_nq, r);
   constexpr int NW = NT / 64;
-  const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
+  // the wave index as a scalar (readfirstlane): the chunk c derived from it is then wave-uniform for the compiler,
+  // so kc(qb, c) is a scalar load (with tid >> 6 in a VGPR it was a vector load and its address math, per quad)
+  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), nch = (nqd + 63) >> 6;
 #pragma unroll
   for (int u = 0; u < MQ; u++) {
     const int c = min(c0 + u * NW + wv, nch - 1);   // wave-uniform
@@ -1483,7 +1485,9 @@ __device__ void map_store_quads(const MapDev &d, uint16_t *out_pairs, int64_t fr
   uint16_t *dst = out_pairs + (int64_t)(blk / d.F) * frame_stride;   // frame data region
   const int nqd = kc(d.slot_nq, r);
   constexpr int NW = NT / 64;
-  const int lane = tid & 63, wv = tid >> 6, nch = (nqd + 63) >> 6;
+  // the wave index as a scalar (readfirstlane): the chunk c derived from it is then wave-uniform for the compiler,
+  // so kc(qb, c) is a scalar load (with tid >> 6 in a VGPR it was a vector load and its address math, per quad)
+  const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6), nch = (nqd + 63) >> 6;
   const uint8_t *ib = idx - 1;   // ib[j + 1] = idx[j], ib[j] = idx[j - 1]
   // entry bits 0..14: j; bit 15: another block's slot (j = 0 then, read and dropped)
   auto pair_of = [&](uint32_t j) -> uint32_t {
